@@ -1,0 +1,187 @@
+"""Benchmark: Mpaths/s of the path-mis.py NEE+MIS integrator on the bedroom
+proxy at 1280x720 (BASELINE.json configs[1]), one process per GPU.
+
+A step renders the full 1280x720 film at `--spp` samples per pixel on every
+rank; rank r traces the global sample range [r*spp, (r+1)*spp) of every pixel
+(weak scaling: per-GPU work is fixed, the job's spp grows with N), and the
+per-rank films are gathered to rank 0 over RCCL and summed in rank order.
+Inputs (scene, BVH) are resident in HBM before the timed region; the film
+stays in HBM and only the gather crosses GPUs.
+
+Prints ONE JSON line on rank 0 (contract in the task statement) with
+`roofline` for the closest-hit traversal kernel (HIP-event time over the
+timed region, algorithmic bytes from in-kernel visit counts) and
+`cpu_baseline` (the oracle/ CPU restatement on a bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mitsuba3-experiments_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
+NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES = 64, 48, 32, 16
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--spp", type=int, default=64)
+    p.add_argument("--width", type=int, default=1280)
+    p.add_argument("--height", type=int, default=720)
+    p.add_argument("--max-depth", type=int, default=8)
+    p.add_argument("--rr-depth", type=int, default=2)
+    p.add_argument("--chunk", type=int, default=0, help="wavefront paths per chunk (0 = library default)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-rows", type=int, default=8, help="film rows of the CPU baseline sample")
+    p.add_argument("--cpu-spp", type=int, default=4)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from mtx import PathIntegrator, scene
+
+    sc = scene.bedroom(width=args.width, height=args.height)
+    integ = PathIntegrator({"max_depth": args.max_depth, "rr_depth": args.rr_depth})
+    W, H, spp = sc.width, sc.height, args.spp
+    film = torch.empty((H + 2, W + 2, 4), dtype=torch.float32, device=f"cuda:{local}")
+    gathered = [torch.empty_like(film) for _ in range(world)] if world > 1 else None
+    total = torch.empty_like(film)
+
+    def step(i, stats=False):
+        r = integ.render_film(sc, seed=i, spp=spp, spp_total=spp * world, sample_offset=spp * rank, out=film,
+                              stats=stats, chunk_paths=args.chunk)
+        if world > 1:
+            dist.all_gather(gathered, film)
+            if rank == 0:
+                total.zero_()
+                for g in gathered:  # fixed rank order: deterministic sum
+                    total.add_(g)
+        return r[1] if stats else None
+
+    for i in range(args.warmup):
+        step(1000 + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    agg = None
+    for i in range(args.steps):
+        st = step(i, stats=True)
+        if agg is None:
+            agg = dict(st)
+        else:
+            for k, v in st.items():
+                agg[k] += v
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    paths_per_rank = W * H * spp
+    value = world * paths_per_rank * args.steps / elapsed / 1e6
+    # roofline of the dominant kernel: closest-hit traversal
+    alg_bytes = (agg["rays_closest"] * (RAY_BYTES + HIT_BYTES) + agg["nodes_closest"] * NODE_BYTES
+                 + agg["tris_closest"] * TRI_BYTES)
+    trace_s = agg["trace_ms"] / 1e3
+    achieved = alg_bytes / trace_s / 1e9 if trace_s > 0 else 0.0
+    launches = max(1, agg["trace_launches"])
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(sc, integ, args)
+        out = {
+            "metric": "Mpaths/sec on bedroom@1280×720 spp=256, 1/2/4/8 GPUs; HBM GB/s vs peak",
+            "value": round(value, 3),
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: deterministic bedroom proxy (scene.xml camera/BSDFs/emitters, "
+                    f"{sc.n_tris} procedural triangles)",
+            "config": {
+                "workload": f"path-mis.py NEE+MIS (BASELINE configs[1]) on bedroom-proxy {W}x{H}, spp={spp} per GPU "
+                            f"(global sample range per rank), max_depth={args.max_depth}, rr_depth={args.rr_depth}",
+                "global_spp": spp * world,
+                "paths_per_step": paths_per_rank * world,
+                "parallelism": f"sample-range shards x{world}, RCCL all_gather of films",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_trace_closest (BVH2 closest-hit traversal)",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_ms": round(agg["trace_ms"] / launches, 4),
+                "alg_bytes_per_launch": int(alg_bytes / launches),
+                "rays": int(agg["rays_closest"]),
+                "node_visits_per_ray": round(agg["nodes_closest"] / max(1, agg["rays_closest"]), 2),
+                "tri_visits_per_ray": round(agg["tris_closest"] / max(1, agg["rays_closest"]), 2),
+            },
+            "kernels_ms_per_step": {
+                "trace_closest": round(agg["trace_ms"] / args.steps, 3),
+                "trace_shadow": round(agg["shadow_ms"] / args.steps, 3),
+                "shade": round(agg["shade_ms"] / args.steps, 3),
+                "other": round(agg["other_ms"] / args.steps, 3),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sc, integ, args):
+    """oracle/ (the CPU restatement, OpenMP) on a bounded sample of the same
+    workload: the first `cpu_rows` film rows at `cpu_spp`, same seed scheme."""
+    import binding as oracle
+
+    oracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    y1 = min(sc.height, args.cpu_rows)
+    a = integ.render_args(sc, 0, args.cpu_spp, 0, y1)
+    oracle.render(sc, oracle.render_args(a.integrator, a.max_depth, a.rr_depth, 0, 1, 0, 1))  # warm
+    t0 = time.perf_counter()
+    oracle.render(sc, a)
+    dt = time.perf_counter() - t0
+    n = sc.width * y1 * args.cpu_spp
+    return {"value": round(n / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": f"{sc.width}x{y1} rows x spp={args.cpu_spp} ({n} paths) of the same workload, "
+                      f"{dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,249 @@
+/* mtx.h — C ABI of libmtx, the MI355X (gfx950) wavefront path-tracing
+ * integrator that replaces the per-bounce `sample()` loop of
+ * DoeringChristian/mitsuba3-experiments.
+ *
+ * Plain C: fixed-width integers, floats, pointers and sizes only. Every entry
+ * point returns 0 on success and a negative MTX_E* code on failure; the
+ * message is available from mtx_last_error() (thread-local). No exceptions
+ * cross the ABI. Host buffers are caller-owned and only read/written during
+ * the call; calls are synchronous with respect to their outputs. A context
+ * is bound to one HIP device and is not thread-safe: one host thread per
+ * context (ctypes releases the GIL during the call, so N Python threads or N
+ * processes can drive N GPUs).
+ *
+ * What each entry point replaces in the reference (file:line under the
+ * reference root) is stated above its declaration. The ctypes binding a
+ * maintainer adds on the reference side is in INTEGRATION.md.
+ */
+#ifndef MTX_H_
+#define MTX_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTX_ABI_VERSION 1
+
+enum {
+  MTX_OK = 0,
+  MTX_E_ARG = -1,     /* bad argument / shape mismatch */
+  MTX_E_HIP = -2,     /* HIP runtime error */
+  MTX_E_NOSCENE = -3, /* no scene uploaded */
+  MTX_E_OOM = -4,     /* device allocation failed */
+  MTX_E_UNSUPPORTED = -5
+};
+
+/* ------------------------------------------------------------------ */
+/* Scene layout (SoA records copied to HBM as-is by mtx_scene_upload). */
+/* ------------------------------------------------------------------ */
+
+/* Material types: the 8 BSDF plugins of data/bedroom/scene.xml:26-219. */
+enum {
+  MTX_MAT_DIFFUSE = 1,         /* diffuse (rgb or bitmap reflectance) */
+  MTX_MAT_ROUGHPLASTIC = 2,    /* roughplastic (ggx/beckmann, nonlinear) */
+  MTX_MAT_CONDUCTOR = 3,       /* conductor (smooth) */
+  MTX_MAT_ROUGHCONDUCTOR = 4,  /* roughconductor (ggx/beckmann) */
+  MTX_MAT_DIELECTRIC = 5,      /* dielectric (smooth) */
+  MTX_MAT_ROUGHDIELECTRIC = 6  /* roughdielectric */
+};
+/* Material flags. A `mask` BSDF is its nested BSDF + MTX_MF_MASK + opacity;
+ * a `twosided` wrapper is MTX_MF_TWOSIDED on the nested BSDF. */
+enum {
+  MTX_MF_TWOSIDED = 1,
+  MTX_MF_MASK = 2,
+  MTX_MF_BECKMANN = 4, /* microfacet distribution: 0 = ggx */
+  MTX_MF_NONLINEAR = 8
+};
+
+#define MTX_ROUGH_TRANSMITTANCE_RES 64
+
+typedef struct mtx_material {
+  uint32_t type;
+  uint32_t flags;
+  int32_t tex;           /* bitmap texture index for (diffuse_)reflectance, -1 = use rgb */
+  float opacity;         /* mask opacity */
+  float rgb[3];          /* reflectance | diffuse_reflectance | specular_reflectance */
+  float alpha;           /* microfacet roughness */
+  float eta;             /* int_ior / ext_ior (dielectric, roughdielectric, roughplastic) */
+  float eta_rgb[3];      /* conductor eta (real part) */
+  float k_rgb[3];        /* conductor k (imaginary part) */
+  float spec_weight;     /* roughplastic specular sampling weight */
+  float internal_refl;   /* roughplastic internal reflectance */
+  int32_t table;         /* roughplastic: offset (floats) of its 64-entry external transmittance table */
+} mtx_material;
+
+typedef struct mtx_texture {
+  uint32_t width, height;
+  uint64_t offset; /* offset (in floats) into texels[], RGB interleaved, linear */
+} mtx_texture;
+
+/* Area emitter on a `rectangle` shape (scene.xml:706-731). */
+typedef struct mtx_emitter {
+  float center[3];  /* to_world translation */
+  float col0[3];    /* to_world * (1,0,0) */
+  float col1[3];    /* to_world * (0,1,0) */
+  float normal[3];  /* normalize(inverse-transpose(to_world) * (0,0,1)) */
+  float inv_area;   /* 1 / |cross(2 col0, 2 col1)| */
+  float radiance[3];
+} mtx_emitter;
+
+typedef struct mtx_shape {
+  uint32_t material;
+  int32_t emitter; /* -1 if not an emitter */
+  uint32_t flags;  /* bit0: face_normals / no vertex normals, bit1: has uv */
+  uint32_t pad;
+} mtx_shape;
+
+/* Perspective sensor (scene.xml:10-25). */
+typedef struct mtx_camera {
+  float origin[3];  /* to_world translation */
+  float axis_x[3];  /* to_world columns */
+  float axis_y[3];
+  float axis_z[3];
+  float tan_x, tan_y; /* tan(fov_x/2), tan(fov_x/2) / aspect */
+  float near_clip, far_clip;
+  uint32_t width, height;
+} mtx_camera;
+
+/* BVH2 node (64 B): bounds of both children, Aila-Laine layout.
+ *   f[0..3]  = c0.lo.x c0.hi.x c0.lo.y c0.hi.y
+ *   f[4..7]  = c1.lo.x c1.hi.x c1.lo.y c1.hi.y
+ *   f[8..11] = c0.lo.z c0.hi.z c1.lo.z c1.hi.z
+ *   i[12], i[13] = child0, child1: >= 0 inner node index,
+ *                  < 0 leaf: ~c = (first_tri << 3) | (count - 1)
+ *   i[14], i[15] = 0
+ * Triangles are stored in leaf order as 12 floats (48 B):
+ *   v0.xyz, 0, e1 = v1-v0 .xyz, 0, e2 = v2-v0 .xyz, 0 */
+#define MTX_BVH_MAX_LEAF 8
+#define MTX_BVH_MAX_DEPTH 40
+
+typedef struct mtx_scene_desc {
+  uint32_t n_tris, n_nodes, n_verts, n_shapes;
+  uint32_t n_materials, n_emitters, n_textures, flags;
+  const int32_t *nodes;      /* 16 words per node */
+  const float *tri_geom;     /* 12 floats per triangle (leaf order) */
+  const uint32_t *tri_vidx;  /* 3 vertex indices per triangle (leaf order) */
+  const uint32_t *tri_shape; /* shape index per triangle (leaf order) */
+  const float *vpos;         /* 3 per vertex */
+  const float *vnormal;      /* 3 per vertex, may be NULL */
+  const float *vuv;          /* 2 per vertex, may be NULL */
+  const mtx_shape *shapes;
+  const mtx_material *materials;
+  const mtx_emitter *emitters;
+  const mtx_texture *textures;
+  const float *texels;
+  uint64_t n_texels;         /* floats */
+  const float *tables;       /* roughplastic transmittance tables */
+  uint32_t n_tables;         /* floats */
+  uint32_t pad0;
+  mtx_camera camera;
+} mtx_scene_desc;
+
+/* Integrators (the reference scripts whose sample() loop is replaced). */
+enum {
+  MTX_INT_PATH = 1,          /* path.py:194-302 ("mypath") */
+  MTX_INT_PATH_MIS = 2,      /* path-mis.py:24-155 ("path_test") */
+  MTX_INT_NRC = 3,           /* nrc.py:25-125 */
+  MTX_INT_PSSMLT_SIMPLE = 4, /* pssmlt.py:167-228 + pssmltsimple.py:16-142 */
+  MTX_INT_RESTIR_GI = 5      /* restirgi.py:182-588 */
+};
+
+typedef struct mtx_render_args {
+  uint32_t integrator;
+  uint32_t max_depth;
+  uint32_t rr_depth;
+  uint32_t seed;
+  uint32_t spp;          /* samples traced per pixel by this call */
+  uint32_t spp_total;    /* samples per pixel of the whole job (lane stride) */
+  uint32_t sample_offset;/* first global sample index of this call (rank shard) */
+  uint32_t y0, y1;       /* film rows [y0, y1) traced by this call */
+  uint32_t chunk_paths;  /* wavefront size (0 = default) */
+  float nrc_c;           /* NRC spread threshold (nrc.py:123) */
+  uint32_t flags;        /* bit0: collect traversal stats, bit1: per-kernel HIP event timing */
+} mtx_render_args;
+
+/* Device-side counters, filled when mtx_render_args.flags has bit0/bit1. */
+typedef struct mtx_stats {
+  uint64_t rays_closest, rays_shadow;
+  uint64_t nodes_closest, tris_closest; /* node / triangle visits */
+  uint64_t nodes_shadow, tris_shadow;
+  uint64_t trace_launches;              /* closest-hit traversal launches */
+  uint64_t shadow_launches;
+  double trace_ms, shadow_ms, shade_ms, other_ms; /* HIP-event time, summed */
+  uint64_t paths;
+} mtx_stats;
+
+/* --------------------------- context ------------------------------ */
+int mtx_abi_version(void);
+const char *mtx_last_error(void);
+typedef struct mtx_ctx mtx_ctx;
+/* One context per HIP device; owns every device allocation. */
+int mtx_ctx_create(int hip_device, mtx_ctx **out);
+void mtx_ctx_destroy(mtx_ctx *ctx);
+
+/* --------------------------- scene -------------------------------- */
+/* Host-only binned-SAH BVH2 build over an indexed triangle mesh (replaces
+ * Embree/OptiX acceleration-structure builds behind mi.load_file, upstream).
+ * nodes_out: capacity 2*n_tris*16 words; tri_geom_out: 12*n_tris floats;
+ * perm_out: n_tris (leaf order -> input triangle index). */
+int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t *tri_vidx, uint32_t n_tris,
+                  int32_t *nodes_out, uint32_t *n_nodes_out, float *tri_geom_out, uint32_t *perm_out,
+                  uint32_t *depth_out);
+/* Host-only roughplastic precompute (upstream roughplastic constructor):
+ * external transmittance table (64 floats) and internal reflectance. */
+int mtx_roughplastic_tables(uint32_t distribution, float alpha, float eta, float *table_out,
+                            float *internal_refl_out);
+/* Copy a scene to HBM (replaces mi.load_file / mi.load_dict scene
+ * construction, path.py:308-309, restirgi.py:599). */
+int mtx_scene_upload(mtx_ctx *ctx, const mtx_scene_desc *scene);
+
+/* --------------------------- integrators -------------------------- */
+/* Render film rows [y0,y1) (+1-pixel tent border) into film_rgbw, an
+ * (y1-y0+2) x (width+2) x 4 float buffer (host pointer, or a device pointer
+ * when film_on_device != 0): un-normalised RGB*weight and weight sums in a
+ * fixed summation order. Replaces mi.render(scene, integrator, spp, seed)
+ * driving SamplingIntegrator::render (transcribed path.py:103-192) with the
+ * sample() of path.py:194-302 / path-mis.py:24-155 / nrc.py:104-125, and
+ * Pssmlt.render (pssmlt.py:167-228). */
+int mtx_render(mtx_ctx *ctx, const mtx_render_args *args, float *film_rgbw, int film_on_device,
+               mtx_stats *stats);
+
+/* Evaluate the integrator's sample() for n given rays (replaces
+ * SamplingIntegrator.sample(scene, sampler, ray), path-mis.py:24-31).
+ * rays: 6n floats (o.xyz, d.xyz); lanes: n sampler lane ids; each lane's
+ * PCG32 stream is seeded with (seed, lane) and advanced by rng_skip draws
+ * before the first bounce (the render loop consumes 2 for the film jitter).
+ * Outputs: L (3n floats), valid (n bytes). Host pointers. */
+int mtx_sample_rays(mtx_ctx *ctx, const mtx_render_args *args, uint64_t n, const float *rays,
+                    const uint32_t *lanes, uint32_t rng_skip, float *L, uint8_t *valid);
+
+/* Raw closest-hit / any-hit traversal (Scene.ray_intersect / ray_test,
+ * path-mis.py:69-71, restirgi.py:320). rays: 8n floats (o.xyz, tmax, d.xyz,
+ * 0); hits: 4n words (t, prim, u, v) for closest-hit, or n words (1 =
+ * occluded) for any-hit. visits (optional, 2n u32): node and triangle visits. */
+int mtx_trace(mtx_ctx *ctx, uint64_t n, const float *rays, int any_hit, uint32_t *hits,
+              uint32_t *visits);
+
+/* --------------------------- primitives --------------------------- */
+/* prefix_sum.py:9-36: inclusive (or exclusive) scan of u32, device-wide
+ * decoupled look-back. Host pointers. */
+int mtx_prefix_sum_u32(mtx_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, int inclusive);
+/* prefix_sum.py:9-36 with f32 data in Hillis-Steele summation order
+ * (floor(log2 n)+1 passes x[j] += x[j-2^i]), bit-identical to the reference. */
+int mtx_prefix_sum_f32_hs(mtx_ctx *ctx, const float *in, float *out, uint64_t n);
+/* hashgrid.py:16-90: cell = hash(trunc((p-bbmin)/(bbmax-bbmin)*res)) % n_cells,
+ * cell_size, exclusive cell_offset, and sample_idx (per-cell order ascending
+ * by sample index). p: 3n floats (x[n], y[n], z[n] planes). */
+int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells,
+                       uint32_t *cell, uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx);
+/* reductions.py:12-54 scatter_reduce_with for op in {ADD=0, MIN=1, MAX=2}:
+ * target[index[i]] = op(target[index[i]], value[i]). ADD sums each target's
+ * values in ascending i order (deterministic). target is read-modify-write. */
+int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
+                           const uint32_t *index, uint64_t n_value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTX_H_ */

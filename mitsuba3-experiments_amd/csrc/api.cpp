@@ -1,0 +1,669 @@
+// api.cpp — libmtx C ABI (include/mtx.h): device context, scene upload,
+// wavefront scheduling and the primitive entry points.
+//
+// The host side of the replaced path: upstream SamplingIntegrator::render
+// (transcribed at path.py:103-192) seeds the sampler over W*H*spp lanes,
+// traces one Dr.Jit wavefront and splats into an ImageBlock. Here the same
+// lanes are processed in chunks of whole pixels; each chunk runs
+// raygen -> [trace, shade, shadow] x max_depth -> film stage 1 on one HIP
+// stream with no host synchronisation (the persistent kernels read their
+// queue lengths from device counters), then one film gather per call.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "mtx.h"
+#include "prims.h"
+#include "wavefront.h"
+
+static thread_local char g_err[1024] = "";
+
+void mtx_set_error(const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) {                                                                       \
+      mtx_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return MTX_E_HIP;                                                                           \
+    }                                                                                             \
+  } while (0)
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+int dalloc(DevBuf &b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return MTX_OK;
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  if (bytes == 0) return MTX_OK;
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) {
+    mtx_set_error("hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    b.p = nullptr;
+    return MTX_E_OOM;
+  }
+  b.bytes = bytes;
+  return MTX_OK;
+}
+
+void dfree(DevBuf &b) {
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+template <class T>
+int upload(DevBuf &b, const T *src, size_t count, hipStream_t st) {
+  if (!src || count == 0) {
+    dfree(b);
+    return MTX_OK;
+  }
+  int rc = dalloc(b, count * sizeof(T));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(b.p, src, count * sizeof(T), hipMemcpyHostToDevice, st));
+  return MTX_OK;
+}
+
+}  // namespace
+
+struct mtx_ctx {
+  int device = 0;
+  int n_cu = 256;
+  hipStream_t stream = nullptr;
+  bool has_scene = false;
+  // scene
+  DevBuf nodes, tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
+  mtxd::DevScene scene{};
+  // wavefront
+  DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
+  uint32_t capacity = 0;
+  // film
+  DevBuf contrib, film;
+  // scratch for sample_rays / trace / primitives
+  DevBuf s0, s1, s2, s3, s4, s5;
+  int trace_grid = 0, shade_grid = 0;
+  std::vector<hipEvent_t> events;
+};
+
+extern "C" {
+
+int mtx_abi_version(void) { return MTX_ABI_VERSION; }
+
+const char *mtx_last_error(void) { return g_err; }
+
+int mtx_ctx_create(int hip_device, mtx_ctx **out) {
+  if (!out) {
+    mtx_set_error("mtx_ctx_create: out is NULL");
+    return MTX_E_ARG;
+  }
+  *out = nullptr;
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (hip_device < 0 || hip_device >= n) {
+    mtx_set_error("mtx_ctx_create: device %d out of range (%d devices)", hip_device, n);
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(hip_device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, hip_device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    mtx_set_error("mtx_ctx_create: device %d is %s, libmtx is built for gfx950", hip_device, prop.gcnArchName);
+    return MTX_E_UNSUPPORTED;
+  }
+  mtx_ctx *c = new mtx_ctx();
+  c->device = hip_device;
+  c->n_cu = prop.multiProcessorCount;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    mtx_set_error("hipStreamCreate failed: %s", hipGetErrorString(e));
+    return MTX_E_HIP;
+  }
+  // Persistent grids: fill every CU (occupancy of the LDS-stack traversal).
+  c->trace_grid = c->n_cu * 8;
+  c->shade_grid = c->n_cu * 8;
+  *out = c;
+  return MTX_OK;
+}
+
+void mtx_ctx_destroy(mtx_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  DevBuf *bufs[] = {&c->nodes,  &c->tri,     &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
+                    &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
+                    &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
+                    &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
+                    &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
+  for (DevBuf *b : bufs) dfree(*b);
+  for (hipEvent_t ev : c->events) hipEventDestroy(ev);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
+  if (!c || !d) {
+    mtx_set_error("mtx_scene_upload: null argument");
+    return MTX_E_ARG;
+  }
+  if (!d->nodes || !d->tri_geom || !d->tri_vidx || !d->tri_shape || !d->vpos || !d->shapes || !d->materials ||
+      d->n_tris == 0 || d->n_nodes == 0 || d->n_emitters == 0 || !d->emitters) {
+    mtx_set_error("mtx_scene_upload: incomplete scene (need geometry, BVH, shapes, materials, >=1 emitter)");
+    return MTX_E_ARG;
+  }
+  // Validate indices on the host so that no kernel can read out of bounds.
+  for (uint32_t i = 0; i < d->n_nodes; ++i)
+    for (int k = 12; k < 14; ++k) {
+      int32_t ch = d->nodes[16 * (size_t)i + k];
+      if (ch >= 0) {
+        if ((uint32_t)ch >= d->n_nodes) {
+          mtx_set_error("mtx_scene_upload: node %u child %d out of range", i, ch);
+          return MTX_E_ARG;
+        }
+      } else {
+        uint32_t x = (uint32_t)(~ch), first = x >> 3, cnt = (x & 7u) + 1;
+        if ((uint64_t)first + cnt > d->n_tris) {
+          mtx_set_error("mtx_scene_upload: leaf [%u,+%u) exceeds %u triangles", first, cnt, d->n_tris);
+          return MTX_E_ARG;
+        }
+      }
+    }
+  for (uint64_t i = 0; i < 3ull * d->n_tris; ++i)
+    if (d->tri_vidx[i] >= d->n_verts) {
+      mtx_set_error("mtx_scene_upload: vertex index out of range");
+      return MTX_E_ARG;
+    }
+  for (uint32_t i = 0; i < d->n_tris; ++i)
+    if (d->tri_shape[i] >= d->n_shapes) {
+      mtx_set_error("mtx_scene_upload: shape index out of range");
+      return MTX_E_ARG;
+    }
+  for (uint32_t i = 0; i < d->n_shapes; ++i) {
+    if (d->shapes[i].material >= d->n_materials ||
+        (d->shapes[i].emitter >= 0 && (uint32_t)d->shapes[i].emitter >= d->n_emitters)) {
+      mtx_set_error("mtx_scene_upload: shape %u references a missing material/emitter", i);
+      return MTX_E_ARG;
+    }
+  }
+  for (uint32_t i = 0; i < d->n_materials; ++i) {
+    const mtx_material &m = d->materials[i];
+    if (m.tex >= 0) {
+      if ((uint32_t)m.tex >= d->n_textures || !d->textures) {
+        mtx_set_error("mtx_scene_upload: material %u texture out of range", i);
+        return MTX_E_ARG;
+      }
+      const mtx_texture &t = d->textures[m.tex];
+      if (t.offset + 3ull * t.width * t.height > d->n_texels || t.width == 0 || t.height == 0) {
+        mtx_set_error("mtx_scene_upload: texture %d exceeds texel buffer", m.tex);
+        return MTX_E_ARG;
+      }
+    }
+    if (m.type == MTX_MAT_ROUGHPLASTIC && (m.table < 0 || (uint32_t)m.table + MTX_ROUGH_TRANSMITTANCE_RES > d->n_tables)) {
+      mtx_set_error("mtx_scene_upload: roughplastic material %u has no transmittance table", i);
+      return MTX_E_ARG;
+    }
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = 0;
+  hipStream_t st = c->stream;
+  if ((rc = upload(c->nodes, d->nodes, 16ull * d->n_nodes, st))) return rc;
+  if ((rc = upload(c->tri, d->tri_geom, 12ull * d->n_tris, st))) return rc;
+  if ((rc = upload(c->tri_vidx, d->tri_vidx, 3ull * d->n_tris, st))) return rc;
+  if ((rc = upload(c->tri_shape, d->tri_shape, (size_t)d->n_tris, st))) return rc;
+  if ((rc = upload(c->vpos, d->vpos, 3ull * d->n_verts, st))) return rc;
+  if ((rc = upload(c->vnormal, d->vnormal, d->vnormal ? 3ull * d->n_verts : 0, st))) return rc;
+  if ((rc = upload(c->vuv, d->vuv, d->vuv ? 2ull * d->n_verts : 0, st))) return rc;
+  if ((rc = upload(c->shapes, d->shapes, d->n_shapes, st))) return rc;
+  if ((rc = upload(c->materials, d->materials, d->n_materials, st))) return rc;
+  if ((rc = upload(c->emitters, d->emitters, d->n_emitters, st))) return rc;
+  if ((rc = upload(c->textures, d->textures, d->n_textures, st))) return rc;
+  if ((rc = upload(c->texels, d->texels, d->n_texels, st))) return rc;
+  if ((rc = upload(c->tables, d->tables, d->n_tables, st))) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  mtxd::DevScene &s = c->scene;
+  s.nodes = (const int4 *)c->nodes.p;
+  s.tri = (const float4 *)c->tri.p;
+  s.tri_vidx = (const uint32_t *)c->tri_vidx.p;
+  s.tri_shape = (const uint32_t *)c->tri_shape.p;
+  s.vpos = (const float *)c->vpos.p;
+  s.vnormal = (const float *)c->vnormal.p;
+  s.vuv = (const float *)c->vuv.p;
+  s.shapes = (const mtx_shape *)c->shapes.p;
+  s.materials = (const mtx_material *)c->materials.p;
+  s.emitters = (const mtx_emitter *)c->emitters.p;
+  s.textures = (const mtx_texture *)c->textures.p;
+  s.texels = (const float *)c->texels.p;
+  s.tables = (const float *)c->tables.p;
+  s.n_tris = d->n_tris;
+  s.n_emitters = d->n_emitters;
+  s.camera = d->camera;
+  c->has_scene = true;
+  return MTX_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+constexpr uint32_t kDefaultChunk = 1u << 22;
+
+int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
+  int rc;
+  if (cap > c->capacity) {
+    if ((rc = dalloc(c->ray_o, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->ray_d, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->thr, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->L, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->prev, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->misc, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->pos, 8ull * cap))) return rc;
+    if ((rc = dalloc(c->hit, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->q0, 4ull * cap))) return rc;
+    if ((rc = dalloc(c->q1, 4ull * cap))) return rc;
+    if ((rc = dalloc(c->shadow, sizeof(mtxd::ShadowRec) * (size_t)cap))) return rc;
+    c->capacity = cap;
+  }
+  if ((rc = dalloc(c->counters, 16ull * (max_depth + 2)))) return rc;
+  if ((rc = dalloc(c->stats, 8 * 8))) return rc;
+  return MTX_OK;
+}
+
+mtxd::WaveBuffers buffers(mtx_ctx *c) {
+  mtxd::WaveBuffers b;
+  b.ray_o = (float4 *)c->ray_o.p;
+  b.ray_d = (float4 *)c->ray_d.p;
+  b.thr = (float4 *)c->thr.p;
+  b.L = (float4 *)c->L.p;
+  b.prev = (float4 *)c->prev.p;
+  b.misc = (uint4 *)c->misc.p;
+  b.pos = (float2 *)c->pos.p;
+  b.hit = (float4 *)c->hit.p;
+  b.queue[0] = (uint32_t *)c->q0.p;
+  b.queue[1] = (uint32_t *)c->q1.p;
+  b.shadow = (mtxd::ShadowRec *)c->shadow.p;
+  b.counters = (uint32_t *)c->counters.p;
+  b.stats = (unsigned long long *)c->stats.p;
+  b.capacity = c->capacity;
+  return b;
+}
+
+int check_args(mtx_ctx *c, const mtx_render_args *a) {
+  if (!c || !a) {
+    mtx_set_error("null context or args");
+    return MTX_E_ARG;
+  }
+  if (!c->has_scene) {
+    mtx_set_error("no scene uploaded");
+    return MTX_E_NOSCENE;
+  }
+  if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC) {
+    mtx_set_error("integrator %u is not supported by this entry point", a->integrator);
+    return MTX_E_UNSUPPORTED;
+  }
+  if (a->max_depth > 0xfffe) {
+    mtx_set_error("max_depth %u too large", a->max_depth);
+    return MTX_E_ARG;
+  }
+  return MTX_OK;
+}
+
+// Event-pair timer per kernel class.
+struct Timer {
+  mtx_ctx *c;
+  bool on;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs[4];
+  size_t next = 0;
+  hipEvent_t get() {
+    if (next >= c->events.size()) {
+      hipEvent_t e;
+      hipEventCreate(&e);
+      c->events.push_back(e);
+    }
+    return c->events[next++];
+  }
+  hipEvent_t begin(int k) {
+    if (!on) return nullptr;
+    hipEvent_t e0 = get();
+    hipEventRecord(e0, c->stream);
+    return e0;
+  }
+  void end(int k, hipEvent_t e0) {
+    if (!on) return;
+    hipEvent_t e1 = get();
+    hipEventRecord(e1, c->stream);
+    pairs[k].push_back({e0, e1});
+  }
+  double total(int k) {
+    double ms = 0;
+    for (auto &p : pairs[k]) {
+      float t = 0;
+      hipEventElapsedTime(&t, p.first, p.second);
+      ms += t;
+    }
+    return ms;
+  }
+};
+
+// Runs one chunk's bounce loop (rays already generated, counters[0] set).
+void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
+                 uint64_t *n_trace, uint64_t *n_shadow) {
+  const mtxd::DevScene &s = c->scene;
+  const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1);
+  for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
+    hipEvent_t e = tm.begin(0);
+    mtxd::launch_trace_closest(s, b, bounce, p.stats, c->trace_grid, c->stream);
+    tm.end(0, e);
+    ++*n_trace;
+    e = tm.begin(2);
+    mtxd::launch_shade(s, b, p, bounce, c->shade_grid, c->stream);
+    tm.end(2, e);
+    e = tm.begin(1);
+    mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
+    tm.end(1, e);
+    ++*n_shadow;
+    // Deep paths (max_depth 65, scene.xml:6): stop launching once the queue
+    // has drained (checked every 8 bounces).
+    if (depth_iters > 16 && (bounce & 7) == 7 && bounce + 1 < depth_iters) {
+      uint32_t cnt = 0;
+      hipMemcpyAsync(&cnt, b.counters + 4 * (bounce + 1), 4, hipMemcpyDeviceToHost, c->stream);
+      hipStreamSynchronize(c->stream);
+      if (cnt == 0) break;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_on_device, mtx_stats *stats) {
+  int rc = check_args(c, a);
+  if (rc) return rc;
+  const mtx_camera &cam = c->scene.camera;
+  const uint32_t W = cam.width, H = cam.height;
+  if (!film_rgbw || a->spp == 0 || a->y1 <= a->y0 || a->y1 > H || a->spp_total < a->sample_offset + a->spp) {
+    mtx_set_error("mtx_render: bad film/rows/spp arguments");
+    return MTX_E_ARG;
+  }
+  if ((uint64_t)W * H * a->spp_total >= (1ull << 32)) {
+    mtx_set_error("mtx_render: W*H*spp_total exceeds the 32-bit sampler lane space");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  uint32_t chunk_paths = a->chunk_paths ? a->chunk_paths : kDefaultChunk;
+  uint32_t px_per_chunk = std::max<uint32_t>(1, chunk_paths / a->spp);
+  const uint32_t band_px = (a->y1 - a->y0) * W;
+  px_per_chunk = std::min(px_per_chunk, band_px);
+  const uint32_t cap = px_per_chunk * a->spp;
+  if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+  if ((rc = dalloc(c->contrib, 9ull * 16 * band_px))) return rc;
+  const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
+  float4 *film_dev = (float4 *)film_rgbw;
+  if (!film_on_device) {
+    if ((rc = dalloc(c->film, film_floats * 4))) return rc;
+    film_dev = (float4 *)c->film.p;
+  }
+  const bool want_stats = stats && (a->flags & 1u);
+  Timer tm{c, stats && (a->flags & 2u)};
+  mtxd::WaveBuffers b = buffers(c);
+  if (want_stats) HIP_TRY(hipMemsetAsync(b.stats, 0, 64, c->stream));
+  uint64_t n_trace = 0, n_shadow = 0;
+  hipEvent_t e_all = tm.begin(3);
+  for (uint32_t px0 = a->y0 * W; px0 < a->y1 * W; px0 += px_per_chunk) {
+    mtxd::ChunkParams p{};
+    p.integrator = a->integrator;
+    p.max_depth = a->max_depth;
+    p.rr_depth = a->rr_depth;
+    p.seed = a->seed;
+    p.spp = a->spp;
+    p.spp_total = a->spp_total;
+    p.sample_offset = a->sample_offset;
+    p.width = W;
+    p.height = H;
+    p.px0 = px0;
+    p.n_px = std::min(px_per_chunk, a->y1 * W - px0);
+    p.band_y0 = a->y0;
+    p.n_paths = p.n_px * a->spp;
+    p.nrc_c = a->nrc_c;
+    p.stats = want_stats ? 1 : 0;
+    HIP_TRY(hipMemsetAsync(b.counters, 0, 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2), c->stream));
+    mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
+    run_bounces(c, b, p, tm, &n_trace, &n_shadow);
+    mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, c->stream);
+  }
+  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, c->stream);
+  tm.end(3, e_all);
+  HIP_TRY(hipGetLastError());
+  if (!film_on_device)
+    HIP_TRY(hipMemcpyAsync(film_rgbw, film_dev, film_floats * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (stats) {
+    memset(stats, 0, sizeof(*stats));
+    if (want_stats) {
+      unsigned long long h[8];
+      HIP_TRY(hipMemcpy(h, b.stats, 64, hipMemcpyDeviceToHost));
+      stats->nodes_closest = h[0];
+      stats->tris_closest = h[1];
+      stats->nodes_shadow = h[2];
+      stats->tris_shadow = h[3];
+      stats->rays_closest = h[4];
+      stats->rays_shadow = h[5];
+    }
+    stats->trace_launches = n_trace;
+    stats->shadow_launches = n_shadow;
+    stats->paths = (uint64_t)band_px * a->spp;
+    if (tm.on) {
+      stats->trace_ms = tm.total(0);
+      stats->shadow_ms = tm.total(1);
+      stats->shade_ms = tm.total(2);
+      stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms;
+    }
+  }
+  return MTX_OK;
+}
+
+int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const float *rays, const uint32_t *lanes,
+                    uint32_t rng_skip, float *L, uint8_t *valid) {
+  int rc = check_args(c, a);
+  if (rc) return rc;
+  if (n == 0) return MTX_OK;
+  if (!rays || !lanes || !L || !valid) {
+    mtx_set_error("mtx_sample_rays: null buffer");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : kDefaultChunk;
+  const uint32_t cap = (uint32_t)std::min<uint64_t>(n, chunk);
+  if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+  if ((rc = dalloc(c->s0, 24ull * cap))) return rc;
+  if ((rc = dalloc(c->s1, 4ull * cap))) return rc;
+  if ((rc = dalloc(c->s2, 12ull * cap))) return rc;
+  if ((rc = dalloc(c->s3, 1ull * cap))) return rc;
+  mtxd::WaveBuffers b = buffers(c);
+  Timer tm{c, false};
+  uint64_t nt = 0, ns = 0;
+  for (uint64_t off = 0; off < n; off += cap) {
+    const uint32_t m = (uint32_t)std::min<uint64_t>(cap, n - off);
+    HIP_TRY(hipMemcpyAsync(c->s0.p, rays + 6 * off, 24ull * m, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->s1.p, lanes + off, 4ull * m, hipMemcpyHostToDevice, c->stream));
+    mtxd::ChunkParams p{};
+    p.integrator = a->integrator;
+    p.max_depth = a->max_depth;
+    p.rr_depth = a->rr_depth;
+    p.seed = a->seed;
+    p.spp = 1;
+    p.spp_total = 1;
+    p.width = c->scene.camera.width;
+    p.height = c->scene.camera.height;
+    p.n_paths = m;
+    p.nrc_c = a->nrc_c;
+    HIP_TRY(hipMemsetAsync(b.counters, 0, 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2), c->stream));
+    mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
+    run_bounces(c, b, p, tm, &nt, &ns);
+    mtxd::launch_collect(b, p, (float *)c->s2.p, (uint8_t *)c->s3.p, c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(valid + off, c->s3.p, m, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return MTX_OK;
+}
+
+int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *hits, uint32_t *visits) {
+  if (!c || !rays || !hits) {
+    mtx_set_error("mtx_trace: null argument");
+    return MTX_E_ARG;
+  }
+  if (!c->has_scene) {
+    mtx_set_error("no scene uploaded");
+    return MTX_E_NOSCENE;
+  }
+  if (n == 0) return MTX_OK;
+  if (n >= (1ull << 31)) {
+    mtx_set_error("mtx_trace: too many rays");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  const size_t hit_words = any_hit ? n : 4 * n;
+  if ((rc = dalloc(c->s0, 32ull * n))) return rc;
+  if ((rc = dalloc(c->s1, 4ull * hit_words))) return rc;
+  if (visits && (rc = dalloc(c->s2, 8ull * n))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->s0.p, rays, 32ull * n, hipMemcpyHostToDevice, c->stream));
+  mtxd::launch_trace_raw(c->scene, (const float4 *)c->s0.p, (uint32_t)n, any_hit, (uint32_t *)c->s1.p,
+                         visits ? (uint32_t *)c->s2.p : nullptr, c->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(hits, c->s1.p, 4ull * hit_words, hipMemcpyDeviceToHost, c->stream));
+  if (visits) HIP_TRY(hipMemcpyAsync(visits, c->s2.p, 8ull * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+// ------------------------------- primitives -------------------------------
+
+int mtx_prefix_sum_u32(mtx_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, int inclusive) {
+  if (!c || (n && (!in || !out))) {
+    mtx_set_error("mtx_prefix_sum_u32: null argument");
+    return MTX_E_ARG;
+  }
+  if (n == 0) return MTX_OK;
+  if (n >= (1ull << 32)) {
+    mtx_set_error("mtx_prefix_sum_u32: n >= 2^32");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = dalloc(c->s0, 4 * n))) return rc;
+  if ((rc = dalloc(c->s1, 4 * n))) return rc;
+  if ((rc = dalloc(c->s2, mtxd::scan_workspace_bytes(n)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->s0.p, in, 4 * n, hipMemcpyHostToDevice, c->stream));
+  rc = mtxd::scan_u32((const uint32_t *)c->s0.p, (uint32_t *)c->s1.p, n, inclusive, c->s2.p, c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->s1.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+int mtx_prefix_sum_f32_hs(mtx_ctx *c, const float *in, float *out, uint64_t n) {
+  if (!c || (n && (!in || !out))) {
+    mtx_set_error("mtx_prefix_sum_f32_hs: null argument");
+    return MTX_E_ARG;
+  }
+  if (n == 0) return MTX_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = dalloc(c->s0, 4 * n))) return rc;
+  if ((rc = dalloc(c->s1, 4 * n))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->s0.p, in, 4 * n, hipMemcpyHostToDevice, c->stream));
+  float *res = nullptr;
+  rc = mtxd::scan_f32_hs((float *)c->s0.p, (float *)c->s1.p, n, &res, c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, res, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+int mtx_hashgrid_build(mtx_ctx *c, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells, uint32_t *cell,
+                       uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx) {
+  if (!c || !p || !cell || !cell_size || !cell_offset || !sample_idx || n == 0 || n_cells == 0) {
+    mtx_set_error("mtx_hashgrid_build: bad argument");
+    return MTX_E_ARG;
+  }
+  if (n >= (1ull << 31)) {
+    mtx_set_error("mtx_hashgrid_build: n too large");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = dalloc(c->s0, 12 * n))) return rc;
+  if ((rc = dalloc(c->s1, 4 * n))) return rc;           // cell
+  if ((rc = dalloc(c->s2, 4 * (size_t)n_cells))) return rc;   // size
+  if ((rc = dalloc(c->s3, 4 * (size_t)n_cells))) return rc;   // offset
+  if ((rc = dalloc(c->s4, 4 * n))) return rc;           // sample_idx
+  if ((rc = dalloc(c->s5, mtxd::hashgrid_workspace_bytes(n, n_cells)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->s0.p, p, 12 * n, hipMemcpyHostToDevice, c->stream));
+  rc = mtxd::hashgrid_build((const float *)c->s0.p, n, resolution, n_cells, (uint32_t *)c->s1.p, (uint32_t *)c->s2.p,
+                            (uint32_t *)c->s3.p, (uint32_t *)c->s4.p, c->s5.p, c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(cell, c->s1.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(cell_size, c->s2.p, 4ull * n_cells, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(cell_offset, c->s3.p, 4ull * n_cells, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(sample_idx, c->s4.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+int mtx_scatter_reduce_f32(mtx_ctx *c, int op, float *target, uint64_t n_target, const float *value,
+                           const uint32_t *index, uint64_t n_value) {
+  if (!c || !target || (n_value && (!value || !index)) || op < 0 || op > 2) {
+    mtx_set_error("mtx_scatter_reduce_f32: bad argument");
+    return MTX_E_ARG;
+  }
+  if (n_value == 0 || n_target == 0) return MTX_OK;
+  if (n_value >= (1ull << 31) || n_target >= (1ull << 31)) {
+    mtx_set_error("mtx_scatter_reduce_f32: size too large");
+    return MTX_E_ARG;
+  }
+  for (uint64_t i = 0; i < n_value; ++i)
+    if (index[i] >= n_target) {
+      mtx_set_error("mtx_scatter_reduce_f32: index[%llu] = %u out of range", (unsigned long long)i, index[i]);
+      return MTX_E_ARG;
+    }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = dalloc(c->s0, 4 * n_target))) return rc;
+  if ((rc = dalloc(c->s1, 4 * n_value))) return rc;
+  if ((rc = dalloc(c->s2, 4 * n_value))) return rc;
+  if ((rc = dalloc(c->s3, mtxd::scatter_workspace_bytes(n_target, n_value)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->s0.p, target, 4 * n_target, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->s1.p, value, 4 * n_value, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->s2.p, index, 4 * n_value, hipMemcpyHostToDevice, c->stream));
+  rc = mtxd::scatter_reduce_f32(op, (float *)c->s0.p, n_target, (const float *)c->s1.p, (const uint32_t *)c->s2.p,
+                                n_value, c->s3.p, c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(target, c->s0.p, 4 * n_target, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,352 @@
+// bvh_build.cpp — host-side scene preprocessing for libmtx.
+//
+// * Binned-SAH BVH2 over an indexed triangle mesh, emitted in the 64-byte
+//   Aila-Laine node layout of mtx.h (both child boxes per node) with the
+//   triangles reordered into leaf order as {v0, e1, e2} records. Replaces the
+//   Embree / OptiX acceleration-structure build that mi.load_file performs
+//   upstream for Scene.ray_intersect (path-mis.py:69-71).
+// * roughplastic precompute (upstream roughplastic constructor): the
+//   64-entry external transmittance table and the internal reflectance.
+//
+// Tree depth is capped at MTX_BVH_MAX_DEPTH inner levels (object-median
+// splits take over when the SAH would exceed it) so that the device
+// traversal's fixed LDS stack can never overflow.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "mtx.h"
+#include "mtx_core/bsdf.h"
+#include "mtx_core/microfacet.h"
+
+void mtx_set_error(const char *fmt, ...);
+
+namespace {
+
+struct Box {
+  float lo[3], hi[3];
+  void reset() {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = INFINITY;
+      hi[a] = -INFINITY;
+    }
+  }
+  void grow(const Box &b) {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], b.lo[a]);
+      hi[a] = std::max(hi[a], b.hi[a]);
+    }
+  }
+  void grow(const float *p) {
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = std::min(lo[a], p[a]);
+      hi[a] = std::max(hi[a], p[a]);
+    }
+  }
+  float area() const {
+    float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (dx < 0 || dy < 0 || dz < 0) return 0.f;
+    return 2.f * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+constexpr int kBins = 32;
+
+struct Builder {
+  const float *vpos;
+  const uint32_t *vidx;
+  uint32_t n;
+  std::vector<Box> tbox;
+  std::vector<float> cen;  // 3 per tri
+  std::vector<uint32_t> idx;
+  std::vector<int32_t> nodes;  // 16 words per node
+  std::vector<uint32_t> order; // leaf order -> input tri
+  uint32_t max_depth_seen = 0;
+
+  static int ceil_log2(uint32_t c) {
+    int l = 0;
+    while ((1u << l) < c) ++l;
+    return l;
+  }
+
+  Box range_box(uint32_t s, uint32_t e) const {
+    Box b;
+    b.reset();
+    for (uint32_t i = s; i < e; ++i) b.grow(tbox[idx[i]]);
+    return b;
+  }
+
+  int32_t make_leaf(uint32_t s, uint32_t e) {
+    uint32_t first = (uint32_t)order.size();
+    for (uint32_t i = s; i < e; ++i) order.push_back(idx[i]);
+    uint32_t code = (first << 3) | (e - s - 1);
+    return ~(int32_t)code;
+  }
+
+  // Partition [s,e) and return the split position; uses binned SAH unless the
+  // depth budget forces an object-median split. Returns 0 when a leaf is best.
+  uint32_t choose_split(uint32_t s, uint32_t e, uint32_t depth) {
+    const uint32_t cnt = e - s;
+    Box cb;
+    cb.reset();
+    for (uint32_t i = s; i < e; ++i) cb.grow(&cen[3 * idx[i]]);
+    int axis_big = 0;
+    float ext_big = -1.f;
+    for (int a = 0; a < 3; ++a) {
+      float ex = cb.hi[a] - cb.lo[a];
+      if (ex > ext_big) {
+        ext_big = ex;
+        axis_big = a;
+      }
+    }
+    bool force_median = depth + (uint32_t)ceil_log2(cnt) >= (uint32_t)MTX_BVH_MAX_DEPTH - 2;
+    if (!force_median && ext_big > 0.f) {
+      float best_cost = INFINITY;
+      int best_axis = -1, best_bin = -1;
+      const Box pb = range_box(s, e);
+      const float pa = pb.area();
+      for (int a = 0; a < 3; ++a) {
+        float ext = cb.hi[a] - cb.lo[a];
+        if (!(ext > 0.f)) continue;
+        Box bins[kBins];
+        uint32_t counts[kBins] = {0};
+        for (int b = 0; b < kBins; ++b) bins[b].reset();
+        const float k = (float)kBins / ext;
+        for (uint32_t i = s; i < e; ++i) {
+          uint32_t t = idx[i];
+          int b = (int)((cen[3 * t + a] - cb.lo[a]) * k);
+          b = std::min(std::max(b, 0), kBins - 1);
+          counts[b]++;
+          bins[b].grow(tbox[t]);
+        }
+        float right_area[kBins];
+        uint32_t right_cnt[kBins];
+        Box acc;
+        acc.reset();
+        uint32_t c = 0;
+        for (int b = kBins - 1; b > 0; --b) {
+          acc.grow(bins[b]);
+          c += counts[b];
+          right_area[b] = acc.area();
+          right_cnt[b] = c;
+        }
+        acc.reset();
+        c = 0;
+        for (int b = 0; b < kBins - 1; ++b) {
+          acc.grow(bins[b]);
+          c += counts[b];
+          if (c == 0 || right_cnt[b + 1] == 0) continue;
+          float cost = 1.f + (acc.area() * (float)c + right_area[b + 1] * (float)right_cnt[b + 1]) / pa;
+          if (cost < best_cost) {
+            best_cost = cost;
+            best_axis = a;
+            best_bin = b;
+          }
+        }
+      }
+      if (cnt <= MTX_BVH_MAX_LEAF && (best_axis < 0 || (float)cnt <= best_cost)) return 0;
+      if (best_axis >= 0) {
+        const float ext = cb.hi[best_axis] - cb.lo[best_axis];
+        const float k = (float)kBins / ext;
+        uint32_t *mid = std::partition(idx.data() + s, idx.data() + e, [&](uint32_t t) {
+          int b = (int)((cen[3 * t + best_axis] - cb.lo[best_axis]) * k);
+          b = std::min(std::max(b, 0), kBins - 1);
+          return b <= best_bin;
+        });
+        uint32_t m = (uint32_t)(mid - idx.data());
+        if (m > s && m < e) return m;
+      }
+    }
+    if (cnt <= MTX_BVH_MAX_LEAF) return 0;
+    // object median along the largest centroid extent (stable for ties)
+    uint32_t m = s + cnt / 2;
+    std::nth_element(idx.data() + s, idx.data() + m, idx.data() + e, [&](uint32_t x, uint32_t y) {
+      float a = cen[3 * x + axis_big], b = cen[3 * y + axis_big];
+      return a < b || (a == b && x < y);
+    });
+    return m;
+  }
+
+  static void pad_box(Box &b) {
+    for (int a = 0; a < 3; ++a) {
+      b.lo[a] -= std::fabs(b.lo[a]) * 2.4e-7f + 1e-30f;
+      b.hi[a] += std::fabs(b.hi[a]) * 2.4e-7f + 1e-30f;
+    }
+  }
+
+  void store_child_boxes(uint32_t node, const Box &b0, const Box &b1) {
+    Box p0 = b0, p1 = b1;
+    pad_box(p0);
+    pad_box(p1);
+    float *f = reinterpret_cast<float *>(&nodes[16 * node]);
+    f[0] = p0.lo[0]; f[1] = p0.hi[0]; f[2] = p0.lo[1]; f[3] = p0.hi[1];
+    f[4] = p1.lo[0]; f[5] = p1.hi[0]; f[6] = p1.lo[1]; f[7] = p1.hi[1];
+    f[8] = p0.lo[2]; f[9] = p0.hi[2]; f[10] = p1.lo[2]; f[11] = p1.hi[2];
+  }
+
+  // Builds the subtree for [s,e) under an inner node at `depth`; returns a child ref.
+  int32_t build(uint32_t s, uint32_t e, uint32_t depth) {
+    uint32_t m = choose_split(s, e, depth);
+    if (m == 0) return make_leaf(s, e);
+    uint32_t node = (uint32_t)(nodes.size() / 16);
+    nodes.resize(nodes.size() + 16, 0);
+    if (depth + 1 > max_depth_seen) max_depth_seen = depth + 1;
+    Box b0 = range_box(s, m), b1 = range_box(m, e);
+    int32_t c0 = build(s, m, depth + 1);
+    int32_t c1 = build(m, e, depth + 1);
+    store_child_boxes(node, b0, b1);
+    nodes[16 * node + 12] = c0;
+    nodes[16 * node + 13] = c1;
+    return (int32_t)node;
+  }
+
+  void run() {
+    tbox.resize(n);
+    cen.resize(3 * (size_t)n);
+    idx.resize(n);
+    for (uint32_t t = 0; t < n; ++t) {
+      Box b;
+      b.reset();
+      for (int k = 0; k < 3; ++k) b.grow(&vpos[3 * (size_t)vidx[3 * (size_t)t + k]]);
+      tbox[t] = b;
+      for (int a = 0; a < 3; ++a) cen[3 * (size_t)t + a] = 0.5f * (b.lo[a] + b.hi[a]);
+      idx[t] = t;
+    }
+    order.reserve(n);
+    nodes.reserve(16 * (size_t)(n / 2 + 2));
+    // The root is always an inner node (index 0).
+    nodes.resize(16, 0);
+    max_depth_seen = 1;
+    if (n == 1) {
+      int32_t leaf = make_leaf(0, 1);
+      Box b = tbox[0];
+      store_child_boxes(0, b, b);
+      nodes[12] = leaf;
+      nodes[13] = leaf;
+      return;
+    }
+    uint32_t m = choose_split(0, n, 0);
+    if (m == 0) m = n / 2;
+    Box b0 = range_box(0, m), b1 = range_box(m, n);
+    int32_t c0 = build(0, m, 1);
+    int32_t c1 = build(m, n, 1);
+    store_child_boxes(0, b0, b1);
+    nodes[12] = c0;
+    nodes[13] = c1;
+  }
+};
+
+}  // namespace
+
+extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t *tri_vidx, uint32_t n_tris,
+                             int32_t *nodes_out, uint32_t *n_nodes_out, float *tri_geom_out, uint32_t *perm_out,
+                             uint32_t *depth_out) {
+  if (!vpos || !tri_vidx || !nodes_out || !n_nodes_out || !tri_geom_out || !perm_out || n_tris == 0) {
+    mtx_set_error("mtx_bvh_build: null argument or empty mesh");
+    return MTX_E_ARG;
+  }
+  if (n_tris >= (1u << 28)) {
+    mtx_set_error("mtx_bvh_build: %u triangles exceed the 2^28 leaf encoding", n_tris);
+    return MTX_E_ARG;
+  }
+  for (uint64_t i = 0; i < 3ull * n_tris; ++i)
+    if (tri_vidx[i] >= n_verts) {
+      mtx_set_error("mtx_bvh_build: vertex index %u out of range (%u vertices)", tri_vidx[i], n_verts);
+      return MTX_E_ARG;
+    }
+  Builder b;
+  b.vpos = vpos;
+  b.vidx = tri_vidx;
+  b.n = n_tris;
+  b.run();
+  if (b.order.size() != n_tris) {
+    mtx_set_error("mtx_bvh_build: internal error (%zu leaf triangles for %u)", b.order.size(), n_tris);
+    return MTX_E_ARG;
+  }
+  uint32_t n_nodes = (uint32_t)(b.nodes.size() / 16);
+  std::memcpy(nodes_out, b.nodes.data(), b.nodes.size() * sizeof(int32_t));
+  *n_nodes_out = n_nodes;
+  for (uint32_t i = 0; i < n_tris; ++i) {
+    uint32_t t = b.order[i];
+    perm_out[i] = t;
+    const float *p0 = &vpos[3 * (size_t)tri_vidx[3 * (size_t)t + 0]];
+    const float *p1 = &vpos[3 * (size_t)tri_vidx[3 * (size_t)t + 1]];
+    const float *p2 = &vpos[3 * (size_t)tri_vidx[3 * (size_t)t + 2]];
+    float *g = &tri_geom_out[12 * (size_t)i];
+    g[0] = p0[0]; g[1] = p0[1]; g[2] = p0[2]; g[3] = 0.f;
+    g[4] = p1[0] - p0[0]; g[5] = p1[1] - p0[1]; g[6] = p1[2] - p0[2]; g[7] = 0.f;
+    g[8] = p2[0] - p0[0]; g[9] = p2[1] - p0[1]; g[10] = p2[2] - p0[2]; g[11] = 0.f;
+  }
+  if (depth_out) *depth_out = b.max_depth_seen;
+  return MTX_OK;
+}
+
+// --------------------------------------------------------------------------
+// roughplastic precompute
+// --------------------------------------------------------------------------
+
+static void gauss_legendre(int n, std::vector<double> &x, std::vector<double> &w) {
+  x.resize(n);
+  w.resize(n);
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5));
+    for (int it = 0; it < 100; ++it) {
+      double p1 = 1.0, p2 = 0.0;
+      for (int j = 1; j <= n; ++j) {
+        double p3 = p2;
+        p2 = p1;
+        p1 = ((2.0 * j - 1.0) * z * p2 - (j - 1.0) * p3) / j;
+      }
+      double pp = n * (z * p1 - p2) / (z * z - 1.0);
+      double z1 = z;
+      z = z1 - p1 / pp;
+      if (std::fabs(z - z1) < 1e-15) {
+        x[i] = -z;
+        w[i] = 2.0 / ((1.0 - z * z) * pp * pp);
+        break;
+      }
+    }
+  }
+}
+
+// Average Fresnel reflectance seen through the microfacet distribution
+// (upstream eval_reflectance): E over visible normals of F(wi.m) G1(wo, m).
+static float eval_reflectance(const mtx::Microfacet &distr, mtx::V3 wi, float eta) {
+  int res = eta > 1.f ? 32 : 128;
+  std::vector<double> xs, ws;
+  gauss_legendre(res, xs, ws);
+  float sum = 0.f;
+  for (int iy = 0; iy < res; ++iy)
+    for (int ix = 0; ix < res; ++ix) {
+      float nx = std::fmaf((float)xs[ix], .5f, .5f), ny = std::fmaf((float)xs[iy], .5f, .5f);
+      float pdf;
+      mtx::V3 m = distr.sample(wi, mtx::V2{nx, ny}, &pdf);
+      mtx::V3 wo = mtx::reflect_m(wi, m);
+      float f = mtx::fresnel_dielectric(mtx::dot(wi, m), eta).r * distr.smith_g1(wo, m);
+      if (!(f == f)) f = 0.f;
+      sum += f * (float)ws[ix] * (float)ws[iy];
+    }
+  return sum * .25f;
+}
+
+extern "C" int mtx_roughplastic_tables(uint32_t distribution, float alpha, float eta, float *table_out,
+                                       float *internal_refl_out) {
+  if (!table_out || !internal_refl_out || !(alpha > 0.f) || !(eta > 0.f)) {
+    mtx_set_error("mtx_roughplastic_tables: bad argument");
+    return MTX_E_ARG;
+  }
+  mtx::Microfacet distr;
+  distr.type = distribution ? mtx::MICROFACET_BECKMANN : mtx::MICROFACET_GGX;
+  distr.alpha = alpha;
+  const int R = MTX_ROUGH_TRANSMITTANCE_RES;
+  float internal = 0.f;
+  for (int i = 0; i < R; ++i) {
+    float mu = std::max(1e-6f, (float)i / (float)(R - 1));
+    mtx::V3 wi = mtx::V3{std::sqrt(1.f - mu * mu), 0.f, mu};
+    table_out[i] = 1.f - eval_reflectance(distr, wi, eta);
+    internal += eval_reflectance(distr, wi, 1.f / eta) * mu;
+  }
+  *internal_refl_out = internal / (float)R * 2.f;
+  return MTX_OK;
+}

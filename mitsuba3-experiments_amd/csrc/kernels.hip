@@ -1,0 +1,682 @@
+// kernels.hip — gfx950 wavefront path-tracing kernels.
+//
+// Replaces the Dr.Jit-traced megakernel that mi.render() builds from the
+// reference sample() loops (path.py:194-302, path-mis.py:24-155,
+// nrc.py:25-125) with explicit kernels over SoA state in HBM:
+//
+//   raygen   camera rays for a chunk of (pixel, sample) lanes
+//            (transcribed render_sample, path.py:27-101)
+//   trace    persistent closest-hit BVH2 traversal, LDS stack per lane,
+//            rays fetched 64 at a time per wave from an atomic counter
+//            (Scene.ray_intersect, path-mis.py:69-71)
+//   shade    one bounce of the integrator: emission + MIS, NEE sampling,
+//            BSDF eval/sample, Russian roulette; survivors and shadow rays are
+//            stream-compacted with wave64 ballot + mbcnt and one atomic/wave
+//   shadow   persistent any-hit traversal of the NEE rays; visible ones add
+//            their contribution to L (Scene.ray_test inside
+//            sample_emitter_direction(..., test_visibility=True), path.py:247)
+//   film     deterministic gather-form tent splat (ImageBlock.put, path.py:101)
+//
+// All arithmetic is IEEE fp32 with -ffp-contract=off; the per-lane
+// primitives are the shared mtx_core headers, so every lane reproduces the
+// CPU restatement in oracle/ bit for bit.
+#include <hip/hip_runtime.h>
+
+#include "mtx_core/bsdf.h"
+#include "mtx_core/geometry.h"
+#include "mtx_core/interaction.h"
+#include "mtx_core/rng.h"
+#include "wavefront.h"
+
+using namespace mtx;
+
+namespace mtxd {
+
+constexpr int kTraceBlock = 128;
+constexpr int kStack = MTX_BVH_MAX_DEPTH + 1;
+constexpr int kShadeBlock = 256;
+
+__device__ __forceinline__ SceneView make_view(const DevScene &s) {
+  SceneView v;
+  v.nodes = reinterpret_cast<const int32_t *>(s.nodes);
+  v.tri_geom = reinterpret_cast<const float *>(s.tri);
+  v.tri_vidx = s.tri_vidx;
+  v.tri_shape = s.tri_shape;
+  v.vpos = s.vpos;
+  v.vnormal = s.vnormal;
+  v.vuv = s.vuv;
+  v.shapes = s.shapes;
+  v.materials = s.materials;
+  v.emitters = s.emitters;
+  v.bsdf.textures = s.textures;
+  v.bsdf.texels = s.texels;
+  v.bsdf.tables = s.tables;
+  v.n_tris = s.n_tris;
+  v.n_emitters = s.n_emitters;
+  v.camera = s.camera;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Wave-level stream compaction: every lane of the wave must call this.
+// Returns the output slot of a lane with pred = true.
+__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
+  const uint64_t mask = __ballot(pred);
+  const uint32_t prefix =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+  const uint32_t total = (uint32_t)__popcll(mask);
+  uint32_t base = 0;
+  if (total) {
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)mask) - 1);
+    if (lane_id() == leader) base = atomicAdd(counter, total);
+    base = __builtin_amdgcn_readlane(base, leader);
+  }
+  return base + prefix;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// BVH2 traversal (shared by closest-hit and any-hit). Child order and
+// tie-breaking match oracle/oracle.cpp:trace_closest exactly.
+// ---------------------------------------------------------------------------
+template <bool ANY>
+__device__ __forceinline__ bool traverse(const DevScene &s, int32_t *stk, const TraceRay &r, float &tbest,
+                                         uint32_t &prim_best, float &bu, float &bv, uint32_t &nv, uint32_t &tv) {
+  int sp = 0;
+  int32_t node = 0;
+  bool hit_any = false;
+  while (true) {
+    if (node >= 0) {
+      const int4 *np = s.nodes + 4 * node;
+      const float4 a = __builtin_bit_cast(float4, np[0]);
+      const float4 b = __builtin_bit_cast(float4, np[1]);
+      const float4 c = __builtin_bit_cast(float4, np[2]);
+      const int4 ch = np[3];
+      ++nv;
+      const float t0 = box_enter(r, a.x, a.y, a.z, a.w, c.x, c.y, tbest);
+      const float t1 = box_enter(r, b.x, b.y, b.z, b.w, c.z, c.w, tbest);
+      const bool h0 = t0 != kInf, h1 = t1 != kInf;
+      if (h0 && h1) {
+        const bool first0 = t0 <= t1;
+        stk[sp * kTraceBlock] = first0 ? ch.y : ch.x;
+        ++sp;
+        node = first0 ? ch.x : ch.y;
+        continue;
+      } else if (h0) {
+        node = ch.x;
+        continue;
+      } else if (h1) {
+        node = ch.y;
+        continue;
+      }
+    } else {
+      uint32_t first, count;
+      leaf_decode(node, &first, &count);
+      for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t prim = first + k;
+        const float4 g0 = s.tri[3 * prim + 0], g1 = s.tri[3 * prim + 1], g2 = s.tri[3 * prim + 2];
+        float t, u, v;
+        ++tv;
+        if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+          if (ANY) {
+            hit_any = true;
+            break;
+          }
+          if (t < tbest || (t == tbest && prim < prim_best)) {
+            tbest = t;
+            prim_best = prim;
+            bu = u;
+            bv = v;
+          }
+        }
+      }
+      if (ANY && hit_any) break;
+    }
+    if (sp == 0) break;
+    --sp;
+    node = stk[sp * kTraceBlock];
+  }
+  return hit_any;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
+  __shared__ int32_t stack[kStack * kTraceBlock];
+  int32_t *stk = stack + threadIdx.x;
+  const uint32_t count = b.counters[4 * bounce + 0];
+  uint32_t *fetch = &b.counters[4 * bounce + 2];
+  const uint32_t *queue = b.queue[bounce & 1];
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t nv = 0, tv = 0, nr = 0;
+  while (true) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(fetch, 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= count) break;
+    const uint32_t i = base + lane;
+    if (i < count) {
+      const uint32_t path = queue[i];
+      const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
+      TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+      float tbest = o4.w, bu = 0.f, bv = 0.f;
+      uint32_t prim = 0xffffffffu;
+      traverse<false>(s, stk, r, tbest, prim, bu, bv, nv, tv);
+      if (prim == 0xffffffffu) tbest = kInf;
+      b.hit[path] = make_float4(tbest, __uint_as_float(prim), bu, bv);
+      ++nr;
+    }
+  }
+  if (STATS) {
+    unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
+    if (lane == 0) {
+      atomicAdd(&b.stats[0], a);
+      atomicAdd(&b.stats[1], c);
+      atomicAdd(&b.stats[4], n);
+    }
+  }
+}
+
+// Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
+// contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
+// form).
+template <bool STATS>
+__global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
+  __shared__ int32_t stack[kStack * kTraceBlock];
+  int32_t *stk = stack + threadIdx.x;
+  const uint32_t count = b.counters[4 * bounce + 1];
+  uint32_t *fetch = &b.counters[4 * bounce + 3];
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t nv = 0, tv = 0, nr = 0;
+  while (true) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(fetch, 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= count) break;
+    const uint32_t i = base + lane;
+    if (i < count) {
+      const ShadowRec rec = b.shadow[i];
+      TraceRay r = make_trace_ray(V3{rec.o.x, rec.o.y, rec.o.z}, V3{rec.d.x, rec.d.y, rec.d.z}, rec.o.w);
+      float tbest = rec.o.w, bu, bv;
+      uint32_t prim = 0xffffffffu;
+      const bool occluded = traverse<true>(s, stk, r, tbest, prim, bu, bv, nv, tv);
+      const uint32_t path = __float_as_uint(rec.d.w);
+      const uint32_t fl = __float_as_uint(rec.t.w);
+      float4 L = b.L[path];
+      if (!occluded) {
+        if (fl & 1u) {
+          L.x = fmaf(rec.t.x, rec.x.x, L.x);
+          L.y = fmaf(rec.t.y, rec.x.y, L.y);
+          L.z = fmaf(rec.t.z, rec.x.z, L.z);
+        } else {
+          L.x = L.x + rec.x.x;
+          L.y = L.y + rec.x.y;
+          L.z = L.z + rec.x.z;
+        }
+      } else {
+        const float qnan = __uint_as_float(0x7fc00000u);
+        if (fl & 2u) L.x = qnan;
+        if (fl & 4u) L.y = qnan;
+        if (fl & 8u) L.z = qnan;
+      }
+      b.L[path] = L;
+      ++nr;
+    }
+  }
+  if (STATS) {
+    unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
+    if (lane == 0) {
+      atomicAdd(&b.stats[2], a);
+      atomicAdd(&b.stats[3], c);
+      atomicAdd(&b.stats[5], n);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Ray generation
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParams &p, uint32_t i, const Ray &ray,
+                                          const Pcg32 &rng, float2 pos) {
+  uint32_t depth = 0, flags = 0;
+  if (p.integrator == MTX_INT_PATH_MIS) {
+    depth = 0;
+    flags = PF_PREV_DELTA;  // prev_bsdf_delta = True (path-mis.py:46)
+  } else {
+    depth = 1;  // path.py:230, nrc.py:39
+  }
+  b.ray_o[i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
+  b.ray_d[i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+  b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+  b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1 (path-mis.py:45)
+  b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  b.pos[i] = pos;
+  b.queue[0][i] = i;
+}
+
+__global__ void k_raygen_camera(DevScene s, WaveBuffers b, ChunkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) b.counters[0] = p.n_paths;
+  if (i >= p.n_paths) return;
+  const uint32_t px_local = i / p.spp, smp = i - px_local * p.spp;
+  const uint32_t pix = p.px0 + px_local;
+  const uint32_t y = pix / p.width, x = pix - y * p.width;
+  const uint32_t lane = pix * p.spp_total + p.sample_offset + smp;
+  Pcg32 rng = sampler_lane(p.seed, lane);
+  const V2 u = rng.next_2d();  // film jitter (path.py:45)
+  const float sx = (float)x + u.x, sy = (float)y + u.y;
+  const V2 adj = V2{sx / (float)p.width, sy / (float)p.height};
+  const Ray ray = camera_ray(s.camera, adj);  // path.py:60-62
+  init_path(b, p, i, ray, rng, make_float2(sx, sy));
+}
+
+__global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const float *rays, const uint32_t *lanes,
+                              uint32_t rng_skip) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) b.counters[0] = p.n_paths;
+  if (i >= p.n_paths) return;
+  Pcg32 rng = sampler_lane(p.seed, lanes[i]);
+  for (uint32_t k = 0; k < rng_skip; ++k) rng.next_u32();
+  const float *r = rays + 6 * (size_t)i;
+  Ray ray{V3{r[0], r[1], r[2]}, V3{r[3], r[4], r[5]}, kLargest};
+  init_path(b, p, i, ray, rng, make_float2(0.f, 0.f));
+}
+
+// ---------------------------------------------------------------------------
+// Shading: one bounce of the integrator for one path.
+// ---------------------------------------------------------------------------
+struct ShadeIO {
+  ShadowRec rec;
+  bool emit;
+};
+
+// Builds the shadow record for an NEE contribution. fma_form: value = (T, X)
+// applied as fma(T, X, L); otherwise X is added. Xo is the contribution the
+// reference forms when the shadow ray is occluded (em_weight = 0).
+__device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteraction &si, const DirectionSample &ds,
+                                            uint32_t path, V3 T, V3 X, V3 Xo, bool fma_form) {
+  uint32_t fl = fma_form ? 1u : 0u;
+  bool vis_noop, occ_noop;
+  if (fma_form) {
+    fl |= (Xo.x == 0.f && isfinite_(T.x)) ? 0u : 2u;
+    fl |= (Xo.y == 0.f && isfinite_(T.y)) ? 0u : 4u;
+    fl |= (Xo.z == 0.f && isfinite_(T.z)) ? 0u : 8u;
+    vis_noop = X.x == 0.f && X.y == 0.f && X.z == 0.f && isfinite_(T.x) && isfinite_(T.y) && isfinite_(T.z);
+  } else {
+    fl |= (Xo.x == 0.f) ? 0u : 2u;
+    fl |= (Xo.y == 0.f) ? 0u : 4u;
+    fl |= (Xo.z == 0.f) ? 0u : 8u;
+    vis_noop = X.x == 0.f && X.y == 0.f && X.z == 0.f;
+  }
+  occ_noop = (fl & 14u) == 0u;
+  io.emit = !(vis_noop && occ_noop);
+  if (!io.emit) return;
+  const Ray sr = spawn_ray_to(si.p, si.n, ds.p);
+  io.rec.o = make_float4(sr.o.x, sr.o.y, sr.o.z, sr.maxt);
+  io.rec.d = make_float4(sr.d.x, sr.d.y, sr.d.z, __uint_as_float(path));
+  io.rec.t = make_float4(T.x, T.y, T.z, __uint_as_float(fl));
+  io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
+}
+
+template <int INT>
+__device__ __forceinline__ bool shade_path(const SceneView &sv, const WaveBuffers &b, const ChunkParams &p,
+                                           uint32_t bounce, uint32_t path, ShadeIO &io) {
+  const float4 ro = b.ray_o[path], rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
+  const uint4 mi = b.misc[path];
+  const float4 h = b.hit[path];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  uint32_t depth = mi.w & 0xffffu, flags = mi.w >> 16;
+  V3 T = V3{th.x, th.y, th.z};
+  float eta = th.w;
+  V3 L = V3{Lr.x, Lr.y, Lr.z};
+  float prev_pdf = Lr.w;
+  V3 prev_p = V3{pv.x, pv.y, pv.z};
+  float spread = pv.w, a0 = rd.w;
+  const V3 ray_d = V3{rd.x, rd.y, rd.z};
+  const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
+  io.emit = false;
+
+  // ------------------------------ head ------------------------------------
+  bool active_next = true;
+  if (INT == MTX_INT_PATH_MIS) {
+    // Direct emission with MIS against the previous BSDF sample (:75-86)
+    const bool prev_delta = (flags & PF_PREV_DELTA) != 0;
+    const V3 rel = si.p - prev_p;
+    const float dist = norm(rel);
+    const float em_pdf = prev_delta ? 0.f : pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    const float mis_bsdf = mis_weight_b(prev_pdf, em_pdf);
+    const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
+    L = fma3v(T, le * mis_bsdf, L);
+    active_next = (depth + 1 < p.max_depth) && si.valid;  // :88
+  } else if (bounce == 0) {
+    if (INT == MTX_INT_PATH) {
+      L = L + emitter_eval(sv, si.emitter, si.wi);  // path.py:239
+      if (!(depth < p.max_depth)) {                // path.py:235
+        b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+        return false;
+      }
+    } else {  // NRC primary (nrc.py:117-121)
+      if (si.valid) flags |= PF_PRIMARY_VALID;
+      a0 = squared_norm(V3{ro.x, ro.y, ro.z} - si.p) / (kFourPi * fabsf(si.wi.z));
+      spread = 0.f;
+    }
+  } else {
+    // path.py:283-300 / nrc.py:79-100: emission of the BSDF-sampled hit
+    const bool bsdf_delta = (flags & PF_PREV_DELTA) != 0;
+    const V3 rel = si.p - prev_p;
+    const float dist = norm(rel);
+    const float em_pdf = bsdf_delta ? 0.f : pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    const float mis_bsdf =
+        INT == MTX_INT_PATH ? mis_weight_a(prev_pdf, em_pdf) : mis_weight_b(prev_pdf, em_pdf);
+    const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
+    L = L + T * le * mis_bsdf;
+    if (INT == MTX_INT_NRC) spread += sqrtf(squared_norm(si.p - prev_p) / (prev_pdf * fabsf(si.wi.z)));
+    depth += 1;
+  }
+  // path.py:235,299-300 / nrc.py:119,272-273: the NRC primary bounce only
+  // requires a valid hit (its depth test runs at the end of an iteration).
+  const bool head_ok =
+      (INT == MTX_INT_NRC && bounce == 0) ? si.valid : (depth < p.max_depth && si.valid);
+  if (INT != MTX_INT_PATH_MIS && !head_ok) {
+    b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+    if (INT == MTX_INT_NRC) b.misc[path] = make_uint4(mi.x, mi.y, mi.z, depth | (flags << 16));
+    return false;
+  }
+  if (INT == MTX_INT_PATH_MIS && !si.valid) {
+    // escaped path: nothing after this point is observable (valid_ray,
+    // result unchanged; throughput becomes 0 -> inactive)
+    b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+    return false;
+  }
+
+  // ------------------------------ body ------------------------------------
+  const mtx_material mat = sv.materials[si.material];
+  const bool smooth = (bsdf_flags(mat) & BF_SMOOTH) != 0;
+  bool active_em = (INT == MTX_INT_PATH_MIS ? active_next : true) && smooth;
+  const V2 u_em = rng.next_2d();
+  DirectionSample ds;
+  ds.p = v3s(0.f);
+  ds.n = v3s(0.f);
+  ds.d = v3s(0.f);
+  ds.dist = 0.f;
+  ds.pdf = 0.f;
+  ds.emitter = -1;
+  V3 em_weight = v3s(0.f);
+  const bool do_nee = (INT == MTX_INT_NRC) ? true : active_em;  // nrc.py:51-53 samples with `active`
+  if (do_nee) em_weight = sample_emitter_direction(sv, si.p, u_em, &ds);
+  if (INT != MTX_INT_PATH_MIS) active_em = active_em && ds.pdf != 0.f;
+  const V3 wo = to_local(si.sh, ds.d);
+  const float s1 = rng.next_1d();
+  const V2 s2 = rng.next_2d();
+  V3 bsdf_val;
+  float bsdf_pdf;
+  BSDFSample bs;
+  bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
+  const V3 bsdf_weight = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+
+  if (INT == MTX_INT_PATH_MIS) {
+    const float mi_em = mis_weight_b(ds.pdf, bsdf_pdf);
+    if (active_em) {
+      const V3 X = bsdf_val * em_weight * mi_em;
+      const V3 Xo = bsdf_val * v3s(0.f) * mi_em;
+      make_shadow(io, si, ds, path, T, X, Xo, true);
+    }
+  } else {
+    const float mis_em = INT == MTX_INT_PATH ? mis_weight_a(ds.pdf, bsdf_pdf) : mis_weight_b(ds.pdf, bsdf_pdf);
+    if (active_em) {
+      const V3 P = T * bsdf_val * em_weight * mis_em;
+      const V3 Po = T * bsdf_val * v3s(0.f) * mis_em;
+      make_shadow(io, si, ds, path, T, P, Po, false);
+    }
+  }
+
+  bool active;
+  const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
+  if (INT == MTX_INT_PATH_MIS) {
+    T = T * bsdf_weight;
+    eta *= bs.eta;
+    if (!(bs.type & BF_NULL)) flags |= PF_VALID_RAY;  // :129-133 (active & si.valid hold here)
+    prev_p = si.p;
+    prev_pdf = bs.pdf;
+    flags = (bs.type & BF_DELTA) ? (flags | PF_PREV_DELTA) : (flags & ~PF_PREV_DELTA);
+    depth += 1;  // :141 (si valid here)
+    const float throughput_max = hmax(T);
+    const float rr_prop = fminf(throughput_max * sqr(eta), 0.95f);
+    const bool rr_active = depth >= p.rr_depth;
+    const bool rr_continue = rng.next_1d() < rr_prop;
+    if (rr_active) T = T * rcp(rr_prop);
+    active = active_next && (!rr_active || rr_continue) && (throughput_max != 0.f);
+  } else if (INT == MTX_INT_PATH) {
+    T = T * bsdf_weight;  // path.py:263
+    eta *= bs.eta;
+    const float fmax_ = hmax(T);
+    const float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+    const bool rr_active = depth >= p.rr_depth;
+    const bool rr_continue = rng.next_1d() < rr_prob;
+    if (rr_active) T = T * rcp(rr_prob);
+    active = (fmax_ != 0.f) && (!rr_active || rr_continue);
+    prev_p = si.p;
+    prev_pdf = bs.pdf;
+    flags = (bs.type & BF_DELTA) ? (flags | PF_PREV_DELTA) : (flags & ~PF_PREV_DELTA);
+  } else {  // NRC
+    T = T * bsdf_weight;
+    eta *= bs.eta;
+    const float a = sqr(spread);  // nrc.py:70-71
+    active = a < p.nrc_c * a0;
+    prev_p = si.p;
+    prev_pdf = bs.pdf;
+    flags = (bs.type & BF_DELTA) ? (flags | PF_PREV_DELTA) : (flags & ~PF_PREV_DELTA);
+  }
+
+  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, a0);
+  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+  b.prev[path] = make_float4(prev_p.x, prev_p.y, prev_p.z, spread);
+  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  return active;
+}
+
+template <int INT>
+__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
+  const SceneView sv = make_view(s);
+  const uint32_t count = b.counters[4 * bounce + 0];
+  const uint32_t *in_q = b.queue[bounce & 1];
+  uint32_t *out_q = b.queue[(bounce + 1) & 1];
+  uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
+  uint32_t *sh_cnt = &b.counters[4 * bounce + 1];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave_base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = wave_base; base < count; base += stride) {
+    const uint32_t i = base + lane;
+    ShadeIO io;
+    io.emit = false;
+    bool cont = false;
+    uint32_t path = 0;
+    if (i < count) {
+      path = in_q[i];
+      cont = shade_path<INT>(sv, b, p, bounce, path, io);
+    }
+    const uint32_t slot = wave_append(out_cnt, cont);
+    if (cont) out_q[slot] = path;
+    const uint32_t sslot = wave_append(sh_cnt, io.emit);
+    if (io.emit) b.shadow[sslot] = io.rec;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Film: stage 1 per source pixel (3x3 tent footprint, samples in order),
+// stage 2 per film pixel (9 neighbours in fixed order). See DESIGN.md.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ V3 final_L(const WaveBuffers &b, const ChunkParams &p, uint32_t path) {
+  const float4 l = b.L[path];
+  V3 L = V3{l.x, l.y, l.z};
+  if (p.integrator == MTX_INT_PATH_MIS) {
+    const uint32_t flags = b.misc[path].w >> 16;
+    if (!(flags & PF_VALID_RAY)) L = v3s(0.f);  // path-mis.py:155
+  }
+  return L;
+}
+
+__global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= p.n_px) return;
+  const uint32_t pix = p.px0 + q;
+  const int y = (int)(pix / p.width), x = (int)(pix - (uint32_t)y * p.width);
+  float4 acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
+    const uint32_t path = q * p.spp + sidx;
+    const float2 ps = b.pos[path];
+    const V3 L = final_L(b, p, path);
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float wy = fmaxf(0.f, 1.f - fabsf(ps.y - ((float)(y + dy - 1) + 0.5f)));
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const float wx = fmaxf(0.f, 1.f - fabsf(ps.x - ((float)(x + dx - 1) + 0.5f)));
+        const float w = wx * wy;
+        float4 &c = acc[dy * 3 + dx];
+        c.x = c.x + L.x * w;
+        c.y = c.y + L.y * w;
+        c.z = c.z + L.z * w;
+        c.w = c.w + w;
+      }
+    }
+  }
+  const size_t o = 9 * ((size_t)(pix - p.band_y0 * p.width));
+#pragma unroll
+  for (int k = 0; k < 9; ++k) contrib[o + k] = acc[k];
+}
+
+__global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, uint32_t y0, uint32_t y1) {
+  const uint32_t FW = W + 2, FH = (y1 - y0) + 2;
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= FW * FH) return;
+  const int px = (int)(q % FW) - 1, py = (int)(y0 + q / FW) - 1;
+  float r = 0.f, g = 0.f, bl = 0.f, w = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int sxp = px - dx + 1, syp = py - dy + 1;
+      if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
+      const float4 c = contrib[9 * ((size_t)(syp - (int)y0) * W + sxp) + dy * 3 + dx];
+      r = r + c.x;
+      g = g + c.y;
+      bl = bl + c.z;
+      w = w + c.w;
+    }
+  film[q] = make_float4(r, g, bl, w);
+}
+
+__global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *valid_out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_paths) return;
+  const V3 L = final_L(b, p, i);
+  L_out[3 * (size_t)i] = L.x;
+  L_out[3 * (size_t)i + 1] = L.y;
+  L_out[3 * (size_t)i + 2] = L.z;
+  const uint32_t flags = b.misc[i].w >> 16;
+  uint8_t v = 1;
+  if (p.integrator == MTX_INT_PATH_MIS) v = (flags & PF_VALID_RAY) ? 1 : 0;
+  if (p.integrator == MTX_INT_NRC) v = (flags & PF_PRIMARY_VALID) ? 1 : 0;
+  valid_out[i] = v;
+}
+
+// Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0).
+__global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const float4 *rays, uint32_t n, int any_hit,
+                                                           uint32_t *hits, uint32_t *visits) {
+  __shared__ int32_t stack[kStack * kTraceBlock];
+  int32_t *stk = stack + threadIdx.x;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 o4 = rays[2 * (size_t)i], d4 = rays[2 * (size_t)i + 1];
+  TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+  float tbest = o4.w, bu = 0.f, bv = 0.f;
+  uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
+  if (any_hit) {
+    hits[i] = traverse<true>(s, stk, r, tbest, prim, bu, bv, nv, tv) ? 1u : 0u;
+  } else {
+    traverse<false>(s, stk, r, tbest, prim, bu, bv, nv, tv);
+    if (prim == 0xffffffffu) tbest = kInf;
+    hits[4 * (size_t)i + 0] = __float_as_uint(tbest);
+    hits[4 * (size_t)i + 1] = prim;
+    hits[4 * (size_t)i + 2] = __float_as_uint(bu);
+    hits[4 * (size_t)i + 3] = __float_as_uint(bv);
+  }
+  if (visits) {
+    visits[2 * (size_t)i] = nv;
+    visits[2 * (size_t)i + 1] = tv;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launch wrappers
+// ---------------------------------------------------------------------------
+static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_raygen_camera, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, s, b, p);
+}
+void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
+                        const uint32_t *lanes, uint32_t rng_skip, hipStream_t st) {
+  hipLaunchKernelGGL(k_raygen_rays, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, s, b, p, rays, lanes,
+                     rng_skip);
+}
+void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
+                          hipStream_t st) {
+  if (stats)
+    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+  else
+    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+}
+void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
+                         hipStream_t st) {
+  if (stats)
+    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+  else
+    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+}
+void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
+                  hipStream_t st) {
+  switch (p.integrator) {
+    case MTX_INT_PATH:
+      hipLaunchKernelGGL(k_shade<MTX_INT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
+    case MTX_INT_NRC:
+      hipLaunchKernelGGL(k_shade<MTX_INT_NRC>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
+    default:
+      hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+  }
+}
+void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st) {
+  hipLaunchKernelGGL(k_film_src, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
+}
+void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
+                        hipStream_t st) {
+  const uint64_t n = (uint64_t)(width + 2) * (y1 - y0 + 2);
+  hipLaunchKernelGGL(k_film_gather, dim3(blocks_for(n, 256)), dim3(256), 0, st, contrib, film, width, y0, y1);
+}
+void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_collect, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, L_out, valid_out);
+}
+void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any_hit, uint32_t *hits,
+                      uint32_t *visits, hipStream_t st) {
+  hipLaunchKernelGGL(k_trace_raw, dim3(blocks_for(n, kTraceBlock)), dim3(kTraceBlock), 0, st, s, rays, n, any_hit,
+                     hits, visits);
+}
+
+}  // namespace mtxd

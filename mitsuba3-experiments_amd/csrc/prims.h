@@ -1,0 +1,25 @@
+// prims.h — device primitives behind the mtx_prefix_sum / hashgrid /
+// scatter_reduce entry points (prefix_sum.py, hashgrid.py, reductions.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mtxd {
+
+size_t scan_workspace_bytes(uint64_t n);
+// Device-wide u32 scan (single pass, decoupled look-back). in/out device.
+int scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, int inclusive, void *ws, hipStream_t st);
+// Hillis-Steele f32 scan in the reference's summation order; a and b are
+// device ping-pong buffers (a holds the input); *result points at the one
+// holding the output.
+int scan_f32_hs(float *a, float *b, uint64_t n, float **result, hipStream_t st);
+
+size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells);
+int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
+                   uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st);
+
+size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value);
+int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
+                       uint64_t n_value, void *ws, hipStream_t st);
+
+}  // namespace mtxd

@@ -1,0 +1,394 @@
+// prims.hip — GPU primitives of the reference repository, MI355X-native.
+//
+// * scan_u32: prefix_sum.py:9-36 on u32 as a single-pass decoupled look-back
+//   scan (Merrill & Garland 2016): 256 threads x 16 items per tile, dynamic
+//   tile tickets, one 8-byte {status, value} granule per tile published with
+//   agent-scope (sc1) stores and polled with sc1 loads; 8 B of HBM traffic
+//   per element instead of the reference's floor(log2 n)+1 full passes.
+// * scan_f32_hs: prefix_sum.py:9-36 on f32 in exactly the reference's
+//   Hillis-Steele summation order (bit-identical results): the first 11
+//   passes run in LDS on a tile plus its 2047-element halo, the remaining
+//   passes (offsets >= 2048) as coalesced full-array passes.
+// * hashgrid_build: hashgrid.py:16-90 — scalar bbox reduction, cell hash,
+//   atomic per-cell rank (the reference's winner election, :52-63), exclusive
+//   scan (:65-76), scatter of sample indices (:79-84).
+// * scatter_reduce_f32: reductions.py:12-54 — winner-election rounds with the
+//   winner chosen as the smallest queued index (atomicMin), so every target
+//   receives its values in ascending index order (deterministic).
+#include <hip/hip_runtime.h>
+
+#include "mtx.h"
+#include "prims.h"
+
+void mtx_set_error(const char *fmt, ...);
+
+namespace mtxd {
+
+namespace {
+
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 16;
+constexpr uint32_t kScanTile = kScanBlock * kScanItems;
+
+__device__ __forceinline__ uint32_t lane() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long *p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ws layout (u64 words): [0] tile ticket (low 32 bits), [1] give-up flag,
+// [2 + t] status of tile t: (status << 32) | value; 1 = aggregate,
+// 2 = inclusive prefix.
+__global__ __launch_bounds__(kScanBlock) void k_scan_u32(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                         uint64_t n, int inclusive, unsigned long long *ws) {
+  __shared__ uint32_t s_tile, s_prefix;
+  __shared__ uint32_t s_wave[kScanBlock / 64];
+  const uint32_t tid = threadIdx.x, wid = tid >> 6, ln = tid & 63;
+  if (tid == 0) s_tile = atomicAdd(reinterpret_cast<unsigned int *>(ws), 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  unsigned long long *status = ws + 2;
+  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+  uint32_t v[kScanItems];
+  if (base + kScanItems <= n) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
+#pragma unroll
+    for (int q = 0; q < kScanItems / 4; ++q) {
+      uint4 x = p[q];
+      v[4 * q] = x.x;
+      v[4 * q + 1] = x.y;
+      v[4 * q + 2] = x.z;
+      v[4 * q + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) v[k] = (base + k < n) ? in[base + k] : 0u;
+  }
+#pragma unroll
+  for (int k = 1; k < kScanItems; ++k) v[k] += v[k - 1];
+  const uint32_t total = v[kScanItems - 1];
+  uint32_t x = total;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(x, off);
+    if (ln >= (uint32_t)off) x += y;
+  }
+  const uint32_t thread_excl = x - total;
+  if (ln == 63) s_wave[wid] = x;
+  __syncthreads();
+  uint32_t wave_prefix = 0, tile_total = 0;
+#pragma unroll
+  for (int w = 0; w < kScanBlock / 64; ++w) {
+    if ((uint32_t)w < wid) wave_prefix += s_wave[w];
+    tile_total += s_wave[w];
+  }
+  if (wid == 0) {
+    uint32_t prefix = 0;
+    if (tile == 0) {
+      if (ln == 0) st_agent(&status[0], (2ull << 32) | tile_total);
+    } else {
+      if (ln == 0) st_agent(&status[tile], (1ull << 32) | tile_total);
+      int64_t pos = (int64_t)tile - 1;
+      while (true) {
+        const int64_t idx = pos - (int64_t)ln;
+        unsigned long long w = 2ull << 32;
+        if (idx >= 0) {
+          uint32_t spins = 0;
+          w = ld_agent(&status[idx]);
+          while ((w >> 32) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            w = ld_agent(&status[idx]);
+            if (++spins > (1u << 26)) {  // never expected: record and give up
+              ws[1] = 1;
+              w = 2ull << 32;
+              break;
+            }
+          }
+        }
+        const uint32_t st = (uint32_t)(w >> 32), val = (uint32_t)w;
+        const uint64_t incl = __ballot(st == 2);
+        if (incl) {
+          const uint32_t k = (uint32_t)(__ffsll((unsigned long long)incl) - 1);
+          prefix += wave_sum(ln <= k ? val : 0u);
+          break;
+        }
+        prefix += wave_sum(val);
+        pos -= 64;
+      }
+      if (ln == 0) st_agent(&status[tile], (2ull << 32) | (uint32_t)(prefix + tile_total));
+    }
+    if (ln == 0) s_prefix = prefix;
+  }
+  __syncthreads();
+  const uint32_t off = s_prefix + wave_prefix + thread_excl;
+  uint32_t o[kScanItems];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) o[k] = (inclusive ? v[k] : (k ? v[k - 1] : 0u)) + off;
+  if (base + kScanItems <= n) {
+    uint4 *p = reinterpret_cast<uint4 *>(out + base);
+#pragma unroll
+    for (int q = 0; q < kScanItems / 4; ++q) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k)
+      if (base + k < n) out[base + k] = o[k];
+  }
+}
+
+// Hillis-Steele in LDS: passes 0..k-1 for a tile of kHsTile outputs.
+constexpr int kHsLog = 11;
+constexpr int kHsTile = 2048;
+constexpr int kHsHalo = (1 << kHsLog) - 1;
+constexpr int kHsSpan = kHsTile + kHsHalo;
+
+__global__ __launch_bounds__(256) void k_hs_local(const float *__restrict__ x, float *__restrict__ y, uint64_t n,
+                                                  int passes) {
+  __shared__ float buf[2][kHsSpan + 1];
+  const int64_t a = (int64_t)blockIdx.x * kHsTile;
+  for (int l = threadIdx.x; l < kHsSpan; l += blockDim.x) {
+    const int64_t g = a - kHsHalo + l;
+    buf[0][l] = (g >= 0 && g < (int64_t)n) ? x[g] : 0.f;
+  }
+  int cur = 0;
+  for (int i = 0; i < passes; ++i) {
+    __syncthreads();
+    const int s = 1 << i;
+    for (int l = threadIdx.x; l < kHsSpan; l += blockDim.x) {
+      const int64_t g = a - kHsHalo + l;
+      float v = buf[cur][l];
+      if (g >= s && l >= s) v = buf[cur][l] + buf[cur][l - s];
+      buf[cur ^ 1][l] = v;
+    }
+    cur ^= 1;
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kHsTile; t += blockDim.x) {
+    const int64_t g = a + t;
+    if (g < (int64_t)n) y[g] = buf[cur][kHsHalo + t];
+  }
+}
+
+__global__ void k_hs_pass(const float *__restrict__ x, float *__restrict__ y, uint64_t n, uint64_t s) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  y[j] = j >= s ? x[j] + x[j - s] : x[j];
+}
+
+// ----------------------------- hash grid ----------------------------------
+__global__ void k_minmax(const float *__restrict__ p, uint64_t n3, float2 *partial) {
+  __shared__ float smin[256], smax[256];
+  float lo = INFINITY, hi = -INFINITY;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3; i += (uint64_t)gridDim.x * blockDim.x) {
+    lo = fminf(lo, p[i]);
+    hi = fmaxf(hi, p[i]);
+  }
+  smin[threadIdx.x] = lo;
+  smax[threadIdx.x] = hi;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s]);
+      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = make_float2(smin[0], smax[0]);
+}
+
+__global__ void k_minmax_final(float2 *partial, int m) {
+  __shared__ float smin[256], smax[256];
+  float lo = INFINITY, hi = -INFINITY;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    lo = fminf(lo, partial[i].x);
+    hi = fmaxf(hi, partial[i].y);
+  }
+  smin[threadIdx.x] = lo;
+  smax[threadIdx.x] = hi;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s]);
+      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[m] = make_float2(smin[0], smax[0]);
+}
+
+__global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t res, uint32_t n_cells,
+                             const float2 *bbox, uint32_t *cell, uint32_t *cell_size, uint32_t *rank) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float2 bb = *bbox;
+  const float bbmin = bb.x, ext = bb.y - bb.x, fres = (float)res;
+  const uint32_t x = (uint32_t)((p[i] - bbmin) / ext * fres);
+  const uint32_t y = (uint32_t)((p[n + i] - bbmin) / ext * fres);
+  const uint32_t z = (uint32_t)((p[2 * n + i] - bbmin) / ext * fres);
+  const uint32_t h = ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
+  cell[i] = h;
+  rank[i] = atomicAdd(&cell_size[h], 1u);
+}
+
+__global__ void k_hash_fill(uint64_t n, const uint32_t *cell, const uint32_t *rank, const uint32_t *cell_offset,
+                            uint32_t *sample_idx) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  sample_idx[cell_offset[cell[i]] + rank[i]] = (uint32_t)i;
+}
+
+// --------------------------- scatter reduce -------------------------------
+__global__ void k_sr_init(uint32_t *q, uint64_t n, uint32_t *slot, uint64_t nt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) q[i] = (uint32_t)i;
+  if (i < nt) slot[i] = 0xffffffffu;
+}
+
+__global__ void k_sr_elect(const uint32_t *q, const uint32_t *cnt, const uint32_t *index, uint32_t *slot) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *cnt) return;
+  const uint32_t v = q[i];
+  atomicMin(&slot[index[v]], v);
+}
+
+__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
+  const uint64_t mask = __ballot(pred);
+  const uint32_t prefix =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+  const uint32_t total = (uint32_t)__popcll(mask);
+  uint32_t base = 0;
+  if (total) {
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)mask) - 1);
+    if (lane() == leader) base = atomicAdd(counter, total);
+    base = __builtin_amdgcn_readlane(base, leader);
+  }
+  return base + prefix;
+}
+
+__global__ void k_sr_apply(int op, float *target, const float *value, const uint32_t *index, const uint32_t *q,
+                           const uint32_t *cnt, uint32_t *slot, uint32_t *q_next, uint32_t *cnt_next) {
+  const uint32_t n = *cnt;
+  const uint32_t wave_base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+  if (wave_base >= n) return;  // wave-uniform
+  const uint32_t i = wave_base + (threadIdx.x & 63);
+  bool requeue = false;
+  uint32_t v = 0;
+  if (i < n) {
+    v = q[i];
+    const uint32_t t = index[v];
+    if (slot[t] == v) {
+      const float a = target[t], b = value[v];
+      target[t] = op == 0 ? a + b : (op == 1 ? fminf(a, b) : fmaxf(a, b));
+      slot[t] = 0xffffffffu;
+    } else {
+      requeue = true;
+    }
+  }
+  const uint32_t s = wave_append(cnt_next, requeue);
+  if (requeue) q_next[s] = v;
+}
+
+inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+size_t scan_workspace_bytes(uint64_t n) { return 8ull * (2 + (n + kScanTile - 1) / kScanTile); }
+
+int scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, int inclusive, void *ws, hipStream_t st) {
+  if (n == 0) return MTX_OK;
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles >= (1ull << 31)) {
+    mtx_set_error("scan_u32: too many tiles");
+    return MTX_E_ARG;
+  }
+  if (hipMemsetAsync(ws, 0, scan_workspace_bytes(n), st) != hipSuccess) {
+    mtx_set_error("scan_u32: memset failed");
+    return MTX_E_HIP;
+  }
+  hipLaunchKernelGGL(k_scan_u32, dim3((unsigned)tiles), dim3(kScanBlock), 0, st, in, out, n, inclusive,
+                     (unsigned long long *)ws);
+  return MTX_OK;
+}
+
+int scan_f32_hs(float *a, float *b, uint64_t n, float **result, hipStream_t st) {
+  *result = a;
+  if (n == 0) return MTX_OK;
+  int passes = 0;  // number of passes with 2^i < n
+  while ((1ull << passes) < n) ++passes;
+  const int local = passes < kHsLog ? passes : kHsLog;
+  hipLaunchKernelGGL(k_hs_local, dim3(nblk(n, kHsTile)), dim3(256), 0, st, a, b, n, local);
+  float *x = b, *y = a;
+  for (int i = local; i < passes; ++i) {
+    hipLaunchKernelGGL(k_hs_pass, dim3(nblk(n, 256)), dim3(256), 0, st, x, y, n, 1ull << i);
+    float *t = x;
+    x = y;
+    y = t;
+  }
+  *result = x;
+  return MTX_OK;
+}
+
+size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells) {
+  return 8ull * 1025 + 4ull * n + scan_workspace_bytes(n_cells) + 16;
+}
+
+int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
+                   uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st) {
+  char *w = (char *)ws;
+  float2 *partial = (float2 *)w;
+  uint32_t *rank = (uint32_t *)(w + 8 * 1025);
+  void *scan_ws = (void *)(w + ((8 * 1025 + 4 * n + 7) & ~(uint64_t)7));
+  const int m = 1024;
+  hipLaunchKernelGGL(k_minmax, dim3(m), dim3(256), 0, st, p, 3 * n, partial);
+  hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(256), 0, st, partial, m);
+  if (hipMemsetAsync(cell_size, 0, 4ull * n_cells, st) != hipSuccess) {
+    mtx_set_error("hashgrid: memset failed");
+    return MTX_E_HIP;
+  }
+  hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell,
+                     cell_size, rank);
+  int rc = scan_u32(cell_size, cell_offset, n_cells, 0, scan_ws, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_hash_fill, dim3(nblk(n, 256)), dim3(256), 0, st, n, cell, rank, cell_offset, sample_idx);
+  return MTX_OK;
+}
+
+size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value) { return 4ull * (2 * n_value + n_target + 64); }
+
+int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
+                       uint64_t n_value, void *ws, hipStream_t st) {
+  uint32_t *qa = (uint32_t *)ws, *qb = qa + n_value, *slot = qb + n_value, *cnts = slot + n_target;
+  const uint64_t init_n = n_value > n_target ? n_value : n_target;
+  hipLaunchKernelGGL(k_sr_init, dim3(nblk(init_n, 256)), dim3(256), 0, st, qa, n_value, slot, n_target);
+  uint32_t nv = (uint32_t)n_value;
+  if (hipMemcpyAsync(&cnts[0], &nv, 4, hipMemcpyHostToDevice, st) != hipSuccess) return MTX_E_HIP;
+  hipStreamSynchronize(st);
+  uint32_t remaining = nv;
+  int r = 0;
+  while (remaining > 0) {
+    uint32_t *cin = &cnts[r & 1], *cout = &cnts[(r + 1) & 1];
+    hipMemsetAsync(cout, 0, 4, st);
+    hipLaunchKernelGGL(k_sr_elect, dim3(nblk(remaining, 256)), dim3(256), 0, st, qa, cin, index, slot);
+    hipLaunchKernelGGL(k_sr_apply, dim3(nblk(remaining, 256)), dim3(256), 0, st, op, target, value, index, qa, cin,
+                       slot, qb, cout);
+    if (hipMemcpyAsync(&remaining, cout, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return MTX_E_HIP;
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      mtx_set_error("scatter_reduce: kernel failure");
+      return MTX_E_HIP;
+    }
+    uint32_t *t = qa;
+    qa = qb;
+    qb = t;
+    ++r;
+  }
+  return MTX_OK;
+}
+
+}  // namespace mtxd

@@ -1,0 +1,99 @@
+// wavefront.h — device-side data layout of the MI355X wavefront integrator
+// and the host-visible launch wrappers implemented in the .hip files.
+//
+// A chunk of C paths lives in HBM as SoA arrays of 16-byte records (one
+// dwordx4 load/store per field group per lane):
+//   ray_o  float4  o.xyz, maxt
+//   ray_d  float4  d.xyz, a0 (NRC footprint, nrc.py:121)
+//   thr    float4  throughput.xyz, eta
+//   L      float4  result.xyz, prev_bsdf_pdf
+//   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93)
+//   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16
+//   pos    float2  film sample position (block.put position, path.py:101)
+//   hit    float4  t, prim, u, v (written by the closest-hit traversal)
+// Queues are u32 path indices compacted with wave64 ballot + mbcnt and one
+// atomic per wave; shadow rays are 64-byte records.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mtx.h"
+
+namespace mtxd {
+
+enum : uint32_t {
+  PF_VALID_RAY = 1u,   // path-mis.py:129-133 valid_ray
+  PF_PREV_DELTA = 2u,  // path-mis.py:137 prev_bsdf_delta
+  PF_PRIMARY_VALID = 4u,
+};
+
+struct DevScene {
+  const int4 *nodes;  // 4 x int4 per node
+  const float4 *tri;  // 3 x float4 per triangle
+  const uint32_t *tri_vidx;
+  const uint32_t *tri_shape;
+  const float *vpos;
+  const float *vnormal;
+  const float *vuv;
+  const mtx_shape *shapes;
+  const mtx_material *materials;
+  const mtx_emitter *emitters;
+  const mtx_texture *textures;
+  const float *texels;
+  const float *tables;
+  uint32_t n_tris, n_emitters;
+  mtx_camera camera;
+};
+
+// Shadow-ray record (64 B): o.xyz maxt | d.xyz path | T.xyz flags | X.xyz 0
+// flags bit0: fma form L = fma(T, X, L) (path-mis.py:117) else L = L + X
+// (path.py:259, nrc.py:62); bits 1..3: the occluded-case contribution of that
+// channel is NaN (non-finite BSDF value / MIS weight), see DESIGN.md.
+struct ShadowRec {
+  float4 o;
+  float4 d;
+  float4 t;
+  float4 x;
+};
+
+struct WaveBuffers {
+  float4 *ray_o, *ray_d, *thr, *L, *prev;
+  uint4 *misc;
+  float2 *pos;
+  float4 *hit;
+  uint32_t *queue[2];
+  ShadowRec *shadow;
+  uint32_t *counters;   // per bounce b: [4b+0] rays, [4b+1] shadow rays, [4b+2] ray fetch, [4b+3] shadow fetch
+  unsigned long long *stats;  // nodes_c, tris_c, nodes_s, tris_s, rays_c, rays_s
+  uint32_t capacity;
+};
+
+struct ChunkParams {
+  uint32_t integrator, max_depth, rr_depth, seed;
+  uint32_t spp, spp_total, sample_offset;
+  uint32_t width, height;
+  uint32_t px0, n_px;   // first film pixel (y*W+x) of the chunk and pixel count
+  uint32_t band_y0;     // first row of the rendered band (film/contrib origin)
+  uint32_t n_paths;
+  float nrc_c;
+  uint32_t stats;
+};
+
+// -------- launch wrappers (kernels.hip) --------
+void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
+void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
+                        const uint32_t *lanes, uint32_t rng_skip, hipStream_t st);
+void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
+                          hipStream_t st);
+void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
+                         hipStream_t st);
+void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
+                  hipStream_t st);
+void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
+void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
+                        hipStream_t st);
+void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st);
+void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any_hit, uint32_t *hits,
+                      uint32_t *visits, hipStream_t st);
+
+}  // namespace mtxd

@@ -1,0 +1,168 @@
+"""ctypes mirror of include/mtx.h (plain C structs, no torch types)."""
+from __future__ import annotations
+
+import ctypes as C
+
+MTX_ABI_VERSION = 1
+
+MTX_MAT_DIFFUSE = 1
+MTX_MAT_ROUGHPLASTIC = 2
+MTX_MAT_CONDUCTOR = 3
+MTX_MAT_ROUGHCONDUCTOR = 4
+MTX_MAT_DIELECTRIC = 5
+MTX_MAT_ROUGHDIELECTRIC = 6
+
+MTX_MF_TWOSIDED = 1
+MTX_MF_MASK = 2
+MTX_MF_BECKMANN = 4
+MTX_MF_NONLINEAR = 8
+
+MTX_INT_PATH = 1
+MTX_INT_PATH_MIS = 2
+MTX_INT_NRC = 3
+MTX_INT_PSSMLT_SIMPLE = 4
+MTX_INT_RESTIR_GI = 5
+
+MTX_ROUGH_TRANSMITTANCE_RES = 64
+MTX_BVH_MAX_LEAF = 8
+MTX_BVH_MAX_DEPTH = 40
+
+ERRORS = {-1: "MTX_E_ARG", -2: "MTX_E_HIP", -3: "MTX_E_NOSCENE", -4: "MTX_E_OOM", -5: "MTX_E_UNSUPPORTED"}
+
+
+class Material(C.Structure):
+    _fields_ = [
+        ("type", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("tex", C.c_int32),
+        ("opacity", C.c_float),
+        ("rgb", C.c_float * 3),
+        ("alpha", C.c_float),
+        ("eta", C.c_float),
+        ("eta_rgb", C.c_float * 3),
+        ("k_rgb", C.c_float * 3),
+        ("spec_weight", C.c_float),
+        ("internal_refl", C.c_float),
+        ("table", C.c_int32),
+    ]
+
+
+class Texture(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("offset", C.c_uint64)]
+
+
+class Emitter(C.Structure):
+    _fields_ = [
+        ("center", C.c_float * 3),
+        ("col0", C.c_float * 3),
+        ("col1", C.c_float * 3),
+        ("normal", C.c_float * 3),
+        ("inv_area", C.c_float),
+        ("radiance", C.c_float * 3),
+    ]
+
+
+class Shape(C.Structure):
+    _fields_ = [("material", C.c_uint32), ("emitter", C.c_int32), ("flags", C.c_uint32), ("pad", C.c_uint32)]
+
+
+class Camera(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 3),
+        ("axis_x", C.c_float * 3),
+        ("axis_y", C.c_float * 3),
+        ("axis_z", C.c_float * 3),
+        ("tan_x", C.c_float),
+        ("tan_y", C.c_float),
+        ("near_clip", C.c_float),
+        ("far_clip", C.c_float),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+    ]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [
+        ("n_tris", C.c_uint32),
+        ("n_nodes", C.c_uint32),
+        ("n_verts", C.c_uint32),
+        ("n_shapes", C.c_uint32),
+        ("n_materials", C.c_uint32),
+        ("n_emitters", C.c_uint32),
+        ("n_textures", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("nodes", C.c_void_p),
+        ("tri_geom", C.c_void_p),
+        ("tri_vidx", C.c_void_p),
+        ("tri_shape", C.c_void_p),
+        ("vpos", C.c_void_p),
+        ("vnormal", C.c_void_p),
+        ("vuv", C.c_void_p),
+        ("shapes", C.c_void_p),
+        ("materials", C.c_void_p),
+        ("emitters", C.c_void_p),
+        ("textures", C.c_void_p),
+        ("texels", C.c_void_p),
+        ("n_texels", C.c_uint64),
+        ("tables", C.c_void_p),
+        ("n_tables", C.c_uint32),
+        ("pad0", C.c_uint32),
+        ("camera", Camera),
+    ]
+
+
+class RenderArgs(C.Structure):
+    _fields_ = [
+        ("integrator", C.c_uint32),
+        ("max_depth", C.c_uint32),
+        ("rr_depth", C.c_uint32),
+        ("seed", C.c_uint32),
+        ("spp", C.c_uint32),
+        ("spp_total", C.c_uint32),
+        ("sample_offset", C.c_uint32),
+        ("y0", C.c_uint32),
+        ("y1", C.c_uint32),
+        ("chunk_paths", C.c_uint32),
+        ("nrc_c", C.c_float),
+        ("flags", C.c_uint32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("rays_closest", C.c_uint64),
+        ("rays_shadow", C.c_uint64),
+        ("nodes_closest", C.c_uint64),
+        ("tris_closest", C.c_uint64),
+        ("nodes_shadow", C.c_uint64),
+        ("tris_shadow", C.c_uint64),
+        ("trace_launches", C.c_uint64),
+        ("shadow_launches", C.c_uint64),
+        ("trace_ms", C.c_double),
+        ("shadow_ms", C.c_double),
+        ("shade_ms", C.c_double),
+        ("other_ms", C.c_double),
+        ("paths", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# Every symbol include/mtx.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "mtx_abi_version",
+    "mtx_last_error",
+    "mtx_ctx_create",
+    "mtx_ctx_destroy",
+    "mtx_bvh_build",
+    "mtx_roughplastic_tables",
+    "mtx_scene_upload",
+    "mtx_render",
+    "mtx_sample_rays",
+    "mtx_trace",
+    "mtx_prefix_sum_u32",
+    "mtx_prefix_sum_f32_hs",
+    "mtx_hashgrid_build",
+    "mtx_scatter_reduce_f32",
+]

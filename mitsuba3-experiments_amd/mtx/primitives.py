@@ -1,0 +1,76 @@
+"""GPU primitives with the reference's function names (prefix_sum.py,
+hashgrid.py, reductions.py), backed by libmtx."""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import check, context, lib
+
+ADD, MIN, MAX = 0, 1, 2
+
+
+def prefix_sum(x, inclusive: bool = True, device: int | None = None):
+    """prefix_sum.py:9-36. u32 input: single-pass decoupled look-back scan.
+    f32 input: Hillis-Steele passes in the reference's exact summation order."""
+    x = np.ascontiguousarray(x)
+    out = np.zeros_like(x)
+    ctx = context(device)
+    if x.dtype == np.uint32:
+        check(lib().mtx_prefix_sum_u32(ctx.handle, x.ctypes.data, out.ctypes.data, len(x), int(inclusive)),
+              "mtx_prefix_sum_u32")
+    elif x.dtype == np.float32:
+        if not inclusive:
+            raise ValueError("the Hillis-Steele f32 scan is inclusive (prefix_sum.py:25-32)")
+        check(lib().mtx_prefix_sum_f32_hs(ctx.handle, x.ctypes.data, out.ctypes.data, len(x)), "mtx_prefix_sum_f32_hs")
+    else:
+        raise TypeError("prefix_sum supports uint32 and float32")
+    return out
+
+
+def hash_cells(p, resolution: int, n_cells: int):
+    """hashgrid.py:8-12 + 86-90 on the host (small inputs / documentation)."""
+    p = np.asarray(p, np.float32).reshape(3, -1)
+    bbmin = np.float32(min(p[0].min(), p[1].min(), p[2].min()))
+    bbmax = np.float32(max(p[0].max(), p[1].max(), p[2].max()))
+    q = ((p - bbmin) / (bbmax - bbmin) * np.float32(resolution)).astype(np.uint32)
+    with np.errstate(over="ignore"):
+        h = (q[0] * np.uint32(73856093)) ^ (q[1] * np.uint32(19349663)) ^ (q[2] * np.uint32(83492791))
+    return h % np.uint32(n_cells)
+
+
+class HashGrid:
+    """hashgrid.py:15-90: build a 3-D spatial hash grid over `sample` points
+    (Point3f as a [3, n] array). Attributes: cell_size, cell_offset (exclusive
+    scan), sample_idx (samples grouped by cell; order within a cell is
+    race-defined, as in the reference), cell (per-sample cell index)."""
+
+    def __init__(self, sample, resolution: int, n_cells: int | None = None, device: int | None = None):
+        p = np.ascontiguousarray(np.asarray(sample, np.float32).reshape(3, -1))
+        n = p.shape[1]
+        self.n_samples = n
+        self.n_cells = int(n_cells if n_cells is not None else n)
+        self.resolution = int(resolution)
+        self.cell = np.zeros(n, np.uint32)
+        self.cell_size = np.zeros(self.n_cells, np.uint32)
+        self.cell_offset = np.zeros(self.n_cells, np.uint32)
+        self.sample_idx = np.zeros(n, np.uint32)
+        ctx = context(device)
+        check(lib().mtx_hashgrid_build(ctx.handle, p.ctypes.data, n, self.resolution, self.n_cells,
+                                       self.cell.ctypes.data, self.cell_size.ctypes.data,
+                                       self.cell_offset.ctypes.data, self.sample_idx.ctypes.data),
+              "mtx_hashgrid_build")
+
+
+def scatter_reduce_with(op, target, value, index, device: int | None = None):
+    """reductions.py:12-54 for op in {ADD, MIN, MAX} (or 'add'/'min'/'max').
+    Returns the updated target; each target receives its values in ascending
+    index order."""
+    if isinstance(op, str):
+        op = {"add": ADD, "min": MIN, "max": MAX}[op]
+    t = np.array(target, np.float32)
+    v = np.ascontiguousarray(value, np.float32)
+    i = np.ascontiguousarray(index, np.uint32)
+    ctx = context(device)
+    check(lib().mtx_scatter_reduce_f32(ctx.handle, int(op), t.ctypes.data, len(t), v.ctypes.data, i.ctypes.data,
+                                       len(v)), "mtx_scatter_reduce_f32")
+    return t

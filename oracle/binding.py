@@ -1,0 +1,145 @@
+"""ctypes binding of oracle/_build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+to check (or time beside) the HIP product path. Never imported by the product
+package `mtx`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+sys.path.insert(0, os.path.join(HERE, "..", "mitsuba3-experiments_amd"))
+
+from mtx import _abi  # noqa: E402  (struct layouts of include/mtx.h)
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        SD, RA = C.POINTER(_abi.SceneDesc), C.POINTER(_abi.RenderArgs)
+        sig = {
+            "orc_trace": [SD, u64, vp, C.c_int, C.c_int, vp, vp],
+            "orc_sample_rays": [SD, RA, u64, vp, vp, u32, vp, vp],
+            "orc_render_samples": [SD, RA, vp, vp],
+            "orc_film": [u32, u32, u32, u32, vp, vp, vp],
+            "orc_render": [SD, RA, vp],
+            "orc_rng_stream": [u32, u32, u32, u32, vp],
+            "orc_prefix_sum_f32_hs": [vp, vp, u64],
+            "orc_prefix_sum_u32": [vp, vp, u64, C.c_int],
+            "orc_hashgrid": [vp, u64, u32, u32, vp, vp, vp, vp],
+            "orc_scatter_reduce_f32": [C.c_int, vp, u64, vp, vp, u64],
+        }
+        for k, a in sig.items():
+            getattr(L, k).argtypes = a
+            getattr(L, k).restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def render_args(integrator, max_depth, rr_depth, seed, spp, y0, y1, spp_total=None, sample_offset=0, nrc_c=0.01):
+    a = _abi.RenderArgs()
+    a.integrator, a.max_depth, a.rr_depth, a.seed = integrator, max_depth, rr_depth, seed
+    a.spp, a.spp_total, a.sample_offset = spp, spp_total or spp, sample_offset
+    a.y0, a.y1, a.nrc_c = y0, y1, nrc_c
+    return a
+
+
+def render_samples(scene, args):
+    """Per-sample (L [n,3], pos [n,2]) in (pixel, sample) order for rows [y0,y1)."""
+    n = (args.y1 - args.y0) * scene.width * args.spp
+    L = np.zeros((n, 3), np.float32)
+    pos = np.zeros((n, 2), np.float32)
+    d = scene.desc()
+    lib().orc_render_samples(C.byref(d), C.byref(args), L.ctypes.data, pos.ctypes.data)
+    return L, pos
+
+
+def film(width, y0, y1, spp, L, pos):
+    f = np.zeros((y1 - y0 + 2, width + 2, 4), np.float32)
+    lib().orc_film(width, y0, y1, spp, np.ascontiguousarray(L).ctypes.data, np.ascontiguousarray(pos).ctypes.data,
+                   f.ctypes.data)
+    return f
+
+
+def render(scene, args):
+    f = np.zeros((args.y1 - args.y0 + 2, scene.width + 2, 4), np.float32)
+    d = scene.desc()
+    lib().orc_render(C.byref(d), C.byref(args), f.ctypes.data)
+    return f
+
+
+def sample_rays(scene, args, rays, lanes, rng_skip=2):
+    n = len(lanes)
+    L = np.zeros((n, 3), np.float32)
+    valid = np.zeros(n, np.uint8)
+    d = scene.desc()
+    lib().orc_sample_rays(C.byref(d), C.byref(args), n, np.ascontiguousarray(rays, np.float32).ctypes.data,
+                          np.ascontiguousarray(lanes, np.uint32).ctypes.data, rng_skip, L.ctypes.data,
+                          valid.ctypes.data)
+    return L, valid
+
+
+def trace(scene, rays, any_hit=False, brute=False):
+    n = len(rays)
+    hits = np.zeros(n if any_hit else 4 * n, np.uint32)
+    visits = np.zeros(2 * n, np.uint32)
+    d = scene.desc()
+    lib().orc_trace(C.byref(d), n, np.ascontiguousarray(rays, np.float32).ctypes.data, int(any_hit), int(brute),
+                    hits.ctypes.data, visits.ctypes.data)
+    return hits, visits.reshape(n, 2)
+
+
+def rng_stream(seed, lane0, n_lanes, n_draws):
+    out = np.zeros((n_lanes, n_draws), np.float32)
+    lib().orc_rng_stream(seed, lane0, n_lanes, n_draws, out.ctypes.data)
+    return out
+
+
+def prefix_sum_f32_hs(x):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros_like(x)
+    lib().orc_prefix_sum_f32_hs(x.ctypes.data, out.ctypes.data, len(x))
+    return out
+
+
+def prefix_sum_u32(x, inclusive=True):
+    x = np.ascontiguousarray(x, np.uint32)
+    out = np.zeros_like(x)
+    lib().orc_prefix_sum_u32(x.ctypes.data, out.ctypes.data, len(x), int(inclusive))
+    return out
+
+
+def hashgrid(p, resolution, n_cells):
+    p = np.ascontiguousarray(p, np.float32).reshape(3, -1)
+    n = p.shape[1]
+    cell = np.zeros(n, np.uint32)
+    size = np.zeros(n_cells, np.uint32)
+    off = np.zeros(n_cells, np.uint32)
+    idx = np.zeros(n, np.uint32)
+    lib().orc_hashgrid(p.ctypes.data, n, resolution, n_cells, cell.ctypes.data, size.ctypes.data, off.ctypes.data,
+                       idx.ctypes.data)
+    return cell, size, off, idx
+
+
+def scatter_reduce(op, target, value, index):
+    t = np.array(target, np.float32)
+    lib().orc_scatter_reduce_f32(op, t.ctypes.data, len(t), np.ascontiguousarray(value, np.float32).ctypes.data,
+                                 np.ascontiguousarray(index, np.uint32).ctypes.data, len(value))
+    return t

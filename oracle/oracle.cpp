@@ -1,0 +1,637 @@
+// oracle/oracle.cpp — CPU restatement of the reference hot path.
+//
+// TEST INFRASTRUCTURE ONLY. Nothing in the product (libmtx, the mtx Python
+// package's render path) may link, load or call this library; it is used by
+// tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+// checker / timed CPU baseline.
+//
+// What it restates, one scalar lane at a time, exactly in the order of the
+// reference source:
+//   * path-mis.py:24-155   PathIntegrator.sample      -> orc_path_mis()
+//   * path.py:194-302      Path.sample                -> orc_path()
+//   * nrc.py:25-125        NRCIntegrator.sample       -> orc_nrc()
+//   * path.py:27-192       transcribed SamplingIntegrator.render/render_sample
+//                          (lane -> pixel, film jitter, camera ray, block.put)
+//   * prefix_sum.py:9-36, hashgrid.py:8-90, reductions.py:12-54
+// The upstream per-lane primitives these loops call (Scene.ray_intersect,
+// BSDF, emitter, sampler) come from include/mtx_core;
+// the BVH traversal below is an independent scalar re-implementation over
+// the scene's node arrays, with the same child-visit order as the device
+// kernel so that visit counts can be compared exactly.
+//
+// Parity status: the reference's own implementation (Mitsuba 3 / Dr.Jit /
+// Embree) is absent from the reference tree (empty submodule, SURVEY.md
+// §8c), so results at the upstream boundary are "parity unpinned"; the
+// in-repo KATs (hashgrid.py:93-98, reductions.py:57-63, prefix_sum.py:39-54)
+// pin the primitives.
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "mtx.h"
+#include "mtx_core/bsdf.h"
+#include "mtx_core/geometry.h"
+#include "mtx_core/interaction.h"
+#include "mtx_core/rng.h"
+#include "mtx_core/warp.h"
+
+using namespace mtx;
+
+namespace {
+
+SceneView make_view(const mtx_scene_desc *d) {
+  SceneView s;
+  s.nodes = d->nodes;
+  s.tri_geom = d->tri_geom;
+  s.tri_vidx = d->tri_vidx;
+  s.tri_shape = d->tri_shape;
+  s.vpos = d->vpos;
+  s.vnormal = d->vnormal;
+  s.vuv = d->vuv;
+  s.shapes = d->shapes;
+  s.materials = d->materials;
+  s.emitters = d->emitters;
+  s.bsdf.textures = d->textures;
+  s.bsdf.texels = d->texels;
+  s.bsdf.tables = d->tables;
+  s.n_tris = d->n_tris;
+  s.n_emitters = d->n_emitters;
+  s.camera = d->camera;
+  return s;
+}
+
+struct Hit {
+  float t, u, v;
+  uint32_t prim;
+};
+
+// Scalar BVH2 traversal. Visit order (shared with the device kernel): at an
+// inner node, if both children are entered, continue with the one with the
+// smaller entry distance (ties -> child 0) and push the other.
+Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
+  TraceRay r = make_trace_ray(o, d, maxt);
+  Hit h{maxt, 0.f, 0.f, 0xffffffffu};
+  float tbest = maxt;
+  int32_t stack[MTX_BVH_MAX_DEPTH + 2];
+  int sp = 0;
+  int32_t node = 0;
+  uint32_t nv = 0, tv = 0;
+  while (true) {
+    if (node >= 0) {
+      const int32_t *ni = s.nodes + 16 * node;
+      const float *nf = reinterpret_cast<const float *>(ni);
+      ++nv;
+      float t0 = box_enter(r, nf[0], nf[1], nf[2], nf[3], nf[8], nf[9], tbest);
+      float t1 = box_enter(r, nf[4], nf[5], nf[6], nf[7], nf[10], nf[11], tbest);
+      bool h0 = t0 != kInf, h1 = t1 != kInf;
+      if (h0 && h1) {
+        bool first0 = t0 <= t1;
+        stack[sp++] = first0 ? ni[13] : ni[12];
+        node = first0 ? ni[12] : ni[13];
+        continue;
+      } else if (h0) {
+        node = ni[12];
+        continue;
+      } else if (h1) {
+        node = ni[13];
+        continue;
+      }
+    } else {
+      uint32_t first, count;
+      leaf_decode(node, &first, &count);
+      for (uint32_t k = 0; k < count; ++k) {
+        uint32_t prim = first + k;
+        const float *g = s.tri_geom + 12 * (size_t)prim;
+        float t, u, v;
+        ++tv;
+        if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
+          if (t < tbest || (t == tbest && prim < h.prim)) {
+            tbest = t;
+            h.t = t;
+            h.u = u;
+            h.v = v;
+            h.prim = prim;
+          }
+        }
+      }
+    }
+    if (sp == 0) break;
+    node = stack[--sp];
+  }
+  if (nodes_visited) *nodes_visited = nv;
+  if (tris_visited) *tris_visited = tv;
+  if (h.prim == 0xffffffffu) h.t = kInf;
+  return h;
+}
+
+bool trace_any(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
+  TraceRay r = make_trace_ray(o, d, maxt);
+  int32_t stack[MTX_BVH_MAX_DEPTH + 2];
+  int sp = 0;
+  int32_t node = 0;
+  uint32_t nv = 0, tv = 0;
+  bool hit = false;
+  while (!hit) {
+    if (node >= 0) {
+      const int32_t *ni = s.nodes + 16 * node;
+      const float *nf = reinterpret_cast<const float *>(ni);
+      ++nv;
+      float t0 = box_enter(r, nf[0], nf[1], nf[2], nf[3], nf[8], nf[9], maxt);
+      float t1 = box_enter(r, nf[4], nf[5], nf[6], nf[7], nf[10], nf[11], maxt);
+      bool h0 = t0 != kInf, h1 = t1 != kInf;
+      if (h0 && h1) {
+        bool first0 = t0 <= t1;
+        stack[sp++] = first0 ? ni[13] : ni[12];
+        node = first0 ? ni[12] : ni[13];
+        continue;
+      } else if (h0) {
+        node = ni[12];
+        continue;
+      } else if (h1) {
+        node = ni[13];
+        continue;
+      }
+    } else {
+      uint32_t first, count;
+      leaf_decode(node, &first, &count);
+      for (uint32_t k = 0; k < count && !hit; ++k) {
+        const float *g = s.tri_geom + 12 * (size_t)(first + k);
+        float t, u, v;
+        ++tv;
+        hit = tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, maxt, &t, &u, &v);
+      }
+      if (hit) break;
+    }
+    if (sp == 0) break;
+    node = stack[--sp];
+  }
+  if (nodes_visited) *nodes_visited = nv;
+  if (tris_visited) *tris_visited = tv;
+  return hit;
+}
+
+Hit brute_closest(const SceneView &s, V3 o, V3 d, float maxt) {
+  TraceRay r = make_trace_ray(o, d, maxt);
+  Hit h{maxt, 0.f, 0.f, 0xffffffffu};
+  float tbest = maxt;
+  for (uint32_t prim = 0; prim < s.n_tris; ++prim) {
+    const float *g = s.tri_geom + 12 * (size_t)prim;
+    float t, u, v;
+    if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
+      if (t < tbest || (t == tbest && prim < h.prim)) {
+        tbest = t;
+        h = Hit{t, u, v, prim};
+      }
+    }
+  }
+  if (h.prim == 0xffffffffu) h.t = kInf;
+  return h;
+}
+
+SurfaceInteraction intersect(const SceneView &s, const Ray &ray) {
+  Hit h = trace_closest(s, ray.o, ray.d, ray.maxt, nullptr, nullptr);
+  return compute_si(s, h.t, h.prim, h.u, h.v, ray.d);
+}
+
+// scene.sample_emitter_direction(si, u, test_visibility=True) (upstream)
+V3 sample_emitter_visible(const SceneView &s, const SurfaceInteraction &si, V2 u, DirectionSample *ds) {
+  V3 spec = sample_emitter_direction(s, si.p, u, ds);
+  Ray sr = spawn_ray_to(si.p, si.n, ds->p);
+  if (trace_any(s, sr.o, sr.d, sr.maxt, nullptr, nullptr)) spec = v3s(0.f);
+  return spec;
+}
+
+bool smooth(const SceneView &s, const SurfaceInteraction &si) {
+  if (!si.valid) return false;
+  return (bsdf_flags(s.materials[si.material]) & BF_SMOOTH) != 0;
+}
+
+// bsdf.eval_pdf_sample on si (null BSDF for an invalid interaction)
+V3 eval_pdf_sample(const SceneView &s, const SurfaceInteraction &si, V3 wo, float u1, V2 u2, V3 *val, float *pdf,
+                   BSDFSample *bs) {
+  if (!si.valid) {
+    *val = v3s(0.f);
+    *pdf = 0.f;
+    bs->wo = v3s(0.f);
+    bs->pdf = 0.f;
+    bs->eta = 0.f;
+    bs->type = 0;
+    return v3s(0.f);
+  }
+  const mtx_material &m = s.materials[si.material];
+  bsdf_eval_pdf(s.bsdf, m, si.uv, si.wi, wo, val, pdf);
+  return bsdf_sample(s.bsdf, m, si.uv, si.wi, u1, u2, bs);
+}
+
+// ------------------------- path-mis.py:24-155 ------------------------------
+V3 orc_path_mis(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_t rr_depth, bool *valid_out) {
+  V3 throughput = v3s(1.f), result = v3s(0.f);
+  float eta = 1.f;
+  uint32_t depth = 0;
+  bool valid_ray = false;  // scene.environment() is None for the bedroom (:41)
+  V3 prev_p = v3s(0.f);
+  float prev_bsdf_pdf = 1.f;
+  bool prev_bsdf_delta = true;
+  bool active = true;
+  while (active) {
+    SurfaceInteraction si = intersect(s, ray);  // :69-71
+    // Direct emission (:75-86)
+    V3 rel = si.p - prev_p;
+    float dist = norm(rel);
+    V3 ds_d = si.valid ? rel / dist : to_world(si.sh, si.wi) * -1.f;
+    float em_pdf = prev_bsdf_delta ? 0.f : pdf_emitter_direction(s, si.emitter, ds_d, dist, si.sh.n);
+    float mis_bsdf = mis_weight_b(prev_bsdf_pdf, em_pdf);
+    V3 le = (prev_bsdf_pdf > 0.f) ? emitter_eval(s, si.emitter, si.wi) : v3s(0.f);
+    result = fma3v(throughput, le * mis_bsdf, result);
+    bool active_next = (depth + 1 < max_depth) && si.valid;  // :88
+    // Emitter sampling (:94-98)
+    bool active_em = active_next && smooth(s, si);
+    V2 u_em = rng.next_2d();
+    DirectionSample ds{};
+    V3 em_weight = v3s(0.f);
+    if (active_em) em_weight = sample_emitter_visible(s, si, u_em, &ds);
+    V3 wo = to_local(si.sh, ds.d);
+    // BSDF eval + sample (:104-109)
+    float s1 = rng.next_1d();
+    V2 s2 = rng.next_2d();
+    V3 bsdf_val;
+    float bsdf_pdf;
+    BSDFSample bs;
+    V3 bsdf_weight = eval_pdf_sample(s, si, wo, s1, s2, &bsdf_val, &bsdf_pdf, &bs);
+    // Emitter sampling contribution (:115-117)
+    float mi_em = mis_weight_b(ds.pdf, bsdf_pdf);
+    if (active_em) result = fma3v(throughput, bsdf_val * em_weight * mi_em, result);
+    // BSDF sampling (:121-137)
+    ray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
+    throughput = throughput * bsdf_weight;
+    eta *= bs.eta;
+    valid_ray = valid_ray || (active && si.valid && !(bs.type & BF_NULL));
+    prev_p = si.p;
+    prev_bsdf_pdf = bs.pdf;
+    prev_bsdf_delta = (bs.type & BF_DELTA) != 0;
+    // Stopping criterion (:141-153)
+    if (si.valid) depth += 1;
+    float throughput_max = hmax(throughput);
+    float rr_prop = fminf(throughput_max * sqr(eta), 0.95f);
+    bool rr_active = depth >= rr_depth;
+    bool rr_continue = rng.next_1d() < rr_prop;
+    if (rr_active) throughput = throughput * rcp(rr_prop);
+    active = active_next && (!rr_active || rr_continue) && (throughput_max != 0.f);
+  }
+  *valid_out = valid_ray;
+  return valid_ray ? result : v3s(0.f);  // :155
+}
+
+// ---------------------------- path.py:194-302 ------------------------------
+V3 orc_path(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_t rr_depth, bool *valid_out) {
+  V3 L = v3s(0.f), f = v3s(1.f);
+  float eta = 1.f;
+  uint32_t depth = 1;
+  bool active = depth < max_depth;  // :235 (self.max_depth)
+  SurfaceInteraction si;
+  if (active) {
+    si = intersect(s, ray);  // :238
+    L = L + emitter_eval(s, si.emitter, si.wi);  // :239
+  } else {
+    si = compute_si(s, kInf, 0xffffffffu, 0.f, 0.f, ray.d);
+  }
+  while (active) {  // :241
+    bool active_em = active && smooth(s, si);  // :245
+    DirectionSample ds{};
+    V3 em_weight = v3s(0.f);
+    V2 u_em = rng.next_2d();
+    if (active_em) em_weight = sample_emitter_visible(s, si, u_em, &ds);  // :247-249
+    active_em = active_em && ds.pdf != 0.f;  // :250
+    V3 wo = to_local(si.sh, ds.d);
+    float s1 = rng.next_1d();
+    V2 s2 = rng.next_2d();
+    V3 bsdf_val;
+    float bsdf_pdf;
+    BSDFSample bs;
+    V3 bsdf_weight = eval_pdf_sample(s, si, wo, s1, s2, &bsdf_val, &bsdf_pdf, &bs);  // :254-256
+    float mis_em = mis_weight_a(ds.pdf, bsdf_pdf);  // :258
+    if (active_em) L = L + f * bsdf_val * em_weight * mis_em;  // :259
+    f = f * bsdf_weight;  // :263
+    eta *= bs.eta;
+    float fmax_ = hmax(f);  // :268
+    float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+    bool rr_active = depth >= rr_depth;
+    bool rr_continue = rng.next_1d() < rr_prob;
+    if (rr_active) f = f * rcp(rr_prob);  // :274
+    active = active && (fmax_ != 0.f);
+    active = active && (!rr_active || rr_continue);
+    Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));  // :280
+    SurfaceInteraction si2 = active ? intersect(s, nray) : compute_si(s, kInf, 0xffffffffu, 0.f, 0.f, nray.d);
+    bool bsdf_delta = (bs.type & BF_DELTA) != 0;
+    V3 rel = si2.p - si.p;
+    float dist = norm(rel);
+    V3 ds_d = si2.valid ? rel / dist : to_world(si2.sh, si2.wi) * -1.f;
+    float em_pdf = bsdf_delta ? 0.f : pdf_emitter_direction(s, si2.emitter, ds_d, dist, si2.sh.n);  // :287-288
+    float mis_bsdf = mis_weight_a(bs.pdf, em_pdf);  // :290
+    V3 le = (bs.pdf > 0.f) ? emitter_eval(s, si2.emitter, si2.wi) : v3s(0.f);
+    if (active) L = L + f * le * mis_bsdf;  // :292
+    si = si2;
+    if (active) depth += 1;  // :297
+    active = active && depth < max_depth;
+    active = active && si.valid;
+  }
+  *valid_out = depth != 0;
+  return L;
+}
+
+// ----------------------------- nrc.py:25-125 -------------------------------
+V3 orc_nrc(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, float c, bool *valid_out) {
+  SurfaceInteraction si = intersect(s, ray);  // :117
+  const bool primary_valid = si.valid;
+  bool active = si.valid;  // :119
+  float a0 = squared_norm(ray.o - si.p) / (kFourPi * fabsf(si.wi.z));  // :121
+  // next_segment (:25-102)
+  V3 L = v3s(0.f), f = v3s(1.f);
+  float eta = 1.f;
+  uint32_t depth = 1;
+  float spread = 0.f;
+  while (active) {
+    bool active_em = active && smooth(s, si);
+    V2 u_em = rng.next_2d();
+    DirectionSample ds{};
+    V3 em_weight = v3s(0.f);
+    if (active) em_weight = sample_emitter_visible(s, si, u_em, &ds);  // :51-53 (uses `active`)
+    active_em = active_em && ds.pdf != 0.f;
+    V3 wo = to_local(si.sh, ds.d);
+    float s1 = rng.next_1d();
+    V2 s2 = rng.next_2d();
+    V3 bsdf_val;
+    float bsdf_pdf;
+    BSDFSample bs;
+    V3 bsdf_weight = eval_pdf_sample(s, si, wo, s1, s2, &bsdf_val, &bsdf_pdf, &bs);
+    float mis_em = mis_weight_b(ds.pdf, bsdf_pdf);
+    if (active_em) L = L + f * bsdf_val * em_weight * mis_em;  // :62
+    f = f * bsdf_weight;
+    eta *= bs.eta;
+    float a = sqr(spread);  // :70-71
+    active = active && (a < c * a0);
+    Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
+    SurfaceInteraction si2 = active ? intersect(s, nray) : compute_si(s, kInf, 0xffffffffu, 0.f, 0.f, nray.d);
+    bool bsdf_delta = (bs.type & BF_DELTA) != 0;
+    V3 rel = si2.p - si.p;
+    float dist = norm(rel);
+    V3 ds_d = si2.valid ? rel / dist : to_world(si2.sh, si2.wi) * -1.f;
+    float em_pdf = bsdf_delta ? 0.f : pdf_emitter_direction(s, si2.emitter, ds_d, dist, si2.sh.n);
+    float mis_bsdf = mis_weight_b(bs.pdf, em_pdf);
+    V3 le = (bs.pdf > 0.f) ? emitter_eval(s, si2.emitter, si2.wi) : v3s(0.f);
+    if (active) L = L + f * le * mis_bsdf;  // :85
+    spread += sqrtf(squared_norm(si2.p - si.p) / (bs.pdf * fabsf(si2.wi.z)));  // :91-93
+    si = si2;
+    if (active) depth += 1;
+    active = active && depth < max_depth;
+    active = active && si.valid;
+  }
+  *valid_out = primary_valid;  // :125
+  return L;
+}
+
+V3 run_integrator(const SceneView &s, const mtx_render_args &a, Pcg32 &rng, const Ray &ray, bool *valid) {
+  switch (a.integrator) {
+    case MTX_INT_PATH: return orc_path(s, rng, ray, a.max_depth, a.rr_depth, valid);
+    case MTX_INT_NRC: return orc_nrc(s, rng, ray, a.max_depth, a.nrc_c, valid);
+    default: return orc_path_mis(s, rng, ray, a.max_depth, a.rr_depth, valid);
+  }
+}
+
+}  // namespace
+
+// ===========================================================================
+// C entry points (ctypes)
+// ===========================================================================
+extern "C" {
+
+int orc_trace(const mtx_scene_desc *d, uint64_t n, const float *rays, int any_hit, int brute, uint32_t *hits,
+              uint32_t *visits) {
+  SceneView s = make_view(d);
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    const float *r = rays + 8 * i;
+    V3 o{r[0], r[1], r[2]}, dd{r[4], r[5], r[6]};
+    float maxt = r[3];
+    uint32_t nv = 0, tv = 0;
+    if (any_hit) {
+      hits[i] = trace_any(s, o, dd, maxt, &nv, &tv) ? 1u : 0u;
+    } else {
+      Hit h = brute ? brute_closest(s, o, dd, maxt) : trace_closest(s, o, dd, maxt, &nv, &tv);
+      hits[4 * i + 0] = f2u(h.t);
+      hits[4 * i + 1] = h.prim;
+      hits[4 * i + 2] = f2u(h.u);
+      hits[4 * i + 3] = f2u(h.v);
+    }
+    if (visits) {
+      visits[2 * i] = nv;
+      visits[2 * i + 1] = tv;
+    }
+  }
+  return 0;
+}
+
+// SamplingIntegrator.sample() for given rays (see mtx_sample_rays).
+int orc_sample_rays(const mtx_scene_desc *d, const mtx_render_args *a, uint64_t n, const float *rays,
+                    const uint32_t *lanes, uint32_t rng_skip, float *L, uint8_t *valid) {
+  SceneView s = make_view(d);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    Pcg32 rng = sampler_lane(a->seed, lanes[i]);
+    for (uint32_t k = 0; k < rng_skip; ++k) rng.next_u32();
+    const float *r = rays + 6 * i;
+    Ray ray{V3{r[0], r[1], r[2]}, V3{r[3], r[4], r[5]}, kLargest};
+    bool v = false;
+    V3 res = run_integrator(s, *a, rng, ray, &v);
+    L[3 * i] = res.x;
+    L[3 * i + 1] = res.y;
+    L[3 * i + 2] = res.z;
+    valid[i] = v ? 1 : 0;
+  }
+  return 0;
+}
+
+// Per-sample radiance for film rows [y0,y1): lane = (y*W + x)*spp_total +
+// sample_offset + s; writes L (3 per sample) and the film position (2 per
+// sample) in (pixel, s) order. Used by the per-lane parity tests.
+int orc_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float *L, float *pos) {
+  SceneView s = make_view(d);
+  const uint32_t W = s.camera.width, H = s.camera.height;
+  const uint64_t npx = (uint64_t)(a->y1 - a->y0) * W;
+  const uint32_t spp = a->spp;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t p = 0; p < (int64_t)npx; ++p) {
+    uint32_t y = a->y0 + (uint32_t)(p / W), x = (uint32_t)(p % W);
+    for (uint32_t k = 0; k < spp; ++k) {
+      uint32_t lane = (uint32_t)(((uint64_t)y * W + x) * a->spp_total + a->sample_offset + k);
+      Pcg32 rng = sampler_lane(a->seed, lane);
+      V2 u = rng.next_2d();  // path.py:45
+      float sx = (float)x + u.x, sy = (float)y + u.y;
+      V2 adj = V2{sx / (float)W, sy / (float)H};
+      Ray ray = camera_ray(s.camera, adj);  // path.py:60-62
+      bool v = false;
+      V3 res = run_integrator(s, *a, rng, ray, &v);
+      uint64_t o = (uint64_t)p * spp + k;
+      L[3 * o] = res.x;
+      L[3 * o + 1] = res.y;
+      L[3 * o + 2] = res.z;
+      pos[2 * o] = sx;
+      pos[2 * o + 1] = sy;
+    }
+  }
+  return 0;
+}
+
+// Film accumulation in the fixed order documented in DESIGN.md ("Film"):
+// stage 1 sums each source pixel's samples (s ascending) into its 3x3 tent
+// footprint; stage 2 gathers the 9 neighbours (dy, dx ascending).
+int orc_film(uint32_t W, uint32_t y0, uint32_t y1, uint32_t spp, const float *L, const float *pos, float *film) {
+  const uint32_t rows = y1 - y0;
+  std::vector<float> acc((size_t)rows * W * 36, 0.f);
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < (int64_t)rows * W; ++p) {
+    int x = (int)(p % W), y = (int)(y0 + p / W);
+    float *a = &acc[36 * (size_t)p];
+    for (uint32_t k = 0; k < spp; ++k) {
+      uint64_t o = (uint64_t)p * spp + k;
+      float sx = pos[2 * o], sy = pos[2 * o + 1];
+      float lr = L[3 * o], lg = L[3 * o + 1], lb = L[3 * o + 2];
+      for (int dy = 0; dy < 3; ++dy) {
+        float wy = fmaxf(0.f, 1.f - fabsf(sy - ((float)(y + dy - 1) + 0.5f)));
+        for (int dx = 0; dx < 3; ++dx) {
+          float wx = fmaxf(0.f, 1.f - fabsf(sx - ((float)(x + dx - 1) + 0.5f)));
+          float w = wx * wy;
+          float *c = a + 4 * (dy * 3 + dx);
+          c[0] = c[0] + lr * w;
+          c[1] = c[1] + lg * w;
+          c[2] = c[2] + lb * w;
+          c[3] = c[3] + w;
+        }
+      }
+    }
+  }
+  const uint32_t FW = W + 2, FH = rows + 2;
+#pragma omp parallel for schedule(static)
+  for (int64_t q = 0; q < (int64_t)FW * FH; ++q) {
+    int px = (int)(q % FW) - 1, py = (int)(y0 + q / FW) - 1;
+    float r = 0.f, g = 0.f, b = 0.f, w = 0.f;
+    for (int dy = 0; dy < 3; ++dy)
+      for (int dx = 0; dx < 3; ++dx) {
+        int sxp = px - dx + 1, syp = py - dy + 1;
+        if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
+        const float *c = &acc[36 * ((size_t)(syp - y0) * W + sxp) + 4 * (dy * 3 + dx)];
+        r = r + c[0];
+        g = g + c[1];
+        b = b + c[2];
+        w = w + c[3];
+      }
+    film[4 * q] = r;
+    film[4 * q + 1] = g;
+    film[4 * q + 2] = b;
+    film[4 * q + 3] = w;
+  }
+  return 0;
+}
+
+int orc_render(const mtx_scene_desc *d, const mtx_render_args *a, float *film) {
+  const uint32_t W = d->camera.width;
+  const uint64_t ns = (uint64_t)(a->y1 - a->y0) * W * a->spp;
+  std::vector<float> L(3 * ns), pos(2 * ns);
+  orc_render_samples(d, a, L.data(), pos.data());
+  return orc_film(W, a->y0, a->y1, a->spp, L.data(), pos.data(), film);
+}
+
+// ------------------------------- RNG KATs ----------------------------------
+int orc_rng_stream(uint32_t seed, uint32_t lane0, uint32_t n_lanes, uint32_t n_draws, float *out) {
+  for (uint32_t l = 0; l < n_lanes; ++l) {
+    Pcg32 r = sampler_lane(seed, lane0 + l);
+    for (uint32_t k = 0; k < n_draws; ++k) out[(size_t)l * n_draws + k] = r.next_1d();
+  }
+  return 0;
+}
+
+// --------------------------- prefix_sum.py:9-36 ----------------------------
+// Hillis-Steele: for i in 0..floor(log2 n): x[j] = x[j] + x[j - 2^i], j >= 2^i,
+// with copy-on-write (gather all, then scatter).
+int orc_prefix_sum_f32_hs(const float *in, float *out, uint64_t n) {
+  std::vector<float> x(in, in + n), y(n);
+  if (n == 0) return 0;
+  int passes = 0;
+  while ((1ull << (passes + 1)) <= n) ++passes;  // floor(log2 n)
+  for (int i = 0; i <= passes; ++i) {
+    uint64_t st = 1ull << i;
+    if (st >= n) break;
+    y = x;
+    for (uint64_t j = st; j < n; ++j) y[j] = x[j] + x[j - st];
+    x.swap(y);
+  }
+  memcpy(out, x.data(), n * sizeof(float));
+  return 0;
+}
+
+int orc_prefix_sum_u32(const uint32_t *in, uint32_t *out, uint64_t n, int inclusive) {
+  uint32_t acc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t v = in[i];
+    if (inclusive) {
+      acc += v;
+      out[i] = acc;
+    } else {
+      out[i] = acc;
+      acc += v;
+    }
+  }
+  return 0;
+}
+
+// ------------------------------ hashgrid.py --------------------------------
+// hash (:8-12) on u32 with wraparound; bbmin/bbmax are scalars over all three
+// axes (:33-41); cell_offset is the exclusive scan of cell_size (:65-76);
+// within a cell, sample indices are listed in ascending order (the reference
+// order is race-defined, :53).
+int orc_hashgrid(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
+                 uint32_t *cell_offset, uint32_t *sample_idx) {
+  const float *px = p, *py = p + n, *pz = p + 2 * n;
+  float bbmin = INFINITY, bbmax = -INFINITY;
+  for (uint64_t i = 0; i < n; ++i) {
+    bbmin = fminf(bbmin, fminf(px[i], fminf(py[i], pz[i])));
+    bbmax = fmaxf(bbmax, fmaxf(px[i], fmaxf(py[i], pz[i])));
+  }
+  float ext = bbmax - bbmin, fres = (float)res;
+  for (uint32_t c = 0; c < n_cells; ++c) cell_size[c] = 0;
+  std::vector<uint32_t> rank(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t x = (uint32_t)((px[i] - bbmin) / ext * fres);
+    uint32_t y = (uint32_t)((py[i] - bbmin) / ext * fres);
+    uint32_t z = (uint32_t)((pz[i] - bbmin) / ext * fres);
+    uint32_t h = ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
+    cell[i] = h;
+    rank[i] = cell_size[h]++;
+  }
+  uint32_t acc = 0;
+  for (uint32_t c = 0; c < n_cells; ++c) {
+    cell_offset[c] = acc;
+    acc += cell_size[c];
+  }
+  for (uint64_t i = 0; i < n; ++i) sample_idx[cell_offset[cell[i]] + rank[i]] = (uint32_t)i;
+  return 0;
+}
+
+// ----------------------------- reductions.py -------------------------------
+// Every target index receives func(target, value) for each of its values,
+// applied in ascending value-index order.
+int orc_scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
+                           uint64_t n_value) {
+  for (uint64_t i = 0; i < n_value; ++i) {
+    uint32_t t = index[i];
+    if (t >= n_target) return -1;
+    float a = target[t], b = value[i];
+    target[t] = op == 0 ? a + b : (op == 1 ? fminf(a, b) : fmaxf(a, b));
+  }
+  return 0;
+}
+
+}  // extern "C"
