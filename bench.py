@@ -39,8 +39,7 @@ def parse():
     p.add_argument("--rr-depth", type=int, default=2)
     p.add_argument("--chunk", type=int, default=0, help="wavefront paths per chunk (0 = library default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-rows", type=int, default=8, help="film rows of the CPU baseline sample")
-    p.add_argument("--cpu-spp", type=int, default=4)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU time of the baseline sample")
     return p.parse_args()
 
 
@@ -63,18 +62,13 @@ def main():
     integ = PathIntegrator({"max_depth": args.max_depth, "rr_depth": args.rr_depth})
     W, H, spp = sc.width, sc.height, args.spp
     film = torch.empty((H + 2, W + 2, 4), dtype=torch.float32, device=f"cuda:{local}")
-    gathered = [torch.empty_like(film) for _ in range(world)] if world > 1 else None
-    total = torch.empty_like(film)
+    from mtx import distributed
 
     def step(i, stats=False):
         r = integ.render_film(sc, seed=i, spp=spp, spp_total=spp * world, sample_offset=spp * rank, out=film,
                               stats=stats, chunk_paths=args.chunk)
         if world > 1:
-            dist.all_gather(gathered, film)
-            if rank == 0:
-                total.zero_()
-                for g in gathered:  # fixed rank order: deterministic sum
-                    total.add_(g)
+            distributed.gather_sum(film)  # RCCL all_gather, rank-order sum on rank 0
         return r[1] if stats else None
 
     for i in range(args.warmup):
@@ -164,23 +158,26 @@ def main():
 
 
 def cpu_baseline(sc, integ, args):
-    """oracle/ (the CPU restatement, OpenMP) on a bounded sample of the same
-    workload: the first `cpu_rows` film rows at `cpu_spp`, same seed scheme."""
+    """oracle/ (the CPU restatement, OpenMP over the host cores) on a bounded
+    sample of the same workload: the full 1280x720 frame at a reduced spp,
+    sized to about `cpu_seconds` of CPU time after a 1-spp calibration run."""
     import binding as oracle
 
     oracle.build()
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    os.environ["OMP_NUM_THREADS"] = str(threads)
-    y1 = min(sc.height, args.cpu_rows)
-    a = integ.render_args(sc, 0, args.cpu_spp, 0, y1)
-    oracle.render(sc, oracle.render_args(a.integrator, a.max_depth, a.rr_depth, 0, 1, 0, 1))  # warm
+    a1 = integ.render_args(sc, 0, 1)
+    t0 = time.perf_counter()
+    oracle.render(sc, a1)
+    t1 = time.perf_counter() - t0
+    spp = max(1, min(64, int(round(args.cpu_seconds / max(t1, 1e-3)))))
+    a = integ.render_args(sc, 0, spp)
     t0 = time.perf_counter()
     oracle.render(sc, a)
     dt = time.perf_counter() - t0
-    n = sc.width * y1 * args.cpu_spp
+    n = sc.width * sc.height * spp
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"{sc.width}x{y1} rows x spp={args.cpu_spp} ({n} paths) of the same workload, "
-                      f"{dt:.2f} s"}
+            "sample": f"full {sc.width}x{sc.height} frame at spp={spp} ({n} paths, {dt:.1f} s), same integrator, "
+                      "scene and seed scheme; oracle/oracle.cpp (OpenMP)"}
 
 
 if __name__ == "__main__":

@@ -168,10 +168,16 @@ struct Builder {
     return m;
   }
 
-  static void pad_box(Box &b) {
+  // Conservative padding: the slab test computes t = fma(b, 1/d, -o/d) with
+  // |error| <= (|o| + |b|) |1/d| 2^-23 for points inside the scene, so a pad
+  // of (|x| + E) 2^-19 (E = largest |coordinate| of the scene) covers it
+  // with a 10x margin and no closest hit can be culled.
+  float extent = 0.f;
+  void pad_box(Box &b) const {
+    const float k = 1.0f / 524288.0f;  // 2^-19
     for (int a = 0; a < 3; ++a) {
-      b.lo[a] -= std::fabs(b.lo[a]) * 2.4e-7f + 1e-30f;
-      b.hi[a] += std::fabs(b.hi[a]) * 2.4e-7f + 1e-30f;
+      b.lo[a] -= (std::fabs(b.lo[a]) + extent) * k;
+      b.hi[a] += (std::fabs(b.hi[a]) + extent) * k;
     }
   }
 
@@ -202,6 +208,9 @@ struct Builder {
   }
 
   void run() {
+    for (uint32_t t = 0; t < n; ++t)
+      for (int k = 0; k < 3; ++k)
+        for (int a = 0; a < 3; ++a) extent = std::max(extent, std::fabs(vpos[3 * (size_t)vidx[3 * (size_t)t + k] + a]));
     tbox.resize(n);
     cen.resize(3 * (size_t)n);
     idx.resize(n);

@@ -45,6 +45,7 @@ def lib():
             "orc_prefix_sum_u32": [vp, vp, u64, C.c_int],
             "orc_hashgrid": [vp, u64, u32, u32, vp, vp, vp, vp],
             "orc_scatter_reduce_f32": [C.c_int, vp, u64, vp, vp, u64],
+            "orc_dmath": [C.c_int, vp, vp, u64],
         }
         for k, a in sig.items():
             getattr(L, k).argtypes = a
@@ -143,3 +144,34 @@ def scatter_reduce(op, target, value, index):
     lib().orc_scatter_reduce_f32(op, t.ctypes.data, len(t), np.ascontiguousarray(value, np.float32).ctypes.data,
                                  np.ascontiguousarray(index, np.uint32).ctypes.data, len(value))
     return t
+
+
+def dmath(op, x):
+    """op in sin, cos, log, exp, erf, erfinv (mtx_core/dmath.h)."""
+    ops = {"sin": 0, "cos": 1, "log": 2, "exp": 3, "erf": 4, "erfinv": 5}
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros_like(x)
+    lib().orc_dmath(ops[op], x.ctypes.data, out.ctypes.data, len(x))
+    return out
+
+
+def bsdf_probe(scene, mat, wi, wo, uv, u):
+    n = len(wi)
+    out = np.zeros((n, 16), np.float32)
+    out2 = np.zeros(n, np.float32)
+    d = scene.desc()
+    L = lib()
+    L.orc_bsdf_probe.argtypes = [C.POINTER(_abi.SceneDesc), C.c_uint32, C.c_uint64] + [C.c_void_p] * 6
+    c = [np.ascontiguousarray(a, np.float32) for a in (wi, wo, uv, u)]
+    L.orc_bsdf_probe(C.byref(d), mat, n, *[a.ctypes.data for a in c], out.ctypes.data, out2.ctypes.data)
+    return out, out2
+
+
+def warp(op, u):
+    ops = {"cosine_hemisphere": 0, "disk_concentric": 1, "disk": 2, "std_normal": 3, "uniform_hemisphere": 4}
+    u = np.ascontiguousarray(u, np.float32)
+    out = np.zeros((len(u), 3), np.float32)
+    L = lib()
+    L.orc_warp.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64]
+    L.orc_warp(ops[op], u.ctypes.data, out.ctypes.data, len(u))
+    return out

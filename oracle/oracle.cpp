@@ -635,3 +635,79 @@ int orc_scatter_reduce_f32(int op, float *target, uint64_t n_target, const float
 }
 
 }  // extern "C"
+
+// --------------------- per-lane primitive probes (tests) -------------------
+extern "C" {
+
+// op: 0 sin, 1 cos, 2 log, 3 exp, 4 erf, 5 erfinv
+int orc_dmath(int op, const float *x, float *out, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    float s, c;
+    switch (op) {
+      case 0: dsincos(x[i], &s, &c); out[i] = s; break;
+      case 1: dsincos(x[i], &s, &c); out[i] = c; break;
+      case 2: out[i] = dlog(x[i]); break;
+      case 3: out[i] = dexp(x[i]); break;
+      case 4: out[i] = derf(x[i]); break;
+      case 5: out[i] = derfinv(x[i]); break;
+      default: return -1;
+    }
+  }
+  return 0;
+}
+
+// BSDF probe for material `mat` of a scene: for each i, with local wi[i],
+// wo[i], uv[i] and samples u[i] = (u1, u2x, u2y):
+//   out[16 i + 0..2]  eval value at wo, [3] eval pdf at wo
+//   out[16 i + 4..6]  sampled wo, [7] sample pdf, [8] eta, [9] type (bits)
+//   out[16 i + 10..12] sample weight, [13..15] eval value at the sampled wo
+//   out2[i]           eval pdf at the sampled wo
+int orc_bsdf_probe(const mtx_scene_desc *d, uint32_t mat, uint64_t n, const float *wi, const float *wo,
+                   const float *uv, const float *u, float *out, float *out2) {
+  SceneView s = make_view(d);
+  if (mat >= d->n_materials) return -1;
+  const mtx_material &m = s.materials[mat];
+  for (uint64_t i = 0; i < n; ++i) {
+    V3 a{wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]}, b{wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]};
+    V2 t{uv[2 * i], uv[2 * i + 1]};
+    V3 val;
+    float pdf;
+    bsdf_eval_pdf(s.bsdf, m, t, a, b, &val, &pdf);
+    BSDFSample bs;
+    V3 w = bsdf_sample(s.bsdf, m, t, a, u[3 * i], V2{u[3 * i + 1], u[3 * i + 2]}, &bs);
+    V3 val2;
+    float pdf2;
+    bsdf_eval_pdf(s.bsdf, m, t, a, bs.wo, &val2, &pdf2);
+    float *o = out + 16 * i;
+    o[0] = val.x; o[1] = val.y; o[2] = val.z; o[3] = pdf;
+    o[4] = bs.wo.x; o[5] = bs.wo.y; o[6] = bs.wo.z; o[7] = bs.pdf; o[8] = bs.eta; o[9] = u2f(bs.type);
+    o[10] = w.x; o[11] = w.y; o[12] = w.z;
+    o[13] = val2.x; o[14] = val2.y; o[15] = val2.z;
+    out2[i] = pdf2;
+  }
+  return 0;
+}
+
+// Warps used by the integrators (upstream mitsuba/core/warp.h).
+// op: 0 cosine hemisphere (3), 1 uniform disk concentric (2), 2 uniform
+// disk (2), 3 std normal (2), 4 uniform hemisphere (3)
+int orc_warp(int op, const float *u, float *out, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) {
+    V2 s{u[2 * i], u[2 * i + 1]};
+    float *o = out + 3 * i;
+    V3 v{0, 0, 0};
+    V2 p{0, 0};
+    switch (op) {
+      case 0: v = square_to_cosine_hemisphere(s); break;
+      case 1: p = square_to_uniform_disk_concentric(s); v = V3{p.x, p.y, 0}; break;
+      case 2: p = square_to_uniform_disk(s); v = V3{p.x, p.y, 0}; break;
+      case 3: p = square_to_std_normal(s); v = V3{p.x, p.y, 0}; break;
+      case 4: v = square_to_uniform_hemisphere(s); break;
+      default: return -1;
+    }
+    o[0] = v.x; o[1] = v.y; o[2] = v.z;
+  }
+  return 0;
+}
+
+}  // extern "C"

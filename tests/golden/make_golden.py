@@ -1,0 +1,69 @@
+"""Regenerate tests/golden/golden.npz from the CPU restatement (oracle/).
+
+The reference implementation (Mitsuba 3 / Dr.Jit / Embree) is not present
+in the reference tree, so these vectors pin the oracle
+against drift; their contents are data (inputs and outputs), nothing from
+the reference's sources. Vectors:
+  rng_seed0 / rng_seed7   first 64 draws of sampler lanes 0..1023
+  trace_rays / trace_hits 4096 rays on the 2 %-budget bedroom proxy
+  film_<integrator>       64x36, spp 16, seed 0 films (path_test, mypath, nrc)
+  hs_scan_sha             sha256 of the Hillis-Steele scan of 10^6 floats
+  scene_sha               sha256 of the test scene arrays
+
+    python tests/golden/make_golden.py
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd"), os.path.join(ROOT, "oracle")]
+
+import binding as oracle  # noqa: E402
+from mtx import load_dict, scene  # noqa: E402
+
+INTEGRATORS = ("path_test", "mypath", "nrc")
+
+
+def scene_digest(s):
+    h = hashlib.sha256()
+    for a in (s.vpos, s.vnormal, s.vuv, s.nodes, s.tri_geom, s.tri_vidx, s.tri_shape, s.texels, s.tables):
+        h.update(np.ascontiguousarray(a).tobytes())
+    for a in (s.shapes, s.materials, s.emitters, s.textures, s.camera):
+        h.update(bytes(a))
+    return h.hexdigest()
+
+
+def golden_rays(s, n=4096, seed=123):
+    rng = np.random.default_rng(seed)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = rng.uniform([-3.0, 0.05, -1.2], [3.8, 2.6, 3.6], (n, 3))
+    d = rng.normal(size=(n, 3))
+    rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 3] = 3e38
+    return rays
+
+
+def compute():
+    s = scene.bedroom(width=64, height=36, scale=0.02, tex_res=64)
+    out = {"scene_sha": np.frombuffer(scene_digest(s).encode(), np.uint8)}
+    out["rng_seed0"] = oracle.rng_stream(0, 0, 1024, 64)
+    out["rng_seed7"] = oracle.rng_stream(7, 0, 1024, 64)
+    rays = golden_rays(s)
+    out["trace_rays"] = rays
+    out["trace_hits"] = oracle.trace(s, rays)[0]
+    for name in INTEGRATORS:
+        integ = load_dict({"type": name})
+        out[f"film_{name}"] = oracle.render(s, integ.render_args(s, 0, 16))
+    x = oracle.rng_stream(0, 0, 1_000_000, 1)[:, 0].copy()
+    out["hs_scan_sha"] = np.frombuffer(hashlib.sha256(oracle.prefix_sum_f32_hs(x).tobytes()).hexdigest().encode(),
+                                       np.uint8)
+    return out
+
+
+if __name__ == "__main__":
+    np.savez_compressed(os.path.join(HERE, "golden.npz"), **compute())
+    print("wrote", os.path.join(HERE, "golden.npz"))

@@ -1,0 +1,78 @@
+"""The C ABI library loads, exports exactly what include/mtx.h declares, and
+its host-only entry points behave (no GPU needed)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+from conftest import ROOT
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "mtx.h")).read()
+    return sorted(set(re.findall(r"\b(mtx_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_and_exports_agree():
+    from mtx import _abi
+
+    assert _declared() == sorted(_abi.EXPORTS)
+
+
+def test_library_loads_and_exports_every_symbol():
+    from mtx import _lib
+
+    L = _lib.lib()
+    for name in _declared():
+        assert hasattr(L, name), name
+    assert L.mtx_abi_version() == 1
+
+
+def test_struct_sizes_match_header():
+    from mtx import _abi
+
+    assert C.sizeof(_abi.Material) == 72
+    assert C.sizeof(_abi.Emitter) == 64
+    assert C.sizeof(_abi.Shape) == 16
+    assert C.sizeof(_abi.Camera) == 72
+    assert C.sizeof(_abi.RenderArgs) == 48
+
+
+def test_ctx_create_without_gpu_fails_cleanly():
+    import torch
+
+    from mtx import _lib
+
+    if torch.cuda.is_available():
+        return
+    h = C.c_void_p()
+    rc = _lib.lib().mtx_ctx_create(0, C.byref(h))
+    assert rc < 0
+    assert _lib.lib().mtx_last_error()
+
+
+def test_bvh_build_rejects_bad_input():
+    from mtx import _lib
+
+    L = _lib.lib()
+    v = np.zeros(9, np.float32)
+    idx = np.array([0, 1, 7], np.uint32)  # vertex 7 does not exist
+    nodes = np.zeros(64, np.int32)
+    geom = np.zeros(12, np.float32)
+    perm = np.zeros(1, np.uint32)
+    nn, dep = C.c_uint32(), C.c_uint32()
+    rc = L.mtx_bvh_build(v.ctypes.data, 3, idx.ctypes.data, 1, nodes.ctypes.data, C.byref(nn), geom.ctypes.data,
+                         perm.ctypes.data, C.byref(dep))
+    assert rc == -1 and b"out of range" in L.mtx_last_error()
+
+
+def test_roughplastic_tables():
+    from mtx import _lib
+
+    tab = np.zeros(64, np.float32)
+    internal = C.c_float()
+    assert _lib.lib().mtx_roughplastic_tables(0, 0.15, 1.5, tab.ctypes.data, C.byref(internal)) == 0
+    assert ((tab > 0) & (tab <= 1)).all()
+    assert tab[-1] > 0.9  # normal incidence: ~4 % Fresnel reflectance
+    assert 0.3 < internal.value < 0.8

@@ -1,0 +1,49 @@
+"""The oracle reproduces the committed golden vectors (tests/golden/), and —
+on a GPU — so does the HIP path."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+GOLDEN = os.path.join(ROOT, "tests", "golden", "golden.npz")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return dict(np.load(GOLDEN, allow_pickle=False))
+
+
+def test_golden_scene_unchanged(golden, small_scene):
+    import make_golden
+
+    assert make_golden.scene_digest(small_scene) == golden["scene_sha"].tobytes().decode()
+
+
+def test_golden_rng(golden, oracle):
+    assert np.array_equal(oracle.rng_stream(0, 0, 1024, 64), golden["rng_seed0"])
+    assert np.array_equal(oracle.rng_stream(7, 0, 1024, 64), golden["rng_seed7"])
+
+
+def test_golden_trace(golden, oracle, small_scene):
+    assert np.array_equal(oracle.trace(small_scene, golden["trace_rays"])[0], golden["trace_hits"])
+
+
+@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc"])
+def test_golden_films_oracle(golden, oracle, small_scene, name):
+    from mtx import load_dict
+
+    integ = load_dict({"type": name})
+    assert np.array_equal(oracle.render(small_scene, integ.render_args(small_scene, 0, 16)), golden[f"film_{name}"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc"])
+def test_golden_films_gpu(golden, small_scene, name):
+    from mtx import load_dict
+
+    integ = load_dict({"type": name})
+    assert np.array_equal(integ.render_film(small_scene, seed=0, spp=16), golden[f"film_{name}"])
