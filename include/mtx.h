@@ -161,6 +161,8 @@ typedef struct mtx_render_args {
   uint32_t chunk_paths;  /* wavefront size (0 = default) */
   float nrc_c;           /* NRC spread threshold (nrc.py:123) */
   uint32_t flags;        /* bit0: collect traversal stats, bit1: per-kernel HIP event timing */
+  uint32_t iterations;   /* PSSMLT Metropolis iterations (pssmlt.py:208: 200; 0 = 200) */
+  uint32_t reserved;
 } mtx_render_args;
 
 /* Device-side counters, filled when mtx_render_args.flags has bit0/bit1. */

@@ -93,6 +93,8 @@ struct mtx_ctx {
   // wavefront
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
   uint32_t capacity = 0;
+  DevBuf mlt_cur, mlt_L, mlt_prop, vpath, vprop;  // PSSMLT chain state
+  uint32_t mlt_capacity = 0, mlt_depth = 0;
   // film
   DevBuf contrib, film;
   // scratch for sample_rays / trace / primitives
@@ -150,6 +152,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
+                    &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
@@ -300,7 +303,28 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.counters = (uint32_t *)c->counters.p;
   b.stats = (unsigned long long *)c->stats.p;
   b.capacity = c->capacity;
+  b.mlt_cur = (float4 *)c->mlt_cur.p;
+  b.mlt_L = (float4 *)c->mlt_L.p;
+  b.mlt_prop = (float2 *)c->mlt_prop.p;
+  b.vpath = (float4 *)c->vpath.p;
+  b.vprop = (float4 *)c->vprop.p;
   return b;
+}
+
+int ensure_mlt(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
+  int rc;
+  if (cap > c->mlt_capacity || max_depth > c->mlt_depth || c->mlt_capacity != c->capacity) {
+    // vertex buffers are indexed [depth * wavefront capacity + chain]
+    const size_t wc = c->capacity;
+    if ((rc = dalloc(c->mlt_cur, 16 * wc))) return rc;
+    if ((rc = dalloc(c->mlt_L, 16 * wc))) return rc;
+    if ((rc = dalloc(c->mlt_prop, 8 * wc))) return rc;
+    if ((rc = dalloc(c->vpath, 16 * wc * max_depth))) return rc;
+    if ((rc = dalloc(c->vprop, 16 * wc * max_depth))) return rc;
+    c->mlt_capacity = c->capacity;
+    c->mlt_depth = max_depth;
+  }
+  return MTX_OK;
 }
 
 int check_args(mtx_ctx *c, const mtx_render_args *a) {
@@ -312,7 +336,8 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
     mtx_set_error("no scene uploaded");
     return MTX_E_NOSCENE;
   }
-  if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC) {
+  if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC &&
+      a->integrator != MTX_INT_PSSMLT_SIMPLE) {
     mtx_set_error("integrator %u is not supported by this entry point", a->integrator);
     return MTX_E_UNSUPPORTED;
   }
@@ -373,10 +398,12 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     e = tm.begin(2);
     mtxd::launch_shade(s, b, p, bounce, c->shade_grid, c->stream);
     tm.end(2, e);
-    e = tm.begin(1);
-    mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
-    tm.end(1, e);
-    ++*n_shadow;
+    if (p.integrator != MTX_INT_PSSMLT_SIMPLE) {  // PSSMLT traces no NEE rays
+      e = tm.begin(1);
+      mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
+      tm.end(1, e);
+      ++*n_shadow;
+    }
     // Deep paths (max_depth 65, scene.xml:6): stop launching once the queue
     // has drained (checked every 8 bounces).
     if (depth_iters > 16 && (bounce & 7) == 7 && bounce + 1 < depth_iters) {
@@ -421,6 +448,14 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   }
   const bool want_stats = stats && (a->flags & 1u);
   Timer tm{c, stats && (a->flags & 2u)};
+  if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
+    if (a->sample_offset != 0 || a->spp_total != a->spp) {
+      mtx_set_error("mtx_render: PSSMLT chains cannot be split by sample range (use row bands)");
+      return MTX_E_ARG;
+    }
+    if ((rc = ensure_mlt(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+    HIP_TRY(hipMemsetAsync(c->contrib.p, 0, 9ull * 16 * band_px, c->stream));
+  }
   mtxd::WaveBuffers b = buffers(c);
   if (want_stats) HIP_TRY(hipMemsetAsync(b.stats, 0, 64, c->stream));
   uint64_t n_trace = 0, n_shadow = 0;
@@ -442,7 +477,22 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.n_paths = p.n_px * a->spp;
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;
-    HIP_TRY(hipMemsetAsync(b.counters, 0, 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2), c->stream));
+    const size_t cbytes = 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2);
+    if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
+      // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains
+      const uint32_t iters = a->iterations ? a->iterations : 200;
+      mtxd::launch_mlt_init(b, p, c->stream);
+      for (uint32_t it = 0; it < iters; ++it) {
+        p.large_step = (it % 50 == 0) ? 1u : 0u;  // reset_interval = 50 (:206)
+        HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, c->stream));
+        mtxd::launch_mlt_begin(c->scene, b, p, c->stream);
+        run_bounces(c, b, p, tm, &n_trace, &n_shadow);
+        mtxd::launch_mlt_end(b, p, c->stream);
+        if (it % 50 > 40) mtxd::launch_mlt_film(b, p, (float4 *)c->contrib.p, c->stream);  // bootstrapping = 40
+      }
+      continue;
+    }
+    HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, c->stream));
     mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
     run_bounces(c, b, p, tm, &n_trace, &n_shadow);
     mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, c->stream);
@@ -482,6 +532,10 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
                     uint32_t rng_skip, float *L, uint8_t *valid) {
   int rc = check_args(c, a);
   if (rc) return rc;
+  if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
+    mtx_set_error("mtx_sample_rays: PSSMLT is a render-level algorithm (use mtx_render)");
+    return MTX_E_UNSUPPORTED;
+  }
   if (n == 0) return MTX_OK;
   if (!rays || !lanes || !L || !valid) {
     mtx_set_error("mtx_sample_rays: null buffer");

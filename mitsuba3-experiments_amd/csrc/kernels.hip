@@ -486,6 +486,75 @@ __device__ __forceinline__ bool shade_path(const SceneView &sv, const WaveBuffer
   return active;
 }
 
+// Dr.Jit clamp(x, lo, hi) = maximum(minimum(x, hi), lo), NaN-ignoring (App. A).
+__device__ __forceinline__ float dr_clamp(float x, float lo, float hi) { return fmaxf(fminf(x, hi), lo); }
+
+// pssmltsimple.py:60-131 — one bounce of a PSSMLT proposal: emission without
+// MIS (:74), BSDF sample masked by active_next (:84), mutation of the local
+// direction against the current path's vertex (:88, mutate :135-142),
+// re-evaluation (:93-96), proposed vertex write (:99), spawn, RR. Every
+// executed bounce consumes 4 draws: the chain's RNG stream continues across
+// the Metropolis iterations.
+__device__ __forceinline__ bool shade_pssmlt(const SceneView &sv, const WaveBuffers &b, const ChunkParams &p,
+                                             uint32_t path) {
+  const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path];
+  const uint4 mi = b.misc[path];
+  const float4 h = b.hit[path];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  uint32_t depth = mi.w & 0xffffu;
+  const uint32_t flags = mi.w >> 16;
+  V3 T = V3{th.x, th.y, th.z};
+  float eta = th.w;
+  V3 L = V3{Lr.x, Lr.y, Lr.z};
+  float prev_pdf = Lr.w;
+  const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{rd.x, rd.y, rd.z});
+  const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
+  L = fma3v(T, le, L);
+  const bool active_next = (depth + 1 < p.max_depth) && si.valid;
+  const float s1 = rng.next_1d();
+  const V2 s2 = rng.next_2d();
+  BSDFSample bs;
+  bs.wo = v3s(0.f);
+  bs.pdf = 0.f;
+  bs.eta = 0.f;
+  bs.type = 0;
+  V3 w = v3s(0.f);
+  mtx_material mat;
+  if (si.valid) {
+    mat = sv.materials[si.material];
+    w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+  }
+  if (!active_next) w = v3s(0.f);
+  const float4 o4 = b.vpath[(size_t)depth * b.capacity + path];
+  const V3 old = V3{o4.x, o4.y, o4.z};
+  V3 vwo = p.large_step ? bs.wo : normalize(old * 0.9f + bs.wo * 0.1f);
+  V3 val = v3s(0.f);
+  float pdf = 0.f;
+  if (si.valid) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, vwo, &val, &pdf);
+  if (pdf <= 0.f) vwo = bs.wo;
+  if (pdf > 0.f) w = val / pdf;
+  b.vprop[(size_t)depth * b.capacity + path] = make_float4(vwo.x, vwo.y, vwo.z, 0.f);
+  const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, vwo));
+  T = T * w;
+  eta *= bs.eta;
+  prev_pdf = bs.pdf;
+  if (si.valid) depth += 1;
+  const float fmax_ = hmax(T);
+  const float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+  const bool rr_active = depth >= p.rr_depth;
+  const bool rr_continue = rng.next_1d() < rr_prob;
+  if (rr_active) T = T * rcp(rr_prob);
+  const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
+  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  return active;
+}
+
 template <int INT>
 __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
@@ -505,7 +574,10 @@ __global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene s, WaveBuffers b
     uint32_t path = 0;
     if (i < count) {
       path = in_q[i];
-      cont = shade_path<INT>(sv, b, p, bounce, path, io);
+      if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
+        cont = shade_pssmlt(sv, b, p, path);
+      else
+        cont = shade_path<INT>(sv, b, p, bounce, path, io);
     }
     const uint32_t slot = wave_append(out_cnt, cont);
     if (cont) out_q[slot] = path;
@@ -623,6 +695,122 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const flo
 }
 
 // ---------------------------------------------------------------------------
+// PSSMLT chain kernels (pssmlt.py:167-228). Chains of a chunk keep their
+// state in HBM across all Metropolis iterations; chain i of the chunk is
+// sampler lane px0*spp + i (pssmlt.py:188-193).
+// ---------------------------------------------------------------------------
+__global__ void k_mlt_init(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_paths) return;
+  const Pcg32 rng = sampler_lane(p.seed, p.px0 * p.spp + i);
+  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+  b.mlt_cur[i] = make_float4(0.5f, 0.5f, 0.f, 0.f);  // offset = 0.5, cumulative_weight = 0 (:198-200)
+  b.mlt_L[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (uint32_t d = 0; d < max_depth; ++d) {
+    b.vpath[(size_t)d * b.capacity + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    b.vprop[(size_t)d * b.capacity + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// render_sample head (:122-129): offset mutation, camera ray, path state.
+__global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) b.counters[0] = p.n_paths;
+  if (i >= p.n_paths) return;
+  const uint4 mi = b.misc[i];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  const V2 u = rng.next_2d();
+  V2 po;
+  if (p.large_step) {
+    po = u;
+  } else {  // mutate_offset (:245-255)
+    const float4 cur = b.mlt_cur[i];
+    const V2 g = square_to_std_normal(u);
+    const float k = 0.31622776601683794f;  // sqrt(0.1)
+    po = V2{dr_clamp(g.x * k + cur.x, 0.f, 1.f), dr_clamp(g.y * k + cur.y, 0.f, 1.f)};
+  }
+  const uint32_t pix = p.px0 + i / p.spp;
+  const uint32_t y = pix / p.width, x = pix - y * p.width;
+  const V2 sp = V2{((float)x + po.x) / (float)p.width, ((float)y + po.y) / (float)p.height};
+  const Ray ray = camera_ray(s.camera, sp);
+  b.mlt_prop[i] = make_float2(po.x, po.y);
+  b.ray_o[i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
+  b.ray_d[i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+  b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+  b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
+  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+  b.queue[0][i] = i;
+}
+
+// render_sample tail (:137-159): acceptance, cumulative weights, state swap.
+__global__ void k_mlt_end(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n_paths) return;
+  const uint4 mi = b.misc[i];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  const float4 lp4 = b.L[i];
+  const V3 Lp = V3{lp4.x, lp4.y, lp4.z};
+  float4 cur = b.mlt_cur[i];
+  const float4 lc4 = b.mlt_L[i];
+  const float a = dr_clamp(luminance(Lp) / luminance(V3{lc4.x, lc4.y, lc4.z}), 0.f, 1.f);
+  const bool accept = rng.next_1d() < a;
+  if (accept) {
+    cur.z = a;
+  } else {
+    cur.z += 1.f - a;
+  }
+  if (accept) {
+    const float2 po = b.mlt_prop[i];
+    cur.x = po.x;
+    cur.y = po.y;
+    b.mlt_L[i] = make_float4(Lp.x, Lp.y, Lp.z, 0.f);
+    for (uint32_t d = 0; d < max_depth; ++d)
+      b.vpath[(size_t)d * b.capacity + i] = b.vprop[(size_t)d * b.capacity + i];
+  }
+  b.mlt_cur[i] = cur;
+  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+}
+
+// block.put(pos, L / cw) at the integer pixel position (:161-165), running
+// accumulation per source pixel: iteration, then chain order.
+__global__ void k_mlt_film(WaveBuffers b, ChunkParams p, float4 *contrib) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= p.n_px) return;
+  const uint32_t pix = p.px0 + q;
+  const int y = (int)(pix / p.width), x = (int)(pix - (uint32_t)y * p.width);
+  const size_t o = 9 * ((size_t)(pix - p.band_y0 * p.width));
+  float4 acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = contrib[o + k];
+  for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
+    const uint32_t c = q * p.spp + sidx;
+    const float4 lc = b.mlt_L[c];
+    const float cw = b.mlt_cur[c].z;
+    const V3 res = V3{lc.x, lc.y, lc.z} / cw;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const float wy = fmaxf(0.f, 1.f - fabsf((float)y - ((float)(y + dy - 1) + 0.5f)));
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const float wx = fmaxf(0.f, 1.f - fabsf((float)x - ((float)(x + dx - 1) + 0.5f)));
+        const float w = wx * wy;
+        float4 &a = acc[dy * 3 + dx];
+        a.x = a.x + res.x * w;
+        a.y = a.y + res.y * w;
+        a.z = a.z + res.z * w;
+        a.w = a.w + w;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) contrib[o + k] = acc[k];
+}
+
+// ---------------------------------------------------------------------------
 // Launch wrappers
 // ---------------------------------------------------------------------------
 static inline unsigned blocks_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -658,9 +846,24 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
     case MTX_INT_NRC:
       hipLaunchKernelGGL(k_shade<MTX_INT_NRC>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
+    case MTX_INT_PSSMLT_SIMPLE:
+      hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_SIMPLE>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
     default:
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
   }
+}
+void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_mlt_init, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);
+}
+void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_mlt_begin, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, s, b, p);
+}
+void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_mlt_end, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);
+}
+void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st) {
+  hipLaunchKernelGGL(k_mlt_film, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
 }
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st) {
   hipLaunchKernelGGL(k_film_src, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);

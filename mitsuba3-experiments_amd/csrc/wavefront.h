@@ -66,6 +66,13 @@ struct WaveBuffers {
   uint32_t *counters;   // per bounce b: [4b+0] rays, [4b+1] shadow rays, [4b+2] ray fetch, [4b+3] shadow fetch
   unsigned long long *stats;  // nodes_c, tris_c, nodes_s, tris_s, rays_c, rays_s
   uint32_t capacity;
+  // PSSMLT chain state (pssmlt.py:196-200): offset.xy, cumulative weight | L | proposed offset,
+  // and the current / proposed path vertices (PathVert.wo, depth-major: [depth * capacity + chain]).
+  float4 *mlt_cur;
+  float4 *mlt_L;
+  float2 *mlt_prop;
+  float4 *vpath;
+  float4 *vprop;
 };
 
 struct ChunkParams {
@@ -77,6 +84,7 @@ struct ChunkParams {
   uint32_t n_paths;
   float nrc_c;
   uint32_t stats;
+  uint32_t large_step;  // PSSMLT: i % 50 == 0 (pssmlt.py:209)
 };
 
 // -------- launch wrappers (kernels.hip) --------
@@ -92,6 +100,10 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
                         hipStream_t st);
+void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
+void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
+void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
+void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st);
 void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any_hit, uint32_t *hits,
                       uint32_t *visits, hipStream_t st);

@@ -12,6 +12,7 @@ from .integrators import (  # noqa: F401
     NRCIntegrator,
     Path,
     PathIntegrator,
+    PssmltSimple,
     develop,
     load_dict,
     register_integrator,

@@ -125,6 +125,8 @@ class RenderArgs(C.Structure):
         ("chunk_paths", C.c_uint32),
         ("nrc_c", C.c_float),
         ("flags", C.c_uint32),
+        ("iterations", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
 

@@ -87,6 +87,7 @@ class SamplingIntegrator:
         a.chunk_paths = int(chunk_paths)
         a.nrc_c = float(getattr(self, "c", 0.01))
         a.flags = int(flags)
+        a.iterations = int(getattr(self, "iterations", 0))
         return a
 
     # --------------------------------------------------------------- render --
@@ -175,7 +176,29 @@ class NRCIntegrator(SamplingIntegrator):
         self.rr_depth = 0
 
 
+class PssmltSimple(SamplingIntegrator):
+    """pssmlt.py:96-255 + pssmltsimple.py:11-145 ("pssmlt_simple"): per-pixel
+    primary-sample-space MLT over W*H*spp chains; 200 Metropolis iterations
+    (large step every 50, aggregation when i % 50 > 40, pssmlt.py:206-210),
+    BSDF-only proposals whose local directions are mutated as
+    normalize(0.9 old + 0.1 new) (pssmltsimple.py:135-142). Chains are
+    independent, so multi-GPU sharding is by row bands."""
+
+    integrator_id = _abi.MTX_INT_PSSMLT_SIMPLE
+    name = "pssmlt_simple"
+
+    def __init__(self, props=None):
+        super().__init__(props)
+        self.max_depth = self.props.get("max_depth", 16)  # pssmlt.py:105
+        self.rr_depth = self.props.get("rr_depth", 4)  # pssmlt.py:106
+        self.iterations = self.props.get("iterations", 200)  # pssmlt.py:208
+
+    def sample(self, *args, **kwargs):
+        raise MtxError("PssmltSimple.sample() needs the Metropolis chain state; use render()")
+
+
 register_integrator("mypath", lambda props: Path(props))
+register_integrator("pssmlt_simple", lambda props: PssmltSimple(props))
 register_integrator("path_test", lambda props: PathIntegrator(props))
 register_integrator("nrc", lambda props: NRCIntegrator(props))
 

@@ -46,6 +46,7 @@ def lib():
             "orc_hashgrid": [vp, u64, u32, u32, vp, vp, vp, vp],
             "orc_scatter_reduce_f32": [C.c_int, vp, u64, vp, vp, u64],
             "orc_dmath": [C.c_int, vp, vp, u64],
+            "orc_pssmlt_render": [SD, RA, u32, vp, vp],
         }
         for k, a in sig.items():
             getattr(L, k).argtypes = a
@@ -175,3 +176,13 @@ def warp(op, u):
     L.orc_warp.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64]
     L.orc_warp(ops[op], u.ctypes.data, out.ctypes.data, len(u))
     return out
+
+
+def pssmlt_render(scene, args, iterations=200, chains=False):
+    """Pssmlt.render (pssmlt.py:167-228) for rows [y0, y1): film (+ chain state)."""
+    f = np.zeros((args.y1 - args.y0 + 2, scene.width + 2, 4), np.float32)
+    n = (args.y1 - args.y0) * scene.width * args.spp
+    ch = np.zeros((n, 6), np.float32) if chains else None
+    d = scene.desc()
+    lib().orc_pssmlt_render(C.byref(d), C.byref(args), iterations, f.ctypes.data, ch.ctypes.data if chains else None)
+    return (f, ch) if chains else f

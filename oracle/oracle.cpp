@@ -393,6 +393,57 @@ V3 orc_nrc(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, float c,
   return L;
 }
 
+// Dr.Jit clamp(x, lo, hi) = maximum(minimum(x, hi), lo) with NaN-ignoring
+// minimum/maximum: clamp(NaN, 0, 1) = 1.
+inline float dr_clamp(float x, float lo, float hi) { return fmaxf(fminf(x, hi), lo); }
+
+// ----------------------- pssmltsimple.py:16-133 ----------------------------
+// One proposal of a chain: BSDF-only tracer (no NEE, no MIS); the local BSDF
+// direction of every bounce is mutated against the current path's vertex
+// (mutate, :135-142) and written to the proposed vertex buffer.
+V3 orc_pssmlt_sample(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_t rr_depth, bool large_step,
+                     const V3 *path_v, V3 *prop_v) {
+  V3 f = v3s(1.f), L = v3s(0.f);
+  float eta = 1.f;
+  uint32_t depth = 0;
+  float prev_bsdf_pdf = 1.f;
+  bool active = true;
+  while (active) {
+    SurfaceInteraction si = intersect(s, ray);  // :62-64
+    V3 le = (prev_bsdf_pdf > 0.f) ? emitter_eval(s, si.emitter, si.wi) : v3s(0.f);
+    L = fma3v(f, le, L);  // :74
+    bool active_next = (depth + 1 < max_depth) && si.valid;  // :76
+    float s1 = rng.next_1d();  // :81-82
+    V2 s2 = rng.next_2d();
+    BSDFSample bs{};
+    V3 w = v3s(0.f);
+    const mtx_material *mat = si.valid ? &s.materials[si.material] : nullptr;
+    if (mat) w = bsdf_sample(s.bsdf, *mat, si.uv, si.wi, s1, s2, &bs);  // :84
+    if (!active_next) w = v3s(0.f);  // sample(..., active_next): weight masked
+    // mutate (:135-142): a = 0.1
+    V3 old = path_v[depth];
+    V3 vwo = large_step ? bs.wo : normalize(old * 0.9f + bs.wo * 0.1f);
+    V3 val = v3s(0.f);
+    float pdf = 0.f;
+    if (mat) bsdf_eval_pdf(s.bsdf, *mat, si.uv, si.wi, vwo, &val, &pdf);  // :93
+    if (pdf <= 0.f) vwo = bs.wo;  // :95
+    if (pdf > 0.f) w = val / pdf;  // :96
+    prop_v[depth] = vwo;  // :99
+    ray = spawn_ray(si.p, si.n, to_world(si.sh, vwo));  // :101
+    f = f * w;
+    eta *= bs.eta;
+    prev_bsdf_pdf = bs.pdf;
+    if (si.valid) depth += 1;  // :121
+    float fmax_ = hmax(f);
+    float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+    bool rr_active = depth >= rr_depth;
+    bool rr_continue = rng.next_1d() < rr_prob;
+    if (rr_active) f = f * rcp(rr_prob);
+    active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
+  }
+  return L;
+}
+
 V3 run_integrator(const SceneView &s, const mtx_render_args &a, Pcg32 &rng, const Ray &ray, bool *valid) {
   switch (a.integrator) {
     case MTX_INT_PATH: return orc_path(s, rng, ray, a.max_depth, a.rr_depth, valid);
@@ -542,6 +593,95 @@ int orc_render(const mtx_scene_desc *d, const mtx_render_args *a, float *film) {
   std::vector<float> L(3 * ns), pos(2 * ns);
   orc_render_samples(d, a, L.data(), pos.data());
   return orc_film(W, a->y0, a->y1, a->spp, L.data(), pos.data(), film);
+}
+
+
+// --------------------------- pssmlt.py:112-228 -----------------------------
+// Pssmlt.render for film rows [y0,y1): chains lane = pixel*spp + s (pssmlt.py
+// :188-193), `iterations` Metropolis steps (200 in the reference, :208) with a
+// large step every 50 (:206-209) and aggregation when i % 50 > 40 (:210).
+// Writes the tent film (fixed order: iteration, then pixel, then chain) and,
+// if chain_out != NULL, the final chain state (Lc.xyz, cw, offset.xy).
+int orc_pssmlt_render(const mtx_scene_desc *d, const mtx_render_args *a, uint32_t iterations, float *film,
+                      float *chain_out) {
+  SceneView s = make_view(d);
+  const uint32_t W = s.camera.width, H = s.camera.height, spp = a->spp, D = a->max_depth;
+  const uint32_t rows = a->y1 - a->y0;
+  const uint64_t npx = (uint64_t)rows * W;
+  std::vector<float> acc(npx * 36, 0.f);
+  const float kSqrt01 = 0.31622776601683794f;
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t p = 0; p < (int64_t)npx; ++p) {
+    const uint32_t y = a->y0 + (uint32_t)(p / W), x = (uint32_t)(p % W);
+    std::vector<V3> path_v((size_t)spp * D, v3s(0.f)), prop_v((size_t)spp * D, v3s(0.f));
+    std::vector<Pcg32> rng(spp);
+    std::vector<V2> off(spp, V2{0.5f, 0.5f});
+    std::vector<V3> Lc(spp, v3s(0.f));
+    std::vector<float> cw(spp, 0.f);
+    for (uint32_t k = 0; k < spp; ++k) rng[k] = sampler_lane(a->seed, (uint32_t)(((uint64_t)y * W + x) * spp + k));
+    float *ac = &acc[36 * (size_t)p];
+    for (uint32_t it = 0; it < iterations; ++it) {
+      const bool large = it % 50 == 0, agg = it % 50 > 40;
+      for (uint32_t k = 0; k < spp; ++k) {
+        Pcg32 &r = rng[k];
+        V2 u = r.next_2d();  // :126
+        V2 po;
+        if (large) {
+          po = u;
+        } else {  // mutate_offset (:245-255)
+          V2 g = square_to_std_normal(u);
+          po = V2{dr_clamp(g.x * kSqrt01 + off[k].x, 0.f, 1.f), dr_clamp(g.y * kSqrt01 + off[k].y, 0.f, 1.f)};
+        }
+        V2 sp = V2{((float)x + po.x) / (float)W, ((float)y + po.y) / (float)H};  // :128
+        Ray ray = camera_ray(s.camera, sp);
+        V3 Lp = orc_pssmlt_sample(s, r, ray, D, a->rr_depth, large, &path_v[(size_t)k * D], &prop_v[(size_t)k * D]);
+        float acc_a = dr_clamp(luminance(Lp) / luminance(Lc[k]), 0.f, 1.f);  // :137
+        bool accept = r.next_1d() < acc_a;                                  // :138-140
+        if (accept) cw[k] = acc_a; else cw[k] += 1.f - acc_a;               // :143-144
+        if (accept) {
+          off[k] = po;
+          Lc[k] = Lp;
+          for (uint32_t dd = 0; dd < D; ++dd) path_v[(size_t)k * D + dd] = prop_v[(size_t)k * D + dd];  // :155-158
+        }
+      }
+      if (agg) {  // block.put(pos, L / cw) at the integer pixel position (:161-165)
+        for (uint32_t k = 0; k < spp; ++k) {
+          V3 res = Lc[k] / cw[k];
+          for (int dy = 0; dy < 3; ++dy) {
+            float wy = fmaxf(0.f, 1.f - fabsf((float)y - ((float)((int)y + dy - 1) + 0.5f)));
+            for (int dx = 0; dx < 3; ++dx) {
+              float wx = fmaxf(0.f, 1.f - fabsf((float)x - ((float)((int)x + dx - 1) + 0.5f)));
+              float w = wx * wy;
+              float *c = ac + 4 * (dy * 3 + dx);
+              c[0] = c[0] + res.x * w;
+              c[1] = c[1] + res.y * w;
+              c[2] = c[2] + res.z * w;
+              c[3] = c[3] + w;
+            }
+          }
+        }
+      }
+    }
+    if (chain_out)
+      for (uint32_t k = 0; k < spp; ++k) {
+        float *o = chain_out + 6 * ((size_t)p * spp + k);
+        o[0] = Lc[k].x; o[1] = Lc[k].y; o[2] = Lc[k].z; o[3] = cw[k]; o[4] = off[k].x; o[5] = off[k].y;
+      }
+  }
+  const uint32_t FW = W + 2, FH = rows + 2;
+  for (int64_t q = 0; q < (int64_t)FW * FH; ++q) {
+    int px = (int)(q % FW) - 1, py = (int)(a->y0 + q / FW) - 1;
+    float r = 0.f, g = 0.f, b = 0.f, w = 0.f;
+    for (int dy = 0; dy < 3; ++dy)
+      for (int dx = 0; dx < 3; ++dx) {
+        int sxp = px - dx + 1, syp = py - dy + 1;
+        if (sxp < 0 || sxp >= (int)W || syp < (int)a->y0 || syp >= (int)a->y1) continue;
+        const float *c = &acc[36 * ((size_t)(syp - a->y0) * W + sxp) + 4 * (dy * 3 + dx)];
+        r = r + c[0]; g = g + c[1]; b = b + c[2]; w = w + c[3];
+      }
+    film[4 * q] = r; film[4 * q + 1] = g; film[4 * q + 2] = b; film[4 * q + 3] = w;
+  }
+  return 0;
 }
 
 // ------------------------------- RNG KATs ----------------------------------

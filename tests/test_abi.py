@@ -36,7 +36,7 @@ def test_struct_sizes_match_header():
     assert C.sizeof(_abi.Emitter) == 64
     assert C.sizeof(_abi.Shape) == 16
     assert C.sizeof(_abi.Camera) == 72
-    assert C.sizeof(_abi.RenderArgs) == 48
+    assert C.sizeof(_abi.RenderArgs) == 56
 
 
 def test_ctx_create_without_gpu_fails_cleanly():
