@@ -21,15 +21,19 @@ import math
 
 import numpy as np
 
-PROXY_VERSION = 1
+PROXY_VERSION = 2
 BYTES_PER_TRI = 96
 
 
 def budget_from_lfs(size: int | None, scale: float = 1.0, minimum: int = 2) -> int:
+    """ceil(size / 96 B); scaled-down test scenes keep >= min(full budget, 64)
+    triangles per shape so that closed shapes (walls, boxes) stay closed."""
     if not size:
         return minimum
     b = math.ceil(size / BYTES_PER_TRI)
-    return max(minimum, int(round(b * scale)))
+    if scale == 1.0:
+        return max(minimum, b)
+    return max(minimum, min(b, 64), int(round(b * scale)))
 
 
 class MeshBuilder:
@@ -79,32 +83,60 @@ def param_patch(mb: MeshBuilder, fn, ntri: int, aspect: float = 1.0, uv_scale=(1
     if ntri <= 0:
         return
     C, R, rem = _grid_dims(ntri, aspect)
-    extra_q = (rem + 1) // 2
-    rows = R + (1 if rem > 0 else 0)
+    if R == 0:  # a single triangle
+        C, R, rem = 1, 1, ntri - 2
     u = np.linspace(0.0, 1.0, C + 1)
-    v = np.linspace(0.0, 1.0, rows + 1)
-    U, V = np.meshgrid(u, v)  # [rows+1, C+1]
-    P = fn(U, V)
-    eps = 1e-5
-    du = fn(np.clip(U + eps, 0, 1), V) - fn(np.clip(U - eps, 0, 1), V)
-    dv = fn(U, np.clip(V + eps, 0, 1)) - fn(U, np.clip(V - eps, 0, 1))
-    N = np.cross(du, dv)
-    ln = np.linalg.norm(N, axis=-1, keepdims=True)
-    N = np.where(ln > 1e-20, N / np.maximum(ln, 1e-30), np.array([0.0, 1.0, 0.0]))
-    idx = np.arange((rows + 1) * (C + 1)).reshape(rows + 1, C + 1)
+    v = np.linspace(0.0, 1.0, R + 1)
+    U, V = np.meshgrid(u, v)  # [R+1, C+1]
+    idx = np.arange((R + 1) * (C + 1)).reshape(R + 1, C + 1)
     a = idx[:R, :C].ravel()
     b = idx[:R, 1:].ravel()
     c = idx[1:R + 1, 1:].ravel()
     d = idx[1:R + 1, :C].ravel()
-    F = [np.stack([a, b, c], 1), np.stack([a, c, d], 1)]
-    F = np.concatenate([F[0].reshape(-1, 1, 3), F[1].reshape(-1, 1, 3)], 1).reshape(-1, 3)
-    if rem > 0:
-        j = np.arange(extra_q)
-        a2, b2, c2, d2 = idx[R, j], idx[R, j + 1], idx[R + 1, j + 1], idx[R + 1, j]
-        ex = np.concatenate([np.stack([a2, b2, c2], 1).reshape(-1, 1, 3),
-                             np.stack([a2, c2, d2], 1).reshape(-1, 1, 3)], 1).reshape(-1, 3)
-        F = np.concatenate([F, ex[:rem]])
-    UV = np.stack([U * uv_scale[0], V * uv_scale[1]], -1)
+    F = np.concatenate([np.stack([a, b, c], 1).reshape(-1, 1, 3), np.stack([a, c, d], 1).reshape(-1, 1, 3)],
+                       1).reshape(-1, 3)
+    Uf, Vf = U.ravel(), V.ravel()
+    if rem < 0:  # fewer triangles than one quad: keep the first
+        F = F[:ntri]
+    elif rem > 0:
+        # Exact budget without holes: split (rem // 2) triangles at their
+        # parametric centroid (1 -> 3) and, for an odd remainder, one
+        # triangle at the midpoint of its edge on the v = 0 boundary (1 -> 2).
+        extra_u, extra_v, newF, drop = [], [], [], []
+        nv = len(Uf)
+        bt = 2 * (C - 1)  # first triangle of the last quad of row 0: edge (a, b) lies on v = 0
+        if rem % 2:
+            ta, tb, tc = F[bt]
+            extra_u.append(0.5 * (Uf[ta] + Uf[tb]))
+            extra_v.append(0.0)
+            newF += [(ta, nv, tc), (nv, tb, tc)]
+            drop.append(bt)
+            nv += 1
+        k = 0
+        t = 0
+        while k < rem // 2:
+            if t != bt or rem % 2 == 0:
+                ta, tb, tc = F[t]
+                extra_u.append((Uf[ta] + Uf[tb] + Uf[tc]) / 3.0)
+                extra_v.append((Vf[ta] + Vf[tb] + Vf[tc]) / 3.0)
+                newF += [(ta, tb, nv), (tb, tc, nv), (tc, ta, nv)]
+                drop.append(t)
+                nv += 1
+                k += 1
+            t += 1
+        keep = np.ones(len(F), bool)
+        keep[drop] = False
+        F = np.concatenate([F[keep], np.array(newF, np.int64)])
+        Uf = np.concatenate([Uf, extra_u])
+        Vf = np.concatenate([Vf, extra_v])
+    P = fn(Uf, Vf)
+    eps = 1e-5
+    du = fn(np.clip(Uf + eps, 0, 1), Vf) - fn(np.clip(Uf - eps, 0, 1), Vf)
+    dv = fn(Uf, np.clip(Vf + eps, 0, 1)) - fn(Uf, np.clip(Vf - eps, 0, 1))
+    N = np.cross(du, dv)
+    ln = np.linalg.norm(N, axis=-1, keepdims=True)
+    N = np.where(ln > 1e-20, N / np.maximum(ln, 1e-30), np.array([0.0, 1.0, 0.0]))
+    UV = np.stack([Uf * uv_scale[0], Vf * uv_scale[1]], -1)
     mb.add(P.reshape(-1, 3), N.reshape(-1, 3), UV.reshape(-1, 2), F.astype(np.int64))
 
 
