@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MTX_ABI_VERSION 1
+#define MTX_ABI_VERSION 2
 
 enum {
   MTX_OK = 0,
@@ -104,6 +104,8 @@ typedef struct mtx_camera {
   float tan_x, tan_y; /* tan(fov_x/2), tan(fov_x/2) / aspect */
   float near_clip, far_clip;
   uint32_t width, height;
+  float inv_rows[9];  /* rows of inverse([axis_x axis_y axis_z]) (world -> camera) */
+  uint32_t pad;
 } mtx_camera;
 
 /* BVH2 node (64 B): bounds of both children, Aila-Laine layout.
@@ -162,8 +164,22 @@ typedef struct mtx_render_args {
   float nrc_c;           /* NRC spread threshold (nrc.py:123) */
   uint32_t flags;        /* bit0: collect traversal stats, bit1: per-kernel HIP event timing */
   uint32_t iterations;   /* PSSMLT Metropolis iterations (pssmlt.py:208: 200; 0 = 200) */
+  uint32_t frame;        /* ReSTIR GI frame index (restirgi.py self.n); 0 resets the reservoirs */
+  /* ReSTIR GI properties (restirgi.py:157-166) */
+  uint32_t restir_flags; /* bit0 bias_correction, bit1 jacobian, bit2 bsdf_sampling, bit3 spatial_spatial_reuse */
+  uint32_t max_M_temporal; /* 0 = None */
+  uint32_t max_M_spatial;  /* 0 = None */
+  float initial_search_radius;
+  float minimal_search_radius;
   uint32_t reserved;
 } mtx_render_args;
+
+enum {
+  MTX_RESTIR_BIAS_CORRECTION = 1,
+  MTX_RESTIR_JACOBIAN = 2,
+  MTX_RESTIR_BSDF_SAMPLING = 4,
+  MTX_RESTIR_SPATIAL_SPATIAL = 8
+};
 
 /* Device-side counters, filled when mtx_render_args.flags has bit0/bit1. */
 typedef struct mtx_stats {
@@ -206,10 +222,25 @@ int mtx_scene_upload(mtx_ctx *ctx, const mtx_scene_desc *scene);
  * when film_on_device != 0): un-normalised RGB*weight and weight sums in a
  * fixed summation order. Replaces mi.render(scene, integrator, spp, seed)
  * driving SamplingIntegrator::render (transcribed path.py:103-192) with the
- * sample() of path.py:194-302 / path-mis.py:24-155 / nrc.py:104-125, and
- * Pssmlt.render (pssmlt.py:167-228). */
+ * sample() of path.py:194-302 / path-mis.py:24-155 / nrc.py:104-125,
+ * Pssmlt.render (pssmlt.py:167-228), and one RestirIntegrator.render frame
+ * (restirgi.py:182-258; whole film only, y0 = 0, y1 = height, spp_total =
+ * spp; args.frame = 0 resets the reservoirs kept in ctx, later frames reuse
+ * them and the camera of the previous frame as prev_sensor). */
 int mtx_render(mtx_ctx *ctx, const mtx_render_args *args, float *film_rgbw, int film_on_device,
                mtx_stats *stats);
+
+/* Replace the sensor of the uploaded scene (mi.traverse(sensor).update,
+ * test-restir-dynamic.py; restirgi.py:247 keeps the old one as prev_sensor
+ * for the next ReSTIR frame). The film size must not change. */
+int mtx_set_camera(mtx_ctx *ctx, const mtx_camera *camera);
+
+/* Read back ReSTIR GI frame state (test / debugging hook for restirgi.py's
+ * self.sample, temporal_reservoir, spatial_reservoir, search_radius):
+ * which = 0 samples (5 float4 planes), 1 temporal reservoirs (6 planes),
+ * 2 spatial reservoirs (6 planes), 3 search radius (1 float per lane);
+ * layout in include/mtx_core/restir.h. n_floats must match exactly. */
+int mtx_restir_state(mtx_ctx *ctx, int which, float *out, uint64_t n_floats);
 
 /* Evaluate the integrator's sample() for n given rays (replaces
  * SamplingIntegrator.sample(scene, sampler, ray), path-mis.py:24-31).

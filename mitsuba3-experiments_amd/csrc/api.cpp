@@ -95,6 +95,11 @@ struct mtx_ctx {
   uint32_t capacity = 0;
   DevBuf mlt_cur, mlt_L, mlt_prop, vpath, vprop;  // PSSMLT chain state
   uint32_t mlt_capacity = 0, mlt_depth = 0;
+  // ReSTIR GI frame state (restirgi.py:217-226): kept across mtx_render calls
+  DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM;
+  uint32_t rs_n = 0, rs_cur = 0;
+  bool rs_valid = false;
+  mtx_camera rs_prev_cam{};
   // film
   DevBuf contrib, film;
   // scratch for sample_rays / trace / primitives
@@ -153,6 +158,8 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
+                    &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
+                    &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
@@ -337,7 +344,7 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
     return MTX_E_NOSCENE;
   }
   if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC &&
-      a->integrator != MTX_INT_PSSMLT_SIMPLE) {
+      a->integrator != MTX_INT_PSSMLT_SIMPLE && a->integrator != MTX_INT_RESTIR_GI) {
     mtx_set_error("integrator %u is not supported by this entry point", a->integrator);
     return MTX_E_UNSUPPORTED;
   }
@@ -415,6 +422,144 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
   }
 }
 
+int ensure_restir(mtx_ctx *c, uint32_t n) {
+  int rc;
+  if (c->rs_n != n) {
+    c->rs_valid = false;
+    const size_t N = n;
+    for (int k = 0; k < 2; ++k)
+      if ((rc = dalloc(c->rs_samp[k], 5 * 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_tres, 6 * 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_sres, 6 * 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_radius, 4 * N))) return rc;
+    if ((rc = dalloc(c->rs_hit, 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_dir, 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_emit, 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_rng, 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_rays, 9 * 32 * N))) return rc;
+    if ((rc = dalloc(c->rs_count, 16))) return rc;
+    if ((rc = dalloc(c->rs_occ, 18 * N))) return rc;
+    if ((rc = dalloc(c->rs_qM, 10 * 4 * N))) return rc;
+    c->rs_n = n;
+  }
+  return MTX_OK;
+}
+
+// One RestirIntegrator.render() frame (restirgi.py:182-258) over the whole
+// film; the kernel sequence is documented in restir.hip.
+int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer &tm, uint64_t *n_trace,
+                  uint64_t *n_shadow) {
+  const mtx_camera &cam = c->scene.camera;
+  const uint32_t W = cam.width, H = cam.height, spp = a->spp;
+  if (a->y0 != 0 || a->y1 != H || a->sample_offset != 0 || a->spp_total != spp) {
+    mtx_set_error("mtx_render: ReSTIR GI renders whole frames (y0=0, y1=height, spp_total=spp, offset 0)");
+    return MTX_E_ARG;
+  }
+  const uint64_t n64 = (uint64_t)W * H * spp;
+  if (n64 * 18 >= (1ull << 32)) {
+    mtx_set_error("mtx_render: ReSTIR GI frame too large (%llu lanes)", (unsigned long long)n64);
+    return MTX_E_ARG;
+  }
+  const uint32_t n = (uint32_t)n64;
+  const uint32_t depth = std::max<uint32_t>(a->max_depth, 1);
+  int rc;
+  if ((rc = ensure_wavefront(c, n, depth))) return rc;
+  if ((rc = ensure_restir(c, n))) return rc;
+  if (a->frame != 0 && !c->rs_valid) {
+    mtx_set_error("mtx_render: ReSTIR GI frame %u without the state of frame 0 (film size or scene changed?)",
+                  a->frame);
+    return MTX_E_ARG;
+  }
+  hipStream_t st = c->stream;
+  if (a->frame == 0) {  // restirgi.py:217-229
+    HIP_TRY(hipMemsetAsync(c->rs_tres.p, 0, 6 * 16 * (size_t)n, st));
+    HIP_TRY(hipMemsetAsync(c->rs_sres.p, 0, 6 * 16 * (size_t)n, st));
+    uint32_t bits;
+    memcpy(&bits, &a->initial_search_radius, 4);
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->rs_radius.p, (int)bits, n, st));
+    c->rs_prev_cam = cam;
+    c->rs_cur = 0;
+  }
+  mtxd::WaveBuffers b = buffers(c);
+  mtxd::RestirBuffers r{};
+  r.cur = (float4 *)c->rs_samp[c->rs_cur].p;
+  r.prev = a->frame == 0 ? r.cur : (const float4 *)c->rs_samp[c->rs_cur ^ 1].p;
+  r.tres = (float4 *)c->rs_tres.p;
+  r.sres = (float4 *)c->rs_sres.p;
+  r.radius = (float *)c->rs_radius.p;
+  r.prim_hit = (float4 *)c->rs_hit.p;
+  r.prim_dir = (float4 *)c->rs_dir.p;
+  r.emit = (float4 *)c->rs_emit.p;
+  r.rng = (uint4 *)c->rs_rng.p;
+  r.test_rays = (float4 *)c->rs_rays.p;
+  r.test_count = (uint32_t *)c->rs_count.p;
+  r.occ = (uint8_t *)c->rs_occ.p;
+  r.qM = (uint32_t *)c->rs_qM.p;
+  r.n = n;
+  r.prev_cam = c->rs_prev_cam;
+  r.flags = a->restir_flags;
+  r.max_M_temporal = a->max_M_temporal;
+  r.max_M_spatial = a->max_M_spatial;
+  r.initial_radius = a->initial_search_radius;
+  r.minimal_radius = a->minimal_search_radius;
+  r.frame = a->frame;
+  b.rs_xs = r.cur + 2 * (size_t)n;
+  b.rs_ns = r.cur + 3 * (size_t)n;
+
+  mtxd::ChunkParams p{};
+  p.integrator = MTX_INT_RESTIR_GI;
+  p.max_depth = a->max_depth;
+  p.rr_depth = a->rr_depth;
+  p.seed = a->seed;
+  p.spp = spp;
+  p.spp_total = spp;
+  p.width = W;
+  p.height = H;
+  p.px0 = 0;
+  p.n_px = W * H;
+  p.band_y0 = 0;
+  p.n_paths = n;
+  p.restir = 1;
+  const size_t cbytes = 16ull * (depth + 2);
+  // sample_initial: primary rays and their closest hits
+  HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
+  mtxd::launch_raygen_camera(c->scene, b, p, st);
+  hipEvent_t e = tm.begin(0);
+  mtxd::launch_trace_closest(c->scene, b, 0, 0, c->trace_grid, st);
+  tm.end(0, e);
+  ++*n_trace;
+  HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
+  mtxd::launch_restir_begin(c->scene, b, p, r, st);
+  run_bounces(c, b, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
+  mtxd::launch_restir_collect(b, p, r, st);
+  mtxd::launch_restir_temporal(r, p, st);
+  // spatial_resampling
+  HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
+  mtxd::launch_restir_spatial_rays(r, p, st);
+  e = tm.begin(1);
+  mtxd::launch_trace_test(c->scene, r, 0, c->trace_grid, st);
+  tm.end(1, e);
+  ++*n_shadow;
+  HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
+  mtxd::launch_restir_spatial_merge(r, p, st);
+  if (a->restir_flags & MTX_RESTIR_BIAS_CORRECTION) {
+    e = tm.begin(1);
+    mtxd::launch_trace_test(c->scene, r, 9 * n, c->trace_grid, st);
+    tm.end(1, e);
+    ++*n_shadow;
+    mtxd::launch_restir_bias_finish(r, p, st);
+  }
+  mtxd::launch_restir_final(c->scene, b, p, r, st);
+  mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, st);
+  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, 0, H, st);
+  HIP_TRY(hipGetLastError());
+  // restirgi.py:245-247: prev_sensor <- sensor, prev_sample <- sample
+  c->rs_prev_cam = cam;
+  c->rs_cur ^= 1;
+  c->rs_valid = true;
+  return MTX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -448,6 +593,28 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   }
   const bool want_stats = stats && (a->flags & 1u);
   Timer tm{c, stats && (a->flags & 2u)};
+  if (a->integrator == MTX_INT_RESTIR_GI) {
+    hipEvent_t e_all = tm.begin(3);
+    uint64_t n_trace = 0, n_shadow = 0;
+    if ((rc = render_restir(c, a, film_dev, tm, &n_trace, &n_shadow))) return rc;
+    tm.end(3, e_all);
+    if (!film_on_device)
+      HIP_TRY(hipMemcpyAsync(film_rgbw, film_dev, film_floats * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (stats) {
+      memset(stats, 0, sizeof(*stats));
+      stats->trace_launches = n_trace;
+      stats->shadow_launches = n_shadow;
+      stats->paths = (uint64_t)W * H * a->spp;
+      if (tm.on) {
+        stats->trace_ms = tm.total(0);
+        stats->shadow_ms = tm.total(1);
+        stats->shade_ms = tm.total(2);
+        stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms;
+      }
+    }
+    return MTX_OK;
+  }
   if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
     if (a->sample_offset != 0 || a->spp_total != a->spp) {
       mtx_set_error("mtx_render: PSSMLT chains cannot be split by sample range (use row bands)");
@@ -528,12 +695,61 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   return MTX_OK;
 }
 
+int mtx_set_camera(mtx_ctx *c, const mtx_camera *cam) {
+  if (!c || !cam) {
+    mtx_set_error("mtx_set_camera: null argument");
+    return MTX_E_ARG;
+  }
+  if (!c->has_scene) {
+    mtx_set_error("no scene uploaded");
+    return MTX_E_NOSCENE;
+  }
+  if (cam->width != c->scene.camera.width || cam->height != c->scene.camera.height) {
+    mtx_set_error("mtx_set_camera: film size changed (%ux%u -> %ux%u)", c->scene.camera.width,
+                  c->scene.camera.height, cam->width, cam->height);
+    return MTX_E_ARG;
+  }
+  c->scene.camera = *cam;
+  return MTX_OK;
+}
+
+int mtx_restir_state(mtx_ctx *c, int which, float *out, uint64_t n_floats) {
+  if (!c || !out) {
+    mtx_set_error("mtx_restir_state: null argument");
+    return MTX_E_ARG;
+  }
+  if (!c->rs_valid) {
+    mtx_set_error("mtx_restir_state: no ReSTIR GI frame rendered");
+    return MTX_E_ARG;
+  }
+  const uint64_t n = c->rs_n;
+  const void *src = nullptr;
+  uint64_t need = 0;
+  switch (which) {
+    case 0: src = c->rs_samp[c->rs_cur ^ 1].p; need = 20 * n; break;  // the frame just rendered
+    case 1: src = c->rs_tres.p; need = 24 * n; break;
+    case 2: src = c->rs_sres.p; need = 24 * n; break;
+    case 3: src = c->rs_radius.p; need = n; break;
+    default:
+      mtx_set_error("mtx_restir_state: which=%d not in 0..3", which);
+      return MTX_E_ARG;
+  }
+  if (n_floats != need) {
+    mtx_set_error("mtx_restir_state: need %llu floats, got %llu", (unsigned long long)need,
+                  (unsigned long long)n_floats);
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpy(out, src, 4 * need, hipMemcpyDeviceToHost));
+  return MTX_OK;
+}
+
 int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const float *rays, const uint32_t *lanes,
                     uint32_t rng_skip, float *L, uint8_t *valid) {
   int rc = check_args(c, a);
   if (rc) return rc;
-  if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
-    mtx_set_error("mtx_sample_rays: PSSMLT is a render-level algorithm (use mtx_render)");
+  if (a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_RESTIR_GI) {
+    mtx_set_error("mtx_sample_rays: PSSMLT / ReSTIR GI are render-level algorithms (use mtx_render)");
     return MTX_E_UNSUPPORTED;
   }
   if (n == 0) return MTX_OK;

@@ -1,0 +1,131 @@
+// device_common.h — device helpers shared by the gfx950 kernel files:
+// scene view, wave64 stream compaction, and the BVH2 traversal whose child
+// order and tie-breaking match oracle/oracle.cpp:trace_closest exactly.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "mtx_core/bsdf.h"
+#include "mtx_core/geometry.h"
+#include "mtx_core/interaction.h"
+#include "mtx_core/rng.h"
+#include "wavefront.h"
+
+namespace mtxd {
+
+using namespace mtx;
+
+constexpr int kTraceBlock = 128;
+constexpr int kStack = MTX_BVH_MAX_DEPTH + 1;
+constexpr int kShadeBlock = 256;
+
+__device__ __forceinline__ SceneView make_view(const DevScene &s) {
+  SceneView v;
+  v.nodes = reinterpret_cast<const int32_t *>(s.nodes);
+  v.tri_geom = reinterpret_cast<const float *>(s.tri);
+  v.tri_vidx = s.tri_vidx;
+  v.tri_shape = s.tri_shape;
+  v.vpos = s.vpos;
+  v.vnormal = s.vnormal;
+  v.vuv = s.vuv;
+  v.shapes = s.shapes;
+  v.materials = s.materials;
+  v.emitters = s.emitters;
+  v.bsdf.textures = s.textures;
+  v.bsdf.texels = s.texels;
+  v.bsdf.tables = s.tables;
+  v.n_tris = s.n_tris;
+  v.n_emitters = s.n_emitters;
+  v.camera = s.camera;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Wave-level stream compaction: every lane of the wave must call this.
+// Returns the output slot of a lane with pred = true.
+__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
+  const uint64_t mask = __ballot(pred);
+  const uint32_t prefix =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+  const uint32_t total = (uint32_t)__popcll(mask);
+  uint32_t base = 0;
+  if (total) {
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)mask) - 1);
+    if (lane_id() == leader) base = atomicAdd(counter, total);
+    base = __builtin_amdgcn_readlane(base, leader);
+  }
+  return base + prefix;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// BVH2 traversal (shared by closest-hit and any-hit). Child order and
+// tie-breaking match oracle/oracle.cpp:trace_closest exactly.
+// ---------------------------------------------------------------------------
+template <bool ANY>
+__device__ __forceinline__ bool traverse(const DevScene &s, int32_t *stk, const TraceRay &r, float &tbest,
+                                         uint32_t &prim_best, float &bu, float &bv, uint32_t &nv, uint32_t &tv) {
+  int sp = 0;
+  int32_t node = 0;
+  bool hit_any = false;
+  while (true) {
+    if (node >= 0) {
+      const int4 *np = s.nodes + 4 * node;
+      const float4 a = __builtin_bit_cast(float4, np[0]);
+      const float4 b = __builtin_bit_cast(float4, np[1]);
+      const float4 c = __builtin_bit_cast(float4, np[2]);
+      const int4 ch = np[3];
+      ++nv;
+      const float t0 = box_enter(r, a.x, a.y, a.z, a.w, c.x, c.y, tbest);
+      const float t1 = box_enter(r, b.x, b.y, b.z, b.w, c.z, c.w, tbest);
+      const bool h0 = t0 != kInf, h1 = t1 != kInf;
+      if (h0 && h1) {
+        const bool first0 = t0 <= t1;
+        stk[sp * kTraceBlock] = first0 ? ch.y : ch.x;
+        ++sp;
+        node = first0 ? ch.x : ch.y;
+        continue;
+      } else if (h0) {
+        node = ch.x;
+        continue;
+      } else if (h1) {
+        node = ch.y;
+        continue;
+      }
+    } else {
+      uint32_t first, count;
+      leaf_decode(node, &first, &count);
+      for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t prim = first + k;
+        const float4 g0 = s.tri[3 * prim + 0], g1 = s.tri[3 * prim + 1], g2 = s.tri[3 * prim + 2];
+        float t, u, v;
+        ++tv;
+        if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+          if (ANY) {
+            hit_any = true;
+            break;
+          }
+          if (t < tbest || (t == tbest && prim < prim_best)) {
+            tbest = t;
+            prim_best = prim;
+            bu = u;
+            bv = v;
+          }
+        }
+      }
+      if (ANY && hit_any) break;
+    }
+    if (sp == 0) break;
+    --sp;
+    node = stk[sp * kTraceBlock];
+  }
+  return hit_any;
+}
+
+}  // namespace mtxd

@@ -1,0 +1,385 @@
+// restir.hip — gfx950 kernels of one ReSTIR GI frame (restirgi.py:182-588).
+//
+// The reference evaluates a frame as four whole-film phases (sample_initial,
+// temporal_resampling, spatial_resampling, render_final); each phase reads
+// other pixels' results of the previous phase, so each becomes one or more
+// kernels over all W*H*spp lanes:
+//
+//   raygen + trace_closest   primary rays (kernels.hip, bounce 0)
+//   k_rs_begin               emittance, BSDF/hemisphere sample, secondary ray
+//   [trace, shade, shadow]*  the path-mis loop of sample_ray (:459-588) on the
+//                            wavefront machinery; shade bounce 0 records x_s,n_s
+//   k_rs_collect             L_o, sampler state
+//   k_rs_temporal            reprojection into the previous camera, merge
+//   k_rs_spatial_rays        9 neighbour candidates -> visibility test rays
+//   k_trace_test             any-hit traversal of the compacted tests
+//   k_rs_spatial_merge       replays the same draws, merges the neighbours
+//   (k_trace_test, k_rs_bias_finish)   bias correction (:334-348) when enabled
+//   k_rs_final               bsdf.eval * L_o * W + emittance, film position
+//
+// The sampler stream of every lane is consumed in the reference order; the
+// per-lane arithmetic is mtx_core/restir.h, shared with oracle/oracle.cpp.
+#include "device_common.h"
+#include "mtx_core/restir.h"
+
+namespace mtxd {
+
+namespace {
+
+__device__ __forceinline__ RSample ld_sample(const float4 *b, uint32_t n, uint32_t i) {
+  const float4 p0 = b[i], p1 = b[(size_t)n + i], p2 = b[2 * (size_t)n + i], p3 = b[3 * (size_t)n + i],
+               p4 = b[4 * (size_t)n + i];
+  RSample s;
+  s.x_v = V3{p0.x, p0.y, p0.z};
+  s.valid = p0.w != 0.f;
+  s.n_v = V3{p1.x, p1.y, p1.z};
+  s.p_q = p1.w;
+  s.x_s = V3{p2.x, p2.y, p2.z};
+  s.n_s = V3{p3.x, p3.y, p3.z};
+  s.L_o = V3{p4.x, p4.y, p4.z};
+  return s;
+}
+
+__device__ __forceinline__ void st_sample(float4 *b, uint32_t n, uint32_t i, const RSample &s) {
+  b[i] = make_float4(s.x_v.x, s.x_v.y, s.x_v.z, s.valid ? 1.f : 0.f);
+  b[(size_t)n + i] = make_float4(s.n_v.x, s.n_v.y, s.n_v.z, s.p_q);
+  b[2 * (size_t)n + i] = make_float4(s.x_s.x, s.x_s.y, s.x_s.z, 0.f);
+  b[3 * (size_t)n + i] = make_float4(s.n_s.x, s.n_s.y, s.n_s.z, 0.f);
+  b[4 * (size_t)n + i] = make_float4(s.L_o.x, s.L_o.y, s.L_o.z, 0.f);
+}
+
+__device__ __forceinline__ RReservoir ld_res(const float4 *b, uint32_t n, uint32_t i) {
+  RReservoir r;
+  r.z = ld_sample(b, n, i);
+  const float4 p5 = b[5 * (size_t)n + i];
+  r.w = p5.x;
+  r.W = p5.y;
+  r.M = __float_as_uint(p5.z);
+  return r;
+}
+
+__device__ __forceinline__ void st_res(float4 *b, uint32_t n, uint32_t i, const RReservoir &r) {
+  st_sample(b, n, i, r.z);
+  b[5 * (size_t)n + i] = make_float4(r.w, r.W, __uint_as_float(r.M), 0.f);
+}
+
+__device__ __forceinline__ Pcg32 ld_rng(uint4 m) {
+  Pcg32 g;
+  g.state = ((uint64_t)m.y << 32) | (uint64_t)m.x;
+  g.seq = m.z;
+  return g;
+}
+
+__device__ __forceinline__ uint4 st_rng(const Pcg32 &g, uint32_t w) {
+  return make_uint4((uint32_t)g.state, (uint32_t)(g.state >> 32), g.seq, w);
+}
+
+__device__ __forceinline__ float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
+
+}  // namespace
+
+// sample_initial after the primary intersection (:419-448). Lanes with a
+// valid primary hit start the path-mis loop on the secondary ray; the others
+// consume the draws of one missed loop iteration.
+__global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffers r) {
+  const SceneView sv = make_view(s);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool enq = false;
+  if (i < r.n) {
+    const float4 h = b.hit[i], d4 = b.ray_d[i];
+    r.prim_hit[i] = h;
+    r.prim_dir[i] = d4;
+    const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
+    r.emit[i] = f4(emitter_eval(sv, si.emitter, si.wi), 0.f);
+    Pcg32 rng = ld_rng(b.misc[i]);
+    V3 wo;
+    float pdf;
+    if (r.flags & MTX_RESTIR_BSDF_SAMPLING) {
+      const float s1 = rng.next_1d();
+      const V2 s2 = rng.next_2d();
+      BSDFSample bs;
+      bs.wo = v3s(0.f);
+      bs.pdf = 0.f;
+      if (si.valid) bsdf_sample(sv.bsdf, sv.materials[si.material], si.uv, si.wi, s1, s2, &bs);
+      wo = bs.wo;
+      pdf = bs.pdf;
+    } else {
+      wo = square_to_uniform_hemisphere(rng.next_2d());
+      pdf = square_to_uniform_hemisphere_pdf(wo);
+    }
+    const size_t n = r.n;
+    r.cur[i] = si.valid ? f4(si.p, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    r.cur[n + i] = si.valid ? f4(si.n, pdf) : make_float4(0.f, 0.f, 0.f, pdf);
+    if (si.valid) {
+      const Ray nr = spawn_ray(si.p, si.n, to_world(si.sh, wo));
+      b.ray_o[i] = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
+      b.ray_d[i] = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
+      b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+      b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
+      b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      b.misc[i] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
+      enq = true;
+    } else {
+      rng.advance(6);
+      b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);
+      b.misc[i] = st_rng(rng, 0u);
+      r.cur[2 * n + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      r.cur[3 * n + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const uint32_t slot = wave_append(&b.counters[0], enq);
+  if (enq) b.queue[0][slot] = i;
+}
+
+// L_o = select(valid_ray, result, 0) (:588) and the sampler position.
+__global__ void k_rs_collect(WaveBuffers b, ChunkParams p, RestirBuffers r) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r.n) return;
+  const float4 l = b.L[i];
+  const uint4 m = b.misc[i];
+  const bool valid_ray = ((m.w >> 16) & PF_VALID_RAY) != 0;
+  r.cur[4 * (size_t)r.n + i] = valid_ray ? make_float4(l.x, l.y, l.z, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+  r.rng[i] = m;
+}
+
+// temporal_resampling (:365-410)
+__global__ void k_rs_temporal(RestirBuffers r, ChunkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r.n) return;
+  const uint32_t smp = i % p.spp;
+  Pcg32 rng = ld_rng(r.rng[i]);
+  const RSample S = ld_sample(r.cur, r.n, i);
+  float ux = 0.f, uy = 0.f;
+  bool valid = project_prev(r.prev_cam, S.x_v, &ux, &uy);
+  RSample Sprev = rsample_zero();
+  if (valid) Sprev = ld_sample(r.prev, r.n, pixel_index((int64_t)ux, (int64_t)uy, p.width, p.height, p.spp, smp));
+  valid = valid && similar(S, Sprev);
+  const RReservoir R = valid ? ld_res(r.tres, r.n, i) : rres_zero();
+  RReservoir Rn = rres_zero();
+  float phat = p_hat(S.L_o);
+  const float w = S.p_q > 0.f ? phat / S.p_q : 0.f;
+  res_update(Rn, S, w, true, rng.next_1d());
+  res_merge(Rn, R, p_hat(R.z.L_o), true, rng.next_1d());
+  phat = p_hat(Rn.z.L_o);
+  Rn.W = (phat * (float)Rn.M > 0.f) ? Rn.w / ((float)Rn.M * phat) : 0.f;
+  if (r.max_M_temporal) Rn.M = min(Rn.M, r.max_M_temporal);
+  st_res(r.tres, r.n, i, Rn);
+  r.rng[i] = st_rng(rng, 0u);
+}
+
+// Neighbour k of lane i in spatial_resampling (:300-313): the disk offset
+// draw, clamped pixel, candidate similarity. Consumes 2 draws.
+struct Neighbour {
+  uint32_t idx;
+  bool active;
+};
+
+__device__ __forceinline__ Neighbour neighbour(const RestirBuffers &r, const ChunkParams &p, Pcg32 &rng, int k,
+                                               int max_iter, float rad, int64_t x, int64_t y, uint32_t smp,
+                                               const RSample &q) {
+  const V2 d2 = square_to_uniform_disk(rng.next_2d());
+  const V2 off = V2{d2.x * rad, d2.y * rad};
+  Neighbour nb;
+  nb.idx = pixel_index(x + (int32_t)off.x, y + (int32_t)off.y, p.width, p.height, p.spp, smp);
+  const RSample qn = ld_sample(r.cur, r.n, nb.idx);
+  nb.active = (k < max_iter) && similar(qn, q);
+  return nb;
+}
+
+__device__ __forceinline__ int spatial_max_iter(const RestirBuffers &r, uint32_t M) {
+  return (r.max_M_spatial == 0 || (double)M < (double)r.max_M_spatial / 2.0) ? 9 : 3;  // :297
+}
+
+__device__ __forceinline__ void emit_test(const RestirBuffers &r, bool pred, const Ray &ray, uint32_t slot) {
+  const uint32_t o = wave_append(&r.test_count[0], pred);
+  if (pred) {
+    r.test_rays[2 * (size_t)o] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
+    r.test_rays[2 * (size_t)o + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(slot));
+  }
+}
+
+// spatial_resampling, pass 1: the visibility rays of :316-318.
+__global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < r.n;
+  const uint32_t ii = live ? i : 0u;
+  const uint32_t smp = ii % p.spp;
+  const int64_t x = (int64_t)(ii / p.spp % p.width), y = (int64_t)(ii / p.width / p.spp);
+  Pcg32 rng = ld_rng(r.rng[ii]);
+  const uint32_t Ms = __float_as_uint(r.sres[5 * (size_t)r.n + ii].z);
+  if (r.flags & MTX_RESTIR_SPATIAL_SPATIAL) rng.next_1d();  // merge draw (:291-293)
+  const int max_iter = spatial_max_iter(r, Ms);
+  const RSample q = ld_sample(r.cur, r.n, ii);
+  const float rad = r.radius[ii];
+  for (int k = 0; k < 9; ++k) {
+    const Neighbour nb = neighbour(r, p, rng, k, max_iter, rad, x, y, smp, q);
+    const bool act = live && nb.active;
+    Ray ray{v3s(0.f), v3s(0.f), 0.f};
+    if (act) {
+      const float4 xs = r.tres[2 * (size_t)r.n + nb.idx];
+      ray = spawn_ray_to(q.x_v, q.n_v, V3{xs.x, xs.y, xs.z});
+    }
+    emit_test(r, act, ray, 9 * ii + (uint32_t)k);
+    rng.next_1d();  // merge draw (:328)
+  }
+}
+
+// spatial_resampling, pass 2: replays the lane's draws with the visibility
+// results, merges (:320-332), and either finishes W (:350) or emits the
+// bias-correction rays (:334-346).
+__global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = i < r.n;
+  const uint32_t ii = live ? i : 0u;
+  const uint32_t smp = ii % p.spp;
+  const int64_t x = (int64_t)(ii / p.spp % p.width), y = (int64_t)(ii / p.width / p.spp);
+  const bool bias = (r.flags & MTX_RESTIR_BIAS_CORRECTION) != 0;
+  const bool jac = (r.flags & MTX_RESTIR_JACOBIAN) != 0;
+  Pcg32 rng = ld_rng(r.rng[ii]);
+  const RReservoir Rs = ld_res(r.sres, r.n, ii);
+  RReservoir Rn = rres_zero();
+  const RSample q = ld_sample(r.cur, r.n, ii);
+  uint32_t Z = 0;
+  if (r.flags & MTX_RESTIR_SPATIAL_SPATIAL) {
+    res_merge(Rn, Rs, p_hat(Rs.z.L_o), true, rng.next_1d());
+    Z += Rs.M;
+  }
+  const int max_iter = spatial_max_iter(r, Rs.M);
+  const float rad = r.radius[ii];
+  bool any_reused = false;
+  uint32_t qM[9];
+  V3 qp[9];
+  uint32_t qa = 0;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) {
+    const Neighbour nb = neighbour(r, p, rng, k, max_iter, rad, x, y, smp, q);
+    const bool active = nb.active;
+    const RReservoir Rk = active ? ld_res(r.tres, r.n, nb.idx) : rres_zero();
+    const bool shadowed = active && r.occ[9 * (size_t)ii + k] != 0;
+    const float jf = jac ? dr_clampf(jacobian_J(q.x_v, Rk), 0.f, 1000.f) : 1.0f;
+    const float phat = (!active || shadowed) ? 0.f : p_hat(Rk.z.L_o) * jf;
+    res_merge(Rn, Rk, phat, active, rng.next_1d());
+    qM[k] = Rk.M;
+    qp[k] = Rk.z.x_v;
+    qa |= active ? (1u << k) : 0u;
+    any_reused = any_reused || active;
+  }
+  const float phat = p_hat(Rn.z.L_o);
+  if (!bias) Rn.W = (phat * (float)Rn.M > 0.f) ? Rn.w / ((float)Rn.M * phat) : 0.f;
+  if (live) {
+    r.radius[ii] = fmaxf(any_reused ? rad : rad / 2.f, r.minimal_radius);  // :353-356
+    if (!bias && r.max_M_spatial) Rn.M = min(Rn.M, r.max_M_spatial);
+    st_res(r.sres, r.n, ii, Rn);
+  }
+  if (bias) {
+    if (live) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) r.qM[10 * (size_t)ii + k] = qM[k] | (((qa >> k) & 1u) << 31);
+      r.qM[10 * (size_t)ii + 9] = Z;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const bool act = live && ((qa >> k) & 1u);
+      Ray ray{v3s(0.f), v3s(0.f), 0.f};
+      if (act) ray = spawn_ray_to(Rn.z.x_s, Rn.z.n_s, qp[k]);
+      emit_test(r, act, ray, 9 * ii + (uint32_t)k);
+    }
+  }
+}
+
+// bias correction tail (:340-348)
+__global__ void k_rs_bias_finish(RestirBuffers r, ChunkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r.n) return;
+  uint32_t Z = r.qM[10 * (size_t)i + 9];
+  for (int k = 0; k < 9; ++k) {
+    const uint32_t e = r.qM[10 * (size_t)i + k];
+    const bool active = (e >> 31) && r.occ[9 * (size_t)r.n + 9 * (size_t)i + k] == 0;
+    Z += active ? (e & 0x7fffffffu) : 0u;
+  }
+  const float4 lo = r.sres[4 * (size_t)r.n + i];
+  const float phat = p_hat(V3{lo.x, lo.y, lo.z});
+  float4 p5 = r.sres[5 * (size_t)r.n + i];
+  uint32_t M = __float_as_uint(p5.z);
+  p5.y = ((float)Z * phat > 0.f) ? p5.x / ((float)Z * phat) : 0.f;
+  if (r.max_M_spatial) M = min(M, r.max_M_spatial);
+  p5.z = __uint_as_float(M);
+  r.sres[5 * (size_t)r.n + i] = p5;
+}
+
+// render_final (:261-272) and the block.put position (:236-242)
+__global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffers r) {
+  const SceneView sv = make_view(s);
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= r.n) return;
+  const RReservoir R = ld_res(r.sres, r.n, i);
+  const float4 h = r.prim_hit[i], d4 = r.prim_dir[i];
+  const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
+  V3 beta = v3s(0.f);
+  if (si.valid) {
+    float pdf_unused;
+    const V3 wo = to_local(si.sh, normalize(R.z.x_s - si.p));
+    bsdf_eval_pdf(sv.bsdf, sv.materials[si.material], si.uv, si.wi, wo, &beta, &pdf_unused);
+  }
+  const float4 em = r.emit[i];
+  const V3 res = beta * R.z.L_o * R.W + V3{em.x, em.y, em.z};
+  b.L[i] = make_float4(res.x, res.y, res.z, 0.f);
+  const uint32_t x = i / p.spp % p.width, y = i / p.width / p.spp;
+  b.pos[i] = make_float2((float)x, (float)y);
+}
+
+// Any-hit traversal of the compacted visibility tests; occ[base + slot].
+__global__ __launch_bounds__(kTraceBlock) void k_trace_test(DevScene s, RestirBuffers r, uint32_t occ_base) {
+  __shared__ int32_t stack[kStack * kTraceBlock];
+  int32_t *stk = stack + threadIdx.x;
+  const uint32_t count = r.test_count[0];
+  uint32_t *fetch = &r.test_count[1];
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t nv = 0, tv = 0;
+  while (true) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(fetch, 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= count) break;
+    const uint32_t k = base + lane;
+    if (k < count) {
+      const float4 o4 = r.test_rays[2 * (size_t)k], d4 = r.test_rays[2 * (size_t)k + 1];
+      TraceRay tr = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+      float tbest = o4.w, bu, bv;
+      uint32_t prim = 0xffffffffu;
+      const bool occluded = traverse<true>(s, stk, tr, tbest, prim, bu, bv, nv, tv);
+      r.occ[occ_base + __float_as_uint(d4.w)] = occluded ? 1 : 0;
+    }
+  }
+}
+
+static inline unsigned rs_blocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+void launch_restir_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_begin, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, s, b, p, r);
+}
+void launch_restir_collect(const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r, hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_collect, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, b, p, r);
+}
+void launch_restir_temporal(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_temporal, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+}
+void launch_restir_spatial_rays(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_spatial_rays, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+}
+void launch_restir_spatial_merge(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_spatial_merge, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+}
+void launch_restir_bias_finish(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_bias_finish, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+}
+void launch_restir_final(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k_rs_final, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, s, b, p, r);
+}
+void launch_trace_test(const DevScene &s, const RestirBuffers &r, uint32_t occ_base, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), 0, st, s, r, occ_base);
+}
+
+}  // namespace mtxd

@@ -73,6 +73,33 @@ struct WaveBuffers {
   float2 *mlt_prop;
   float4 *vpath;
   float4 *vprop;
+  // ReSTIR GI: first hit of the secondary path (restirgi.py:452-455), written
+  // by the bounce-0 shade into the current sample planes 2 and 3.
+  float4 *rs_xs;
+  float4 *rs_ns;
+};
+
+// ReSTIR GI frame state (restirgi.py:217-226, 230-231). Sample / reservoir
+// planes as in mtx_core/restir.h; `n` = W*H*spp lanes of one frame.
+struct RestirBuffers {
+  float4 *cur;        // 5 planes: this frame's samples
+  const float4 *prev; // 5 planes: previous frame's samples (== cur at frame 0)
+  float4 *tres;       // 6 planes: temporal reservoirs
+  float4 *sres;       // 6 planes: spatial reservoirs
+  float *radius;      // search radius per lane
+  float4 *prim_hit;   // primary closest hit (t, prim, u, v)
+  float4 *prim_dir;   // primary ray direction
+  float4 *emit;       // emittance at the primary hit (:421-423)
+  uint4 *rng;         // sampler state between the phases
+  float4 *test_rays;  // compacted visibility tests: (o, maxt), (d, slot)
+  uint32_t *test_count;  // [0] count, [1] fetch cursor
+  uint8_t *occ;       // 18 per lane: spatial tests [0,9), bias-correction tests [9,18)
+  uint32_t *qM;       // 10 per lane: Q.M with bit 31 = active, [9] = Z before the loop
+  uint32_t n;
+  mtx_camera prev_cam;
+  uint32_t flags, max_M_temporal, max_M_spatial;
+  float initial_radius, minimal_radius;
+  uint32_t frame;
 };
 
 struct ChunkParams {
@@ -85,6 +112,7 @@ struct ChunkParams {
   float nrc_c;
   uint32_t stats;
   uint32_t large_step;  // PSSMLT: i % 50 == 0 (pssmlt.py:209)
+  uint32_t restir;      // ReSTIR GI secondary paths (path-mis loop, restirgi.py:459-588)
 };
 
 // -------- launch wrappers (kernels.hip) --------
@@ -105,6 +133,17 @@ void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams
 void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st);
+// ReSTIR GI (restir.hip)
+void launch_restir_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
+                         hipStream_t st);
+void launch_restir_collect(const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r, hipStream_t st);
+void launch_restir_temporal(const RestirBuffers &r, const ChunkParams &p, hipStream_t st);
+void launch_restir_spatial_rays(const RestirBuffers &r, const ChunkParams &p, hipStream_t st);
+void launch_restir_spatial_merge(const RestirBuffers &r, const ChunkParams &p, hipStream_t st);
+void launch_restir_bias_finish(const RestirBuffers &r, const ChunkParams &p, hipStream_t st);
+void launch_restir_final(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
+                         hipStream_t st);
+void launch_trace_test(const DevScene &s, const RestirBuffers &r, uint32_t occ_base, int grid, hipStream_t st);
 void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any_hit, uint32_t *hits,
                       uint32_t *visits, hipStream_t st);
 

@@ -13,6 +13,7 @@ from .integrators import (  # noqa: F401
     Path,
     PathIntegrator,
     PssmltSimple,
+    RestirIntegrator,
     develop,
     load_dict,
     register_integrator,

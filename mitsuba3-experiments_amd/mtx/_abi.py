@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 1
+MTX_ABI_VERSION = 2
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -22,6 +22,11 @@ MTX_INT_PATH_MIS = 2
 MTX_INT_NRC = 3
 MTX_INT_PSSMLT_SIMPLE = 4
 MTX_INT_RESTIR_GI = 5
+
+MTX_RESTIR_BIAS_CORRECTION = 1
+MTX_RESTIR_JACOBIAN = 2
+MTX_RESTIR_BSDF_SAMPLING = 4
+MTX_RESTIR_SPATIAL_SPATIAL = 8
 
 MTX_ROUGH_TRANSMITTANCE_RES = 64
 MTX_BVH_MAX_LEAF = 8
@@ -78,6 +83,8 @@ class Camera(C.Structure):
         ("far_clip", C.c_float),
         ("width", C.c_uint32),
         ("height", C.c_uint32),
+        ("inv_rows", C.c_float * 9),
+        ("pad", C.c_uint32),
     ]
 
 
@@ -126,6 +133,12 @@ class RenderArgs(C.Structure):
         ("nrc_c", C.c_float),
         ("flags", C.c_uint32),
         ("iterations", C.c_uint32),
+        ("frame", C.c_uint32),
+        ("restir_flags", C.c_uint32),
+        ("max_M_temporal", C.c_uint32),
+        ("max_M_spatial", C.c_uint32),
+        ("initial_search_radius", C.c_float),
+        ("minimal_search_radius", C.c_float),
         ("reserved", C.c_uint32),
     ]
 
@@ -161,6 +174,8 @@ EXPORTS = [
     "mtx_roughplastic_tables",
     "mtx_scene_upload",
     "mtx_render",
+    "mtx_set_camera",
+    "mtx_restir_state",
     "mtx_sample_rays",
     "mtx_trace",
     "mtx_prefix_sum_u32",

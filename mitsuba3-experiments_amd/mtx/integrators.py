@@ -197,6 +197,90 @@ class PssmltSimple(SamplingIntegrator):
         raise MtxError("PssmltSimple.sample() needs the Metropolis chain state; use render()")
 
 
+class RestirIntegrator(SamplingIntegrator):
+    """restirgi.py:151-588 ("restirgi"): ReSTIR GI. Each render() call is one
+    frame: an initial sample per lane (camera hit x_v + a path-mis secondary
+    path giving L_o at x_s), temporal resampling against the previous frame's
+    sample reprojected through the previous camera, spatial resampling of up
+    to 9 neighbours' temporal reservoirs (visibility-tested, optional jacobian
+    and bias correction), then bsdf.eval * L_o * W + emittance splatted at the
+    integer pixel. Reservoirs, the previous samples and the search radii stay
+    in HBM inside the device context between frames.
+
+    Properties and defaults follow restirgi.py:157-166. ``max_M_spatial=None``
+    (the reference default, which raises a TypeError at :297) is treated as
+    "no clamp, always 9 neighbours"."""
+
+    integrator_id = _abi.MTX_INT_RESTIR_GI
+    name = "restirgi"
+
+    def __init__(self, props=None):
+        super().__init__(props)
+        g = self.props.get
+        self.max_depth = g("max_depth", 8)
+        self.rr_depth = g("rr_depth", 2)
+        self.bias_correction = bool(g("bias_correction", True))
+        self.jacobian = bool(g("jacobian", True))
+        self.bsdf_sampling = bool(g("bsdf_sampling", True))
+        self.max_M_temporal = g("max_M_temporal", None)
+        self.max_M_spatial = g("max_M_spatial", None)
+        self.initial_search_radius = float(g("initial_search_radius", 10.0))
+        self.minimal_search_radius = float(g("minimal_search_radius", 3.0))
+        self.spatial_spatial_reuse = bool(g("spatial_spatial_reuse", False))
+        self.n = 0
+        self.film_size = None
+
+    def render_args(self, scene, seed: int, spp: int, *args, **kwargs) -> _abi.RenderArgs:
+        a = super().render_args(scene, seed, spp, *args, **kwargs)
+        a.frame = int(self.n)
+        a.restir_flags = ((_abi.MTX_RESTIR_BIAS_CORRECTION if self.bias_correction else 0)
+                          | (_abi.MTX_RESTIR_JACOBIAN if self.jacobian else 0)
+                          | (_abi.MTX_RESTIR_BSDF_SAMPLING if self.bsdf_sampling else 0)
+                          | (_abi.MTX_RESTIR_SPATIAL_SPATIAL if self.spatial_spatial_reuse else 0))
+        a.max_M_temporal = int(self.max_M_temporal or 0)
+        a.max_M_spatial = int(self.max_M_spatial or 0)
+        a.initial_search_radius = self.initial_search_radius
+        a.minimal_search_radius = self.minimal_search_radius
+        return a
+
+    def render_film(self, scene, seed: int = 0, spp: int = 1, device: int | None = None, out=None,
+                    stats: bool = False, **kwargs):
+        """One frame (restirgi.py:182-258); advances the frame counter."""
+        if kwargs.get("y0", 0) != 0 or kwargs.get("y1") not in (None, scene.height) or kwargs.get("sample_offset", 0):
+            raise MtxError("ReSTIR GI renders whole frames")
+        ctx = context(device)
+        _bind_scene(ctx, scene)
+        size = (scene.width, scene.height, int(spp))
+        if self.film_size is None:
+            self.film_size = size
+        if size != self.film_size:
+            raise MtxError(f"film size / spp changed between frames: {self.film_size} -> {size}")
+        owner = getattr(ctx, "_restir_owner", None)
+        if self.n > 0 and owner is not self:
+            raise MtxError("another ReSTIR integrator rendered on this device since the last frame")
+        ctx._restir_owner = self
+        cam = scene.camera
+        check(lib().mtx_set_camera(ctx.handle, C.byref(cam)), "mtx_set_camera")
+        result = super().render_film(scene, seed=seed, spp=spp, device=device, out=out, stats=stats)
+        self.n += 1  # restirgi.py:245
+        return result
+
+    def state(self, which: str, device: int | None = None) -> np.ndarray:
+        """Device state of the last frame: 'sample' (5 planes x lanes x 4),
+        'temporal' / 'spatial' (6 planes), 'radius' (lanes)."""
+        idx, planes = {"sample": (0, 5), "temporal": (1, 6), "spatial": (2, 6), "radius": (3, 0)}[which]
+        W, H, spp = self.film_size
+        n = W * H * spp
+        shape = (planes, n, 4) if planes else (n,)
+        out = np.zeros(shape, np.float32)
+        check(lib().mtx_restir_state(context(device).handle, idx, out.ctypes.data, out.size), "mtx_restir_state")
+        return out
+
+    def sample(self, *args, **kwargs):
+        raise MtxError("RestirIntegrator.sample() needs the frame's reservoirs; use render()")
+
+
+register_integrator("restirgi", lambda props: RestirIntegrator(props))
 register_integrator("mypath", lambda props: Path(props))
 register_integrator("pssmlt_simple", lambda props: PssmltSimple(props))
 register_integrator("path_test", lambda props: PathIntegrator(props))

@@ -326,6 +326,7 @@ def _camera(sensor: dict, W: int, H: int) -> _abi.Camera:
     cam.near_clip = float(sensor.get("near_clip", 1e-2))
     cam.far_clip = float(sensor.get("far_clip", 1e4))
     cam.width, cam.height = W, H
+    cam.inv_rows[:] = np.linalg.inv(M[:3, :3]).reshape(-1)
     return cam
 
 
@@ -338,7 +339,7 @@ def bedroom(width=None, height=None, scale: float = 1.0, tex_res: int = 512, cac
     if key not in _cache:
         path = None
         if cache_dir:
-            path = os.path.join(cache_dir, f"bedroom_v{proxy.PROXY_VERSION}_s{scale:g}_t{tex_res}.npz")
+            path = os.path.join(cache_dir, f"bedroom_v{proxy.PROXY_VERSION}a{_abi.MTX_ABI_VERSION}_s{scale:g}_t{tex_res}.npz")
         if path and os.path.exists(path):
             _cache[key] = Scene.load(path)
         else:

@@ -47,6 +47,7 @@ def lib():
             "orc_scatter_reduce_f32": [C.c_int, vp, u64, vp, vp, u64],
             "orc_dmath": [C.c_int, vp, vp, u64],
             "orc_pssmlt_render": [SD, RA, u32, vp, vp],
+            "orc_restir_frame": [SD, RA, C.POINTER(_abi.Camera), vp, vp, vp, vp, vp, vp],
         }
         for k, a in sig.items():
             getattr(L, k).argtypes = a
@@ -186,3 +187,32 @@ def pssmlt_render(scene, args, iterations=200, chains=False):
     d = scene.desc()
     lib().orc_pssmlt_render(C.byref(d), C.byref(args), iterations, f.ctypes.data, ch.ctypes.data if chains else None)
     return (f, ch) if chains else f
+
+
+class RestirOracle:
+    """RestirIntegrator (restirgi.py:151-588) frame by frame on the CPU; the
+    state arrays use the device layout (mtx_core/restir.h)."""
+
+    def __init__(self, scene, spp=1):
+        n = scene.width * scene.height * spp
+        self.n = n
+        self.cur = np.zeros((5, n, 4), np.float32)
+        self.prev = np.zeros((5, n, 4), np.float32)
+        self.tres = np.zeros((6, n, 4), np.float32)
+        self.sres = np.zeros((6, n, 4), np.float32)
+        self.radius = np.zeros(n, np.float32)
+        self.prev_cam = None
+
+    def frame(self, scene, args):
+        """One render() call; `args` carries frame, seed and the properties."""
+        if args.frame == 0:
+            self.prev_cam = scene.camera
+        f = np.zeros((scene.height + 2, scene.width + 2, 4), np.float32)
+        d = scene.desc()
+        cam = _abi.Camera.from_buffer_copy(bytes(self.prev_cam))
+        lib().orc_restir_frame(C.byref(d), C.byref(args), C.byref(cam), self.cur.ctypes.data,
+                               self.prev.ctypes.data, self.tres.ctypes.data, self.sres.ctypes.data,
+                               self.radius.ctypes.data, f.ctypes.data)
+        self.prev[...] = self.cur  # restirgi.py:247
+        self.prev_cam = _abi.Camera.from_buffer_copy(bytes(scene.camera))
+        return f

@@ -12,6 +12,8 @@
 //   * nrc.py:25-125        NRCIntegrator.sample       -> orc_nrc()
 //   * path.py:27-192       transcribed SamplingIntegrator.render/render_sample
 //                          (lane -> pixel, film jitter, camera ray, block.put)
+//   * pssmlt.py / pssmltsimple.py Pssmlt.render      -> orc_pssmlt_render()
+//   * restirgi.py:182-457 RestirIntegrator.render    -> orc_restir_frame()
 //   * prefix_sum.py:9-36, hashgrid.py:8-90, reductions.py:12-54
 // The upstream per-lane primitives these loops call (Scene.ray_intersect,
 // BSDF, emitter, sampler) come from include/mtx_core;
@@ -35,6 +37,7 @@
 #include "mtx_core/bsdf.h"
 #include "mtx_core/geometry.h"
 #include "mtx_core/interaction.h"
+#include "mtx_core/restir.h"
 #include "mtx_core/rng.h"
 #include "mtx_core/warp.h"
 
@@ -683,6 +686,244 @@ int orc_pssmlt_render(const mtx_scene_desc *d, const mtx_render_args *a, uint32_
   }
   return 0;
 }
+
+}  // extern "C"
+
+// ------------------------- restirgi.py:182-457 -----------------------------
+// One RestirIntegrator.render() call (one frame) over the whole film, phase by
+// phase exactly as the reference evaluates them: sample_initial (:412-457),
+// temporal_resampling (:365-410), spatial_resampling (:274-363),
+// render_final (:261-272) and block.put at the integer pixel (:236-242).
+// Persistent state (float planes, layout in mtx_core/restir.h) is owned by
+// the caller: cur (5 planes, written), prev (5 planes, read; ignored at frame
+// 0 where prev_sample = sample), tres / sres (6 planes), radius (1 float).
+namespace {
+
+RSample rs_load(const float *b, size_t n, size_t i) {
+  const float *p0 = b + 4 * i, *p1 = b + 4 * (n + i), *p2 = b + 4 * (2 * n + i), *p3 = b + 4 * (3 * n + i),
+              *p4 = b + 4 * (4 * n + i);
+  RSample s;
+  s.x_v = V3{p0[0], p0[1], p0[2]};
+  s.valid = p0[3] != 0.f;
+  s.n_v = V3{p1[0], p1[1], p1[2]};
+  s.p_q = p1[3];
+  s.x_s = V3{p2[0], p2[1], p2[2]};
+  s.n_s = V3{p3[0], p3[1], p3[2]};
+  s.L_o = V3{p4[0], p4[1], p4[2]};
+  return s;
+}
+
+void rs_store(float *b, size_t n, size_t i, const RSample &s) {
+  float *p0 = b + 4 * i, *p1 = b + 4 * (n + i), *p2 = b + 4 * (2 * n + i), *p3 = b + 4 * (3 * n + i),
+        *p4 = b + 4 * (4 * n + i);
+  p0[0] = s.x_v.x; p0[1] = s.x_v.y; p0[2] = s.x_v.z; p0[3] = s.valid ? 1.f : 0.f;
+  p1[0] = s.n_v.x; p1[1] = s.n_v.y; p1[2] = s.n_v.z; p1[3] = s.p_q;
+  p2[0] = s.x_s.x; p2[1] = s.x_s.y; p2[2] = s.x_s.z; p2[3] = 0.f;
+  p3[0] = s.n_s.x; p3[1] = s.n_s.y; p3[2] = s.n_s.z; p3[3] = 0.f;
+  p4[0] = s.L_o.x; p4[1] = s.L_o.y; p4[2] = s.L_o.z; p4[3] = 0.f;
+}
+
+RReservoir rr_load(const float *b, size_t n, size_t i) {
+  RReservoir r;
+  r.z = rs_load(b, n, i);
+  const float *p5 = b + 4 * (5 * n + i);
+  r.w = p5[0];
+  r.W = p5[1];
+  memcpy(&r.M, &p5[2], 4);
+  return r;
+}
+
+void rr_store(float *b, size_t n, size_t i, const RReservoir &r) {
+  rs_store(b, n, i, r.z);
+  float *p5 = b + 4 * (5 * n + i);
+  p5[0] = r.w;
+  p5[1] = r.W;
+  memcpy(&p5[2], &r.M, 4);
+  p5[3] = 0.f;
+}
+
+}  // namespace
+
+extern "C" int orc_restir_frame(const mtx_scene_desc *d, const mtx_render_args *a, const mtx_camera *prev_cam,
+                                float *cur, const float *prev, float *tres, float *sres, float *radius,
+                                float *film) {
+  SceneView s = make_view(d);
+  const uint32_t W = s.camera.width, H = s.camera.height, spp = a->spp;
+  const size_t n = (size_t)W * H * spp;
+  const bool bias = a->restir_flags & MTX_RESTIR_BIAS_CORRECTION;
+  const bool jac = a->restir_flags & MTX_RESTIR_JACOBIAN;
+  const bool bsdf_sampling = a->restir_flags & MTX_RESTIR_BSDF_SAMPLING;
+  const bool ss_reuse = a->restir_flags & MTX_RESTIR_SPATIAL_SPATIAL;
+  if (a->frame == 0) {  // :217-226
+    memset(tres, 0, sizeof(float) * 24 * n);
+    memset(sres, 0, sizeof(float) * 24 * n);
+    for (size_t i = 0; i < n; ++i) radius[i] = a->initial_search_radius;
+    prev = cur;  // :230-231 prev_sample = sample (read after sample_initial)
+  }
+  std::vector<Pcg32> rng(n);
+  std::vector<float> hitrec(4 * n), pdir(3 * n), emit(3 * n);
+
+  // ---- sample_initial (:412-457)
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    const uint32_t x = (uint32_t)(i / spp % W), y = (uint32_t)(i / W / spp);  // :206-208
+    Pcg32 r = sampler_lane(a->seed, (uint32_t)i);
+    const V2 u = r.next_2d();  // :211-213
+    const V2 sp = V2{((float)x + u.x) / (float)W, ((float)y + u.y) / (float)H};
+    const Ray ray = camera_ray(s.camera, sp);
+    const Hit h = trace_closest(s, ray.o, ray.d, ray.maxt, nullptr, nullptr);
+    const SurfaceInteraction si = compute_si(s, h.t, h.prim, h.u, h.v, ray.d);
+    hitrec[4 * i] = h.t;
+    memcpy(&hitrec[4 * i + 1], &h.prim, 4);
+    hitrec[4 * i + 2] = h.u;
+    hitrec[4 * i + 3] = h.v;
+    pdir[3 * i] = ray.d.x; pdir[3 * i + 1] = ray.d.y; pdir[3 * i + 2] = ray.d.z;
+    const V3 em = emitter_eval(s, si.emitter, si.wi);  // :421-423
+    emit[3 * i] = em.x; emit[3 * i + 1] = em.y; emit[3 * i + 2] = em.z;
+    RSample S = rsample_zero();
+    S.valid = si.valid;
+    if (si.valid) {
+      S.x_v = si.p;
+      S.n_v = si.n;
+    }
+    V3 wo;
+    float pdf;
+    if (bsdf_sampling) {  // :431-438
+      const float s1 = r.next_1d();
+      const V2 s2 = r.next_2d();
+      BSDFSample bs;
+      bs.wo = v3s(0.f);
+      bs.pdf = 0.f;
+      if (si.valid) bsdf_sample(s.bsdf, s.materials[si.material], si.uv, si.wi, s1, s2, &bs);
+      wo = bs.wo;
+      pdf = bs.pdf;
+    } else {  // :440-444
+      wo = square_to_uniform_hemisphere(r.next_2d());
+      pdf = square_to_uniform_hemisphere_pdf(wo);
+    }
+    S.p_q = pdf;
+    if (si.valid) {
+      const Ray ray2 = spawn_ray(si.p, si.n, to_world(si.sh, wo));  // :448
+      bool v = false;
+      S.L_o = orc_path_mis(s, r, ray2, a->max_depth, a->rr_depth, &v);  // :450 (sample_ray :459-588)
+      const SurfaceInteraction si2 = intersect(s, ray2);                // :452
+      if (si2.valid) {
+        S.x_s = si2.p;
+        S.n_s = si2.n;
+      }
+    } else {
+      // zero-direction ray from an invalid interaction: one missed iteration
+      // of sample_ray (6 draws), radiance 0 (ReSTIR GI)
+      for (int k = 0; k < 6; ++k) r.next_u32();
+    }
+    rs_store(cur, n, i, S);
+    rng[i] = r;
+  }
+
+  // ---- temporal_resampling (:365-410)
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    const uint32_t smp = (uint32_t)(i % spp);
+    Pcg32 &r = rng[i];
+    const RSample S = rs_load(cur, n, i);
+    float ux = 0.f, uy = 0.f;
+    bool valid = project_prev(*prev_cam, S.x_v, &ux, &uy);
+    RSample Sprev = rsample_zero();
+    if (valid) Sprev = rs_load(prev, n, pixel_index((int64_t)ux, (int64_t)uy, W, H, spp, smp));
+    valid = valid && similar(S, Sprev);
+    const RReservoir R = valid ? rr_load(tres, n, i) : rres_zero();
+    RReservoir Rn = rres_zero();
+    float phat = p_hat(S.L_o);
+    const float w = S.p_q > 0.f ? phat / S.p_q : 0.f;
+    res_update(Rn, S, w, true, r.next_1d());
+    res_merge(Rn, R, p_hat(R.z.L_o), true, r.next_1d());
+    phat = p_hat(Rn.z.L_o);
+    Rn.W = (phat * (float)Rn.M > 0.f) ? Rn.w / ((float)Rn.M * phat) : 0.f;
+    if (a->max_M_temporal) Rn.M = std::min(Rn.M, a->max_M_temporal);
+    rr_store(tres, n, i, Rn);
+  }
+
+  // ---- spatial_resampling (:274-363)
+  std::vector<float> result(3 * n), pos(2 * n);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    const uint32_t smp = (uint32_t)(i % spp);
+    const int64_t x = (int64_t)(i / spp % W), y = (int64_t)(i / W / spp);
+    Pcg32 &r = rng[i];
+    const RReservoir Rs = rr_load(sres, n, i);
+    RReservoir Rn = rres_zero();
+    const RSample q = rs_load(cur, n, i);
+    uint32_t Z = 0;
+    if (ss_reuse) {
+      res_merge(Rn, Rs, p_hat(Rs.z.L_o), true, r.next_1d());
+      Z += Rs.M;
+    }
+    const int max_iter = (a->max_M_spatial == 0 || (double)Rs.M < a->max_M_spatial / 2.0) ? 9 : 3;
+    bool any_reused = false;
+    uint32_t qM[9];
+    V3 qp[9];
+    bool qa[9];
+    const float rad = radius[i];
+    for (int k = 0; k < 9; ++k) {
+      bool active = k < max_iter;
+      const V2 d2 = square_to_uniform_disk(r.next_2d());
+      const V2 off = V2{d2.x * rad, d2.y * rad};
+      const uint32_t idx = pixel_index(x + (int32_t)off.x, y + (int32_t)off.y, W, H, spp, smp);
+      const RSample qn = rs_load(cur, n, idx);
+      active = active && similar(qn, q);
+      const RReservoir Rk = active ? rr_load(tres, n, idx) : rres_zero();
+      bool shadowed = false;
+      if (active) {
+        const Ray sr = spawn_ray_to(q.x_v, q.n_v, Rk.z.x_s);
+        shadowed = trace_any(s, sr.o, sr.d, sr.maxt, nullptr, nullptr);
+      }
+      const float jf = jac ? dr_clampf(jacobian_J(q.x_v, Rk), 0.f, 1000.f) : 1.0f;
+      const float phat = (!active || shadowed) ? 0.f : p_hat(Rk.z.L_o) * jf;
+      res_merge(Rn, Rk, phat, active, r.next_1d());
+      qM[k] = Rk.M;
+      qp[k] = Rk.z.x_v;
+      qa[k] = active;
+      any_reused = any_reused || active;
+    }
+    const float phat = p_hat(Rn.z.L_o);
+    if (bias) {
+      for (int k = 0; k < 9; ++k) {
+        bool active = qa[k];
+        if (active) {
+          const Ray br = spawn_ray_to(Rn.z.x_s, Rn.z.n_s, qp[k]);
+          active = !trace_any(s, br.o, br.d, br.maxt, nullptr, nullptr);
+        }
+        Z += active ? qM[k] : 0u;
+      }
+      Rn.W = ((float)Z * phat > 0.f) ? Rn.w / ((float)Z * phat) : 0.f;
+    } else {
+      Rn.W = (phat * (float)Rn.M > 0.f) ? Rn.w / ((float)Rn.M * phat) : 0.f;
+    }
+    radius[i] = fmaxf(any_reused ? rad : rad / 2.f, a->minimal_search_radius);
+    if (a->max_M_spatial) Rn.M = std::min(Rn.M, a->max_M_spatial);
+    rr_store(sres, n, i, Rn);
+
+    // ---- render_final (:261-272)
+    uint32_t prim;
+    memcpy(&prim, &hitrec[4 * i + 1], 4);
+    const SurfaceInteraction si =
+        compute_si(s, hitrec[4 * i], prim, hitrec[4 * i + 2], hitrec[4 * i + 3],
+                   V3{pdir[3 * i], pdir[3 * i + 1], pdir[3 * i + 2]});
+    V3 beta = v3s(0.f);
+    if (si.valid) {
+      float pdf_unused;
+      const V3 wo = to_local(si.sh, normalize(Rn.z.x_s - si.p));
+      bsdf_eval_pdf(s.bsdf, s.materials[si.material], si.uv, si.wi, wo, &beta, &pdf_unused);
+    }
+    const V3 res = beta * Rn.z.L_o * Rn.W + V3{emit[3 * i], emit[3 * i + 1], emit[3 * i + 2]};
+    result[3 * i] = res.x; result[3 * i + 1] = res.y; result[3 * i + 2] = res.z;
+    pos[2 * i] = (float)x;
+    pos[2 * i + 1] = (float)y;
+  }
+  return orc_film(W, 0, H, spp, result.data(), pos.data(), film);
+}
+
+extern "C" {
 
 // ------------------------------- RNG KATs ----------------------------------
 int orc_rng_stream(uint32_t seed, uint32_t lane0, uint32_t n_lanes, uint32_t n_draws, float *out) {

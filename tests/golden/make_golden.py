@@ -7,6 +7,9 @@ the reference's sources. Vectors:
   rng_seed0 / rng_seed7   first 64 draws of sampler lanes 0..1023
   trace_rays / trace_hits 4096 rays on the 2 %-budget bedroom proxy
   film_<integrator>       64x36, spp 16, seed 0 films (path_test, mypath, nrc)
+  film_pssmlt_simple      32x18, spp 2, seed 2, 60 Metropolis iterations
+  film_restirgi_f<k>      64x36 ReSTIR GI frames 0..2 (test-restir-spatial.py
+                          "unbiased" properties)
   hs_scan_sha             sha256 of the Hillis-Steele scan of 10^6 floats
   scene_sha               sha256 of the test scene arrays
 
@@ -26,6 +29,17 @@ import binding as oracle  # noqa: E402
 from mtx import load_dict, scene  # noqa: E402
 
 INTEGRATORS = ("path_test", "mypath", "nrc")
+RESTIR_PROPS = {"jacobian": False, "bias_correction": True, "max_M_spatial": 500, "max_M_temporal": 30}
+
+
+def restir_frames(s, frames=3):
+    integ = load_dict({"type": "restirgi", **RESTIR_PROPS})
+    orc = oracle.RestirOracle(s)
+    out = []
+    for fr in range(frames):
+        integ.n = fr
+        out.append(orc.frame(s, integ.render_args(s, fr, 1)))
+    return out
 
 
 def scene_digest(s):
@@ -58,6 +72,10 @@ def compute():
     for name in INTEGRATORS:
         integ = load_dict({"type": name})
         out[f"film_{name}"] = oracle.render(s, integ.render_args(s, 0, 16))
+    sp = s.with_film(32, 18)
+    out["film_pssmlt_simple"] = oracle.pssmlt_render(sp, load_dict({"type": "pssmlt_simple"}).render_args(sp, 2, 2), 60)
+    for k, f in enumerate(restir_frames(s)):
+        out[f"film_restirgi_f{k}"] = f
     x = oracle.rng_stream(0, 0, 1_000_000, 1)[:, 0].copy()
     out["hs_scan_sha"] = np.frombuffer(hashlib.sha256(oracle.prefix_sum_f32_hs(x).tobytes()).hexdigest().encode(),
                                        np.uint8)

@@ -26,7 +26,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.mtx_abi_version() == 1
+    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 2
 
 
 def test_struct_sizes_match_header():
@@ -35,8 +35,8 @@ def test_struct_sizes_match_header():
     assert C.sizeof(_abi.Material) == 72
     assert C.sizeof(_abi.Emitter) == 64
     assert C.sizeof(_abi.Shape) == 16
-    assert C.sizeof(_abi.Camera) == 72
-    assert C.sizeof(_abi.RenderArgs) == 56
+    assert C.sizeof(_abi.Camera) == 112
+    assert C.sizeof(_abi.RenderArgs) == 80
 
 
 def test_ctx_create_without_gpu_fails_cleanly():

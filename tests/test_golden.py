@@ -47,3 +47,27 @@ def test_golden_films_gpu(golden, small_scene, name):
 
     integ = load_dict({"type": name})
     assert np.array_equal(integ.render_film(small_scene, seed=0, spp=16), golden[f"film_{name}"])
+
+
+def test_golden_pssmlt_and_restir_oracle(golden, oracle, small_scene):
+    import make_golden
+    from mtx import load_dict
+
+    sp = small_scene.with_film(32, 18)
+    f = oracle.pssmlt_render(sp, load_dict({"type": "pssmlt_simple"}).render_args(sp, 2, 2), 60)
+    assert np.array_equal(f, golden["film_pssmlt_simple"])
+    for k, f in enumerate(make_golden.restir_frames(small_scene)):
+        assert np.array_equal(f, golden[f"film_restirgi_f{k}"])
+
+
+@pytest.mark.gpu
+def test_golden_pssmlt_and_restir_gpu(golden, small_scene):
+    from mtx import load_dict
+    import make_golden
+
+    sp = small_scene.with_film(32, 18)
+    integ = load_dict({"type": "pssmlt_simple", "iterations": 60})
+    assert np.array_equal(integ.render_film(sp, seed=2, spp=2), golden["film_pssmlt_simple"])
+    integ = load_dict({"type": "restirgi", **make_golden.RESTIR_PROPS})
+    for k in range(3):
+        assert np.array_equal(integ.render_film(small_scene, seed=k, spp=1), golden[f"film_restirgi_f{k}"])
