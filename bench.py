@@ -1,5 +1,6 @@
-"""Benchmark: Mpaths/s of the path-mis.py NEE+MIS integrator on the bedroom
-proxy at 1280x720 (BASELINE.json configs[1]), one process per GPU.
+"""Benchmark: Mpaths/s of the path-mis.py NEE+MIS integrator (BASELINE.json
+configs[1]) on the bedroom proxy at 1280x720 spp=256 (the metric's
+resolution and spp), one process per GPU.
 
 A step renders the full 1280x720 film at `--spp` samples per pixel on every
 rank; rank r traces the global sample range [r*spp, (r+1)*spp) of every pixel
@@ -9,8 +10,9 @@ Inputs (scene, BVH) are resident in HBM before the timed region; the film
 stays in HBM and only the gather crosses GPUs.
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
-`roofline` for the closest-hit traversal kernel (HIP-event time over the
-timed region, algorithmic bytes from in-kernel visit counts) and
+`roofline` for the closest-hit traversal kernel (HIP-event time per launch
+over the timed region; algorithmic bytes from the in-kernel visit counters of
+one extra, untimed step with the same seed as the first timed step) and
 `cpu_baseline` (the oracle/ CPU restatement on a bounded sample).
 """
 import argparse
@@ -32,7 +34,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--spp", type=int, default=64)
+    p.add_argument("--spp", type=int, default=256)
     p.add_argument("--width", type=int, default=1280)
     p.add_argument("--height", type=int, default=720)
     p.add_argument("--max-depth", type=int, default=8)
@@ -64,9 +66,9 @@ def main():
     film = torch.empty((H + 2, W + 2, 4), dtype=torch.float32, device=f"cuda:{local}")
     from mtx import distributed
 
-    def step(i, stats=False):
+    def step(i, stats=False, counters=False):
         r = integ.render_film(sc, seed=i, spp=spp, spp_total=spp * world, sample_offset=spp * rank, out=film,
-                              stats=stats, chunk_paths=args.chunk)
+                              stats=stats, chunk_paths=args.chunk, counters=counters)
         if world > 1:
             distributed.gather_sum(film)  # RCCL all_gather, rank-order sum on rank 0
         return r[1] if stats else None
@@ -95,15 +97,17 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # visit counters (deterministic): one untimed step, same seed as step 0
+    cnt = step(0, stats=True, counters=True)
 
     paths_per_rank = W * H * spp
     value = world * paths_per_rank * args.steps / elapsed / 1e6
     # roofline of the dominant kernel: closest-hit traversal
-    alg_bytes = (agg["rays_closest"] * (RAY_BYTES + HIT_BYTES) + agg["nodes_closest"] * NODE_BYTES
-                 + agg["tris_closest"] * TRI_BYTES)
-    trace_s = agg["trace_ms"] / 1e3
+    alg_bytes = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
+                 + cnt["tris_closest"] * TRI_BYTES)  # per step
+    launches = max(1, cnt["trace_launches"])  # per step
+    trace_s = agg["trace_ms"] / 1e3 / args.steps  # per step, counters off
     achieved = alg_bytes / trace_s / 1e9 if trace_s > 0 else 0.0
-    launches = max(1, agg["trace_launches"])
 
     if rank == 0:
         cpu = None
@@ -138,11 +142,12 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
-                "avg_launch_ms": round(agg["trace_ms"] / launches, 4),
+                "avg_launch_ms": round(trace_s * 1e3 / launches, 4),
+                "launches_per_step": int(launches),
                 "alg_bytes_per_launch": int(alg_bytes / launches),
-                "rays": int(agg["rays_closest"]),
-                "node_visits_per_ray": round(agg["nodes_closest"] / max(1, agg["rays_closest"]), 2),
-                "tri_visits_per_ray": round(agg["tris_closest"] / max(1, agg["rays_closest"]), 2),
+                "rays_per_step": int(cnt["rays_closest"]),
+                "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
+                "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2),
             },
             "kernels_ms_per_step": {
                 "trace_closest": round(agg["trace_ms"] / args.steps, 3),

@@ -194,6 +194,25 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
         }
       }
     }
+  // BVH depth (stack entries of the traversal kernels); also rejects cycles.
+  uint32_t bvh_depth = 0;
+  {
+    std::vector<std::pair<int32_t, uint32_t>> todo{{0, 0u}};
+    uint64_t visited = 0;
+    while (!todo.empty()) {
+      auto [nd, dep] = todo.back();
+      todo.pop_back();
+      bvh_depth = std::max(bvh_depth, dep);
+      if (++visited > d->n_nodes || dep > MTX_BVH_MAX_DEPTH) {
+        mtx_set_error("mtx_scene_upload: BVH is not a tree of depth <= %d", MTX_BVH_MAX_DEPTH);
+        return MTX_E_ARG;
+      }
+      for (int k = 12; k < 14; ++k) {
+        int32_t ch = d->nodes[16 * (size_t)nd + k];
+        if (ch >= 0) todo.push_back({ch, dep + 1});
+      }
+    }
+  }
   for (uint64_t i = 0; i < 3ull * d->n_tris; ++i)
     if (d->tri_vidx[i] >= d->n_verts) {
       mtx_set_error("mtx_scene_upload: vertex index out of range");
@@ -262,6 +281,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.tables = (const float *)c->tables.p;
   s.n_tris = d->n_tris;
   s.n_emitters = d->n_emitters;
+  s.stack_entries = bvh_depth + 1;
   s.camera = d->camera;
   c->has_scene = true;
   return MTX_OK;

@@ -15,7 +15,10 @@ namespace mtxd {
 using namespace mtx;
 
 constexpr int kTraceBlock = 128;
-constexpr int kStack = MTX_BVH_MAX_DEPTH + 1;
+// Traversal stacks live in LDS, one column per lane ([entry][lane]); the
+// number of entries is the uploaded BVH's depth + 1 (at most
+// MTX_BVH_MAX_DEPTH + 1), so shallow trees leave LDS for more waves per CU.
+inline size_t stack_bytes(const DevScene &s) { return (size_t)s.stack_entries * kTraceBlock * sizeof(int32_t); }
 constexpr int kShadeBlock = 256;
 
 __device__ __forceinline__ SceneView make_view(const DevScene &s) {
@@ -126,6 +129,132 @@ __device__ __forceinline__ bool traverse(const DevScene &s, int32_t *stk, const 
     node = stk[sp * kTraceBlock];
   }
   return hit_any;
+}
+
+}  // namespace mtxd
+
+namespace mtxd {
+
+// ---------------------------------------------------------------------------
+// Persistent while-while traversal with per-lane ray replacement.
+//
+// Every lane owns one ray at a time. A wave alternates an inner-node phase
+// (each lane descends until it reaches a leaf or runs out of nodes) with a
+// leaf phase (one leaf per lane), so inner-node and triangle code do not
+// serialise against each other inside one iteration. When at least
+// kRefillLanes lanes of the wave have finished, their slots are refilled from
+// the ray queue with one atomic per wave (ballot + mbcnt). The visit order
+// of each ray is exactly that of `traverse` above (same results and counts).
+// ---------------------------------------------------------------------------
+constexpr int32_t kTravDone = INT32_MIN;  // never a valid leaf reference
+constexpr uint32_t kRefillLanes = 16;
+
+// Src provides: load(k, TraceRay&, float &tmax, uint32_t &payload) and
+// finish(payload, bool any_hit, float t, uint32_t prim, float u, float v).
+template <bool ANY, class Src>
+__device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *fetch,
+                                           int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr) {
+  const uint32_t lane = lane_id();
+  bool has = false, exhausted = false, hit = false;
+  uint32_t payload = 0, prim = 0xffffffffu;
+  TraceRay r;
+  float tbest = 0.f, bu = 0.f, bv = 0.f;
+  int32_t node = kTravDone;
+  int sp = 0;
+  while (true) {
+    if (!exhausted) {
+      const uint64_t idle = __ballot(!has);
+      if (idle) {
+        const uint32_t n = (uint32_t)__popcll(idle);
+        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(fetch, n);
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (base + n >= count) exhausted = true;
+        if (!has) {
+          const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+          if (k < count) {
+            src.load(k, r, tbest, payload);
+            prim = 0xffffffffu;
+            bu = bv = 0.f;
+            hit = false;
+            node = 0;
+            sp = 0;
+            has = true;
+          }
+        }
+      }
+    }
+    if (__ballot(has) == 0) break;
+    while (true) {
+      // inner-node phase
+      while (has && node >= 0) {
+        const int4 *np = s.nodes + 4 * node;
+        const float4 a = __builtin_bit_cast(float4, np[0]);
+        const float4 b = __builtin_bit_cast(float4, np[1]);
+        const float4 c = __builtin_bit_cast(float4, np[2]);
+        const int4 ch = np[3];
+        ++nv;
+        const float t0 = box_enter(r, a.x, a.y, a.z, a.w, c.x, c.y, tbest);
+        const float t1 = box_enter(r, b.x, b.y, b.z, b.w, c.z, c.w, tbest);
+        const bool h0 = t0 != kInf, h1 = t1 != kInf;
+        if (h0 && h1) {
+          const bool first0 = t0 <= t1;
+          stk[sp * kTraceBlock] = first0 ? ch.y : ch.x;
+          ++sp;
+          node = first0 ? ch.x : ch.y;
+        } else if (h0) {
+          node = ch.x;
+        } else if (h1) {
+          node = ch.y;
+        } else if (sp > 0) {
+          --sp;
+          node = stk[sp * kTraceBlock];
+        } else {
+          node = kTravDone;
+        }
+      }
+      // leaf phase: one leaf per lane
+      if (has && node != kTravDone) {
+        uint32_t first, cnt;
+        leaf_decode(node, &first, &cnt);
+        for (uint32_t k = 0; k < cnt; ++k) {
+          const uint32_t pr = first + k;
+          const float4 g0 = s.tri[3 * pr + 0], g1 = s.tri[3 * pr + 1], g2 = s.tri[3 * pr + 2];
+          float t, u, v;
+          ++tv;
+          if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+            if (ANY) {
+              hit = true;
+              break;
+            }
+            if (t < tbest || (t == tbest && pr < prim)) {
+              tbest = t;
+              prim = pr;
+              bu = u;
+              bv = v;
+            }
+          }
+        }
+        if (ANY && hit) {
+          node = kTravDone;
+        } else if (sp > 0) {
+          --sp;
+          node = stk[sp * kTraceBlock];
+        } else {
+          node = kTravDone;
+        }
+      }
+      if (has && node == kTravDone) {
+        src.finish(payload, hit, tbest, prim, bu, bv);
+        has = false;
+        ++nr;
+      }
+      const uint64_t idle = __ballot(!has);
+      if (idle == ~0ull || (!exhausted && (uint32_t)__popcll(idle) >= kRefillLanes)) break;
+    }
+  }
 }
 
 }  // namespace mtxd

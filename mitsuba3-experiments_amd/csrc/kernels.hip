@@ -28,36 +28,31 @@ using namespace mtx;
 
 namespace mtxd {
 
+// Closest-hit queries of bounce `bounce`: queue entries are path indices.
+struct ClosestSrc {
+  WaveBuffers b;
+  const uint32_t *queue;
+  __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
+    const uint32_t path = queue[k];
+    const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
+    r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+    tmax = o4.w;
+    payload = path;
+  }
+  __device__ __forceinline__ void finish(uint32_t path, bool, float t, uint32_t prim, float u, float v) const {
+    b.hit[path] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
+  }
+};
+
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
-  __shared__ int32_t stack[kStack * kTraceBlock];
-  int32_t *stk = stack + threadIdx.x;
-  const uint32_t count = b.counters[4 * bounce + 0];
-  uint32_t *fetch = &b.counters[4 * bounce + 2];
-  const uint32_t *queue = b.queue[bounce & 1];
-  const uint32_t lane = threadIdx.x & 63;
+  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
+  const ClosestSrc src{b, b.queue[bounce & 1]};
   uint32_t nv = 0, tv = 0, nr = 0;
-  while (true) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(fetch, 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base >= count) break;
-    const uint32_t i = base + lane;
-    if (i < count) {
-      const uint32_t path = queue[i];
-      const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
-      TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
-      float tbest = o4.w, bu = 0.f, bv = 0.f;
-      uint32_t prim = 0xffffffffu;
-      traverse<false>(s, stk, r, tbest, prim, bu, bv, nv, tv);
-      if (prim == 0xffffffffu) tbest = kInf;
-      b.hit[path] = make_float4(tbest, __uint_as_float(prim), bu, bv);
-      ++nr;
-    }
-  }
+  trace_loop<false>(s, src, b.counters[4 * bounce + 0], &b.counters[4 * bounce + 2], stack + threadIdx.x, nv, tv, nr);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) {
       atomicAdd(&b.stats[0], a);
       atomicAdd(&b.stats[1], c);
       atomicAdd(&b.stats[4], n);
@@ -68,52 +63,49 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveB
 // Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
 // contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
 // form).
+struct ShadowSrc {
+  WaveBuffers b;
+  __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
+    const float4 o4 = b.shadow[k].o, d4 = b.shadow[k].d;
+    r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+    tmax = o4.w;
+    payload = k;
+  }
+  __device__ __forceinline__ void finish(uint32_t k, bool occluded, float, uint32_t, float, float) const {
+    const ShadowRec &rec = b.shadow[k];
+    const float4 rd = rec.d, rt = rec.t, rx = rec.x;
+    const uint32_t path = __float_as_uint(rd.w);
+    const uint32_t fl = __float_as_uint(rt.w);
+    float4 L = b.L[path];
+    if (!occluded) {
+      if (fl & 1u) {
+        L.x = fmaf(rt.x, rx.x, L.x);
+        L.y = fmaf(rt.y, rx.y, L.y);
+        L.z = fmaf(rt.z, rx.z, L.z);
+      } else {
+        L.x = L.x + rx.x;
+        L.y = L.y + rx.y;
+        L.z = L.z + rx.z;
+      }
+    } else {
+      const float qnan = __uint_as_float(0x7fc00000u);
+      if (fl & 2u) L.x = qnan;
+      if (fl & 4u) L.y = qnan;
+      if (fl & 8u) L.z = qnan;
+    }
+    b.L[path] = L;
+  }
+};
+
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
-  __shared__ int32_t stack[kStack * kTraceBlock];
-  int32_t *stk = stack + threadIdx.x;
-  const uint32_t count = b.counters[4 * bounce + 1];
-  uint32_t *fetch = &b.counters[4 * bounce + 3];
-  const uint32_t lane = threadIdx.x & 63;
+  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
+  const ShadowSrc src{b};
   uint32_t nv = 0, tv = 0, nr = 0;
-  while (true) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(fetch, 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base >= count) break;
-    const uint32_t i = base + lane;
-    if (i < count) {
-      const ShadowRec rec = b.shadow[i];
-      TraceRay r = make_trace_ray(V3{rec.o.x, rec.o.y, rec.o.z}, V3{rec.d.x, rec.d.y, rec.d.z}, rec.o.w);
-      float tbest = rec.o.w, bu, bv;
-      uint32_t prim = 0xffffffffu;
-      const bool occluded = traverse<true>(s, stk, r, tbest, prim, bu, bv, nv, tv);
-      const uint32_t path = __float_as_uint(rec.d.w);
-      const uint32_t fl = __float_as_uint(rec.t.w);
-      float4 L = b.L[path];
-      if (!occluded) {
-        if (fl & 1u) {
-          L.x = fmaf(rec.t.x, rec.x.x, L.x);
-          L.y = fmaf(rec.t.y, rec.x.y, L.y);
-          L.z = fmaf(rec.t.z, rec.x.z, L.z);
-        } else {
-          L.x = L.x + rec.x.x;
-          L.y = L.y + rec.x.y;
-          L.z = L.z + rec.x.z;
-        }
-      } else {
-        const float qnan = __uint_as_float(0x7fc00000u);
-        if (fl & 2u) L.x = qnan;
-        if (fl & 4u) L.y = qnan;
-        if (fl & 8u) L.z = qnan;
-      }
-      b.L[path] = L;
-      ++nr;
-    }
-  }
+  trace_loop<true>(s, src, b.counters[4 * bounce + 1], &b.counters[4 * bounce + 3], stack + threadIdx.x, nv, tv, nr);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) {
       atomicAdd(&b.stats[2], a);
       atomicAdd(&b.stats[3], c);
       atomicAdd(&b.stats[5], n);
@@ -562,7 +554,7 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
 // Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0).
 __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const float4 *rays, uint32_t n, int any_hit,
                                                            uint32_t *hits, uint32_t *visits) {
-  __shared__ int32_t stack[kStack * kTraceBlock];
+  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   int32_t *stk = stack + threadIdx.x;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -718,16 +710,16 @@ void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkPara
 void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                           hipStream_t st) {
   if (stats)
-    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
   else
-    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
 }
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st) {
   if (stats)
-    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
   else
-    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), 0, st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
 }
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
                   hipStream_t st) {
@@ -770,7 +762,7 @@ void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, ui
 }
 void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any_hit, uint32_t *hits,
                       uint32_t *visits, hipStream_t st) {
-  hipLaunchKernelGGL(k_trace_raw, dim3(blocks_for(n, kTraceBlock)), dim3(kTraceBlock), 0, st, s, rays, n, any_hit,
+  hipLaunchKernelGGL(k_trace_raw, dim3(blocks_for(n, kTraceBlock)), dim3(kTraceBlock), stack_bytes(s), st, s, rays, n, any_hit,
                      hits, visits);
 }
 

@@ -329,28 +329,25 @@ __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
 }
 
 // Any-hit traversal of the compacted visibility tests; occ[base + slot].
-__global__ __launch_bounds__(kTraceBlock) void k_trace_test(DevScene s, RestirBuffers r, uint32_t occ_base) {
-  __shared__ int32_t stack[kStack * kTraceBlock];
-  int32_t *stk = stack + threadIdx.x;
-  const uint32_t count = r.test_count[0];
-  uint32_t *fetch = &r.test_count[1];
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t nv = 0, tv = 0;
-  while (true) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(fetch, 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base >= count) break;
-    const uint32_t k = base + lane;
-    if (k < count) {
-      const float4 o4 = r.test_rays[2 * (size_t)k], d4 = r.test_rays[2 * (size_t)k + 1];
-      TraceRay tr = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
-      float tbest = o4.w, bu, bv;
-      uint32_t prim = 0xffffffffu;
-      const bool occluded = traverse<true>(s, stk, tr, tbest, prim, bu, bv, nv, tv);
-      r.occ[occ_base + __float_as_uint(d4.w)] = occluded ? 1 : 0;
-    }
+struct TestSrc {
+  RestirBuffers r;
+  uint32_t occ_base;
+  __device__ __forceinline__ void load(uint32_t k, TraceRay &tr, float &tmax, uint32_t &payload) const {
+    const float4 o4 = r.test_rays[2 * (size_t)k], d4 = r.test_rays[2 * (size_t)k + 1];
+    tr = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+    tmax = o4.w;
+    payload = __float_as_uint(d4.w);
   }
+  __device__ __forceinline__ void finish(uint32_t slot, bool occluded, float, uint32_t, float, float) const {
+    r.occ[occ_base + slot] = occluded ? 1 : 0;
+  }
+};
+
+__global__ __launch_bounds__(kTraceBlock) void k_trace_test(DevScene s, RestirBuffers r, uint32_t occ_base) {
+  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
+  const TestSrc src{r, occ_base};
+  uint32_t nv = 0, tv = 0, nr = 0;
+  trace_loop<true>(s, src, r.test_count[0], &r.test_count[1], stack + threadIdx.x, nv, tv, nr);
 }
 
 static inline unsigned rs_blocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -379,7 +376,7 @@ void launch_restir_final(const DevScene &s, const WaveBuffers &b, const ChunkPar
   hipLaunchKernelGGL(k_rs_final, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, s, b, p, r);
 }
 void launch_trace_test(const DevScene &s, const RestirBuffers &r, uint32_t occ_base, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), 0, st, s, r, occ_base);
+  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, r, occ_base);
 }
 
 }  // namespace mtxd

@@ -42,6 +42,7 @@ struct DevScene {
   const float *texels;
   const float *tables;
   uint32_t n_tris, n_emitters;
+  uint32_t stack_entries;  // BVH depth + 1 (LDS traversal stack entries per lane)
   mtx_camera camera;
 };
 

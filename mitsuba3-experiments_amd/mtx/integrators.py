@@ -93,13 +93,16 @@ class SamplingIntegrator:
     # --------------------------------------------------------------- render --
     def render_film(self, scene, seed: int = 0, spp: int = 1, y0: int = 0, y1: int | None = None,
                     spp_total: int | None = None, sample_offset: int = 0, device: int | None = None,
-                    out=None, stats: bool = False, chunk_paths: int = 0):
+                    out=None, stats: bool = False, chunk_paths: int = 0, counters: bool = False):
         """Raw film (rows y0-1..y1, cols -1..W) x RGBW. `out` may be a
-        device tensor (torch, on the context's device) to keep the film in HBM."""
+        device tensor (torch, on the context's device) to keep the film in HBM.
+        stats=True returns (film, stats) with per-kernel-class HIP-event
+        times; counters=True also collects the traversal visit counters
+        (slower kernels: use it outside timed regions)."""
         ctx = context(device)
         _bind_scene(ctx, scene)
         a = self.render_args(scene, seed, spp, y0, y1, spp_total, sample_offset, chunk_paths,
-                             flags=3 if stats else 0)
+                             flags=(2 if stats else 0) | (1 if stats and counters else 0))
         shape = (a.y1 - a.y0 + 2, scene.width + 2, 4)
         st = _abi.Stats()
         if out is None:
@@ -244,7 +247,7 @@ class RestirIntegrator(SamplingIntegrator):
         return a
 
     def render_film(self, scene, seed: int = 0, spp: int = 1, device: int | None = None, out=None,
-                    stats: bool = False, **kwargs):
+                    stats: bool = False, counters: bool = False, **kwargs):
         """One frame (restirgi.py:182-258); advances the frame counter."""
         if kwargs.get("y0", 0) != 0 or kwargs.get("y1") not in (None, scene.height) or kwargs.get("sample_offset", 0):
             raise MtxError("ReSTIR GI renders whole frames")
@@ -261,7 +264,8 @@ class RestirIntegrator(SamplingIntegrator):
         ctx._restir_owner = self
         cam = scene.camera
         check(lib().mtx_set_camera(ctx.handle, C.byref(cam)), "mtx_set_camera")
-        result = super().render_film(scene, seed=seed, spp=spp, device=device, out=out, stats=stats)
+        result = super().render_film(scene, seed=seed, spp=spp, device=device, out=out, stats=stats,
+                                     counters=counters)
         self.n += 1  # restirgi.py:245
         return result
 
