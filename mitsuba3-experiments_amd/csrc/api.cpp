@@ -88,6 +88,7 @@ struct mtx_ctx {
   hipStream_t stream = nullptr;
   bool has_scene = false;
   // scene
+  DevBuf stack_ovf;  // traversal stack entries beyond the LDS part
   DevBuf nodes, tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
@@ -96,7 +97,7 @@ struct mtx_ctx {
   DevBuf mlt_cur, mlt_L, mlt_prop, vpath, vprop;  // PSSMLT chain state
   uint32_t mlt_capacity = 0, mlt_depth = 0;
   // ReSTIR GI frame state (restirgi.py:217-226): kept across mtx_render calls
-  DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM;
+  DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM, rs_xs, rs_ns;
   uint32_t rs_n = 0, rs_cur = 0;
   bool rs_valid = false;
   mtx_camera rs_prev_cam{};
@@ -142,9 +143,10 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
     mtx_set_error("hipStreamCreate failed: %s", hipGetErrorString(e));
     return MTX_E_HIP;
   }
-  // Persistent grids: fill every CU (occupancy of the LDS-stack traversal).
+  // Persistent grids: every CU filled to the kernels' occupancy (the trace
+  // grid is recomputed per scene: its LDS stack depends on the BVH depth).
   c->trace_grid = c->n_cu * 8;
-  c->shade_grid = c->n_cu * 8;
+  c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
   *out = c;
   return MTX_OK;
 }
@@ -158,8 +160,8 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
-                    &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
-                    &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM,
+                    &c->stack_ovf, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
+                    &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
@@ -283,6 +285,13 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.n_emitters = d->n_emitters;
   s.stack_entries = bvh_depth + 1;
   s.camera = d->camera;
+  c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
+  s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
+  {
+    const size_t deep = s.stack_entries > mtxd::kLdsStack ? s.stack_entries - mtxd::kLdsStack : 0;
+    if ((rc = dalloc(c->stack_ovf, std::max<size_t>(4, deep * s.ovf_threads * sizeof(int32_t))))) return rc;
+    s.stack_ovf = (int32_t *)c->stack_ovf.p;
+  }
   c->has_scene = true;
   return MTX_OK;
 }
@@ -291,7 +300,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
 
 namespace {
 
-constexpr uint32_t kDefaultChunk = 1u << 22;
+constexpr uint32_t kDefaultChunk = 1u << 26;  // 64 Mi paths (~13 GB of path state)
 
 int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   int rc;
@@ -460,6 +469,8 @@ int ensure_restir(mtx_ctx *c, uint32_t n) {
     if ((rc = dalloc(c->rs_count, 16))) return rc;
     if ((rc = dalloc(c->rs_occ, 18 * N))) return rc;
     if ((rc = dalloc(c->rs_qM, 10 * 4 * N))) return rc;
+    if ((rc = dalloc(c->rs_xs, 16 * N))) return rc;
+    if ((rc = dalloc(c->rs_ns, 16 * N))) return rc;
     c->rs_n = n;
   }
   return MTX_OK;
@@ -523,8 +534,8 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   r.initial_radius = a->initial_search_radius;
   r.minimal_radius = a->minimal_search_radius;
   r.frame = a->frame;
-  b.rs_xs = r.cur + 2 * (size_t)n;
-  b.rs_ns = r.cur + 3 * (size_t)n;
+  b.rs_xs = (float4 *)c->rs_xs.p;
+  b.rs_ns = (float4 *)c->rs_ns.p;
 
   mtxd::ChunkParams p{};
   p.integrator = MTX_INT_RESTIR_GI;

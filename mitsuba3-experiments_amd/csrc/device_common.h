@@ -14,11 +14,19 @@ namespace mtxd {
 
 using namespace mtx;
 
-constexpr int kTraceBlock = 128;
 // Traversal stacks live in LDS, one column per lane ([entry][lane]); the
 // number of entries is the uploaded BVH's depth + 1 (at most
 // MTX_BVH_MAX_DEPTH + 1), so shallow trees leave LDS for more waves per CU.
 inline size_t stack_bytes(const DevScene &s) { return (size_t)s.stack_entries * kTraceBlock * sizeof(int32_t); }
+// The persistent kernels keep only the top kLdsStack entries in LDS (so LDS
+// does not cap occupancy) and spill deeper entries to a per-thread global
+// area ([entry - kLdsStack][thread], coalesced per depth), rarely touched.
+inline uint32_t lds_stack_entries(const DevScene &s) {
+  return s.stack_entries < kLdsStack ? s.stack_entries : kLdsStack;
+}
+inline size_t persistent_stack_bytes(const DevScene &s) {
+  return (size_t)lds_stack_entries(s) * kTraceBlock * sizeof(int32_t);
+}
 constexpr int kShadeBlock = 256;
 
 __device__ __forceinline__ SceneView make_view(const DevScene &s) {
@@ -155,6 +163,7 @@ template <bool ANY, class Src>
 __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *fetch,
                                            int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr) {
   const uint32_t lane = lane_id();
+  int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
   bool has = false, exhausted = false, hit = false;
   uint32_t payload = 0, prim = 0xffffffffu;
   TraceRay r;
@@ -201,7 +210,11 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
         const bool h0 = t0 != kInf, h1 = t1 != kInf;
         if (h0 && h1) {
           const bool first0 = t0 <= t1;
-          stk[sp * kTraceBlock] = first0 ? ch.y : ch.x;
+          const int32_t far = first0 ? ch.y : ch.x;
+          if ((uint32_t)sp < kLdsStack)
+            stk[sp * kTraceBlock] = far;
+          else
+            ovf[(size_t)(sp - (int)kLdsStack) * s.ovf_threads] = far;
           ++sp;
           node = first0 ? ch.x : ch.y;
         } else if (h0) {
@@ -210,7 +223,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
           node = ch.y;
         } else if (sp > 0) {
           --sp;
-          node = stk[sp * kTraceBlock];
+          node = (uint32_t)sp < kLdsStack ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - (int)kLdsStack) * s.ovf_threads];
         } else {
           node = kTravDone;
         }
@@ -241,7 +254,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
           node = kTravDone;
         } else if (sp > 0) {
           --sp;
-          node = stk[sp * kTraceBlock];
+          node = (uint32_t)sp < kLdsStack ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - (int)kLdsStack) * s.ovf_threads];
         } else {
           node = kTravDone;
         }

@@ -26,6 +26,11 @@
 
 using namespace mtx;
 
+// Tuning knob: minimum resident shade blocks per CU (caps VGPRs; 1 = none).
+#ifndef MTX_SHADE_MIN_BLOCKS
+#define MTX_SHADE_MIN_BLOCKS 1
+#endif
+
 namespace mtxd {
 
 // Closest-hit queries of bounce `bounce`: queue entries are path indices.
@@ -139,7 +144,9 @@ __global__ void k_raygen_camera(DevScene s, WaveBuffers b, ChunkParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) b.counters[0] = p.n_paths;
   if (i >= p.n_paths) return;
-  const uint32_t px_local = i / p.spp, smp = i - px_local * p.spp;
+  // sample-major path order (path = s * n_px + q): film stage 1 then reads
+  // each pixel's samples with lanes on consecutive pixels (coalesced)
+  const uint32_t smp = i / p.n_px, px_local = i - smp * p.n_px;
   const uint32_t pix = p.px0 + px_local;
   const uint32_t y = pix / p.width, x = pix - y * p.width;
   const uint32_t lane = pix * p.spp_total + p.sample_offset + smp;
@@ -440,7 +447,7 @@ __device__ __forceinline__ bool shade_pssmlt(const SceneView &sv, const WaveBuff
 }
 
 template <int INT>
-__global__ __launch_bounds__(kShadeBlock) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
+__global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
   const uint32_t count = b.counters[4 * bounce + 0];
   const uint32_t *in_q = b.queue[bounce & 1];
@@ -493,7 +500,7 @@ __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
-    const uint32_t path = q * p.spp + sidx;
+    const uint32_t path = sidx * p.n_px + q;
     const float2 ps = b.pos[path];
     const V3 L = final_L(b, p, path);
 #pragma unroll
@@ -710,16 +717,16 @@ void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkPara
 void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                           hipStream_t st) {
   if (stats)
-    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
   else
-    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
 }
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st) {
   if (stats)
-    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
   else
-    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
 }
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
                   hipStream_t st) {
@@ -736,6 +743,22 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
     default:
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
   }
+}
+// Resident blocks per CU of the persistent kernels (grid = n_cu x this).
+int trace_blocks_per_cu(const DevScene &s) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace_closest<false>, kTraceBlock, persistent_stack_bytes(s)) !=
+          hipSuccess ||
+      nb <= 0)
+    nb = 4;
+  return nb;
+}
+int shade_blocks_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<MTX_INT_PATH_MIS>, kShadeBlock, 0) != hipSuccess ||
+      nb <= 0)
+    nb = 2;
+  return nb;
 }
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
   hipLaunchKernelGGL(k_mlt_init, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);

@@ -76,6 +76,13 @@ __device__ __forceinline__ uint4 st_rng(const Pcg32 &g, uint32_t w) {
 
 __device__ __forceinline__ float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
+// lane i = q * spp + s (pixel-major, the sampler lane order) -> wavefront
+// path index s * n_px + q (sample-major, see wavefront.h)
+__device__ __forceinline__ uint32_t path_of(uint32_t i, const ChunkParams &p) {
+  const uint32_t q = i / p.spp;
+  return (i - q * p.spp) * p.n_px + q;
+}
+
 }  // namespace
 
 // sample_initial after the primary intersection (:419-448). Lanes with a
@@ -85,13 +92,14 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   const SceneView sv = make_view(s);
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool enq = false;
+  const uint32_t path = i < r.n ? path_of(i, p) : 0u;
   if (i < r.n) {
-    const float4 h = b.hit[i], d4 = b.ray_d[i];
+    const float4 h = b.hit[path], d4 = b.ray_d[path];
     r.prim_hit[i] = h;
     r.prim_dir[i] = d4;
     const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
     r.emit[i] = f4(emitter_eval(sv, si.emitter, si.wi), 0.f);
-    Pcg32 rng = ld_rng(b.misc[i]);
+    Pcg32 rng = ld_rng(b.misc[path]);
     V3 wo;
     float pdf;
     if (r.flags & MTX_RESTIR_BSDF_SAMPLING) {
@@ -112,32 +120,35 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
     r.cur[n + i] = si.valid ? f4(si.n, pdf) : make_float4(0.f, 0.f, 0.f, pdf);
     if (si.valid) {
       const Ray nr = spawn_ray(si.p, si.n, to_world(si.sh, wo));
-      b.ray_o[i] = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
-      b.ray_d[i] = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
-      b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
-      b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
-      b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      b.misc[i] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
+      b.ray_o[path] = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
+      b.ray_d[path] = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
+      b.thr[path] = make_float4(1.f, 1.f, 1.f, 1.f);
+      b.L[path] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
+      b.prev[path] = make_float4(0.f, 0.f, 0.f, 0.f);
+      b.misc[path] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
       enq = true;
     } else {
       rng.advance(6);
-      b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);
-      b.misc[i] = st_rng(rng, 0u);
-      r.cur[2 * n + i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      r.cur[3 * n + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      b.L[path] = make_float4(0.f, 0.f, 0.f, 1.f);
+      b.misc[path] = st_rng(rng, 0u);
+      b.rs_xs[path] = make_float4(0.f, 0.f, 0.f, 0.f);
+      b.rs_ns[path] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
   const uint32_t slot = wave_append(&b.counters[0], enq);
-  if (enq) b.queue[0][slot] = i;
+  if (enq) b.queue[0][slot] = path;
 }
 
 // L_o = select(valid_ray, result, 0) (:588) and the sampler position.
 __global__ void k_rs_collect(WaveBuffers b, ChunkParams p, RestirBuffers r) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= r.n) return;
-  const float4 l = b.L[i];
-  const uint4 m = b.misc[i];
+  const uint32_t path = path_of(i, p);
+  const float4 l = b.L[path];
+  const uint4 m = b.misc[path];
   const bool valid_ray = ((m.w >> 16) & PF_VALID_RAY) != 0;
+  r.cur[2 * (size_t)r.n + i] = b.rs_xs[path];
+  r.cur[3 * (size_t)r.n + i] = b.rs_ns[path];
   r.cur[4 * (size_t)r.n + i] = valid_ray ? make_float4(l.x, l.y, l.z, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
   r.rng[i] = m;
 }
@@ -323,9 +334,10 @@ __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   }
   const float4 em = r.emit[i];
   const V3 res = beta * R.z.L_o * R.W + V3{em.x, em.y, em.z};
-  b.L[i] = make_float4(res.x, res.y, res.z, 0.f);
+  const uint32_t path = path_of(i, p);
+  b.L[path] = make_float4(res.x, res.y, res.z, 0.f);
   const uint32_t x = i / p.spp % p.width, y = i / p.width / p.spp;
-  b.pos[i] = make_float2((float)x, (float)y);
+  b.pos[path] = make_float2((float)x, (float)y);
 }
 
 // Any-hit traversal of the compacted visibility tests; occ[base + slot].
@@ -376,7 +388,7 @@ void launch_restir_final(const DevScene &s, const WaveBuffers &b, const ChunkPar
   hipLaunchKernelGGL(k_rs_final, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, s, b, p, r);
 }
 void launch_trace_test(const DevScene &s, const RestirBuffers &r, uint32_t occ_base, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), stack_bytes(s), st, s, r, occ_base);
+  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, r, occ_base);
 }
 
 }  // namespace mtxd

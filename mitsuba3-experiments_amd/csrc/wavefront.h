@@ -11,6 +11,8 @@
 //   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16
 //   pos    float2  film sample position (block.put position, path.py:101)
 //   hit    float4  t, prim, u, v (written by the closest-hit traversal)
+// Paths of a chunk are stored sample-major: path = s * n_px + q for sample s
+// of the chunk's pixel q (raygen_camera, film_src).
 // Queues are u32 path indices compacted with wave64 ballot + mbcnt and one
 // atomic per wave; shadow rays are 64-byte records.
 #pragma once
@@ -27,6 +29,9 @@ enum : uint32_t {
   PF_PRIMARY_VALID = 4u,
 };
 
+constexpr int kTraceBlock = 128;     // threads per traversal block
+constexpr uint32_t kLdsStack = 16;   // traversal stack entries per lane held in LDS (persistent kernels)
+
 struct DevScene {
   const int4 *nodes;  // 4 x int4 per node
   const float4 *tri;  // 3 x float4 per triangle
@@ -42,7 +47,9 @@ struct DevScene {
   const float *texels;
   const float *tables;
   uint32_t n_tris, n_emitters;
-  uint32_t stack_entries;  // BVH depth + 1 (LDS traversal stack entries per lane)
+  uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane)
+  int32_t *stack_ovf;      // persistent kernels: entries beyond kLdsStack, [entry][thread]
+  uint32_t ovf_threads;    // threads of the persistent trace grid
   mtx_camera camera;
 };
 
@@ -75,7 +82,7 @@ struct WaveBuffers {
   float4 *vpath;
   float4 *vprop;
   // ReSTIR GI: first hit of the secondary path (restirgi.py:452-455), written
-  // by the bounce-0 shade into the current sample planes 2 and 3.
+  // by the bounce-0 shade (path order).
   float4 *rs_xs;
   float4 *rs_ns;
 };
@@ -117,6 +124,8 @@ struct ChunkParams {
 };
 
 // -------- launch wrappers (kernels.hip) --------
+int trace_blocks_per_cu(const DevScene &s);
+int shade_blocks_per_cu();
 void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
                         const uint32_t *lanes, uint32_t rng_skip, hipStream_t st);

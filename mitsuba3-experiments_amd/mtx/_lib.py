@@ -20,7 +20,11 @@ try:  # one HIP runtime per process: torch's, if torch is present
 except Exception:  # pragma: no cover - torch is optional for host-only use
     _torch = None
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmtx.so")
+# MTX_LIB_VARIANT selects an in-tree tuning build (e.g. "shade4" ->
+# libmtx_shade4.so, see csrc/Makefile `variants`); default libmtx.so.
+_VARIANT = os.environ.get("MTX_LIB_VARIANT", "")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        f"libmtx_{_VARIANT}.so" if _VARIANT else "libmtx.so")
 
 
 class MtxError(RuntimeError):

@@ -24,17 +24,17 @@ CONFIGS = {
 }
 
 
-def _oracle_frames(oracle, scene, props, frames, cameras=None):
+def _oracle_frames(oracle, scene, props, frames, cameras=None, spp=1):
     from mtx import load_dict
 
     integ = load_dict({"type": "restirgi", **props})
-    orc = oracle.RestirOracle(scene)
+    orc = oracle.RestirOracle(scene, spp)
     out = []
     for fr in range(frames):
         if cameras is not None:
             scene.camera = cameras[fr]
         integ.n = fr
-        out.append(orc.frame(scene, integ.render_args(scene, fr, 1)))
+        out.append(orc.frame(scene, integ.render_args(scene, fr, spp)))
     return out, orc
 
 
@@ -83,6 +83,19 @@ def test_restir_frames_bit_exact(small_scene, oracle, cfg):
     np.testing.assert_array_equal(integ.state("spatial"), orc.sres)
     np.testing.assert_array_equal(integ.state("radius"), orc.radius)
     assert ref[-1][..., :3].sum() > 0
+
+
+@pytest.mark.gpu
+def test_restir_two_samples_per_pixel_bit_exact(small_scene, oracle):
+    """spp = 2 lanes per pixel (to_idx's sample_offset, restirgi.py:173)."""
+    from mtx import load_dict
+
+    sc = small_scene.with_film(24, 16)
+    ref, orc = _oracle_frames(oracle, sc, CONFIGS["unbiased"], 3, spp=2)
+    integ = load_dict({"type": "restirgi", **CONFIGS["unbiased"]})
+    for fr in range(3):
+        np.testing.assert_array_equal(integ.render_film(sc, seed=fr, spp=2), ref[fr], err_msg=f"frame {fr}")
+    np.testing.assert_array_equal(integ.state("spatial"), orc.sres)
 
 
 @pytest.mark.gpu
