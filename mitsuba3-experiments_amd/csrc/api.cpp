@@ -10,6 +10,7 @@
 // queue lengths from device counters), then one film gather per call.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -106,6 +107,10 @@ struct mtx_ctx {
   // scratch for sample_rays / trace / primitives
   DevBuf s0, s1, s2, s3, s4, s5;
   int trace_grid = 0, shade_grid = 0;
+  // tuning knobs (environment, read at context creation): LDS stack entries
+  // of the persistent traversal, chunk path order
+  uint32_t lds_stack = mtxd::kLdsStack;
+  uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
 };
 
@@ -147,6 +152,8 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   // grid is recomputed per scene: its LDS stack depends on the BVH depth).
   c->trace_grid = c->n_cu * 8;
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
+  if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
+  if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   *out = c;
   return MTX_OK;
 }
@@ -285,10 +292,11 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.n_emitters = d->n_emitters;
   s.stack_entries = bvh_depth + 1;
   s.camera = d->camera;
+  s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {
-    const size_t deep = s.stack_entries > mtxd::kLdsStack ? s.stack_entries - mtxd::kLdsStack : 0;
+    const size_t deep = s.stack_entries - s.lds_entries;
     if ((rc = dalloc(c->stack_ovf, std::max<size_t>(4, deep * s.ovf_threads * sizeof(int32_t))))) return rc;
     s.stack_ovf = (int32_t *)c->stack_ovf.p;
   }
@@ -551,6 +559,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   p.band_y0 = 0;
   p.n_paths = n;
   p.restir = 1;
+  p.sample_major = c->sample_major;
   const size_t cbytes = 16ull * (depth + 2);
   // sample_initial: primary rays and their closest hits
   HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
@@ -675,6 +684,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.n_paths = p.n_px * a->spp;
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;
+    p.sample_major = c->sample_major;
     const size_t cbytes = 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2);
     if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
       // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains

@@ -18,14 +18,11 @@ using namespace mtx;
 // number of entries is the uploaded BVH's depth + 1 (at most
 // MTX_BVH_MAX_DEPTH + 1), so shallow trees leave LDS for more waves per CU.
 inline size_t stack_bytes(const DevScene &s) { return (size_t)s.stack_entries * kTraceBlock * sizeof(int32_t); }
-// The persistent kernels keep only the top kLdsStack entries in LDS (so LDS
-// does not cap occupancy) and spill deeper entries to a per-thread global
-// area ([entry - kLdsStack][thread], coalesced per depth), rarely touched.
-inline uint32_t lds_stack_entries(const DevScene &s) {
-  return s.stack_entries < kLdsStack ? s.stack_entries : kLdsStack;
-}
+// The persistent kernels keep only the top s.lds_entries entries in LDS (so
+// LDS does not cap occupancy) and spill deeper entries to a per-thread global
+// area ([entry - lds_entries][thread], coalesced per depth), rarely touched.
 inline size_t persistent_stack_bytes(const DevScene &s) {
-  return (size_t)lds_stack_entries(s) * kTraceBlock * sizeof(int32_t);
+  return (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t);
 }
 constexpr int kShadeBlock = 256;
 
@@ -164,6 +161,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
                                            int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr) {
   const uint32_t lane = lane_id();
   int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
+  const int lds_n = (int)s.lds_entries;
   bool has = false, exhausted = false, hit = false;
   uint32_t payload = 0, prim = 0xffffffffu;
   TraceRay r;
@@ -211,10 +209,10 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
         if (h0 && h1) {
           const bool first0 = t0 <= t1;
           const int32_t far = first0 ? ch.y : ch.x;
-          if ((uint32_t)sp < kLdsStack)
+          if (sp < lds_n)
             stk[sp * kTraceBlock] = far;
           else
-            ovf[(size_t)(sp - (int)kLdsStack) * s.ovf_threads] = far;
+            ovf[(size_t)(sp - lds_n) * s.ovf_threads] = far;
           ++sp;
           node = first0 ? ch.x : ch.y;
         } else if (h0) {
@@ -223,7 +221,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
           node = ch.y;
         } else if (sp > 0) {
           --sp;
-          node = (uint32_t)sp < kLdsStack ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - (int)kLdsStack) * s.ovf_threads];
+          node = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];
         } else {
           node = kTravDone;
         }
@@ -254,7 +252,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
           node = kTravDone;
         } else if (sp > 0) {
           --sp;
-          node = (uint32_t)sp < kLdsStack ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - (int)kLdsStack) * s.ovf_threads];
+          node = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];
         } else {
           node = kTravDone;
         }

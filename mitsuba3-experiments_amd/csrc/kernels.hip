@@ -144,9 +144,17 @@ __global__ void k_raygen_camera(DevScene s, WaveBuffers b, ChunkParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) b.counters[0] = p.n_paths;
   if (i >= p.n_paths) return;
-  // sample-major path order (path = s * n_px + q): film stage 1 then reads
-  // each pixel's samples with lanes on consecutive pixels (coalesced)
-  const uint32_t smp = i / p.n_px, px_local = i - smp * p.n_px;
+  // path order within the chunk (wavefront.h): pixel-major keeps the samples
+  // of one pixel in one wave (coherent traversal); sample-major puts
+  // consecutive pixels in a wave
+  uint32_t smp, px_local;
+  if (p.sample_major) {
+    smp = i / p.n_px;
+    px_local = i - smp * p.n_px;
+  } else {
+    px_local = i / p.spp;
+    smp = i - px_local * p.spp;
+  }
   const uint32_t pix = p.px0 + px_local;
   const uint32_t y = pix / p.width, x = pix - y * p.width;
   const uint32_t lane = pix * p.spp_total + p.sample_offset + smp;
@@ -500,7 +508,7 @@ __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
-    const uint32_t path = sidx * p.n_px + q;
+    const uint32_t path = p.sample_major ? sidx * p.n_px + q : q * p.spp + sidx;
     const float2 ps = b.pos[path];
     const V3 L = final_L(b, p, path);
 #pragma unroll

@@ -77,8 +77,9 @@ __device__ __forceinline__ uint4 st_rng(const Pcg32 &g, uint32_t w) {
 __device__ __forceinline__ float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
 // lane i = q * spp + s (pixel-major, the sampler lane order) -> wavefront
-// path index s * n_px + q (sample-major, see wavefront.h)
+// path index (see wavefront.h)
 __device__ __forceinline__ uint32_t path_of(uint32_t i, const ChunkParams &p) {
+  if (!p.sample_major) return i;
   const uint32_t q = i / p.spp;
   return (i - q * p.spp) * p.n_px + q;
 }

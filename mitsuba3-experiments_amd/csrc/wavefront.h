@@ -30,7 +30,7 @@ enum : uint32_t {
 };
 
 constexpr int kTraceBlock = 128;     // threads per traversal block
-constexpr uint32_t kLdsStack = 16;   // traversal stack entries per lane held in LDS (persistent kernels)
+constexpr uint32_t kLdsStack = 16;   // default LDS part of the persistent traversal stack (entries per lane)
 
 struct DevScene {
   const int4 *nodes;  // 4 x int4 per node
@@ -48,7 +48,8 @@ struct DevScene {
   const float *tables;
   uint32_t n_tris, n_emitters;
   uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane)
-  int32_t *stack_ovf;      // persistent kernels: entries beyond kLdsStack, [entry][thread]
+  uint32_t lds_entries;    // persistent kernels: stack entries kept in LDS
+  int32_t *stack_ovf;      // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
   mtx_camera camera;
 };
@@ -121,6 +122,7 @@ struct ChunkParams {
   uint32_t stats;
   uint32_t large_step;  // PSSMLT: i % 50 == 0 (pssmlt.py:209)
   uint32_t restir;      // ReSTIR GI secondary paths (path-mis loop, restirgi.py:459-588)
+  uint32_t sample_major;  // chunk path order: 1 = s * n_px + q, 0 = q * spp + s
 };
 
 // -------- launch wrappers (kernels.hip) --------
