@@ -108,15 +108,19 @@ typedef struct mtx_camera {
   uint32_t pad;
 } mtx_camera;
 
-/* BVH2 node (64 B): bounds of both children, Aila-Laine layout.
- *   f[0..3]  = c0.lo.x c0.hi.x c0.lo.y c0.hi.y
- *   f[4..7]  = c1.lo.x c1.hi.x c1.lo.y c1.hi.y
- *   f[8..11] = c0.lo.z c0.hi.z c1.lo.z c1.hi.z
- *   i[12], i[13] = child0, child1: >= 0 inner node index,
- *                  < 0 leaf: ~c = (first_tri << 3) | (count - 1)
- *   i[14], i[15] = 0
+/* BVH node (64 B): up to 4 children with 8-bit quantised boxes, collapsed
+ * from a binned-SAH BVH2 (bvh_build.cpp). Words:
+ *   f[0..2] = origin.xyz (fp32);  w[3] = bytes [ex, ey, ez, n_children],
+ *             e* int8: axis scale 2^e
+ *   i[4..7] = child refs: >= 0 inner node index,
+ *             < 0 leaf: ~c = (first_tri << 3) | (count - 1)
+ *   w[8..13] = q_lo.x, q_hi.x, q_lo.y, q_hi.y, q_lo.z, q_hi.z: one byte per
+ *             child (child k in bits 8k..8k+7); bound = origin + q * 2^e in
+ *             fp32, conservative (contains the child's padded box)
+ *   w[14], w[15] = 0
  * Triangles are stored in leaf order as 12 floats (48 B):
  *   v0.xyz, 0, e1 = v1-v0 .xyz, 0, e2 = v2-v0 .xyz, 0 */
+#define MTX_BVH_WIDTH 4
 #define MTX_BVH_MAX_LEAF 8
 #define MTX_BVH_MAX_DEPTH 40
 

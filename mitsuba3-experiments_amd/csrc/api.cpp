@@ -186,24 +186,9 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     mtx_set_error("mtx_scene_upload: incomplete scene (need geometry, BVH, shapes, materials, >=1 emitter)");
     return MTX_E_ARG;
   }
-  // Validate indices on the host so that no kernel can read out of bounds.
-  for (uint32_t i = 0; i < d->n_nodes; ++i)
-    for (int k = 12; k < 14; ++k) {
-      int32_t ch = d->nodes[16 * (size_t)i + k];
-      if (ch >= 0) {
-        if ((uint32_t)ch >= d->n_nodes) {
-          mtx_set_error("mtx_scene_upload: node %u child %d out of range", i, ch);
-          return MTX_E_ARG;
-        }
-      } else {
-        uint32_t x = (uint32_t)(~ch), first = x >> 3, cnt = (x & 7u) + 1;
-        if ((uint64_t)first + cnt > d->n_tris) {
-          mtx_set_error("mtx_scene_upload: leaf [%u,+%u) exceeds %u triangles", first, cnt, d->n_tris);
-          return MTX_E_ARG;
-        }
-      }
-    }
-  // BVH depth (stack entries of the traversal kernels); also rejects cycles.
+  // Validate indices on the host so that no kernel can read out of bounds,
+  // and find the tree depth (stack entries of the traversal kernels: each
+  // wide level pushes at most 3 entries); also rejects cycles.
   uint32_t bvh_depth = 0;
   {
     std::vector<std::pair<int32_t, uint32_t>> todo{{0, 0u}};
@@ -211,14 +196,32 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     while (!todo.empty()) {
       auto [nd, dep] = todo.back();
       todo.pop_back();
-      bvh_depth = std::max(bvh_depth, dep);
-      if (++visited > d->n_nodes || dep > MTX_BVH_MAX_DEPTH) {
+      bvh_depth = std::max(bvh_depth, dep + 1);
+      if (++visited > d->n_nodes || dep >= MTX_BVH_MAX_DEPTH) {
         mtx_set_error("mtx_scene_upload: BVH is not a tree of depth <= %d", MTX_BVH_MAX_DEPTH);
         return MTX_E_ARG;
       }
-      for (int k = 12; k < 14; ++k) {
-        int32_t ch = d->nodes[16 * (size_t)nd + k];
-        if (ch >= 0) todo.push_back({ch, dep + 1});
+      const int32_t *w = d->nodes + 16 * (size_t)nd;
+      const uint32_t nch = (uint32_t)w[3] >> 24;
+      if (nch < 1 || nch > MTX_BVH_WIDTH) {
+        mtx_set_error("mtx_scene_upload: node %d has %u children", nd, nch);
+        return MTX_E_ARG;
+      }
+      for (uint32_t k = 0; k < nch; ++k) {
+        const int32_t ch = w[4 + k];
+        if (ch >= 0) {
+          if ((uint32_t)ch >= d->n_nodes) {
+            mtx_set_error("mtx_scene_upload: node %d child %d out of range", nd, ch);
+            return MTX_E_ARG;
+          }
+          todo.push_back({ch, dep + 1});
+        } else {
+          uint32_t x = (uint32_t)(~ch), first = x >> 3, cnt = (x & 7u) + 1;
+          if ((uint64_t)first + cnt > d->n_tris) {
+            mtx_set_error("mtx_scene_upload: leaf [%u,+%u) exceeds %u triangles", first, cnt, d->n_tris);
+            return MTX_E_ARG;
+          }
+        }
       }
     }
   }
@@ -290,7 +293,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.tables = (const float *)c->tables.p;
   s.n_tris = d->n_tris;
   s.n_emitters = d->n_emitters;
-  s.stack_entries = bvh_depth + 1;
+  s.stack_entries = 3 * bvh_depth + 1;
   s.camera = d->camera;
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);

@@ -1,10 +1,11 @@
 // bvh_build.cpp — host-side scene preprocessing for libmtx.
 //
-// * Binned-SAH BVH2 over an indexed triangle mesh, emitted in the 64-byte
-//   Aila-Laine node layout of mtx.h (both child boxes per node) with the
+// * Binned-SAH BVH2 over an indexed triangle mesh, collapsed into 4-wide
+//   nodes with 8-bit quantised child boxes (64 B, layout in mtx.h) with the
 //   triangles reordered into leaf order as {v0, e1, e2} records. Replaces the
 //   Embree / OptiX acceleration-structure build that mi.load_file performs
-//   upstream for Scene.ray_intersect (path-mis.py:69-71).
+//   upstream for Scene.ray_intersect (path-mis.py:69-71). The wide node
+//   halves the node fetches per ray of the memory-pipeline-bound traversal.
 // * roughplastic precompute (upstream roughplastic constructor): the
 //   64-entry external transmittance table and the internal reflectance.
 //
@@ -18,6 +19,7 @@
 
 #include "mtx.h"
 #include "mtx_core/bsdf.h"
+#include "mtx_core/geometry.h"
 #include "mtx_core/microfacet.h"
 
 void mtx_set_error(const char *fmt, ...);
@@ -207,6 +209,96 @@ struct Builder {
     return (int32_t)node;
   }
 
+  // ---- collapse to 4-wide quantised nodes --------------------------------
+  struct Child {
+    int32_t ref;  // BVH2 ref (inner index or leaf code)
+    Box box;      // padded fp32 box
+  };
+  std::vector<int32_t> wnodes;  // 16 words per wide node
+  uint32_t wide_depth = 0;
+
+  Box child_box2(uint32_t node, int c) const {
+    const float *f = reinterpret_cast<const float *>(&nodes[16 * (size_t)node]);
+    Box b;
+    if (c == 0) {
+      b.lo[0] = f[0]; b.hi[0] = f[1]; b.lo[1] = f[2]; b.hi[1] = f[3]; b.lo[2] = f[8]; b.hi[2] = f[9];
+    } else {
+      b.lo[0] = f[4]; b.hi[0] = f[5]; b.lo[1] = f[6]; b.hi[1] = f[7]; b.lo[2] = f[10]; b.hi[2] = f[11];
+    }
+    return b;
+  }
+
+  // Opens the inner child with the largest surface area (ties: first) until
+  // the node has 4 children or only leaves remain.
+  int32_t collapse(uint32_t node2, uint32_t depth) {
+    std::vector<Child> ch = {{nodes[16 * (size_t)node2 + 12], child_box2(node2, 0)},
+                             {nodes[16 * (size_t)node2 + 13], child_box2(node2, 1)}};
+    while (ch.size() < MTX_BVH_WIDTH) {
+      int best = -1;
+      float best_area = -1.f;
+      for (int i = 0; i < (int)ch.size(); ++i)
+        if (ch[i].ref >= 0 && ch[i].box.area() > best_area) {
+          best_area = ch[i].box.area();
+          best = i;
+        }
+      if (best < 0) break;
+      const uint32_t n2 = (uint32_t)ch[best].ref;
+      Child a{nodes[16 * (size_t)n2 + 12], child_box2(n2, 0)}, b{nodes[16 * (size_t)n2 + 13], child_box2(n2, 1)};
+      ch[best] = a;
+      ch.insert(ch.begin() + best + 1, b);
+    }
+    const uint32_t w = (uint32_t)(wnodes.size() / 16);
+    wnodes.resize(wnodes.size() + 16, 0);
+    wide_depth = std::max(wide_depth, depth + 1);
+    int32_t refs[MTX_BVH_WIDTH] = {0, 0, 0, 0};
+    for (size_t k = 0; k < ch.size(); ++k)
+      refs[k] = ch[k].ref >= 0 ? collapse((uint32_t)ch[k].ref, depth + 1) : ch[k].ref;
+    return encode(w, ch, refs) ? (int32_t)w : INT32_MIN;
+  }
+
+  bool quant_ok = true;
+
+  bool encode(uint32_t w, const std::vector<Child> &ch, const int32_t *refs) {
+    Box u;
+    u.reset();
+    for (const Child &c : ch) u.grow(c.box);
+    int32_t *W = &wnodes[16 * (size_t)w];
+    uint32_t q[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t ebytes = 0;
+    for (int a = 0; a < 3; ++a) {
+      const float org = u.lo[a];
+      const double ext = (double)u.hi[a] - (double)org;
+      int e = -126;
+      if (ext > 0.0) {
+        int ee;
+        std::frexp(ext / 255.0, &ee);
+        e = std::max(-126, std::min(127, ee));
+      }
+      while (e < 127 && mtx::wide_decode(org, mtx::wide_scale((uint32_t)(e & 255)), 255u) < u.hi[a]) ++e;
+      const float sc = mtx::wide_scale((uint32_t)(e & 255));
+      const double dsc = std::ldexp(1.0, e);
+      for (size_t k = 0; k < ch.size(); ++k) {
+        double flo = std::floor(((double)ch[k].box.lo[a] - (double)org) / dsc);
+        double fhi = std::ceil(((double)ch[k].box.hi[a] - (double)org) / dsc);
+        uint32_t qlo = (uint32_t)std::max(0.0, std::min(255.0, flo));
+        uint32_t qhi = (uint32_t)std::max(0.0, std::min(255.0, fhi));
+        while (qlo > 0 && mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a]) --qlo;
+        while (qhi < 255 && mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a]) ++qhi;
+        if (mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a] || mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a])
+          quant_ok = false;
+        q[2 * a] |= qlo << (8 * k);
+        q[2 * a + 1] |= qhi << (8 * k);
+      }
+      std::memcpy(&W[a], &org, 4);
+      ebytes |= (uint32_t)(e & 255) << (8 * a);
+    }
+    ebytes |= (uint32_t)ch.size() << 24;
+    W[3] = (int32_t)ebytes;
+    for (int k = 0; k < MTX_BVH_WIDTH; ++k) W[4 + k] = refs[k];
+    for (int k = 0; k < 6; ++k) W[8 + k] = (int32_t)q[k];
+    return true;
+  }
+
   void run() {
     for (uint32_t t = 0; t < n; ++t)
       for (int k = 0; k < 3; ++k)
@@ -273,8 +365,14 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     mtx_set_error("mtx_bvh_build: internal error (%zu leaf triangles for %u)", b.order.size(), n_tris);
     return MTX_E_ARG;
   }
-  uint32_t n_nodes = (uint32_t)(b.nodes.size() / 16);
-  std::memcpy(nodes_out, b.nodes.data(), b.nodes.size() * sizeof(int32_t));
+  b.wnodes.reserve(b.nodes.size() / 2 + 16);
+  b.collapse(0, 0);
+  if (!b.quant_ok) {
+    mtx_set_error("mtx_bvh_build: child box quantisation failed (non-finite or huge coordinates?)");
+    return MTX_E_ARG;
+  }
+  uint32_t n_nodes = (uint32_t)(b.wnodes.size() / 16);
+  std::memcpy(nodes_out, b.wnodes.data(), b.wnodes.size() * sizeof(int32_t));
   *n_nodes_out = n_nodes;
   for (uint32_t i = 0; i < n_tris; ++i) {
     uint32_t t = b.order[i];
@@ -287,7 +385,7 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     g[4] = p1[0] - p0[0]; g[5] = p1[1] - p0[1]; g[6] = p1[2] - p0[2]; g[7] = 0.f;
     g[8] = p2[0] - p0[0]; g[9] = p2[1] - p0[1]; g[10] = p2[2] - p0[2]; g[11] = 0.f;
   }
-  if (depth_out) *depth_out = b.max_depth_seen;
+  if (depth_out) *depth_out = b.wide_depth;
   return MTX_OK;
 }
 

@@ -71,35 +71,41 @@ struct Hit {
   uint32_t prim;
 };
 
-// Scalar BVH2 traversal. Visit order (shared with the device kernel): at an
-// inner node, if both children are entered, continue with the one with the
-// smaller entry distance (ties -> child 0) and push the other.
-Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
+// Scalar traversal of the 4-wide BVH. Visit order (shared with the device
+// kernels through mtx_core/geometry.h wide_ranks): hit children by ascending
+// entry distance (ties by slot); the nearest is visited next, the others are
+// pushed farthest first. Closest-hit ties on t go to the smaller prim, so the
+// hit does not depend on the order; the visit counts do, and match the device.
+template <bool ANY>
+bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *nodes_visited,
+                uint32_t *tris_visited) {
   TraceRay r = make_trace_ray(o, d, maxt);
   Hit h{maxt, 0.f, 0.f, 0xffffffffu};
   float tbest = maxt;
-  int32_t stack[MTX_BVH_MAX_DEPTH + 2];
+  int32_t stack[3 * MTX_BVH_MAX_DEPTH + 2];
   int sp = 0;
   int32_t node = 0;
   uint32_t nv = 0, tv = 0;
+  bool hit = false;
   while (true) {
     if (node >= 0) {
-      const int32_t *ni = s.nodes + 16 * node;
-      const float *nf = reinterpret_cast<const float *>(ni);
+      const int32_t *w = s.nodes + 16 * (size_t)node;
+      const float *f = reinterpret_cast<const float *>(w);
       ++nv;
-      float t0 = box_enter(r, nf[0], nf[1], nf[2], nf[3], nf[8], nf[9], tbest);
-      float t1 = box_enter(r, nf[4], nf[5], nf[6], nf[7], nf[10], nf[11], tbest);
-      bool h0 = t0 != kInf, h1 = t1 != kInf;
-      if (h0 && h1) {
-        bool first0 = t0 <= t1;
-        stack[sp++] = first0 ? ni[13] : ni[12];
-        node = first0 ? ni[12] : ni[13];
-        continue;
-      } else if (h0) {
-        node = ni[12];
-        continue;
-      } else if (h1) {
-        node = ni[13];
+      const uint32_t eb = (uint32_t)w[3];
+      const int nch = (int)(eb >> 24);
+      const float sx = wide_scale(eb), sy = wide_scale(eb >> 8), sz = wide_scale(eb >> 16);
+      float t[4];
+      for (int k = 0; k < 4; ++k)
+        t[k] = k < nch ? wide_child_enter(r, f[0], f[1], f[2], sx, sy, sz, (uint32_t)w[8], (uint32_t)w[9],
+                                          (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], k,
+                                          tbest)
+                       : kInf;
+      int rank[4];
+      const int n = wide_ranks(t, rank);
+      if (n > 0) {
+        for (int rr = n - 1; rr >= 1; --rr) stack[sp++] = wide_pick(rank, w + 4, rr);
+        node = wide_pick(rank, w + 4, 0);
         continue;
       }
     } else {
@@ -111,6 +117,10 @@ Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_vi
         float t, u, v;
         ++tv;
         if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
+          if (ANY) {
+            hit = true;
+            break;
+          }
           if (t < tbest || (t == tbest && prim < h.prim)) {
             tbest = t;
             h.t = t;
@@ -120,6 +130,7 @@ Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_vi
           }
         }
       }
+      if (ANY && hit) break;
     }
     if (sp == 0) break;
     node = stack[--sp];
@@ -127,53 +138,18 @@ Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_vi
   if (nodes_visited) *nodes_visited = nv;
   if (tris_visited) *tris_visited = tv;
   if (h.prim == 0xffffffffu) h.t = kInf;
+  if (out) *out = h;
+  return ANY ? hit : h.prim != 0xffffffffu;
+}
+
+Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
+  Hit h;
+  trace_wide<false>(s, o, d, maxt, &h, nodes_visited, tris_visited);
   return h;
 }
 
 bool trace_any(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
-  TraceRay r = make_trace_ray(o, d, maxt);
-  int32_t stack[MTX_BVH_MAX_DEPTH + 2];
-  int sp = 0;
-  int32_t node = 0;
-  uint32_t nv = 0, tv = 0;
-  bool hit = false;
-  while (!hit) {
-    if (node >= 0) {
-      const int32_t *ni = s.nodes + 16 * node;
-      const float *nf = reinterpret_cast<const float *>(ni);
-      ++nv;
-      float t0 = box_enter(r, nf[0], nf[1], nf[2], nf[3], nf[8], nf[9], maxt);
-      float t1 = box_enter(r, nf[4], nf[5], nf[6], nf[7], nf[10], nf[11], maxt);
-      bool h0 = t0 != kInf, h1 = t1 != kInf;
-      if (h0 && h1) {
-        bool first0 = t0 <= t1;
-        stack[sp++] = first0 ? ni[13] : ni[12];
-        node = first0 ? ni[12] : ni[13];
-        continue;
-      } else if (h0) {
-        node = ni[12];
-        continue;
-      } else if (h1) {
-        node = ni[13];
-        continue;
-      }
-    } else {
-      uint32_t first, count;
-      leaf_decode(node, &first, &count);
-      for (uint32_t k = 0; k < count && !hit; ++k) {
-        const float *g = s.tri_geom + 12 * (size_t)(first + k);
-        float t, u, v;
-        ++tv;
-        hit = tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, maxt, &t, &u, &v);
-      }
-      if (hit) break;
-    }
-    if (sp == 0) break;
-    node = stack[--sp];
-  }
-  if (nodes_visited) *nodes_visited = nv;
-  if (tris_visited) *tris_visited = tv;
-  return hit;
+  return trace_wide<true>(s, o, d, maxt, nullptr, nodes_visited, tris_visited);
 }
 
 Hit brute_closest(const SceneView &s, V3 o, V3 d, float maxt) {

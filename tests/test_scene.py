@@ -60,10 +60,20 @@ def test_scene_is_deterministic(small_scene):
     assert digest(small_scene) == digest(other)
 
 
+def _decode(org, e, q):
+    """Child bound = origin + q * 2^e in fp32 (mtx.h / geometry.h wide_decode)."""
+    sc = np.float32(2.0) ** np.float32(e)
+    return np.float32(org) + np.float32(q) * sc
+
+
 def test_bvh_invariants(small_scene):
+    """4-wide quantised nodes (mtx.h): every triangle in exactly one leaf of
+    at most 8, children's decoded boxes contain their triangles / subtrees,
+    depth as reported."""
     s = small_scene
     nodes = s.nodes.reshape(-1, 16)
     f = nodes.view(np.float32)
+    u = nodes.view(np.uint32)
     seen = np.zeros(s.n_tris, np.int32)
     geom = s.tri_geom.reshape(-1, 12)
     v0 = geom[:, 0:3]
@@ -71,25 +81,47 @@ def test_bvh_invariants(small_scene):
     v2 = v0 + geom[:, 8:11]
     lo = np.minimum(np.minimum(v0, v1), v2)
     hi = np.maximum(np.maximum(v0, v1), v2)
-    depth = np.zeros(len(nodes), np.int32)
-    stack = [0]
-    max_depth = 1
+
+    def subtree_box(ref):
+        if ref < 0:
+            x = ~int(ref)
+            a, c = x >> 3, (x & 7) + 1
+            return lo[a:a + c].min(0), hi[a:a + c].max(0)
+        return boxes[ref]
+
+    boxes = {}
+    order = []
+    stack = [(0, 1)]
+    max_depth = 0
     while stack:
-        i = stack.pop()
-        for c, bx in ((nodes[i, 12], (0, 1, 2, 3, 8, 9)), (nodes[i, 13], (4, 5, 6, 7, 10, 11))):
-            b = f[i, list(bx)]
-            blo, bhi = b[[0, 2, 4]], b[[1, 3, 5]]
+        i, dep = stack.pop()
+        order.append(i)
+        max_depth = max(max_depth, dep)
+        nch = int(u[i, 3] >> 24)
+        assert 1 <= nch <= 4
+        for k in range(nch):
+            c = int(nodes[i, 4 + k])
             if c >= 0:
-                depth[c] = depth[i] + 1
-                max_depth = max(max_depth, depth[c] + 1)
-                stack.append(c)
-                continue
-            x = ~int(c)
-            first, cnt = x >> 3, (x & 7) + 1
-            assert cnt <= 8
-            seen[first:first + cnt] += 1
-            assert (lo[first:first + cnt] >= blo).all() and (hi[first:first + cnt] <= bhi).all()
-    assert (seen >= 1).all()
+                stack.append((c, dep + 1))
+            else:
+                x = ~c
+                first, cnt = x >> 3, (x & 7) + 1
+                assert cnt <= 8
+                seen[first:first + cnt] += 1
+    for i in reversed(order):  # children before parents
+        nch = int(u[i, 3] >> 24)
+        e = [np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)) for a in range(3)]
+        blo = np.full(3, np.inf, np.float32)
+        bhi = np.full(3, -np.inf, np.float32)
+        for k in range(nch):
+            clo, chi = subtree_box(int(nodes[i, 4 + k]))
+            for a in range(3):
+                qlo = (u[i, 8 + 2 * a] >> (8 * k)) & 255
+                qhi = (u[i, 9 + 2 * a] >> (8 * k)) & 255
+                assert _decode(f[i, a], e[a], qlo) <= clo[a] and _decode(f[i, a], e[a], qhi) >= chi[a]
+            blo, bhi = np.minimum(blo, clo), np.maximum(bhi, chi)
+        boxes[i] = (blo, bhi)
+    assert (seen == 1).all() or ((seen >= 1).all() and s.n_tris == 1)
     assert max_depth <= 40 and max_depth == s.bvh_depth
 
 
