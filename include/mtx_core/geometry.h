@@ -68,39 +68,50 @@ MTX_HD float wide_scale(uint32_t e_byte) {
 }
 MTX_HD float wide_decode(float origin, float scale, uint32_t q) { return origin + (float)q * scale; }
 
-// Entry distance of child k (slot 0..3), +inf if missed. qlx.. hold the four
-// children's 8-bit bounds, child k in bits [8k, 8k+8).
-MTX_HD float wide_child_enter(const TraceRay &r, float ox, float oy, float oz, float sx, float sy, float sz,
-                              uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
-                              int k, float tfar) {
-  const int sh = 8 * k;
-  return box_enter(r, wide_decode(ox, sx, (qlx >> sh) & 255u), wide_decode(ox, sx, (qhx >> sh) & 255u),
-                   wide_decode(oy, sy, (qly >> sh) & 255u), wide_decode(oy, sy, (qhy >> sh) & 255u),
-                   wide_decode(oz, sz, (qlz >> sh) & 255u), wide_decode(oz, sz, (qhz >> sh) & 255u), tfar);
-}
-
-// Visit order of a node's children: hits by ascending entry distance, ties by
-// slot; rank[k] is child k's position (misses rank after all hits). Returns
-// the number of hits. The nearest hit is visited next, the others are pushed
-// farthest first.
-MTX_HD int wide_ranks(const float t[4], int rank[4]) {
-  int n = 0;
+// Slab tests of a node's children in the node's quantised frame: with
+// a = 2^e / d and b = (origin - o) / d per axis, a bound q is at
+// t = fma(q, a, b). Children hit within (0, tfar] get the sort key
+// (t bits with the 2 low bits cleared) | slot, misses 0x7f800000 | slot; the
+// four keys are sorted ascending (5 compare-exchanges), so the visit order is
+// by entry distance, near-ties by slot. Returns the number of hits.
+// qlx.. hold the four children's 8-bit bounds, child k in bits [8k, 8k+8).
+MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint32_t eb, uint32_t qlx,
+                           uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz, float tfar,
+                           uint32_t key[4]) {
+  const int nch = (int)(eb >> 24);
+  const float ax = wide_scale(eb) * r.idir.x, bx = (ox - r.o.x) * r.idir.x;
+  const float ay = wide_scale(eb >> 8) * r.idir.y, by = (oy - r.o.y) * r.idir.y;
+  const float az = wide_scale(eb >> 16) * r.idir.z, bz = (oz - r.o.z) * r.idir.z;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    int rk = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) rk += (j != k && (t[j] < t[k] || (t[j] == t[k] && j < k))) ? 1 : 0;
-    rank[k] = rk;
-    n += t[k] != kInf ? 1 : 0;
+    const int sh = 8 * k;
+    const float lx = fmaf((float)((qlx >> sh) & 255u), ax, bx), hx = fmaf((float)((qhx >> sh) & 255u), ax, bx);
+    const float ly = fmaf((float)((qly >> sh) & 255u), ay, by), hy = fmaf((float)((qhy >> sh) & 255u), ay, by);
+    const float lz = fmaf((float)((qlz >> sh) & 255u), az, bz), hz = fmaf((float)((qhz >> sh) & 255u), az, bz);
+    const float tmin = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
+    const float tmax = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tfar));
+    const bool hit = k < nch && tmin <= tmax;
+    key[k] = hit ? ((f2u(tmin) & 0x7ffffffcu) | (uint32_t)k) : (0x7f800000u | (uint32_t)k);
   }
+#define MTX_CAS(i, j)                                   \
+  {                                                     \
+    const uint32_t lo_ = key[i] < key[j] ? key[i] : key[j]; \
+    const uint32_t hi_ = key[i] < key[j] ? key[j] : key[i]; \
+    key[i] = lo_;                                       \
+    key[j] = hi_;                                       \
+  }
+  MTX_CAS(0, 1) MTX_CAS(2, 3) MTX_CAS(0, 2) MTX_CAS(1, 3) MTX_CAS(1, 2)
+#undef MTX_CAS
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) n += key[k] < 0x7f800000u ? 1 : 0;
   return n;
 }
 
-MTX_HD int32_t wide_pick(const int rank[4], const int32_t ref[4], int r) {
-  int32_t v = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) v = rank[k] == r ? ref[k] : v;
-  return v;
+// Child reference of the slot encoded in a sort key.
+MTX_HD int32_t wide_ref(uint32_t key, int32_t r0, int32_t r1, int32_t r2, int32_t r3) {
+  const uint32_t k = key & 3u;
+  return k == 0u ? r0 : (k == 1u ? r1 : (k == 2u ? r2 : r3));
 }
 
 MTX_HD void leaf_decode(int32_t c, uint32_t *first, uint32_t *count) {

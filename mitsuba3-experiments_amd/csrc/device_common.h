@@ -72,30 +72,18 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// One visit of a 4-wide node (mtx.h layout): four loads (the last one 8 B),
-// four quantised slab tests, ordering by mtx_core/geometry.h wide_ranks.
-// Returns the number of children hit; ref[] / rank[] give the visit order.
+// One visit of a 4-wide node (mtx.h layout): four loads (the last one 8 B)
+// and mtx_core/geometry.h wide_node_order. Returns the number of children
+// hit; key[0..n) in visit order, rf the child references.
 __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
-                                          int32_t ref[4], int rank[4]) {
+                                          int4 &rf, uint32_t key[4]) {
   const int4 *np = s.nodes + 4 * node;
   const float4 a = __builtin_bit_cast(float4, np[0]);
-  const int4 rf = np[1];
+  rf = np[1];
   const int4 qa = np[2];
   const int2 qb = *reinterpret_cast<const int2 *>(np + 3);
-  const uint32_t eb = __float_as_uint(a.w);
-  const int nch = (int)(eb >> 24);
-  const float sx = wide_scale(eb), sy = wide_scale(eb >> 8), sz = wide_scale(eb >> 16);
-  float t[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    t[k] = k < nch ? wide_child_enter(r, a.x, a.y, a.z, sx, sy, sz, (uint32_t)qa.x, (uint32_t)qa.y, (uint32_t)qa.z,
-                                      (uint32_t)qa.w, (uint32_t)qb.x, (uint32_t)qb.y, k, tbest)
-                   : kInf;
-  ref[0] = rf.x;
-  ref[1] = rf.y;
-  ref[2] = rf.z;
-  ref[3] = rf.w;
-  return wide_ranks(t, rank);
+  return wide_node_order(r, a.x, a.y, a.z, __float_as_uint(a.w), (uint32_t)qa.x, (uint32_t)qa.y, (uint32_t)qa.z,
+                         (uint32_t)qa.w, (uint32_t)qb.x, (uint32_t)qb.y, tbest, key);
 }
 
 // ---------------------------------------------------------------------------
@@ -110,18 +98,18 @@ __device__ __forceinline__ bool traverse(const DevScene &s, int32_t *stk, const 
   bool hit_any = false;
   while (true) {
     if (node >= 0) {
-      int32_t ref[4];
-      int rank[4];
+      int4 rf;
+      uint32_t key[4];
       ++nv;
-      const int n = wide_visit(s, r, node, tbest, ref, rank);
+      const int n = wide_visit(s, r, node, tbest, rf, key);
       if (n > 0) {
 #pragma unroll
         for (int rr = 3; rr >= 1; --rr)
           if (rr < n) {
-            stk[sp * kTraceBlock] = wide_pick(rank, ref, rr);
+            stk[sp * kTraceBlock] = wide_ref(key[rr], rf.x, rf.y, rf.z, rf.w);
             ++sp;
           }
-        node = wide_pick(rank, ref, 0);
+        node = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
         continue;
       }
     } else {
@@ -215,22 +203,22 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     while (true) {
       // inner-node phase
       while (has && node >= 0) {
-        int32_t ref[4];
-        int rank[4];
+        int4 rf;
+        uint32_t key[4];
         ++nv;
-        const int n = wide_visit(s, r, node, tbest, ref, rank);
+        const int n = wide_visit(s, r, node, tbest, rf, key);
         if (n > 0) {
 #pragma unroll
           for (int rr = 3; rr >= 1; --rr)
             if (rr < n) {
-              const int32_t far = wide_pick(rank, ref, rr);
+              const int32_t far = wide_ref(key[rr], rf.x, rf.y, rf.z, rf.w);
               if (sp < lds_n)
                 stk[sp * kTraceBlock] = far;
               else
                 ovf[(size_t)(sp - lds_n) * s.ovf_threads] = far;
               ++sp;
             }
-          node = wide_pick(rank, ref, 0);
+          node = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
         } else if (sp > 0) {
           --sp;
           node = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];

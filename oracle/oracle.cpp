@@ -72,9 +72,9 @@ struct Hit {
 };
 
 // Scalar traversal of the 4-wide BVH. Visit order (shared with the device
-// kernels through mtx_core/geometry.h wide_ranks): hit children by ascending
-// entry distance (ties by slot); the nearest is visited next, the others are
-// pushed farthest first. Closest-hit ties on t go to the smaller prim, so the
+// kernels through mtx_core/geometry.h wide_node_order): hit children by
+// ascending entry distance (near-ties by slot); the nearest is visited next,
+// the others are pushed farthest first. Closest-hit ties on t go to the smaller prim, so the
 // hit does not depend on the order; the visit counts do, and match the device.
 template <bool ANY>
 bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *nodes_visited,
@@ -92,20 +92,12 @@ bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *
       const int32_t *w = s.nodes + 16 * (size_t)node;
       const float *f = reinterpret_cast<const float *>(w);
       ++nv;
-      const uint32_t eb = (uint32_t)w[3];
-      const int nch = (int)(eb >> 24);
-      const float sx = wide_scale(eb), sy = wide_scale(eb >> 8), sz = wide_scale(eb >> 16);
-      float t[4];
-      for (int k = 0; k < 4; ++k)
-        t[k] = k < nch ? wide_child_enter(r, f[0], f[1], f[2], sx, sy, sz, (uint32_t)w[8], (uint32_t)w[9],
-                                          (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], k,
-                                          tbest)
-                       : kInf;
-      int rank[4];
-      const int n = wide_ranks(t, rank);
+      uint32_t key[4];
+      const int n = wide_node_order(r, f[0], f[1], f[2], (uint32_t)w[3], (uint32_t)w[8], (uint32_t)w[9],
+                                    (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], tbest, key);
       if (n > 0) {
-        for (int rr = n - 1; rr >= 1; --rr) stack[sp++] = wide_pick(rank, w + 4, rr);
-        node = wide_pick(rank, w + 4, 0);
+        for (int rr = n - 1; rr >= 1; --rr) stack[sp++] = wide_ref(key[rr], w[4], w[5], w[6], w[7]);
+        node = wide_ref(key[0], w[4], w[5], w[6], w[7]);
         continue;
       }
     } else {
