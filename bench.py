@@ -148,6 +148,8 @@ def main():
                 "rays_per_step": int(cnt["rays_closest"]),
                 "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
                 "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2),
+                "simd_util_node_phase": round(cnt["nodes_closest"] / max(1, 64 * cnt["wave_node_iters"]), 3),
+                "simd_util_leaf_phase": round(cnt["tris_closest"] / max(1, 64 * cnt["wave_leaf_iters"]), 3),
             },
             "kernels_ms_per_step": {
                 "trace_closest": round(agg["trace_ms"] / args.steps, 3),

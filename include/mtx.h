@@ -194,6 +194,9 @@ typedef struct mtx_stats {
   uint64_t shadow_launches;
   double trace_ms, shadow_ms, shade_ms, other_ms; /* HIP-event time, summed */
   uint64_t paths;
+  /* closest-hit traversal wave iterations (node phase, leaf phase): SIMD
+   * utilisation = visits / (64 * iterations) */
+  uint64_t wave_node_iters, wave_leaf_iters;
 } mtx_stats;
 
 /* --------------------------- context ------------------------------ */

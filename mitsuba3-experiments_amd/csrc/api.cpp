@@ -725,6 +725,8 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       stats->tris_shadow = h[3];
       stats->rays_closest = h[4];
       stats->rays_shadow = h[5];
+      stats->wave_node_iters = h[6];
+      stats->wave_leaf_iters = h[7];
     }
     stats->trace_launches = n_trace;
     stats->shadow_launches = n_shadow;

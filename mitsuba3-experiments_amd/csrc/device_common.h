@@ -162,9 +162,10 @@ constexpr uint32_t kRefillLanes = 16;
 
 // Src provides: load(k, TraceRay&, float &tmax, uint32_t &payload) and
 // finish(payload, bool any_hit, float t, uint32_t prim, float u, float v).
-template <bool ANY, class Src>
+template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *fetch,
-                                           int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr) {
+                                           int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
+                                           uint32_t *wave_iters = nullptr) {
   const uint32_t lane = lane_id();
   int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
   const int lds_n = (int)s.lds_entries;
@@ -203,6 +204,10 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     while (true) {
       // inner-node phase
       while (has && node >= 0) {
+        if (STATS) {
+          const uint64_t m = __ballot(true);
+          if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[0];
+        }
         int4 rf;
         uint32_t key[4];
         ++nv;
@@ -228,6 +233,10 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
       }
       // leaf phase: one leaf per lane
       if (has && node != kTravDone) {
+        if (STATS) {
+          const uint64_t m = __ballot(true);
+          if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
+        }
         uint32_t first, cnt;
         leaf_decode(node, &first, &cnt);
         for (uint32_t k = 0; k < cnt; ++k) {

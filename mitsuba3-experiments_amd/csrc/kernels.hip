@@ -53,14 +53,18 @@ template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   const ClosestSrc src{b, b.queue[bounce & 1]};
-  uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop<false>(s, src, b.counters[4 * bounce + 0], &b.counters[4 * bounce + 2], stack + threadIdx.x, nv, tv, nr);
+  uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
+  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], &b.counters[4 * bounce + 2], stack + threadIdx.x, nv,
+                           tv, nr, wi);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
+    unsigned long long w0 = wave_sum_u64(wi[0]), w1 = wave_sum_u64(wi[1]);
     if ((threadIdx.x & 63) == 0) {
       atomicAdd(&b.stats[0], a);
       atomicAdd(&b.stats[1], c);
       atomicAdd(&b.stats[4], n);
+      atomicAdd(&b.stats[6], w0);
+      atomicAdd(&b.stats[7], w1);
     }
   }
 }

@@ -158,6 +158,8 @@ class Stats(C.Structure):
         ("shade_ms", C.c_double),
         ("other_ms", C.c_double),
         ("paths", C.c_uint64),
+        ("wave_node_iters", C.c_uint64),
+        ("wave_leaf_iters", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
