@@ -169,7 +169,8 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   const uint32_t lane = lane_id();
   int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
   const int lds_n = (int)s.lds_entries;
-  bool has = false, exhausted = false, hit = false;
+  bool has = false, exhausted = false, hit = false, drained = false;
+  uint32_t res_lo = 0, res_hi = 0;
   uint32_t payload = 0, prim = 0xffffffffu;
   TraceRay r;
   float tbest = 0.f, bu = 0.f, bv = 0.f;
@@ -177,27 +178,56 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   int sp = 0;
   while (true) {
     if (!exhausted) {
+      // Idle lanes take rays from the wave's reservoir of claimed queue
+      // indices [res_lo, res_hi); the reservoir is topped up with one atomic
+      // per s.trace_batch rays (contention on the device-scope counter, not
+      // the traversal, bounded short batches).
       const uint64_t idle = __ballot(!has);
       if (idle) {
         const uint32_t n = (uint32_t)__popcll(idle);
-        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(fetch, n);
-        base = __builtin_amdgcn_readlane(base, leader);
-        if (base + n >= count) exhausted = true;
-        if (!has) {
-          const uint32_t k = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-          if (k < count) {
-            src.load(k, r, tbest, payload);
-            prim = 0xffffffffu;
-            bu = bv = 0.f;
-            hit = false;
-            node = 0;
-            sp = 0;
-            has = true;
+        const uint32_t left = res_hi - res_lo;
+        uint32_t base2 = 0, got2 = 0;
+        if (left < n && !drained) {
+          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
+          uint32_t b = 0;
+          if (lane == leader) b = atomicAdd(fetch, s.trace_batch);
+          b = __builtin_amdgcn_readlane(b, leader);
+          if (b >= count) {
+            drained = true;
+          } else {
+            base2 = b;
+            got2 = min(s.trace_batch, count - b);
+            if (count - b <= s.trace_batch) drained = true;
           }
         }
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        uint32_t k = 0;
+        bool ok = false;
+        if (rk < left) {
+          k = res_lo + rk;
+          ok = true;
+        } else if (rk - left < got2) {
+          k = base2 + (rk - left);
+          ok = true;
+        }
+        if (n <= left) {
+          res_lo += n;
+        } else {
+          const uint32_t used2 = min(n - left, got2);
+          res_lo = base2 + used2;
+          res_hi = base2 + got2;
+        }
+        if (!has && ok) {
+          src.load(k, r, tbest, payload);
+          prim = 0xffffffffu;
+          bu = bv = 0.f;
+          hit = false;
+          node = 0;
+          sp = 0;
+          has = true;
+        }
+        exhausted = drained && res_lo >= res_hi;
       }
     }
     if (__ballot(has) == 0) break;

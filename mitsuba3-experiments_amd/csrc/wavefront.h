@@ -49,6 +49,7 @@ struct DevScene {
   uint32_t n_tris, n_emitters;
   uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane)
   uint32_t lds_entries;    // persistent kernels: stack entries kept in LDS
+  uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
   int32_t *stack_ovf;      // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
   mtx_camera camera;
