@@ -67,6 +67,44 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
   return base + prefix;
 }
 
+// Block-level stream compaction into two queues: one device-scope atomic
+// per queue per block step (instead of one per wave) -- same-address atomics
+// from every wave of the chip serialise. All threads of the block must call
+// it once per step; `parity` alternates between consecutive steps so that the
+// LDS slots of one step are not overwritten while a slow wave still reads them.
+template <int BLOCK>
+__device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c0, uint32_t *c1, uint32_t parity,
+                                              uint32_t &s0, uint32_t &s1) {
+  constexpr int W = BLOCK / 64;
+  __shared__ uint32_t wcnt[2][2][W];
+  __shared__ uint32_t bbase[2][2];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+  if (lane == 0) {
+    wcnt[parity][0][wave] = (uint32_t)__popcll(m0);
+    wcnt[parity][1][wave] = (uint32_t)__popcll(m1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t0 = 0, t1 = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      t0 += wcnt[parity][0][w];
+      t1 += wcnt[parity][1][w];
+    }
+    bbase[parity][0] = t0 ? atomicAdd(c0, t0) : 0u;
+    bbase[parity][1] = t1 ? atomicAdd(c1, t1) : 0u;
+  }
+  __syncthreads();
+  uint32_t o0 = bbase[parity][0], o1 = bbase[parity][1];
+  for (uint32_t w = 0; w < wave; ++w) {
+    o0 += wcnt[parity][0][w];
+    o1 += wcnt[parity][1][w];
+  }
+  s0 = o0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+  s1 = o1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+}
+
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;

@@ -466,11 +466,10 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
   uint32_t *out_q = b.queue[(bounce + 1) & 1];
   uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
   uint32_t *sh_cnt = &b.counters[4 * bounce + 1];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave_base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t base = wave_base; base < count; base += stride) {
-    const uint32_t i = base + lane;
+  const uint32_t stride = gridDim.x * kShadeBlock;
+  uint32_t parity = 0;
+  for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += stride, parity ^= 1u) {
+    const uint32_t i = base + threadIdx.x;
     ShadeIO io;
     io.emit = false;
     bool cont = false;
@@ -482,9 +481,9 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
       else
         cont = shade_path<INT>(sv, b, p, bounce, path, io);
     }
-    const uint32_t slot = wave_append(out_cnt, cont);
+    uint32_t slot, sslot;
+    block_append2<kShadeBlock>(cont, io.emit, out_cnt, sh_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path;
-    const uint32_t sslot = wave_append(sh_cnt, io.emit);
     if (io.emit) b.shadow[sslot] = io.rec;
   }
 }
