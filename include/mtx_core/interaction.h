@@ -47,40 +47,41 @@ MTX_HD V3 load3(const float *p, uint32_t i) { return V3{p[3 * i + 0], p[3 * i + 
 // Hit record -> SurfaceInteraction (upstream Mesh::compute_surface_interaction:
 // p = b0*p0 + b1*p1 + b2*p2, geometric normal from the winding, shading
 // normal from barycentric vertex normals unless face_normals; frame from the
-// shading normal with coordinate_system()).
-MTX_HD SurfaceInteraction compute_si(const SceneView &s, float t, uint32_t prim, float u, float v, V3 ray_d) {
+// shading normal with coordinate_system()). si_from_vertices is the shared
+// arithmetic; the host gathers the vertices through tri_vidx, the device from
+// per-triangle shading records holding the same floats.
+MTX_HD SurfaceInteraction si_invalid(float t, uint32_t prim, V3 ray_d) {
+  SurfaceInteraction si;
+  si.t = kInf;
+  si.prim = prim;
+  si.valid = false;
+  si.material = -1;
+  si.emitter = -1;
+  si.p = v3s(0.f);
+  si.n = V3{0.f, 0.f, 1.f};
+  si.sh = frame_from_normal(si.n);
+  si.uv = V2{0.f, 0.f};
+  si.wi = -ray_d;
+  (void)t;
+  return si;
+}
+
+MTX_HD SurfaceInteraction si_from_vertices(float t, uint32_t prim, float u, float v, V3 ray_d, V3 p0, V3 p1, V3 p2,
+                                           uint32_t material, int32_t emitter, bool use_n, V3 n0, V3 n1, V3 n2,
+                                           bool use_uv, V2 t0, V2 t1, V2 t2) {
   SurfaceInteraction si;
   si.t = t;
   si.prim = prim;
-  si.valid = prim != 0xffffffffu;
-  si.material = -1;
-  si.emitter = -1;
-  if (!si.valid) {
-    si.p = v3s(0.f);
-    si.n = V3{0.f, 0.f, 1.f};
-    si.sh = frame_from_normal(si.n);
-    si.uv = V2{0.f, 0.f};
-    si.wi = -ray_d;
-    si.t = kInf;
-    return si;
-  }
-  const uint32_t i0 = s.tri_vidx[3 * prim + 0], i1 = s.tri_vidx[3 * prim + 1], i2 = s.tri_vidx[3 * prim + 2];
-  const V3 p0 = load3(s.vpos, i0), p1 = load3(s.vpos, i1), p2 = load3(s.vpos, i2);
+  si.valid = true;
   float b1 = u, b2 = v, b0 = 1.f - b1 - b2;
   si.p = fma3(p0, b0, fma3(p1, b1, p2 * b2));
   V3 dp0 = p1 - p0, dp1 = p2 - p0;
   si.n = normalize(cross(dp0, dp1));
-  const mtx_shape sh = s.shapes[s.tri_shape[prim]];
-  si.material = (int32_t)sh.material;
-  si.emitter = sh.emitter;
+  si.material = (int32_t)material;
+  si.emitter = emitter;
   V3 ns = si.n;
-  if (!(sh.flags & 1u) && s.vnormal) {
-    V3 n0 = load3(s.vnormal, i0), n1 = load3(s.vnormal, i1), n2 = load3(s.vnormal, i2);
-    ns = normalize(fma3(n0, b0, fma3(n1, b1, n2 * b2)));
-  }
-  if ((sh.flags & 2u) && s.vuv) {
-    V2 t0 = V2{s.vuv[2 * i0], s.vuv[2 * i0 + 1]}, t1 = V2{s.vuv[2 * i1], s.vuv[2 * i1 + 1]},
-       t2 = V2{s.vuv[2 * i2], s.vuv[2 * i2 + 1]};
+  if (use_n) ns = normalize(fma3(n0, b0, fma3(n1, b1, n2 * b2)));
+  if (use_uv) {
     si.uv = V2{fmaf(t0.x, b0, fmaf(t1.x, b1, t2.x * b2)), fmaf(t0.y, b0, fmaf(t1.y, b1, t2.y * b2))};
   } else {
     si.uv = V2{b1, b2};
@@ -88,6 +89,29 @@ MTX_HD SurfaceInteraction compute_si(const SceneView &s, float t, uint32_t prim,
   si.sh = frame_from_normal(ns);
   si.wi = to_local(si.sh, -ray_d);
   return si;
+}
+
+MTX_HD SurfaceInteraction compute_si(const SceneView &s, float t, uint32_t prim, float u, float v, V3 ray_d) {
+  if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
+  const uint32_t i0 = s.tri_vidx[3 * prim + 0], i1 = s.tri_vidx[3 * prim + 1], i2 = s.tri_vidx[3 * prim + 2];
+  const V3 p0 = load3(s.vpos, i0), p1 = load3(s.vpos, i1), p2 = load3(s.vpos, i2);
+  const mtx_shape sh = s.shapes[s.tri_shape[prim]];
+  const bool use_n = !(sh.flags & 1u) && s.vnormal;
+  const bool use_uv = (sh.flags & 2u) && s.vuv;
+  V3 n0 = v3s(0.f), n1 = v3s(0.f), n2 = v3s(0.f);
+  V2 t0 = V2{0.f, 0.f}, t1 = t0, t2 = t0;
+  if (use_n) {
+    n0 = load3(s.vnormal, i0);
+    n1 = load3(s.vnormal, i1);
+    n2 = load3(s.vnormal, i2);
+  }
+  if (use_uv) {
+    t0 = V2{s.vuv[2 * i0], s.vuv[2 * i0 + 1]};
+    t1 = V2{s.vuv[2 * i1], s.vuv[2 * i1 + 1]};
+    t2 = V2{s.vuv[2 * i2], s.vuv[2 * i2 + 1]};
+  }
+  return si_from_vertices(t, prim, u, v, ray_d, p0, p1, p2, sh.material, sh.emitter, use_n, n0, n1, n2, use_uv, t0,
+                          t1, t2);
 }
 
 // Interaction::offset_p / spawn_ray / spawn_ray_to

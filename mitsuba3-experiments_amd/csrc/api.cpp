@@ -90,6 +90,7 @@ struct mtx_ctx {
   bool has_scene = false;
   // scene
   DevBuf stack_ovf;  // traversal stack entries beyond the LDS part
+  DevBuf shade_rec;  // per-triangle shading records
   DevBuf nodes, tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
@@ -169,7 +170,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
-                    &c->stack_ovf, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
+                    &c->stack_ovf, &c->shade_rec, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
@@ -278,6 +279,33 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   if ((rc = upload(c->textures, d->textures, d->n_textures, st))) return rc;
   if ((rc = upload(c->texels, d->texels, d->n_texels, st))) return rc;
   if ((rc = upload(c->tables, d->tables, d->n_tables, st))) return rc;
+  {
+    // per-triangle shading records (compute_si_dev)
+    std::vector<float> rec(32 * (size_t)d->n_tris, 0.f);
+    for (uint32_t t = 0; t < d->n_tris; ++t) {
+      float *r = &rec[32 * (size_t)t];
+      const mtx_shape &sh = d->shapes[d->tri_shape[t]];
+      const uint32_t use_n = (!(sh.flags & 1u) && d->vnormal) ? 1u : 0u;
+      const uint32_t use_uv = ((sh.flags & 2u) && d->vuv) ? 2u : 0u;
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t vi = d->tri_vidx[3 * (size_t)t + k];
+        for (int a = 0; a < 3; ++a) r[4 * k + a] = d->vpos[3 * (size_t)vi + a];
+        if (use_n)
+          for (int a = 0; a < 3; ++a) r[12 + 4 * k + a] = d->vnormal[3 * (size_t)vi + a];
+        if (use_uv) {
+          r[24 + 2 * k] = d->vuv[2 * (size_t)vi];
+          r[24 + 2 * k + 1] = d->vuv[2 * (size_t)vi + 1];
+        }
+      }
+      const uint32_t mat = sh.material, fl = use_n | use_uv;
+      const int32_t em = sh.emitter;
+      memcpy(&r[3], &mat, 4);
+      memcpy(&r[7], &em, 4);
+      memcpy(&r[11], &fl, 4);
+    }
+    if ((rc = upload(c->shade_rec, rec.data(), rec.size(), st))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));  // rec is freed at scope exit
+  }
   HIP_TRY(hipStreamSynchronize(st));
   mtxd::DevScene &s = c->scene;
   s.nodes = (const int4 *)c->nodes.p;
@@ -288,6 +316,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.vnormal = (const float *)c->vnormal.p;
   s.vuv = (const float *)c->vuv.p;
   s.shapes = (const mtx_shape *)c->shapes.p;
+  s.shade_rec = (const float4 *)c->shade_rec.p;
   s.materials = (const mtx_material *)c->materials.p;
   s.emitters = (const mtx_emitter *)c->emitters.p;
   s.textures = (const mtx_texture *)c->textures.p;

@@ -47,6 +47,37 @@ __device__ __forceinline__ SceneView make_view(const DevScene &s) {
   return v;
 }
 
+// Device compute_si: the triangle's vertices, normals, uvs and shape fields
+// come from one 128-B shading record (DevScene::shade_rec, built at upload in
+// leaf order) instead of the tri_vidx -> vertex gathers; same floats, same
+// arithmetic (si_from_vertices), so identical to the host compute_si.
+//   r0 p0.xyz material | r1 p1.xyz emitter | r2 p2.xyz use flags (bit0 vertex
+//   normals, bit1 uvs) | r3..r5 n0..n2 | r6 uv0, uv1 | r7 uv2
+__device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, float t, uint32_t prim, float u,
+                                                             float v, V3 ray_d) {
+  if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
+  const float4 *r = s.shade_rec + 8 * (size_t)prim;
+  const float4 a = r[0], b = r[1], c = r[2];
+  const uint32_t fl = __float_as_uint(c.w);
+  const bool use_n = (fl & 1u) != 0, use_uv = (fl & 2u) != 0;
+  V3 n0 = v3s(0.f), n1 = v3s(0.f), n2 = v3s(0.f);
+  V2 t0 = V2{0.f, 0.f}, t1 = t0, t2 = t0;
+  if (use_n) {
+    const float4 x = r[3], y = r[4], z = r[5];
+    n0 = V3{x.x, x.y, x.z};
+    n1 = V3{y.x, y.y, y.z};
+    n2 = V3{z.x, z.y, z.z};
+  }
+  if (use_uv) {
+    const float4 x = r[6], y = r[7];
+    t0 = V2{x.x, x.y};
+    t1 = V2{x.z, x.w};
+    t2 = V2{y.x, y.y};
+  }
+  return si_from_vertices(t, prim, u, v, ray_d, V3{a.x, a.y, a.z}, V3{b.x, b.y, b.z}, V3{c.x, c.y, c.z},
+                          __float_as_uint(a.w), (int32_t)__float_as_uint(b.w), use_n, n0, n1, n2, use_uv, t0, t1, t2);
+}
+
 __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }

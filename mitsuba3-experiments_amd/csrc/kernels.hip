@@ -28,7 +28,7 @@ using namespace mtx;
 
 // Tuning knob: minimum resident shade blocks per CU (caps VGPRs; 1 = none).
 #ifndef MTX_SHADE_MIN_BLOCKS
-#define MTX_SHADE_MIN_BLOCKS 1
+#define MTX_SHADE_MIN_BLOCKS 3
 #endif
 
 namespace mtxd {
@@ -219,7 +219,8 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
 }
 
 template <int INT>
-__device__ __forceinline__ bool shade_path(const SceneView &sv, const WaveBuffers &b, const ChunkParams &p,
+__device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
+                                           const ChunkParams &p,
                                            uint32_t bounce, uint32_t path, ShadeIO &io) {
   const float4 ro = b.ray_o[path], rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
   const uint4 mi = b.misc[path];
@@ -235,7 +236,7 @@ __device__ __forceinline__ bool shade_path(const SceneView &sv, const WaveBuffer
   V3 prev_p = V3{pv.x, pv.y, pv.z};
   float spread = pv.w, a0 = rd.w;
   const V3 ray_d = V3{rd.x, rd.y, rd.z};
-  const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
   io.emit = false;
 
   // ------------------------------ head ------------------------------------
@@ -398,7 +399,8 @@ __device__ __forceinline__ float dr_clamp(float x, float lo, float hi) { return 
 // re-evaluation (:93-96), proposed vertex write (:99), spawn, RR. Every
 // executed bounce consumes 4 draws: the chain's RNG stream continues across
 // the Metropolis iterations.
-__device__ __forceinline__ bool shade_pssmlt(const SceneView &sv, const WaveBuffers &b, const ChunkParams &p,
+__device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
+                                             const ChunkParams &p,
                                              uint32_t path) {
   const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path];
   const uint4 mi = b.misc[path];
@@ -412,7 +414,7 @@ __device__ __forceinline__ bool shade_pssmlt(const SceneView &sv, const WaveBuff
   float eta = th.w;
   V3 L = V3{Lr.x, Lr.y, Lr.z};
   float prev_pdf = Lr.w;
-  const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{rd.x, rd.y, rd.z});
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{rd.x, rd.y, rd.z});
   const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
   L = fma3v(T, le, L);
   const bool active_next = (depth + 1 < p.max_depth) && si.valid;
@@ -477,9 +479,9 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     if (i < count) {
       path = in_q[i];
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
-        cont = shade_pssmlt(sv, b, p, path);
+        cont = shade_pssmlt(s, sv, b, p, path);
       else
-        cont = shade_path<INT>(sv, b, p, bounce, path, io);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, io);
     }
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, sh_cnt, parity, slot, sslot);

@@ -98,7 +98,7 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
     const float4 h = b.hit[path], d4 = b.ray_d[path];
     r.prim_hit[i] = h;
     r.prim_dir[i] = d4;
-    const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
+    const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
     r.emit[i] = f4(emitter_eval(sv, si.emitter, si.wi), 0.f);
     Pcg32 rng = ld_rng(b.misc[path]);
     V3 wo;
@@ -326,7 +326,7 @@ __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   if (i >= r.n) return;
   const RReservoir R = ld_res(r.sres, r.n, i);
   const float4 h = r.prim_hit[i], d4 = r.prim_dir[i];
-  const SurfaceInteraction si = compute_si(sv, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
   V3 beta = v3s(0.f);
   if (si.valid) {
     float pdf_unused;

@@ -41,6 +41,7 @@ struct DevScene {
   const float *vnormal;
   const float *vuv;
   const mtx_shape *shapes;
+  const float4 *shade_rec;  // 8 float4 per triangle (device_common.h compute_si_dev)
   const mtx_material *materials;
   const mtx_emitter *emitters;
   const mtx_texture *textures;
