@@ -343,7 +343,17 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
 
 namespace {
 
-constexpr uint32_t kDefaultChunk = 1u << 26;  // 64 Mi paths (~13 GB of path state)
+// Default wavefront: up to 256 Mi paths (~200 B of state each, ~50 GB) so a
+// 1280x720 spp=256 frame runs as one chunk (fewer queue tails), bounded by
+// 40 % of the free HBM.
+constexpr uint32_t kDefaultChunk = 1u << 28;
+constexpr size_t kPathStateBytes = 200;
+uint32_t default_chunk(mtx_ctx *c) {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
+  const size_t fit = (size_t)((double)free_b * 0.4) / kPathStateBytes;
+  return (uint32_t)std::max<size_t>(1u << 20, std::min<size_t>(kDefaultChunk, fit));
+}
 
 int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   int rc;
@@ -653,7 +663,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     return MTX_E_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  uint32_t chunk_paths = a->chunk_paths ? a->chunk_paths : kDefaultChunk;
+  uint32_t chunk_paths = a->chunk_paths ? a->chunk_paths : default_chunk(c);
   uint32_t px_per_chunk = std::max<uint32_t>(1, chunk_paths / a->spp);
   const uint32_t band_px = (a->y1 - a->y0) * W;
   px_per_chunk = std::min(px_per_chunk, band_px);
@@ -836,7 +846,7 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     return MTX_E_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : kDefaultChunk;
+  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : default_chunk(c);
   const uint32_t cap = (uint32_t)std::min<uint64_t>(n, chunk);
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   if ((rc = dalloc(c->s0, 24ull * cap))) return rc;

@@ -504,6 +504,68 @@ __device__ __forceinline__ V3 final_L(const WaveBuffers &b, const ChunkParams &p
   return L;
 }
 
+// Pixel-major chunks: a pixel's samples are contiguous, so one wave stages
+// 64 pixels x kFilmStage samples through LDS with coalesced loads, then each
+// lane accumulates its own pixel in sample order (same order as below).
+constexpr int kFilmStage = 16;
+
+__device__ __forceinline__ void film_accumulate(float4 acc[9], int x, int y, float2 ps, V3 L) {
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const float wy = fmaxf(0.f, 1.f - fabsf(ps.y - ((float)(y + dy - 1) + 0.5f)));
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const float wx = fmaxf(0.f, 1.f - fabsf(ps.x - ((float)(x + dx - 1) + 0.5f)));
+      const float w = wx * wy;
+      float4 &c = acc[dy * 3 + dx];
+      c.x = c.x + L.x * w;
+      c.y = c.y + L.y * w;
+      c.z = c.z + L.z * w;
+      c.w = c.w + w;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkParams p, float4 *contrib) {
+  constexpr int S = kFilmStage;
+  __shared__ float sv[5][64][S + 1];  // L.xyz, pos.xy
+  const uint32_t q0 = blockIdx.x * 64, lane = threadIdx.x, q = q0 + lane;
+  const uint32_t pix = p.px0 + q;
+  const int y = (int)(pix / p.width), x = (int)(pix - (uint32_t)y * p.width);
+  const bool mask_valid = p.integrator == MTX_INT_PATH_MIS;
+  float4 acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (uint32_t s0 = 0; s0 < p.spp; s0 += S) {
+    const uint32_t ns = min((uint32_t)S, p.spp - s0);
+#pragma unroll 4
+    for (int it = 0; it < S; ++it) {
+      const uint32_t e = (uint32_t)it * 64 + lane, j = e / S, sm = e % S;
+      if (q0 + j < p.n_px && sm < ns) {
+        const uint32_t path = (q0 + j) * p.spp + s0 + sm;
+        float4 l = b.L[path];
+        if (mask_valid && !((b.misc[path].w >> 16) & PF_VALID_RAY)) l = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float2 ps = b.pos[path];
+        sv[0][j][sm] = l.x;
+        sv[1][j][sm] = l.y;
+        sv[2][j][sm] = l.z;
+        sv[3][j][sm] = ps.x;
+        sv[4][j][sm] = ps.y;
+      }
+    }
+    __syncthreads();
+    if (q < p.n_px)
+      for (uint32_t sm = 0; sm < ns; ++sm)
+        film_accumulate(acc, x, y, make_float2(sv[3][lane][sm], sv[4][lane][sm]),
+                        V3{sv[0][lane][sm], sv[1][lane][sm], sv[2][lane][sm]});
+    __syncthreads();
+  }
+  if (q >= p.n_px) return;
+  const size_t o = 9 * ((size_t)(pix - p.band_y0 * p.width));
+#pragma unroll
+  for (int k = 0; k < 9; ++k) contrib[o + k] = acc[k];
+}
+
 __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= p.n_px) return;
@@ -786,7 +848,10 @@ void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib
   hipLaunchKernelGGL(k_mlt_film, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
 }
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st) {
-  hipLaunchKernelGGL(k_film_src, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
+  if (p.sample_major || p.spp < 4)
+    hipLaunchKernelGGL(k_film_src, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
+  else
+    hipLaunchKernelGGL(k_film_src_staged, dim3(blocks_for(p.n_px, 64)), dim3(64), 0, st, b, p, contrib);
 }
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
                         hipStream_t st) {
