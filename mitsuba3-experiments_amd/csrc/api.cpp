@@ -351,7 +351,8 @@ constexpr size_t kPathStateBytes = 200;
 uint32_t default_chunk(mtx_ctx *c) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
-  const size_t fit = (size_t)((double)free_b * 0.4) / kPathStateBytes;
+  // buffers this context already holds count as available
+  const size_t fit = std::max<size_t>((size_t)((double)free_b * 0.4) / kPathStateBytes, c->capacity);
   return (uint32_t)std::max<size_t>(1u << 20, std::min<size_t>(kDefaultChunk, fit));
 }
 
