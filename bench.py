@@ -109,6 +109,7 @@ def main():
     trace_s = agg["trace_ms"] / 1e3 / args.steps  # per step, counters off
     achieved = alg_bytes / trace_s / 1e9 if trace_s > 0 else 0.0
 
+    traffic, traffic_src = measured_traffic("mtxd::k_trace_closest<false>")
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline:
@@ -136,12 +137,13 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_trace_closest (BVH2 closest-hit traversal)",
+                "kernel": "k_trace_closest (4-wide quantised BVH, closest hit)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": round(trace_s * 1e3 / launches, 4),
                 "launches_per_step": int(launches),
                 "alg_bytes_per_launch": int(alg_bytes / launches),
@@ -162,6 +164,22 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measured_traffic(kernel):
+    """HBM-side bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE, made by
+    tools/profile_session.sh + tools/pmc_summary.py on this bench command)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return int(k["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(sc, integ, args):
