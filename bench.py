@@ -42,11 +42,21 @@ def parse():
     p.add_argument("--chunk", type=int, default=0, help="wavefront paths per chunk (0 = library default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU time of the baseline sample")
+    p.add_argument("--workload", default="path_mis", choices=["path_mis", "pssmlt", "restir", "nrc", "prims"],
+                   help="path_mis = the driver's headline line (default); the others measure the remaining "
+                        "SURVEY §8 configurations on one GPU (C3 PSSMLT, C4 ReSTIR GI, C5 NRC, primitives)")
+    p.add_argument("--iterations", type=int, default=20, help="PSSMLT Metropolis iterations (C3 short variant)")
+    p.add_argument("--frames", type=int, default=10, help="ReSTIR GI timed frames")
     return p.parse_args()
 
 
 def main():
     args = parse()
+    if args.workload != "path_mis":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_workloads
+
+        return bench_workloads.run(args)
     import numpy as np
     import torch
     import torch.distributed as dist

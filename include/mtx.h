@@ -283,6 +283,11 @@ int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolu
 int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value);
 
+/* HIP-event time (ms) of the device work of the last primitive call on ctx
+ * (the scan / hash / scatter kernels, without the host<->device copies);
+ * used by bench.py to report the primitives against their rooflines. */
+double mtx_last_device_ms(mtx_ctx *ctx);
+
 #ifdef __cplusplus
 }
 #endif

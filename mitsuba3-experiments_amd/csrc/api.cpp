@@ -114,6 +114,8 @@ struct mtx_ctx {
   uint32_t trace_batch = 256;
   uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
+  hipEvent_t prim_ev[2] = {nullptr, nullptr};
+  double last_device_ms = 0.0;
 };
 
 extern "C" {
@@ -175,6 +177,8 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
+  for (hipEvent_t ev : c->prim_ev)
+    if (ev) hipEventDestroy(ev);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
@@ -348,11 +352,14 @@ namespace {
 // 40 % of the free HBM.
 constexpr uint32_t kDefaultChunk = 1u << 28;
 constexpr size_t kPathStateBytes = 200;
-uint32_t default_chunk(mtx_ctx *c) {
+uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
+  // PSSMLT chains also keep the current and proposed path vertices
+  const size_t per_path =
+      kPathStateBytes + (a->integrator == MTX_INT_PSSMLT_SIMPLE ? 32ull * std::max<uint32_t>(a->max_depth, 1) + 48 : 0);
   // buffers this context already holds count as available
-  const size_t fit = std::max<size_t>((size_t)((double)free_b * 0.4) / kPathStateBytes, c->capacity);
+  const size_t fit = std::max<size_t>((size_t)((double)free_b * 0.4) / per_path, c->capacity);
   return (uint32_t)std::max<size_t>(1u << 20, std::min<size_t>(kDefaultChunk, fit));
 }
 
@@ -505,6 +512,34 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
   }
 }
 
+int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_t n_trace, uint64_t n_shadow,
+               uint64_t paths) {
+  if (!stats) return MTX_OK;
+  memset(stats, 0, sizeof(*stats));
+  if (want_stats) {
+    unsigned long long h[8];
+    HIP_TRY(hipMemcpy(h, c->stats.p, 64, hipMemcpyDeviceToHost));
+    stats->nodes_closest = h[0];
+    stats->tris_closest = h[1];
+    stats->nodes_shadow = h[2];
+    stats->tris_shadow = h[3];
+    stats->rays_closest = h[4];
+    stats->rays_shadow = h[5];
+    stats->wave_node_iters = h[6];
+    stats->wave_leaf_iters = h[7];
+  }
+  stats->trace_launches = n_trace;
+  stats->shadow_launches = n_shadow;
+  stats->paths = paths;
+  if (tm.on) {
+    stats->trace_ms = tm.total(0);
+    stats->shadow_ms = tm.total(1);
+    stats->shade_ms = tm.total(2);
+    stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms;
+  }
+  return MTX_OK;
+}
+
 int ensure_restir(mtx_ctx *c, uint32_t n) {
   int rc;
   if (c->rs_n != n) {
@@ -533,7 +568,7 @@ int ensure_restir(mtx_ctx *c, uint32_t n) {
 // One RestirIntegrator.render() frame (restirgi.py:182-258) over the whole
 // film; the kernel sequence is documented in restir.hip.
 int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer &tm, uint64_t *n_trace,
-                  uint64_t *n_shadow) {
+                  uint64_t *n_shadow, bool want_stats) {
   const mtx_camera &cam = c->scene.camera;
   const uint32_t W = cam.width, H = cam.height, spp = a->spp;
   if (a->y0 != 0 || a->y1 != H || a->sample_offset != 0 || a->spp_total != spp) {
@@ -606,12 +641,14 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   p.n_paths = n;
   p.restir = 1;
   p.sample_major = c->sample_major;
+  p.stats = want_stats ? 1 : 0;
+  if (want_stats) HIP_TRY(hipMemsetAsync(c->stats.p, 0, 64, c->stream));
   const size_t cbytes = 16ull * (depth + 2);
   // sample_initial: primary rays and their closest hits
   HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
   mtxd::launch_raygen_camera(c->scene, b, p, st);
   hipEvent_t e = tm.begin(0);
-  mtxd::launch_trace_closest(c->scene, b, 0, 0, c->trace_grid, st);
+  mtxd::launch_trace_closest(c->scene, b, 0, p.stats, c->trace_grid, st);
   tm.end(0, e);
   ++*n_trace;
   HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
@@ -664,7 +701,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     return MTX_E_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  uint32_t chunk_paths = a->chunk_paths ? a->chunk_paths : default_chunk(c);
+  uint32_t chunk_paths = a->chunk_paths ? a->chunk_paths : default_chunk(c, a);
   uint32_t px_per_chunk = std::max<uint32_t>(1, chunk_paths / a->spp);
   const uint32_t band_px = (a->y1 - a->y0) * W;
   px_per_chunk = std::min(px_per_chunk, band_px);
@@ -682,24 +719,12 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   if (a->integrator == MTX_INT_RESTIR_GI) {
     hipEvent_t e_all = tm.begin(3);
     uint64_t n_trace = 0, n_shadow = 0;
-    if ((rc = render_restir(c, a, film_dev, tm, &n_trace, &n_shadow))) return rc;
+    if ((rc = render_restir(c, a, film_dev, tm, &n_trace, &n_shadow, want_stats))) return rc;
     tm.end(3, e_all);
     if (!film_on_device)
       HIP_TRY(hipMemcpyAsync(film_rgbw, film_dev, film_floats * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (stats) {
-      memset(stats, 0, sizeof(*stats));
-      stats->trace_launches = n_trace;
-      stats->shadow_launches = n_shadow;
-      stats->paths = (uint64_t)W * H * a->spp;
-      if (tm.on) {
-        stats->trace_ms = tm.total(0);
-        stats->shadow_ms = tm.total(1);
-        stats->shade_ms = tm.total(2);
-        stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms;
-      }
-    }
-    return MTX_OK;
+    return fill_stats(c, stats, want_stats, tm, n_trace, n_shadow, (uint64_t)W * H * a->spp);
   }
   if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
     if (a->sample_offset != 0 || a->spp_total != a->spp) {
@@ -757,31 +782,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   if (!film_on_device)
     HIP_TRY(hipMemcpyAsync(film_rgbw, film_dev, film_floats * 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (stats) {
-    memset(stats, 0, sizeof(*stats));
-    if (want_stats) {
-      unsigned long long h[8];
-      HIP_TRY(hipMemcpy(h, b.stats, 64, hipMemcpyDeviceToHost));
-      stats->nodes_closest = h[0];
-      stats->tris_closest = h[1];
-      stats->nodes_shadow = h[2];
-      stats->tris_shadow = h[3];
-      stats->rays_closest = h[4];
-      stats->rays_shadow = h[5];
-      stats->wave_node_iters = h[6];
-      stats->wave_leaf_iters = h[7];
-    }
-    stats->trace_launches = n_trace;
-    stats->shadow_launches = n_shadow;
-    stats->paths = (uint64_t)band_px * a->spp;
-    if (tm.on) {
-      stats->trace_ms = tm.total(0);
-      stats->shadow_ms = tm.total(1);
-      stats->shade_ms = tm.total(2);
-      stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms;
-    }
-  }
-  return MTX_OK;
+  return fill_stats(c, stats, want_stats, tm, n_trace, n_shadow, (uint64_t)band_px * a->spp);
 }
 
 int mtx_set_camera(mtx_ctx *c, const mtx_camera *cam) {
@@ -847,7 +848,7 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     return MTX_E_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : default_chunk(c);
+  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : default_chunk(c, a);
   const uint32_t cap = (uint32_t)std::min<uint64_t>(n, chunk);
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   if ((rc = dalloc(c->s0, 24ull * cap))) return rc;
@@ -916,6 +917,24 @@ int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *
 
 // ------------------------------- primitives -------------------------------
 
+// HIP-event bracket around the device work of one primitive call.
+static int prim_timer_begin(mtx_ctx *c) {
+  for (int k = 0; k < 2; ++k)
+    if (!c->prim_ev[k]) HIP_TRY(hipEventCreate(&c->prim_ev[k]));
+  HIP_TRY(hipEventRecord(c->prim_ev[0], c->stream));
+  return MTX_OK;
+}
+static int prim_timer_end(mtx_ctx *c) {
+  HIP_TRY(hipEventRecord(c->prim_ev[1], c->stream));
+  return MTX_OK;
+}
+static void prim_timer_read(mtx_ctx *c) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, c->prim_ev[0], c->prim_ev[1]) == hipSuccess) c->last_device_ms = ms;
+}
+
+double mtx_last_device_ms(mtx_ctx *c) { return c ? c->last_device_ms : 0.0; }
+
 int mtx_prefix_sum_u32(mtx_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, int inclusive) {
   if (!c || (n && (!in || !out))) {
     mtx_set_error("mtx_prefix_sum_u32: null argument");
@@ -932,11 +951,14 @@ int mtx_prefix_sum_u32(mtx_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n
   if ((rc = dalloc(c->s1, 4 * n))) return rc;
   if ((rc = dalloc(c->s2, mtxd::scan_workspace_bytes(n)))) return rc;
   HIP_TRY(hipMemcpyAsync(c->s0.p, in, 4 * n, hipMemcpyHostToDevice, c->stream));
+  if ((rc = prim_timer_begin(c))) return rc;
   rc = mtxd::scan_u32((const uint32_t *)c->s0.p, (uint32_t *)c->s1.p, n, inclusive, c->s2.p, c->stream);
   if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, c->s1.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
   return MTX_OK;
 }
 
@@ -952,11 +974,14 @@ int mtx_prefix_sum_f32_hs(mtx_ctx *c, const float *in, float *out, uint64_t n) {
   if ((rc = dalloc(c->s1, 4 * n))) return rc;
   HIP_TRY(hipMemcpyAsync(c->s0.p, in, 4 * n, hipMemcpyHostToDevice, c->stream));
   float *res = nullptr;
+  if ((rc = prim_timer_begin(c))) return rc;
   rc = mtxd::scan_f32_hs((float *)c->s0.p, (float *)c->s1.p, n, &res, c->stream);
   if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, res, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
   return MTX_OK;
 }
 
@@ -979,15 +1004,18 @@ int mtx_hashgrid_build(mtx_ctx *c, const float *p, uint64_t n, uint32_t resoluti
   if ((rc = dalloc(c->s4, 4 * n))) return rc;           // sample_idx
   if ((rc = dalloc(c->s5, mtxd::hashgrid_workspace_bytes(n, n_cells)))) return rc;
   HIP_TRY(hipMemcpyAsync(c->s0.p, p, 12 * n, hipMemcpyHostToDevice, c->stream));
+  if ((rc = prim_timer_begin(c))) return rc;
   rc = mtxd::hashgrid_build((const float *)c->s0.p, n, resolution, n_cells, (uint32_t *)c->s1.p, (uint32_t *)c->s2.p,
                             (uint32_t *)c->s3.p, (uint32_t *)c->s4.p, c->s5.p, c->stream);
   if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(cell, c->s1.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(cell_size, c->s2.p, 4ull * n_cells, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(cell_offset, c->s3.p, 4ull * n_cells, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(sample_idx, c->s4.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
   return MTX_OK;
 }
 
@@ -1016,12 +1044,15 @@ int mtx_scatter_reduce_f32(mtx_ctx *c, int op, float *target, uint64_t n_target,
   HIP_TRY(hipMemcpyAsync(c->s0.p, target, 4 * n_target, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->s1.p, value, 4 * n_value, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemcpyAsync(c->s2.p, index, 4 * n_value, hipMemcpyHostToDevice, c->stream));
+  if ((rc = prim_timer_begin(c))) return rc;
   rc = mtxd::scatter_reduce_f32(op, (float *)c->s0.p, n_target, (const float *)c->s1.p, (const uint32_t *)c->s2.p,
                                 n_value, c->s3.p, c->stream);
   if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(target, c->s0.p, 4 * n_target, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
   return MTX_OK;
 }
 

@@ -184,4 +184,5 @@ EXPORTS = [
     "mtx_prefix_sum_f32_hs",
     "mtx_hashgrid_build",
     "mtx_scatter_reduce_f32",
+    "mtx_last_device_ms",
 ]

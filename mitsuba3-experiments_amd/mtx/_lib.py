@@ -55,6 +55,7 @@ def lib() -> C.CDLL:
         "mtx_roughplastic_tables": ([u32, C.c_float, C.c_float, vp, C.POINTER(C.c_float)], C.c_int),
         "mtx_scene_upload": ([vp, C.POINTER(_abi.SceneDesc)], C.c_int),
         "mtx_render": ([vp, C.POINTER(_abi.RenderArgs), vp, C.c_int, C.POINTER(_abi.Stats)], C.c_int),
+        "mtx_last_device_ms": ([vp], C.c_double),
         "mtx_set_camera": ([vp, C.POINTER(_abi.Camera)], C.c_int),
         "mtx_restir_state": ([vp, C.c_int, vp, u64], C.c_int),
         "mtx_sample_rays": ([vp, C.POINTER(_abi.RenderArgs), u64, vp, vp, u32, vp, vp], C.c_int),

@@ -1,0 +1,282 @@
+"""Single-GPU measurements of the SURVEY §8 configurations other than the
+headline path-mis line (run through `python bench.py --workload X`; this
+module is imported by bench.py, which sets up sys.path):
+
+  pssmlt  C3  pssmltsimple.py PSSMLT, bedroom 1280x720, 256 chains/pixel,
+              --iterations Metropolis iterations (20 = the SURVEY's CI variant)
+  restir  C4  restirgi.py ReSTIR GI, bedroom 1920x1080, props of
+              restirgi.py:610-620, --frames timed frames
+  nrc     C5  nrc.py NRC path segments, bedroom 1280x720 spp 4
+  prims       prefix_sum.py / hashgrid.py / reductions.py at the §8d sizes
+
+Each prints one JSON line per measurement with the same fields as bench.py:
+`roofline` for the dominant kernel and `cpu_baseline` from oracle/ on a
+bounded sample. Inputs are resident on the device before the timed region.
+"""
+import json
+import os
+import time
+
+import numpy as np
+
+import bench
+
+NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES = bench.NODE_BYTES, bench.TRI_BYTES, bench.RAY_BYTES, bench.HIT_BYTES
+
+
+def _threads():
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def _trace_roofline(cnt, trace_ms_per_unit, units_label):
+    alg = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
+           + cnt["tris_closest"] * TRI_BYTES)
+    launches = max(1, cnt["trace_launches"])
+    s = trace_ms_per_unit / 1e3
+    ach = alg / s / 1e9 if s > 0 else 0.0
+    return {"bound": "hbm", "kernel": "k_trace_closest (4-wide quantised BVH, closest hit)",
+            "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
+            "avg_launch_ms": round(trace_ms_per_unit / launches, 4), "launches_per_" + units_label: int(launches),
+            "alg_bytes_per_launch": int(alg / launches),
+            "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
+            "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2)}
+
+
+def _line(metric, value, unit, steps, warmup, ms, config, roofline, cpu, extra=None, dtype="f32"):
+    out = {"metric": metric, "value": round(value, 4), "unit": unit, "n_gpus": 1, "steps": steps, "warmup": warmup,
+           "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": dtype, "data": "synthetic: deterministic bedroom proxy / seeded PCG32 inputs",
+           "config": config, "roofline": roofline, "cpu_baseline": cpu}
+    if extra:
+        out.update(extra)
+    print(json.dumps(out), flush=True)
+
+
+def _sync():
+    import torch
+
+    torch.cuda.synchronize()
+
+
+# --------------------------------------------------------------- PSSMLT (C3) --
+def pssmlt(args):
+    import binding as oracle
+    import torch
+    from mtx import PssmltSimple, scene
+
+    torch.cuda.set_device(0)
+    sc = scene.bedroom(1280, 720)
+    spp, it = args.spp, args.iterations
+    integ = PssmltSimple({"iterations": it})
+    film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
+    PssmltSimple({"iterations": 1}).render_film(sc, seed=99, spp=spp, out=film)  # allocation warm-up
+    _sync()
+    t0 = time.perf_counter()
+    st = None
+    for k in range(args.steps):
+        st = integ.render_film(sc, seed=k, spp=spp, out=film, stats=True)[1]
+    _sync()
+    dt = (time.perf_counter() - t0) / args.steps
+    cnt = integ.render_film(sc, seed=0, spp=spp, out=film, stats=True, counters=True)[1]
+    chains = sc.width * sc.height * spp
+    # CPU: the oracle on a band of rows, same chains per pixel and iterations
+    oracle.build()
+    a1 = integ.render_args(sc, 0, spp, 0, 1)
+    t1 = time.perf_counter()
+    oracle.pssmlt_render(sc, a1, it)
+    c1 = time.perf_counter() - t1
+    rows = max(1, min(sc.height, int(args.cpu_seconds / max(c1, 1e-3))))
+    a = integ.render_args(sc, 0, spp, 0, rows)
+    t1 = time.perf_counter()
+    oracle.pssmlt_render(sc, a, it)
+    c = time.perf_counter() - t1
+    cpu = {"value": round(sc.width * rows * spp * it / c / 1e6, 4), "unit": "Mchain-iterations/s",
+           "cores": _threads(), "kind": "port",
+           "sample": f"{rows} of {sc.height} rows x {sc.width} px x {spp} chains x {it} iterations ({c:.1f} s); "
+                     "oracle/oracle.cpp orc_pssmlt_render (OpenMP)"}
+    _line("PSSMLT Mchain-iterations/sec on bedroom@1280x720, 256 chains/pixel (C3)", chains * it / dt / 1e6,
+          "Mchain-iterations/s", args.steps, 1, dt * 1e3,
+          {"workload": f"pssmltsimple.py + pssmlt.py render, {it} iterations (large step every 50, aggregate "
+                       f"i%50>40), max_depth 16, rr_depth 4, {chains} chains", "chains": chains, "iterations": it},
+          _trace_roofline(cnt, st["trace_ms"], "step"), cpu,
+          {"kernels_ms_per_step": {"trace_closest": round(st["trace_ms"], 3), "shade": round(st["shade_ms"], 3),
+                                   "other": round(st["other_ms"], 3)}})
+
+
+# -------------------------------------------------------------- ReSTIR (C4) --
+RESTIR_C4 = {"jacobian": False, "bias_correction": False, "bsdf_sampling": True, "max_M_spatial": 500,
+             "max_M_temporal": 30, "initial_search_radius": 10}
+
+
+def restir(args):
+    import binding as oracle
+    import torch
+    from mtx import RestirIntegrator, scene
+
+    torch.cuda.set_device(0)
+    sc = scene.bedroom(1920, 1080)
+    integ = RestirIntegrator(RESTIR_C4)
+    film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
+    W = max(1, args.warmup)
+    for k in range(W):
+        integ.render_film(sc, seed=k, spp=1, out=film)
+    _sync()
+    agg = None
+    t0 = time.perf_counter()
+    for k in range(args.frames):
+        st = integ.render_film(sc, seed=W + k, spp=1, out=film, stats=True)[1]
+        agg = dict(st) if agg is None else {x: agg[x] + st[x] for x in st}
+    _sync()
+    dt = (time.perf_counter() - t0) / args.frames
+    cnt = integ.render_film(sc, seed=W + args.frames, spp=1, out=film, stats=True, counters=True)[1]
+    px = sc.width * sc.height
+    # CPU: the oracle's frame loop on a reduced film
+    oracle.build()
+    small = sc.with_film(240, 135)
+    orc = oracle.RestirOracle(small)
+    ci = RestirIntegrator(RESTIR_C4)
+    t1 = time.perf_counter()
+    nf = 0
+    while nf < 3 and (nf == 0 or time.perf_counter() - t1 < args.cpu_seconds):
+        ci.n = nf
+        orc.frame(small, ci.render_args(small, nf, 1))
+        nf += 1
+    c = time.perf_counter() - t1
+    cpu = {"value": round(240 * 135 * nf / c / 1e6, 4), "unit": "Mpixel-frames/s", "cores": _threads(),
+           "kind": "port", "sample": f"{nf} frames at 240x135 ({c:.1f} s), same properties; oracle/oracle.cpp "
+                                     "orc_restir_frame (OpenMP)"}
+    _line("ReSTIR GI Mpixel-frames/sec on bedroom@1920x1080 (C4, 1 GPU)", px / dt / 1e6, "Mpixel-frames/s",
+          args.frames, W, dt * 1e3,
+          {"workload": "restirgi.py render per frame: initial sample + path-mis secondary path (max_depth 8), "
+                       "temporal + 9-tap spatial reuse with visibility, props restirgi.py:610-620",
+           "frames_per_s": round(1.0 / dt, 2), "pixels": px},
+          _trace_roofline(cnt, agg["trace_ms"] / args.frames, "frame"), cpu,
+          {"kernels_ms_per_frame": {"trace_closest": round(agg["trace_ms"] / args.frames, 3),
+                                    "trace_shadow_and_visibility": round(agg["shadow_ms"] / args.frames, 3),
+                                    "shade": round(agg["shade_ms"] / args.frames, 3),
+                                    "other": round(agg["other_ms"] / args.frames, 3)}})
+
+
+# ----------------------------------------------------------------- NRC (C5) --
+def nrc(args):
+    import torch
+    from mtx import NRCIntegrator, scene
+
+    torch.cuda.set_device(0)
+    sc = scene.bedroom(1280, 720)
+    integ = NRCIntegrator({})
+    spp = 4
+    film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
+    integ.render_film(sc, seed=99, spp=spp, out=film)
+    _sync()
+    reps = max(args.steps, 5)
+    agg = None
+    t0 = time.perf_counter()
+    for k in range(reps):
+        st = integ.render_film(sc, seed=k, spp=spp, out=film, stats=True)[1]
+        agg = dict(st) if agg is None else {x: agg[x] + st[x] for x in st}
+    _sync()
+    dt = (time.perf_counter() - t0) / reps
+    cnt = integ.render_film(sc, seed=0, spp=spp, out=film, stats=True, counters=True)[1]
+    n = sc.width * sc.height * spp
+
+    class A:  # cpu_baseline wants args.cpu_seconds only
+        cpu_seconds = args.cpu_seconds
+
+    cpu = bench.cpu_baseline(sc, integ, A)
+    _line("NRC Mpaths/sec on bedroom@1280x720 spp=4 (C5)", n / dt / 1e6, "Mpaths/s", reps, 1, dt * 1e3,
+          {"workload": "nrc.py NRCIntegrator.sample: NEE+MIS segments, spread heuristic c=0.01, max_depth 10",
+           "paths_per_step": n}, _trace_roofline(cnt, agg["trace_ms"] / reps, "step"), cpu)
+
+
+# ------------------------------------------------------------- primitives --
+def prims(args):
+    import binding as oracle
+    from mtx import primitives
+    from mtx._lib import context, lib
+
+    ctx = context(0)
+    dev_ms = lambda: lib().mtx_last_device_ms(ctx.handle)  # noqa: E731
+    oracle.build()
+
+    def best(fn, reps=3):
+        t = []
+        for _ in range(reps):
+            fn()
+            t.append(dev_ms())
+        return min(t)
+
+    def cpu_time(fn):
+        t0 = time.perf_counter()
+        fn()
+        return time.perf_counter() - t0
+
+    rng = np.random.default_rng(0)
+    # prefix_sum u32, n = 2^28: 8 B/element
+    n = 1 << 28
+    x = rng.integers(0, 1 << 16, n, dtype=np.uint32)
+    ms = best(lambda: primitives.prefix_sum(x))
+    nc = 1 << 26
+    c = cpu_time(lambda: oracle.prefix_sum_u32(x[:nc]))
+    ach = 8 * n / (ms / 1e3) / 1e9
+    _line("prefix_sum u32 Gelem/sec (prefix_sum.py:9-36), n=2^28", n / (ms / 1e3) / 1e9, "Gelem/s", 3, 1, ms,
+          {"workload": "inclusive scan of 2^28 u32, decoupled look-back", "n": n},
+          {"bound": "hbm", "kernel": "scan_u32 (decoupled look-back)", "achieved": round(ach, 1),
+           "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
+           "alg_bytes_per_launch": 8 * n},
+          {"value": round(nc / c / 1e9, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
+           "sample": f"2^26 elements ({c:.2f} s), oracle orc_prefix_sum_u32"}, dtype="u32")
+    del x
+    # prefix_sum f32 in Hillis-Steele order, n = 2^24
+    n = 1 << 24
+    xf = rng.random(n, dtype=np.float32)
+    ms = best(lambda: primitives.prefix_sum(xf))
+    c = cpu_time(lambda: oracle.prefix_sum_f32_hs(xf[: 1 << 22]))
+    passes = int(np.floor(np.log2(n))) + 1
+    ach = 8 * n / (ms / 1e3) / 1e9
+    _line("prefix_sum f32 Hillis-Steele Gelem/sec (prefix_sum.py:9-36), n=2^24", n / (ms / 1e3) / 1e9, "Gelem/s", 3,
+          1, ms, {"workload": f"{passes} Hillis-Steele passes in the reference's summation order (bit-exact)",
+                  "n": n},
+          {"bound": "hbm", "kernel": "scan_f32_hs (LDS passes + global passes)", "achieved": round(ach, 1),
+           "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
+           "alg_bytes_per_launch": 8 * n, "note": "algorithmic bytes = one read + one write per element"},
+          {"value": round((1 << 22) / c / 1e9, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
+           "sample": f"2^22 elements ({c:.2f} s), oracle orc_prefix_sum_f32_hs"})
+    # hash grid, n = 2^24 points, res 100, n_cells = n (hashgrid.py:16-84)
+    n = 1 << 24
+    p = rng.random((3, n), dtype=np.float32)
+    ms = best(lambda: primitives.HashGrid(p, 100, n))
+    nc = 1 << 22
+    pc = np.ascontiguousarray(p[:, :nc])
+    c = cpu_time(lambda: oracle.hashgrid(pc, 100, nc))
+    ach = 32 * n / (ms / 1e3) / 1e9
+    _line("hashgrid build Msamples/sec (hashgrid.py:16-84), n=2^24", n / (ms / 1e3) / 1e6, "Msamples/s", 3, 1, ms,
+          {"workload": "bbox reduce, hash + rank, scan, fill; res 100, n_cells = n", "n": n},
+          {"bound": "hbm", "kernel": "hashgrid_build (4 kernels)", "achieved": round(ach, 1),
+           "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
+           "alg_bytes_per_launch": 32 * n, "note": "SURVEY §8d: ~32 B/sample"},
+          {"value": round(nc / c / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "sample": f"2^22 points ({c:.2f} s), oracle orc_hashgrid"}, dtype="u32")
+    del p, pc
+    # scatter_reduce add, nv = 2^24, nt = 2^20 (reductions.py:12-54)
+    nv, nt = 1 << 24, 1 << 20
+    idx = rng.integers(0, nt, nv, dtype=np.uint32)
+    val = rng.random(nv, dtype=np.float32)
+    tgt = np.zeros(nt, np.float32)
+    ms = best(lambda: primitives.scatter_reduce_with("add", tgt, val, idx))
+    c = cpu_time(lambda: oracle.scatter_reduce(0, tgt, val, idx))
+    ach = 16 * nv / (ms / 1e3) / 1e9
+    _line("scatter_reduce add Gvalues/sec (reductions.py:12-54), nv=2^24 nt=2^20", nv / (ms / 1e3) / 1e9,
+          "Gvalues/s", 3, 1, ms,
+          {"workload": "deterministic winner-election rounds (ascending index per target)", "n_value": nv,
+           "n_target": nt},
+          {"bound": "hbm", "kernel": "scatter_reduce rounds", "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_launch": 16 * nv,
+           "note": "SURVEY §8d: 16 B/value"},
+          {"value": round(nv / c / 1e9, 4), "unit": "Gvalues/s", "cores": 1, "kind": "port",
+           "sample": f"same {nv} values ({c:.2f} s), oracle orc_scatter_reduce_f32"})
+
+
+def run(args):
+    {"pssmlt": pssmlt, "restir": restir, "nrc": nrc, "prims": prims}[args.workload](args)
