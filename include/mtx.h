@@ -182,7 +182,13 @@ enum {
   MTX_RESTIR_BIAS_CORRECTION = 1,
   MTX_RESTIR_JACOBIAN = 2,
   MTX_RESTIR_BSDF_SAMPLING = 4,
-  MTX_RESTIR_SPATIAL_SPATIAL = 8
+  MTX_RESTIR_SPATIAL_SPATIAL = 8,
+  /* row-banded frames (multi-GPU): stage A = sample_initial + temporal
+   * resampling of rows [y0,y1); stage B = spatial resampling + render_final +
+   * film of the same rows. Between them the caller imports the neighbours'
+   * halo rows (mtx_restir_rows). Neither flag: the whole frame in one call. */
+  MTX_RESTIR_STAGE_A = 16,
+  MTX_RESTIR_STAGE_B = 32
 };
 
 /* Device-side counters, filled when mtx_render_args.flags has bit0/bit1. */
@@ -241,6 +247,13 @@ int mtx_render(mtx_ctx *ctx, const mtx_render_args *args, float *film_rgbw, int 
  * test-restir-dynamic.py; restirgi.py:247 keeps the old one as prev_sensor
  * for the next ReSTIR frame). The film size must not change. */
 int mtx_set_camera(mtx_ctx *ctx, const mtx_camera *camera);
+
+/* Copy rows [row0, row0+nrows) of the ReSTIR GI state to (to_state = 0) or
+ * from (to_state = 1) a device buffer, plane-major (planes x rows x W*spp
+ * float4): which = 0 the current frame's samples (5 planes), 1 the temporal
+ * reservoirs (6 planes). The halo exchange of a row-banded frame
+ * (restirgi.py:301-313 reads up to search_radius rows away). */
+int mtx_restir_rows(mtx_ctx *ctx, int which, uint32_t row0, uint32_t nrows, void *buf, int to_state);
 
 /* Read back ReSTIR GI frame state (test / debugging hook for restirgi.py's
  * self.sample, temporal_reservoir, spatial_reservoir, search_radius):

@@ -100,8 +100,8 @@ struct mtx_ctx {
   uint32_t mlt_capacity = 0, mlt_depth = 0;
   // ReSTIR GI frame state (restirgi.py:217-226): kept across mtx_render calls
   DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM, rs_xs, rs_ns;
-  uint32_t rs_n = 0, rs_cur = 0;
-  bool rs_valid = false;
+  uint32_t rs_n = 0, rs_cur = 0, rs_pending_frame = 0;
+  bool rs_valid = false, rs_pending_b = false;
   mtx_camera rs_prev_cam{};
   // film
   DevBuf contrib, film;
@@ -571,8 +571,8 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
                   uint64_t *n_shadow, bool want_stats) {
   const mtx_camera &cam = c->scene.camera;
   const uint32_t W = cam.width, H = cam.height, spp = a->spp;
-  if (a->y0 != 0 || a->y1 != H || a->sample_offset != 0 || a->spp_total != spp) {
-    mtx_set_error("mtx_render: ReSTIR GI renders whole frames (y0=0, y1=height, spp_total=spp, offset 0)");
+  if (a->sample_offset != 0 || a->spp_total != spp) {
+    mtx_set_error("mtx_render: ReSTIR GI needs spp_total = spp and sample_offset = 0");
     return MTX_E_ARG;
   }
   const uint64_t n64 = (uint64_t)W * H * spp;
@@ -580,20 +580,34 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     mtx_set_error("mtx_render: ReSTIR GI frame too large (%llu lanes)", (unsigned long long)n64);
     return MTX_E_ARG;
   }
+  const bool only_a = (a->restir_flags & MTX_RESTIR_STAGE_A) != 0;
+  const bool only_b = (a->restir_flags & MTX_RESTIR_STAGE_B) != 0;
+  if (only_a && only_b) {
+    mtx_set_error("mtx_render: ReSTIR stage A and stage B flags are exclusive");
+    return MTX_E_ARG;
+  }
+  const bool run_a = !only_b, run_b = !only_a;
   const uint32_t n = (uint32_t)n64;
+  const uint32_t lane0 = a->y0 * W * spp, nb = (a->y1 - a->y0) * W * spp;
   const uint32_t depth = std::max<uint32_t>(a->max_depth, 1);
   int rc;
-  if ((rc = ensure_wavefront(c, n, depth))) return rc;
+  if ((rc = ensure_wavefront(c, nb, depth))) return rc;
   if ((rc = ensure_restir(c, n))) return rc;
-  if (a->frame != 0 && !c->rs_valid) {
+  if (run_a && a->frame != 0 && !c->rs_valid) {
     mtx_set_error("mtx_render: ReSTIR GI frame %u without the state of frame 0 (film size or scene changed?)",
                   a->frame);
     return MTX_E_ARG;
   }
+  if (only_b && (!c->rs_pending_b || c->rs_pending_frame != a->frame)) {
+    mtx_set_error("mtx_render: ReSTIR stage B of frame %u without its stage A", a->frame);
+    return MTX_E_ARG;
+  }
   hipStream_t st = c->stream;
-  if (a->frame == 0) {  // restirgi.py:217-229
+  if (run_a && a->frame == 0) {  // restirgi.py:217-229
     HIP_TRY(hipMemsetAsync(c->rs_tres.p, 0, 6 * 16 * (size_t)n, st));
     HIP_TRY(hipMemsetAsync(c->rs_sres.p, 0, 6 * 16 * (size_t)n, st));
+    HIP_TRY(hipMemsetAsync(c->rs_samp[0].p, 0, 5 * 16 * (size_t)n, st));
+    HIP_TRY(hipMemsetAsync(c->rs_samp[1].p, 0, 5 * 16 * (size_t)n, st));
     uint32_t bits;
     memcpy(&bits, &a->initial_search_radius, 4);
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->rs_radius.p, (int)bits, n, st));
@@ -616,6 +630,8 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   r.occ = (uint8_t *)c->rs_occ.p;
   r.qM = (uint32_t *)c->rs_qM.p;
   r.n = n;
+  r.lane0 = lane0;
+  r.nb = nb;
   r.prev_cam = c->rs_prev_cam;
   r.flags = a->restir_flags;
   r.max_M_temporal = a->max_M_temporal;
@@ -635,48 +651,61 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   p.spp_total = spp;
   p.width = W;
   p.height = H;
-  p.px0 = 0;
-  p.n_px = W * H;
-  p.band_y0 = 0;
-  p.n_paths = n;
+  p.px0 = a->y0 * W;
+  p.n_px = (a->y1 - a->y0) * W;
+  p.band_y0 = a->y0;
+  p.n_paths = nb;
   p.restir = 1;
   p.sample_major = c->sample_major;
   p.stats = want_stats ? 1 : 0;
   if (want_stats) HIP_TRY(hipMemsetAsync(c->stats.p, 0, 64, c->stream));
   const size_t cbytes = 16ull * (depth + 2);
-  // sample_initial: primary rays and their closest hits
-  HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
-  mtxd::launch_raygen_camera(c->scene, b, p, st);
-  hipEvent_t e = tm.begin(0);
-  mtxd::launch_trace_closest(c->scene, b, 0, p.stats, c->trace_grid, st);
-  tm.end(0, e);
-  ++*n_trace;
-  HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
-  mtxd::launch_restir_begin(c->scene, b, p, r, st);
-  run_bounces(c, b, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
-  mtxd::launch_restir_collect(b, p, r, st);
-  mtxd::launch_restir_temporal(r, p, st);
-  // spatial_resampling
-  HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
-  mtxd::launch_restir_spatial_rays(r, p, st);
-  e = tm.begin(1);
-  mtxd::launch_trace_test(c->scene, r, 0, c->trace_grid, st);
-  tm.end(1, e);
-  ++*n_shadow;
-  HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
-  mtxd::launch_restir_spatial_merge(r, p, st);
-  if (a->restir_flags & MTX_RESTIR_BIAS_CORRECTION) {
+  hipEvent_t e;
+  if (run_a) {
+    // sample_initial: primary rays and their closest hits
+    HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
+    mtxd::launch_raygen_camera(c->scene, b, p, st);
+    e = tm.begin(0);
+    mtxd::launch_trace_closest(c->scene, b, 0, p.stats, c->trace_grid, st);
+    tm.end(0, e);
+    ++*n_trace;
+    HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
+    mtxd::launch_restir_begin(c->scene, b, p, r, st);
+    run_bounces(c, b, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
+    mtxd::launch_restir_collect(b, p, r, st);
+    mtxd::launch_restir_temporal(r, p, st);
+  }
+  if (run_b) {
+    // spatial_resampling (reads samples / temporal reservoirs of rows outside
+    // the band: a row-banded caller imports them between stage A and B)
+    HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
+    mtxd::launch_restir_spatial_rays(r, p, st);
     e = tm.begin(1);
-    mtxd::launch_trace_test(c->scene, r, 9 * n, c->trace_grid, st);
+    mtxd::launch_trace_test(c->scene, r, 0, c->trace_grid, st);
     tm.end(1, e);
     ++*n_shadow;
-    mtxd::launch_restir_bias_finish(r, p, st);
+    HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
+    mtxd::launch_restir_spatial_merge(r, p, st);
+    if (a->restir_flags & MTX_RESTIR_BIAS_CORRECTION) {
+      e = tm.begin(1);
+      mtxd::launch_trace_test(c->scene, r, 9 * n, c->trace_grid, st);
+      tm.end(1, e);
+      ++*n_shadow;
+      mtxd::launch_restir_bias_finish(r, p, st);
+    }
+    mtxd::launch_restir_final(c->scene, b, p, r, st);
+    mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, st);
+    mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, st);
   }
-  mtxd::launch_restir_final(c->scene, b, p, r, st);
-  mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, st);
-  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, 0, H, st);
   HIP_TRY(hipGetLastError());
+  if (only_a) {
+    c->rs_pending_b = true;
+    c->rs_pending_frame = a->frame;
+    c->rs_valid = a->frame != 0 ? c->rs_valid : false;
+    return MTX_OK;
+  }
   // restirgi.py:245-247: prev_sensor <- sensor, prev_sample <- sample
+  c->rs_pending_b = false;
   c->rs_prev_cam = cam;
   c->rs_cur ^= 1;
   c->rs_valid = true;
@@ -800,6 +829,37 @@ int mtx_set_camera(mtx_ctx *c, const mtx_camera *cam) {
     return MTX_E_ARG;
   }
   c->scene.camera = *cam;
+  return MTX_OK;
+}
+
+int mtx_restir_rows(mtx_ctx *c, int which, uint32_t row0, uint32_t nrows, void *buf, int to_state) {
+  if (!c || !buf || which < 0 || which > 1) {
+    mtx_set_error("mtx_restir_rows: bad argument");
+    return MTX_E_ARG;
+  }
+  if (!c->rs_n || !c->has_scene) {
+    mtx_set_error("mtx_restir_rows: no ReSTIR GI state");
+    return MTX_E_ARG;
+  }
+  const uint32_t W = c->scene.camera.width, H = c->scene.camera.height;
+  if (row0 + nrows > H || nrows == 0) {
+    mtx_set_error("mtx_restir_rows: rows [%u, %u) outside the film", row0, row0 + nrows);
+    return MTX_E_ARG;
+  }
+  const size_t n = c->rs_n, per_row = n / H;  // lanes per row (W * spp)
+  (void)W;
+  const int planes = which == 0 ? 5 : 6;
+  // which = 0: the current frame's samples (before stage B swaps them)
+  char *state = (char *)(which == 0 ? c->rs_samp[c->rs_cur].p : c->rs_tres.p);
+  char *dev = (char *)buf;
+  HIP_TRY(hipSetDevice(c->device));
+  for (int k = 0; k < planes; ++k) {
+    char *s = state + 16 * ((size_t)k * n + (size_t)row0 * per_row);
+    char *d = dev + 16 * (size_t)k * nrows * per_row;
+    const size_t bytes = 16 * (size_t)nrows * per_row;
+    HIP_TRY(hipMemcpyAsync(to_state ? s : d, to_state ? d : s, bytes, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return MTX_OK;
 }
 

@@ -12,10 +12,16 @@
 // * hashgrid_build: hashgrid.py:16-90 — scalar bbox reduction, cell hash,
 //   atomic per-cell rank (the reference's winner election, :52-63), exclusive
 //   scan (:65-76), scatter of sample indices (:79-84).
-// * scatter_reduce_f32: reductions.py:12-54 — winner-election rounds with the
-//   winner chosen as the smallest queued index (atomicMin), so every target
-//   receives its values in ascending index order (deterministic).
+// * scatter_reduce_f32: reductions.py:12-54 — the reference serialises each
+//   target with host-synchronised winner-election rounds (race-defined
+//   order). Here: one stable radix sort of (index, value) pairs (rocPRIM,
+//   header-only), segment bounds from the sorted keys, then one thread per
+//   target folds its segment in ascending original position — every target
+//   receives its values in ascending index order (deterministic), with no
+//   host round trips.
 #include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "mtx.h"
 #include "prims.h"
@@ -30,7 +36,6 @@ constexpr int kScanBlock = 256;
 constexpr int kScanItems = 16;
 constexpr uint32_t kScanTile = kScanBlock * kScanItems;
 
-__device__ __forceinline__ uint32_t lane() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -245,55 +250,29 @@ __global__ void k_hash_fill(uint64_t n, const uint32_t *cell, const uint32_t *ra
 }
 
 // --------------------------- scatter reduce -------------------------------
-__global__ void k_sr_init(uint32_t *q, uint64_t n, uint32_t *slot, uint64_t nt) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) q[i] = (uint32_t)i;
-  if (i < nt) slot[i] = 0xffffffffu;
+__global__ void k_sr_bounds(const uint32_t *keys, uint64_t n, uint32_t *seg_start, uint32_t *seg_end) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t key = keys[k];
+  if (k == 0 || keys[k - 1] != key) seg_start[key] = (uint32_t)k;
+  if (k == n - 1 || keys[k + 1] != key) seg_end[key] = (uint32_t)(k + 1);
 }
 
-__global__ void k_sr_elect(const uint32_t *q, const uint32_t *cnt, const uint32_t *index, uint32_t *slot) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= *cnt) return;
-  const uint32_t v = q[i];
-  atomicMin(&slot[index[v]], v);
-}
-
-__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
-  const uint64_t mask = __ballot(pred);
-  const uint32_t prefix =
-      __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-  const uint32_t total = (uint32_t)__popcll(mask);
-  uint32_t base = 0;
-  if (total) {
-    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)mask) - 1);
-    if (lane() == leader) base = atomicAdd(counter, total);
-    base = __builtin_amdgcn_readlane(base, leader);
+__global__ void k_sr_fold(int op, float *target, uint64_t nt, const float *vals, const uint32_t *seg_start,
+                          const uint32_t *seg_end) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  const uint32_t b = seg_start[t], e = seg_end[t];
+  if (b >= e) return;
+  float acc = target[t];
+  for (uint32_t k = b; k < e; ++k) {
+    const float v = vals[k];
+    acc = op == 0 ? acc + v : (op == 1 ? fminf(acc, v) : fmaxf(acc, v));
   }
-  return base + prefix;
+  target[t] = acc;
 }
 
-__global__ void k_sr_apply(int op, float *target, const float *value, const uint32_t *index, const uint32_t *q,
-                           const uint32_t *cnt, uint32_t *slot, uint32_t *q_next, uint32_t *cnt_next) {
-  const uint32_t n = *cnt;
-  const uint32_t wave_base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
-  if (wave_base >= n) return;  // wave-uniform
-  const uint32_t i = wave_base + (threadIdx.x & 63);
-  bool requeue = false;
-  uint32_t v = 0;
-  if (i < n) {
-    v = q[i];
-    const uint32_t t = index[v];
-    if (slot[t] == v) {
-      const float a = target[t], b = value[v];
-      target[t] = op == 0 ? a + b : (op == 1 ? fminf(a, b) : fmaxf(a, b));
-      slot[t] = 0xffffffffu;
-    } else {
-      requeue = true;
-    }
-  }
-  const uint32_t s = wave_append(cnt_next, requeue);
-  if (requeue) q_next[s] = v;
-}
+
 
 inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
@@ -360,34 +339,39 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
   return MTX_OK;
 }
 
-size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value) { return 4ull * (2 * n_value + n_target + 64); }
+static unsigned key_bits(uint64_t n_target) {
+  unsigned b = 1;
+  while (b < 32 && (1ull << b) < n_target) ++b;
+  return b;
+}
+
+static size_t sort_temp_bytes(uint64_t n_value, uint64_t n_target) {
+  size_t bytes = 0;
+  rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, (const float *)nullptr,
+                            (float *)nullptr, (size_t)n_value, 0u, key_bits(n_target));
+  return bytes;
+}
+
+size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value) {
+  return 8ull * n_value + 8ull * n_target + sort_temp_bytes(n_value, n_target) + 256;
+}
 
 int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
                        uint64_t n_value, void *ws, hipStream_t st) {
-  uint32_t *qa = (uint32_t *)ws, *qb = qa + n_value, *slot = qb + n_value, *cnts = slot + n_target;
-  const uint64_t init_n = n_value > n_target ? n_value : n_target;
-  hipLaunchKernelGGL(k_sr_init, dim3(nblk(init_n, 256)), dim3(256), 0, st, qa, n_value, slot, n_target);
-  uint32_t nv = (uint32_t)n_value;
-  if (hipMemcpyAsync(&cnts[0], &nv, 4, hipMemcpyHostToDevice, st) != hipSuccess) return MTX_E_HIP;
-  hipStreamSynchronize(st);
-  uint32_t remaining = nv;
-  int r = 0;
-  while (remaining > 0) {
-    uint32_t *cin = &cnts[r & 1], *cout = &cnts[(r + 1) & 1];
-    hipMemsetAsync(cout, 0, 4, st);
-    hipLaunchKernelGGL(k_sr_elect, dim3(nblk(remaining, 256)), dim3(256), 0, st, qa, cin, index, slot);
-    hipLaunchKernelGGL(k_sr_apply, dim3(nblk(remaining, 256)), dim3(256), 0, st, op, target, value, index, qa, cin,
-                       slot, qb, cout);
-    if (hipMemcpyAsync(&remaining, cout, 4, hipMemcpyDeviceToHost, st) != hipSuccess) return MTX_E_HIP;
-    if (hipStreamSynchronize(st) != hipSuccess) {
-      mtx_set_error("scatter_reduce: kernel failure");
-      return MTX_E_HIP;
-    }
-    uint32_t *t = qa;
-    qa = qb;
-    qb = t;
-    ++r;
+  uint32_t *keys = (uint32_t *)ws;
+  float *vals = (float *)(keys + n_value);
+  uint32_t *seg_start = (uint32_t *)(vals + n_value), *seg_end = seg_start + n_target;
+  void *temp = (void *)(((uintptr_t)(seg_end + n_target) + 255) & ~(uintptr_t)255);
+  size_t temp_bytes = sort_temp_bytes(n_value, n_target);
+  if (rocprim::radix_sort_pairs(temp, temp_bytes, index, keys, value, vals, (size_t)n_value, 0u,
+                                key_bits(n_target), st) != hipSuccess) {
+    mtx_set_error("scatter_reduce: radix sort failed");
+    return MTX_E_HIP;
   }
+  if (hipMemsetAsync(seg_start, 0, 8ull * n_target, st) != hipSuccess) return MTX_E_HIP;
+  hipLaunchKernelGGL(k_sr_bounds, dim3(nblk(n_value, 256)), dim3(256), 0, st, keys, n_value, seg_start, seg_end);
+  hipLaunchKernelGGL(k_sr_fold, dim3(nblk(n_target, 256)), dim3(256), 0, st, op, target, n_target, vals, seg_start,
+                     seg_end);
   return MTX_OK;
 }
 

@@ -76,8 +76,8 @@ __device__ __forceinline__ uint4 st_rng(const Pcg32 &g, uint32_t w) {
 
 __device__ __forceinline__ float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
-// lane i = q * spp + s (pixel-major, the sampler lane order) -> wavefront
-// path index (see wavefront.h)
+// band-local lane t = q * spp + s (pixel-major, the sampler lane order) ->
+// wavefront path index (see wavefront.h); global lane = r.lane0 + t
 __device__ __forceinline__ uint32_t path_of(uint32_t i, const ChunkParams &p) {
   if (!p.sample_major) return i;
   const uint32_t q = i / p.spp;
@@ -91,10 +91,11 @@ __device__ __forceinline__ uint32_t path_of(uint32_t i, const ChunkParams &p) {
 // consume the draws of one missed loop iteration.
 __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffers r) {
   const SceneView sv = make_view(s);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = r.lane0 + t;
   bool enq = false;
-  const uint32_t path = i < r.n ? path_of(i, p) : 0u;
-  if (i < r.n) {
+  const uint32_t path = t < r.nb ? path_of(t, p) : 0u;
+  if (t < r.nb) {
     const float4 h = b.hit[path], d4 = b.ray_d[path];
     r.prim_hit[i] = h;
     r.prim_dir[i] = d4;
@@ -142,9 +143,9 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
 
 // L_o = select(valid_ray, result, 0) (:588) and the sampler position.
 __global__ void k_rs_collect(WaveBuffers b, ChunkParams p, RestirBuffers r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= r.n) return;
-  const uint32_t path = path_of(i, p);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= r.nb) return;
+  const uint32_t i = r.lane0 + t, path = path_of(t, p);
   const float4 l = b.L[path];
   const uint4 m = b.misc[path];
   const bool valid_ray = ((m.w >> 16) & PF_VALID_RAY) != 0;
@@ -156,8 +157,9 @@ __global__ void k_rs_collect(WaveBuffers b, ChunkParams p, RestirBuffers r) {
 
 // temporal_resampling (:365-410)
 __global__ void k_rs_temporal(RestirBuffers r, ChunkParams p) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= r.n) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= r.nb) return;
+  const uint32_t i = r.lane0 + t;
   const uint32_t smp = i % p.spp;
   Pcg32 rng = ld_rng(r.rng[i]);
   const RSample S = ld_sample(r.cur, r.n, i);
@@ -212,9 +214,9 @@ __device__ __forceinline__ void emit_test(const RestirBuffers &r, bool pred, con
 
 // spatial_resampling, pass 1: the visibility rays of :316-318.
 __global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < r.n;
-  const uint32_t ii = live ? i : 0u;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = t < r.nb;
+  const uint32_t ii = r.lane0 + (live ? t : 0u);
   const uint32_t smp = ii % p.spp;
   const int64_t x = (int64_t)(ii / p.spp % p.width), y = (int64_t)(ii / p.width / p.spp);
   Pcg32 rng = ld_rng(r.rng[ii]);
@@ -240,9 +242,9 @@ __global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
 // results, merges (:320-332), and either finishes W (:350) or emits the
 // bias-correction rays (:334-346).
 __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = i < r.n;
-  const uint32_t ii = live ? i : 0u;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = t < r.nb;
+  const uint32_t ii = r.lane0 + (live ? t : 0u);
   const uint32_t smp = ii % p.spp;
   const int64_t x = (int64_t)(ii / p.spp % p.width), y = (int64_t)(ii / p.width / p.spp);
   const bool bias = (r.flags & MTX_RESTIR_BIAS_CORRECTION) != 0;
@@ -301,8 +303,9 @@ __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
 
 // bias correction tail (:340-348)
 __global__ void k_rs_bias_finish(RestirBuffers r, ChunkParams p) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= r.n) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= r.nb) return;
+  const uint32_t i = r.lane0 + t;
   uint32_t Z = r.qM[10 * (size_t)i + 9];
   for (int k = 0; k < 9; ++k) {
     const uint32_t e = r.qM[10 * (size_t)i + k];
@@ -322,8 +325,9 @@ __global__ void k_rs_bias_finish(RestirBuffers r, ChunkParams p) {
 // render_final (:261-272) and the block.put position (:236-242)
 __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffers r) {
   const SceneView sv = make_view(s);
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= r.n) return;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= r.nb) return;
+  const uint32_t i = r.lane0 + t;
   const RReservoir R = ld_res(r.sres, r.n, i);
   const float4 h = r.prim_hit[i], d4 = r.prim_dir[i];
   const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
@@ -335,7 +339,7 @@ __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   }
   const float4 em = r.emit[i];
   const V3 res = beta * R.z.L_o * R.W + V3{em.x, em.y, em.z};
-  const uint32_t path = path_of(i, p);
+  const uint32_t path = path_of(t, p);
   b.L[path] = make_float4(res.x, res.y, res.z, 0.f);
   const uint32_t x = i / p.spp % p.width, y = i / p.width / p.spp;
   b.pos[path] = make_float2((float)x, (float)y);
@@ -367,26 +371,26 @@ static inline unsigned rs_blocks(uint64_t n, unsigned bs) { return (unsigned)((n
 
 void launch_restir_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
                          hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_begin, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, s, b, p, r);
+  hipLaunchKernelGGL(k_rs_begin, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, s, b, p, r);
 }
 void launch_restir_collect(const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r, hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_collect, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, b, p, r);
+  hipLaunchKernelGGL(k_rs_collect, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, b, p, r);
 }
 void launch_restir_temporal(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_temporal, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+  hipLaunchKernelGGL(k_rs_temporal, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, r, p);
 }
 void launch_restir_spatial_rays(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_spatial_rays, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+  hipLaunchKernelGGL(k_rs_spatial_rays, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, r, p);
 }
 void launch_restir_spatial_merge(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_spatial_merge, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+  hipLaunchKernelGGL(k_rs_spatial_merge, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, r, p);
 }
 void launch_restir_bias_finish(const RestirBuffers &r, const ChunkParams &p, hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_bias_finish, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, r, p);
+  hipLaunchKernelGGL(k_rs_bias_finish, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, r, p);
 }
 void launch_restir_final(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
                          hipStream_t st) {
-  hipLaunchKernelGGL(k_rs_final, dim3(rs_blocks(r.n, 256)), dim3(256), 0, st, s, b, p, r);
+  hipLaunchKernelGGL(k_rs_final, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, s, b, p, r);
 }
 void launch_trace_test(const DevScene &s, const RestirBuffers &r, uint32_t occ_base, int grid, hipStream_t st) {
   hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, r, occ_base);

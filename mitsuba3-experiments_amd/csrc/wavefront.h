@@ -106,7 +106,9 @@ struct RestirBuffers {
   uint32_t *test_count;  // [0] count, [1] fetch cursor
   uint8_t *occ;       // 18 per lane: spatial tests [0,9), bias-correction tests [9,18)
   uint32_t *qM;       // 10 per lane: Q.M with bit 31 = active, [9] = Z before the loop
-  uint32_t n;
+  uint32_t n;      // lanes of the whole frame (state arrays)
+  uint32_t lane0;  // first lane of the rows this call computes
+  uint32_t nb;     // lanes this call computes (row band)
   mtx_camera prev_cam;
   uint32_t flags, max_M_temporal, max_M_spatial;
   float initial_radius, minimal_radius;

@@ -27,6 +27,8 @@ MTX_RESTIR_BIAS_CORRECTION = 1
 MTX_RESTIR_JACOBIAN = 2
 MTX_RESTIR_BSDF_SAMPLING = 4
 MTX_RESTIR_SPATIAL_SPATIAL = 8
+MTX_RESTIR_STAGE_A = 16
+MTX_RESTIR_STAGE_B = 32
 
 MTX_ROUGH_TRANSMITTANCE_RES = 64
 MTX_BVH_MAX_LEAF = 8
@@ -177,6 +179,7 @@ EXPORTS = [
     "mtx_scene_upload",
     "mtx_render",
     "mtx_set_camera",
+    "mtx_restir_rows",
     "mtx_restir_state",
     "mtx_sample_rays",
     "mtx_trace",

@@ -57,6 +57,7 @@ def lib() -> C.CDLL:
         "mtx_render": ([vp, C.POINTER(_abi.RenderArgs), vp, C.c_int, C.POINTER(_abi.Stats)], C.c_int),
         "mtx_last_device_ms": ([vp], C.c_double),
         "mtx_set_camera": ([vp, C.POINTER(_abi.Camera)], C.c_int),
+        "mtx_restir_rows": ([vp, C.c_int, u32, u32, vp, C.c_int], C.c_int),
         "mtx_restir_state": ([vp, C.c_int, vp, u64], C.c_int),
         "mtx_sample_rays": ([vp, C.POINTER(_abi.RenderArgs), u64, vp, vp, u32, vp, vp], C.c_int),
         "mtx_trace": ([vp, u64, vp, C.c_int, vp, vp], C.c_int),

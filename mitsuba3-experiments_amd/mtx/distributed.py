@@ -10,6 +10,13 @@ naturally (§8e):
     adding the overlapping halo rows in rank order.
 One collective per render (an all_gather of ~15 MB films for 1280x720);
 no data-path exchange during tracing.
+
+ReSTIR GI (restirgi.py) is the one path with an exchange step: its spatial
+reuse reads samples and temporal reservoirs up to `initial_search_radius`
+rows away (:301-313) and its temporal reuse reprojects into the previous
+frame. A row-banded frame runs stage A (initial sample + temporal) on the
+band, swaps a halo of ceil(radius) rows of samples and temporal reservoirs
+with the neighbouring bands (point-to-point), then stage B (spatial + final).
 """
 from __future__ import annotations
 
@@ -87,3 +94,99 @@ def render_sharded(render, height: int, spp: int, mode: str = "samples", group=N
         film = render(spp, spp, 0, y0, y1)
         return gather_bands(film, y0, y1, height, group)
     raise ValueError(mode)
+
+
+# ------------------------------------------------------------ ReSTIR bands --
+def restir_halo(integ) -> int:
+    """Halo rows a band needs from each neighbour: the spatial taps reach
+    trunc(radius) <= initial_search_radius rows (the radius only shrinks), the
+    temporal reprojection of a static camera one row."""
+    import math
+
+    return max(1, int(math.ceil(float(integ.initial_search_radius))))
+
+
+def halo_plan(y0: int, y1: int, height: int, halo: int):
+    """(send_up, send_down, recv_up, recv_down) row ranges (row0, nrows) for
+    band [y0, y1): the previous band needs rows [y0, y0 + min(halo, H - y0)),
+    the next band rows [y1 - min(halo, y1), y1); this band receives the
+    min(halo, y0) rows above it and the min(halo, H - y1) rows below it."""
+    send_up = (y0, min(halo, height - y0))
+    send_down = (y1 - min(halo, y1), min(halo, y1))
+    recv_up = (y0 - min(halo, y0), min(halo, y0))
+    recv_down = (y1, min(halo, height - y1))
+    return send_up, send_down, recv_up, recv_down
+
+
+def exchange_halos(export_rows, import_rows, y0: int, y1: int, height: int, halo: int, group=None):
+    """Swap halo rows with the neighbouring ranks (torch.distributed P2P).
+
+    export_rows(which, row0, nrows) -> contiguous tensor; import_rows(which,
+    row0, tensor). which in ('sample', 'temporal'). Bands must be at least
+    `halo` rows tall so the neighbours own every halo row."""
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    send_up, send_down, recv_up, recv_down = halo_plan(y0, y1, height, halo)
+    if (rank > 0 and send_up[1] > y1 - y0) or (rank < world - 1 and send_down[1] > y1 - y0):
+        raise ValueError(f"band [{y0}, {y1}) is shorter than the {halo}-row halo")
+    for which in ("sample", "temporal"):
+        ops, recvs = [], []
+        if rank > 0 and send_up[1]:
+            ops.append(dist.P2POp(dist.isend, export_rows(which, *send_up), rank - 1, group))
+        if rank < world - 1 and send_down[1]:
+            ops.append(dist.P2POp(dist.isend, export_rows(which, *send_down), rank + 1, group))
+        if rank > 0 and recv_up[1]:
+            t = export_rows(which, recv_up[0], recv_up[1]).clone()  # shape / dtype / device template
+            ops.append(dist.P2POp(dist.irecv, t, rank - 1, group))
+            recvs.append((recv_up[0], t))
+        if rank < world - 1 and recv_down[1]:
+            t = export_rows(which, recv_down[0], recv_down[1]).clone()
+            ops.append(dist.P2POp(dist.irecv, t, rank + 1, group))
+            recvs.append((recv_down[0], t))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        for row0, t in recvs:
+            import_rows(which, row0, t)
+
+
+def restir_band_frame(integ, scene, seed: int, y0: int, y1: int, exchange, spp: int = 1, out=None, ctx=None):
+    """One ReSTIR GI frame for rows [y0, y1): stage A, exchange(), stage B.
+    Returns the band film (rows y0-1 .. y1)."""
+    integ.render_film(scene, seed=seed, spp=spp, y0=y0, y1=y1, stage="A", ctx=ctx)
+    exchange()
+    return integ.render_film(scene, seed=seed, spp=spp, y0=y0, y1=y1, stage="B", out=out, ctx=ctx)
+
+
+def device_row_io(integ, scene, spp: int = 1, ctx=None):
+    """export_rows / import_rows over mtx_restir_rows with device tensors."""
+    import torch
+
+    lanes_per_row = scene.width * spp
+    dev = torch.device("cuda", (ctx.device if ctx is not None else torch.cuda.current_device()))
+
+    def export_rows(which, row0, nrows):
+        planes = 5 if which == "sample" else 6
+        t = torch.empty((planes, nrows, lanes_per_row, 4), dtype=torch.float32, device=dev)
+        integ.rows(which, row0, nrows, t, to_state=False, ctx=ctx)
+        return t
+
+    def import_rows(which, row0, t):
+        integ.rows(which, row0, t.shape[1], t.contiguous(), to_state=True, ctx=ctx)
+
+    return export_rows, import_rows
+
+
+def render_restir_sharded(integ, scene, seed: int, spp: int = 1, group=None):
+    """Row-banded ReSTIR GI frame over torch.distributed (one rank per GPU):
+    returns the stitched film on rank 0 (None elsewhere)."""
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    y0, y1 = row_bands(scene.height, world)[rank]
+    halo = restir_halo(integ)
+    ex, im = device_row_io(integ, scene, spp)
+    film = restir_band_frame(integ, scene, seed, y0, y1,
+                             lambda: exchange_halos(ex, im, y0, y1, scene.height, halo, group), spp)
+    return gather_bands(film, y0, y1, scene.height, group)

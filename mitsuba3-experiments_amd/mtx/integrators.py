@@ -93,16 +93,18 @@ class SamplingIntegrator:
     # --------------------------------------------------------------- render --
     def render_film(self, scene, seed: int = 0, spp: int = 1, y0: int = 0, y1: int | None = None,
                     spp_total: int | None = None, sample_offset: int = 0, device: int | None = None,
-                    out=None, stats: bool = False, chunk_paths: int = 0, counters: bool = False):
+                    out=None, stats: bool = False, chunk_paths: int = 0, counters: bool = False, ctx=None,
+                    extra_flags: int = 0):
         """Raw film (rows y0-1..y1, cols -1..W) x RGBW. `out` may be a
         device tensor (torch, on the context's device) to keep the film in HBM.
         stats=True returns (film, stats) with per-kernel-class HIP-event
         times; counters=True also collects the traversal visit counters
         (slower kernels: use it outside timed regions)."""
-        ctx = context(device)
+        ctx = ctx or context(device)
         _bind_scene(ctx, scene)
         a = self.render_args(scene, seed, spp, y0, y1, spp_total, sample_offset, chunk_paths,
                              flags=(2 if stats else 0) | (1 if stats and counters else 0))
+        a.restir_flags |= int(extra_flags)
         shape = (a.y1 - a.y0 + 2, scene.width + 2, 4)
         st = _abi.Stats()
         if out is None:
@@ -247,11 +249,20 @@ class RestirIntegrator(SamplingIntegrator):
         return a
 
     def render_film(self, scene, seed: int = 0, spp: int = 1, device: int | None = None, out=None,
-                    stats: bool = False, counters: bool = False, **kwargs):
-        """One frame (restirgi.py:182-258); advances the frame counter."""
-        if kwargs.get("y0", 0) != 0 or kwargs.get("y1") not in (None, scene.height) or kwargs.get("sample_offset", 0):
-            raise MtxError("ReSTIR GI renders whole frames")
-        ctx = context(device)
+                    stats: bool = False, counters: bool = False, y0: int = 0, y1: int | None = None,
+                    stage: str | None = None, ctx=None, **kwargs):
+        """One frame (restirgi.py:182-258); advances the frame counter.
+
+        Row bands (multi-GPU): render rows [y0, y1) in two calls,
+        stage="A" (initial sample + temporal) and stage="B" (spatial + final +
+        film), importing the neighbours' halo rows in between
+        (:func:`mtx.distributed.restir_band_frame`)."""
+        if kwargs.get("sample_offset", 0) or kwargs.get("spp_total") not in (None, spp):
+            raise MtxError("ReSTIR GI renders all samples of its pixels")
+        y1 = scene.height if y1 is None else int(y1)
+        if stage not in (None, "A", "B"):
+            raise MtxError(f"stage must be None, 'A' or 'B', not {stage!r}")
+        ctx = ctx or context(device)
         _bind_scene(ctx, scene)
         size = (scene.width, scene.height, int(spp))
         if self.film_size is None:
@@ -260,16 +271,28 @@ class RestirIntegrator(SamplingIntegrator):
             raise MtxError(f"film size / spp changed between frames: {self.film_size} -> {size}")
         owner = getattr(ctx, "_restir_owner", None)
         if self.n > 0 and owner is not self:
-            raise MtxError("another ReSTIR integrator rendered on this device since the last frame")
+            raise MtxError("another ReSTIR integrator rendered on this device context since the last frame")
         ctx._restir_owner = self
+        self._ctx = ctx
         cam = scene.camera
         check(lib().mtx_set_camera(ctx.handle, C.byref(cam)), "mtx_set_camera")
+        flags = {None: 0, "A": _abi.MTX_RESTIR_STAGE_A, "B": _abi.MTX_RESTIR_STAGE_B}[stage]
         result = super().render_film(scene, seed=seed, spp=spp, device=device, out=out, stats=stats,
-                                     counters=counters)
-        self.n += 1  # restirgi.py:245
+                                     counters=counters, y0=y0, y1=y1, ctx=ctx, extra_flags=flags)
+        if stage != "A":
+            self.n += 1  # restirgi.py:245
         return result
 
-    def state(self, which: str, device: int | None = None) -> np.ndarray:
+    def rows(self, which: str, row0: int, nrows: int, buf, to_state: bool, ctx=None) -> None:
+        """Copy state rows to / from a device tensor (halo exchange):
+        which = 'sample' (5 planes) or 'temporal' (6 planes); buf is a
+        contiguous [planes, nrows, W*spp, 4] float32 tensor on the device."""
+        ctx = ctx or getattr(self, "_ctx", None) or context()
+        idx = {"sample": 0, "temporal": 1}[which]
+        check(lib().mtx_restir_rows(ctx.handle, idx, int(row0), int(nrows), C.c_void_p(buf.data_ptr()),
+                                    int(bool(to_state))), "mtx_restir_rows")
+
+    def state(self, which: str, device: int | None = None, ctx=None) -> np.ndarray:
         """Device state of the last frame: 'sample' (5 planes x lanes x 4),
         'temporal' / 'spatial' (6 planes), 'radius' (lanes)."""
         idx, planes = {"sample": (0, 5), "temporal": (1, 6), "spatial": (2, 6), "radius": (3, 0)}[which]
@@ -277,7 +300,8 @@ class RestirIntegrator(SamplingIntegrator):
         n = W * H * spp
         shape = (planes, n, 4) if planes else (n,)
         out = np.zeros(shape, np.float32)
-        check(lib().mtx_restir_state(context(device).handle, idx, out.ctypes.data, out.size), "mtx_restir_state")
+        ctx = ctx or getattr(self, "_ctx", None) or context(device)
+        check(lib().mtx_restir_state(ctx.handle, idx, out.ctypes.data, out.size), "mtx_restir_state")
         return out
 
     def sample(self, *args, **kwargs):

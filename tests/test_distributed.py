@@ -60,3 +60,71 @@ def test_two_rank_combine(tmp_path, oracle, mode):
     else:
         ref = oracle.render(sc, integ.render_args(sc, 4, 4, 0, sc.height))
     np.testing.assert_allclose(got, ref, rtol=2e-6, atol=1e-6)
+
+
+def _halo_worker(rank, world, port, height, halo, out_dir):
+    """ReSTIR row-band halo exchange (mtx.distributed.exchange_halos) with a
+    fake state: each rank owns rows of two plane stacks filled with a value
+    that encodes (which, plane, row, lane); after the exchange every rank must
+    hold its neighbours' halo rows exactly."""
+    import sys
+
+    sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd")]
+    import torch
+    import torch.distributed as dist
+
+    from mtx import distributed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    y0, y1 = distributed.row_bands(height, world)[rank]
+    lanes = 5
+
+    def truth(which, planes):
+        w = 0 if which == "sample" else 1
+        p = torch.arange(planes).view(planes, 1, 1, 1)
+        r = torch.arange(height).view(1, height, 1, 1)
+        l = torch.arange(lanes).view(1, 1, lanes, 1)
+        c = torch.arange(4).view(1, 1, 1, 4)
+        return (((w * 10 + p) * 1000 + r) * 100 + l) * 10 + c + 0.0
+
+    state = {}
+    for which, planes in (("sample", 5), ("temporal", 6)):
+        s = torch.full((planes, height, lanes, 4), -1.0)
+        s[:, y0:y1] = truth(which, planes)[:, y0:y1]
+        state[which] = s
+
+    def export_rows(which, row0, nrows):
+        return state[which][:, row0:row0 + nrows].contiguous()
+
+    def import_rows(which, row0, t):
+        state[which][:, row0:row0 + t.shape[1]] = t
+
+    distributed.exchange_halos(export_rows, import_rows, y0, y1, height, halo)
+    ok = True
+    lo, hi = max(0, y0 - halo), min(height, y1 + halo)
+    for which, planes in (("sample", 5), ("temporal", 6)):
+        t = truth(which, planes)
+        ok &= bool(torch.equal(state[which][:, lo:hi], t[:, lo:hi]))
+        ok &= bool((state[which][:, :lo] == -1).all()) and bool((state[which][:, hi:] == -1).all())
+    np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.array([ok]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height,halo", [(2, 27, 10), (3, 40, 10), (4, 16, 3)])
+def test_restir_halo_exchange(tmp_path, world, height, halo):
+    mp.start_processes(_halo_worker, args=(world, _free_port(), height, halo, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        assert bool(np.load(os.path.join(tmp_path, f"ok{r}.npy"))[0]), f"rank {r}"
+
+
+def test_halo_plan_edges():
+    from mtx import distributed
+
+    # first band: nothing above; last band: nothing below
+    su, sd, ru, rd = distributed.halo_plan(0, 10, 30, 4)
+    assert ru == (0, 0) and sd == (6, 4) and rd == (10, 4)
+    su, sd, ru, rd = distributed.halo_plan(20, 30, 30, 4)
+    assert rd == (30, 0) and su == (20, 4) and ru == (16, 4)
