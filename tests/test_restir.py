@@ -126,8 +126,10 @@ def test_restir_errors():
 
     sc = scene.bedroom(32, 18, scale=0.02, tex_res=32)
     integ = load_dict({"type": "restirgi", "max_M_spatial": 500})
+    with pytest.raises(MtxError):  # stage B without its stage A
+        integ.render_film(sc, seed=0, spp=1, y0=4, stage="B")
     with pytest.raises(MtxError):
-        integ.render_film(sc, seed=0, spp=1, y0=4)
+        integ.render_film(sc, seed=0, spp=1, stage="C")
     integ.render_film(sc, seed=0, spp=1)
     with pytest.raises(MtxError):
         integ.render_film(sc.with_film(16, 16), seed=1, spp=1)
