@@ -42,9 +42,14 @@ class Scene:
     # ------------------------------------------------------------ building --
     @classmethod
     def bedroom(cls, width: int | None = None, height: int | None = None, scale: float = 1.0,
-                tex_res: int = 512, spec: dict | None = None) -> "Scene":
+                tex_res: int = 512, spec: dict | None = None, base_dir: str | None = None) -> "Scene":
         """The bedroom proxy. `scale` multiplies every triangle budget
-        (1.0 = the versioned ≈1.83 M-triangle benchmark scene)."""
+        (1.0 = the versioned ≈1.83 M-triangle benchmark scene).
+
+        With `base_dir` (the directory of the scene XML), meshes and bitmaps
+        whose files exist there (and are not Git-LFS pointers) are loaded
+        from disk (:mod:`mtx.obj`); the others fall back to the proxy."""
+        from . import obj as objio
         spec = spec or load_bedroom_spec()
         s = cls()
         film = spec["sensor"]["film"]
@@ -55,15 +60,21 @@ class Scene:
         tex_names, texels, textures = [], [], []
         tables = []
         mats, mat_index = [], {}
+        loaded = []  # files read from base_dir
 
         def texture_id(t):
             fn = t.get("filename", "tex")
             if fn in tex_names:
                 return tex_names.index(fn)
-            img = proxy.procedural_texture(fn, tex_res)
+            full = os.path.join(base_dir, fn) if base_dir else None
+            if full and objio.is_real_file(full):
+                img = objio.load_bitmap(full)
+                loaded.append(fn)
+            else:
+                img = proxy.procedural_texture(fn, tex_res)
             off = sum(x.size for x in texels)
-            texels.append(img.reshape(-1))
-            textures.append((tex_res, tex_res, off))
+            texels.append(np.ascontiguousarray(img, np.float32).reshape(-1))
+            textures.append((img.shape[1], img.shape[0], off))
             tex_names.append(fn)
             return len(tex_names) - 1
 
@@ -153,6 +164,26 @@ class Scene:
                 N = np.zeros_like(P)
                 UV = (loc[:, :2] + 1) * 0.5
                 flags = 1  # face normals
+            elif base_dir and sd.get("filename") and objio.is_real_file(os.path.join(base_dir, sd["filename"])):
+                if sd["type"] != "obj":
+                    raise ValueError(f"shape type {sd['type']!r} is not supported (obj, rectangle)")
+                face_n = bool(sd.get("face_normals", False))
+                P, N, UV, F = objio.load_obj(os.path.join(base_dir, sd["filename"]), face_normals=face_n,
+                                             flip_tex_coords=bool(sd.get("flip_tex_coords", True)))
+                loaded.append(sd["filename"])
+                P = P @ M[:3, :3].T + M[:3, 3]
+                flags = 0
+                if N is None:
+                    N = np.zeros_like(P)
+                    flags |= 1
+                else:
+                    N = N @ np.linalg.inv(M[:3, :3])  # normals transform with the inverse transpose
+                    N /= np.maximum(np.linalg.norm(N, axis=1, keepdims=True), 1e-30)
+                if UV is None:
+                    UV = np.zeros((len(P), 2))
+                else:
+                    flags |= 2
+                budgets[sd["id"]] = len(F)
             else:
                 fam = sd["id"].split("_")[0]
                 k = family_count.get(fam, 0)
@@ -207,10 +238,21 @@ class Scene:
         s.n_tables = int(sum(x.size for x in tables))
         s.camera = _camera(spec["sensor"], W, H)
         s._build_bvh(tri_vidx, tri_shape)
-        s.meta = {"scene": "bedroom-proxy", "proxy_version": proxy.PROXY_VERSION, "scale": scale,
-                  "width": W, "height": H, "n_tris": int(s.n_tris), "budgets": budgets,
-                  "bvh_depth": s.bvh_depth, "n_nodes": int(s.n_nodes)}
+        s.meta = {"scene": "bedroom-proxy" if not loaded else "xml", "proxy_version": proxy.PROXY_VERSION,
+                  "scale": scale, "width": W, "height": H, "n_tris": int(s.n_tris), "budgets": budgets,
+                  "bvh_depth": s.bvh_depth, "n_nodes": int(s.n_nodes), "loaded_files": loaded}
         return s
+
+    @classmethod
+    def from_xml(cls, path: str, width: int | None = None, height: int | None = None, tex_res: int = 512,
+                 scale: float = 1.0) -> "Scene":
+        """mi.load_file(path) for the supported XML subset (mtx/xmlscene.py):
+        OBJ meshes and bitmaps are read from disk where present; meshes that
+        are Git-LFS pointers get the deterministic proxy of their budget."""
+        from .xmlscene import parse_scene_xml
+        spec = parse_scene_xml(path)
+        return cls.bedroom(width, height, scale=scale, tex_res=tex_res, spec=spec,
+                           base_dir=os.path.dirname(os.path.abspath(path)))
 
     def _build_bvh(self, tri_vidx, tri_shape):
         from ._lib import check, lib
