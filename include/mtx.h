@@ -296,6 +296,27 @@ int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolu
 int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value);
 
+/* --------------------------- radiance field ----------------------- */
+/* nerad.py:54-106 Field (hash-grid + SH encoding, fp16 MLP with LeakyReLU,
+ * no bias), the radiance cache queried by NRC. */
+typedef struct mtx_field_desc {
+  uint32_t n_levels, n_features, log2_table, base_res; /* grid encoding */
+  float per_level_scale;
+  float bbox_min[3], bbox_max[3];                     /* scene.bbox() */
+  uint32_t n_in;      /* features per query: 3 + n_levels*n_features + 3 + 16, <= 64 */
+  uint32_t n_hidden;  /* hidden 64x64 layers (nerad.py:61: 4) */
+  const uint16_t *table;   /* fp16 bits [n_levels][2^log2_table][n_features] */
+  const uint16_t *weights; /* fp16 bits, row-major W0[64][n_in], W1..Wn[64][64], Wout[3][64] */
+} mtx_field_desc;
+/* Copy a field to HBM (weights prepacked as MFMA fragments). */
+int mtx_field_upload(mtx_ctx *ctx, const mtx_field_desc *field);
+/* Features (n x 64 fp16 bits) of n queries (p, wi: 3n floats). Host pointers. */
+int mtx_field_features(mtx_ctx *ctx, uint64_t n, const float *p, const float *wi, uint16_t *feat);
+/* MLP on n feature rows (n x 64 fp16 bits) -> out (3n floats). Host pointers. */
+int mtx_field_mlp(mtx_ctx *ctx, uint64_t n, const uint16_t *feat, float *out);
+/* Field(si) for n queries: encode + MLP -> out (3n floats). Host pointers. */
+int mtx_field_eval(mtx_ctx *ctx, uint64_t n, const float *p, const float *wi, float *out);
+
 /* HIP-event time (ms) of the device work of the last primitive call on ctx
  * (the scan / hash / scatter kernels, without the host<->device copies);
  * used by bench.py to report the primitives against their rooflines. */

@@ -1,0 +1,154 @@
+// Radiance-field feature encoding (nerad.py:54-106 Field.__call__), shared by
+// the device encoder and the CPU reference restatement used by the tests.
+//
+//   p_norm = (p - bbox.min) / (bbox.max - bbox.min)            nerad.py:92-94
+//   p_enc  = multiresolution hash-grid encoding of p_norm        nerad.py:96
+//            (drjit.nn.HashGridEncoding; the coopvec-hashgrid branch of
+//            Dr.Jit is not available, so this restates the published
+//            Instant-NGP / tiny-cuda-nn grid encoding: parity unpinned)
+//   wi_enc = real spherical harmonics up to degree `sh_order`     nerad.py:101
+//            (dr.sh_eval, Sloan's generated evaluation)
+//   features = (p_norm, p_enc, wi, wi_enc) -> fp16                nerad.py:103
+#pragma once
+#include "common.h"
+
+namespace mtx {
+
+constexpr uint32_t kFieldMaxLevels = 32;
+
+struct FieldEncoding {
+  const uint16_t *table;  // fp16 bits, [level][2^log2_table][n_features]
+  uint32_t n_levels, n_features, log2_table;
+  // per level: scale = base_res * per_level_scale^l - 1 (computed once on the
+  // host in double, tiny-cuda-nn grid_scale) and resolution = ceil(scale) + 1
+  float level_scale[kFieldMaxLevels];
+  uint32_t level_res[kFieldMaxLevels];
+  float bbox_min[3], bbox_max[3];
+};
+
+constexpr uint32_t kFieldPrimes[3] = {1u, 2654435761u, 805459861u};
+
+// fp16 bits -> float (round-trip exact)
+MTX_HD float half_bits_to_float(uint16_t h) {
+  const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  if (e == 0) {
+    if (m == 0) return u2f(s);
+    float f = (float)m * 5.9604644775390625e-08f;  // 2^-24
+    return s ? -f : f;
+  }
+  if (e == 31) return u2f(s | 0x7f800000u | (m << 13));
+  return u2f(s | ((e + 112u) << 23) | (m << 13));
+}
+
+// float -> fp16 bits, round to nearest even (IEEE binary16, with subnormals)
+MTX_HD uint16_t float_to_half_bits(float f) {
+  const uint32_t x = f2u(f);
+  const uint32_t s = (x >> 16) & 0x8000u;
+  const uint32_t a = x & 0x7fffffffu;
+  if (a >= 0x7f800000u) return (uint16_t)(s | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+  if (a >= 0x477ff000u) return (uint16_t)(s | 0x7c00u);  // >= 65520 rounds to inf
+  if (a < 0x38800000u) {                                   // subnormal half (< 2^-14)
+    if (a < 0x33000000u) return (uint16_t)s;                // < 2^-25 -> 0
+    const uint32_t e = a >> 23, m = (a & 0x7fffffu) | 0x800000u;
+    const uint32_t shift = 126u - e;                        // 14 - (e - 127) + 13 - ...
+    uint32_t r = m >> shift;
+    const uint32_t rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1u);
+    if (rem > half || (rem == half && (r & 1u))) ++r;
+    return (uint16_t)(s | r);
+  }
+  uint32_t r = ((a - 0x38000000u) >> 13);
+  const uint32_t rem = a & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (r & 1u))) ++r;
+  return (uint16_t)(s | r);
+}
+
+MTX_HD float round_half(float f) { return half_bits_to_float(float_to_half_bits(f)); }
+
+// Hash-grid encoding of one point (p_norm in [0,1]^3): fp16 bits of the
+// n_levels * n_features interpolated features (f32 interpolation, one
+// rounding to fp16 per feature).
+MTX_HD void field_hashgrid(const FieldEncoding &e, V3 pn, uint16_t *out) {
+  const uint32_t T = 1u << e.log2_table;
+  for (uint32_t l = 0; l < e.n_levels; ++l) {
+    const float scale = e.level_scale[l];
+    const uint32_t res = e.level_res[l];
+    const bool dense = (uint64_t)res * res * res <= (uint64_t)T;
+    const float px = fmaf(pn.x, scale, 0.5f), py = fmaf(pn.y, scale, 0.5f), pz = fmaf(pn.z, scale, 0.5f);
+    const float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
+    const float tx = px - fx, ty = py - fy, tz = pz - fz;
+    const uint32_t gx = (uint32_t)(int32_t)fx, gy = (uint32_t)(int32_t)fy, gz = (uint32_t)(int32_t)fz;
+    float acc0 = 0.f, acc1 = 0.f;
+    for (uint32_t c = 0; c < 8; ++c) {
+      const uint32_t bx = c & 1u, by = (c >> 1) & 1u, bz = (c >> 2) & 1u;
+      const uint32_t x = gx + bx, y = gy + by, z = gz + bz;
+      uint32_t idx;
+      if (dense)
+        idx = x + y * res + z * res * res;
+      else
+        idx = (x * kFieldPrimes[0]) ^ (y * kFieldPrimes[1]) ^ (z * kFieldPrimes[2]);
+      idx &= T - 1u;  // T is a power of two
+      const float w = (bx ? tx : 1.f - tx) * (by ? ty : 1.f - ty) * (bz ? tz : 1.f - tz);
+      const uint16_t *f = e.table + ((size_t)l * T + idx) * e.n_features;
+      acc0 = fmaf(w, half_bits_to_float(f[0]), acc0);
+      if (e.n_features > 1) acc1 = fmaf(w, half_bits_to_float(f[1]), acc1);
+    }
+    out[e.n_features * l] = float_to_half_bits(acc0);
+    if (e.n_features > 1) out[e.n_features * l + 1] = float_to_half_bits(acc1);
+  }
+}
+
+// Real spherical harmonics, degrees 0..3 (16 coefficients, index l*(l+1)+m).
+MTX_HD void field_sh3(V3 d, float *r) {
+  const float x = d.x, y = d.y, z = d.z, z2 = z * z;
+  r[0] = 0.28209479177387814f;
+  r[2] = z * 0.488602511902919923f;
+  r[6] = fmaf(z2, 0.94617469575756008f, -0.315391565252520045f);
+  r[12] = z * fmaf(z2, 1.865881662950577f, -1.1195289977703462f);
+  float c0 = x, s0 = y;
+  float ta = -0.488602511902919978f;
+  r[3] = ta * c0;
+  r[1] = ta * s0;
+  float tb = z * -1.09254843059207896f;
+  r[7] = tb * c0;
+  r[5] = tb * s0;
+  float tc = fmaf(z2, -2.28522899732232876f, 0.457045799464465774f);
+  r[13] = tc * c0;
+  r[11] = tc * s0;
+  float c1 = fmaf(x, c0, -(y * s0)), s1 = fmaf(x, s0, y * c0);
+  ta = 0.546274215296039478f;
+  r[8] = ta * c1;
+  r[4] = ta * s1;
+  tb = z * 1.44530572132027735f;
+  r[14] = tb * c1;
+  r[10] = tb * s1;
+  c0 = fmaf(x, c1, -(y * s1));
+  s0 = fmaf(x, s1, y * c1);
+  tc = -0.590043589926643519f;
+  r[15] = tc * c0;
+  r[9] = tc * s0;
+}
+
+// Feature vector (fp16 bits) of one query: p_norm(3), p_enc(L*F), wi(3),
+// sh(16), zero padding up to n_pad. Returns the number of real features.
+MTX_HD uint32_t field_features(const FieldEncoding &e, V3 p, V3 wi, uint16_t *out, uint32_t n_pad) {
+  const V3 pn = V3{(p.x - e.bbox_min[0]) / (e.bbox_max[0] - e.bbox_min[0]),
+                   (p.y - e.bbox_min[1]) / (e.bbox_max[1] - e.bbox_min[1]),
+                   (p.z - e.bbox_min[2]) / (e.bbox_max[2] - e.bbox_min[2])};
+  float sh[16];
+  field_sh3(wi, sh);
+  uint32_t k = 0;
+  out[k++] = float_to_half_bits(pn.x);
+  out[k++] = float_to_half_bits(pn.y);
+  out[k++] = float_to_half_bits(pn.z);
+  field_hashgrid(e, pn, out + k);
+  k += e.n_levels * e.n_features;
+  out[k++] = float_to_half_bits(wi.x);
+  out[k++] = float_to_half_bits(wi.y);
+  out[k++] = float_to_half_bits(wi.z);
+  for (int i = 0; i < 16; ++i) out[k++] = float_to_half_bits(sh[i]);
+  const uint32_t n = k;
+  while (k < n_pad) out[k++] = 0;
+  return n;
+}
+
+}  // namespace mtx

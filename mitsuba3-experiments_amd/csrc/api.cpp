@@ -91,6 +91,11 @@ struct mtx_ctx {
   // scene
   DevBuf stack_ovf;  // traversal stack entries beyond the LDS part
   DevBuf shade_rec;  // per-triangle shading records
+  // radiance field (mtx_field_upload)
+  DevBuf field_table, field_frag, fq_p, fq_d, f_feat, f_out;
+  mtx::FieldEncoding field{};
+  uint32_t field_hidden = 0;
+  bool has_field = false;
   DevBuf nodes, tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
@@ -172,7 +177,8 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
-                    &c->stack_ovf, &c->shade_rec, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
+                    &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
+                    &c->f_feat, &c->f_out, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
@@ -994,6 +1000,143 @@ static void prim_timer_read(mtx_ctx *c) {
 }
 
 double mtx_last_device_ms(mtx_ctx *c) { return c ? c->last_device_ms : 0.0; }
+
+int mtx_field_upload(mtx_ctx *c, const mtx_field_desc *f) {
+  if (!c || !f || !f->table || !f->weights) {
+    mtx_set_error("mtx_field_upload: null argument");
+    return MTX_E_ARG;
+  }
+  if (f->n_levels == 0 || f->n_levels > mtx::kFieldMaxLevels || f->n_features < 1 || f->n_features > 2 ||
+      f->log2_table < 4 || f->log2_table > 26 || f->n_hidden > 16 ||
+      f->n_in != 3 + f->n_levels * f->n_features + 3 + 16 || f->n_in > 64 || f->base_res < 1 ||
+      !(f->per_level_scale >= 1.f)) {
+    mtx_set_error("mtx_field_upload: unsupported field shape (n_in must be 3 + L*F + 19 <= 64)");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  const size_t table_halfs = (size_t)f->n_levels * ((size_t)1 << f->log2_table) * f->n_features;
+  if ((rc = upload(c->field_table, f->table, table_halfs, c->stream))) return rc;
+  const uint32_t n_frag = mtxd::field_frag_count(f->n_hidden);
+  std::vector<uint16_t> frag((size_t)n_frag * 64 * 8);
+  mtxd::field_prepack(f->weights, f->n_in, f->n_hidden, frag.data());
+  if ((rc = upload(c->field_frag, frag.data(), frag.size(), c->stream))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  mtx::FieldEncoding &e = c->field;
+  e.table = (const uint16_t *)c->field_table.p;
+  e.n_levels = f->n_levels;
+  e.n_features = f->n_features;
+  e.log2_table = f->log2_table;
+  for (uint32_t l = 0; l < f->n_levels; ++l) {
+    const double scale = std::exp2((double)l * std::log2((double)f->per_level_scale)) * f->base_res - 1.0;
+    e.level_scale[l] = (float)scale;
+    e.level_res[l] = (uint32_t)std::ceil((double)(float)scale) + 1u;
+  }
+  for (int k = 0; k < 3; ++k) {
+    e.bbox_min[k] = f->bbox_min[k];
+    e.bbox_max[k] = f->bbox_max[k];
+  }
+  c->field_hidden = f->n_hidden;
+  c->has_field = true;
+  return MTX_OK;
+}
+
+static int field_stage_queries(mtx_ctx *c, uint64_t n, const float *p, const float *wi) {
+  int rc;
+  if ((rc = dalloc(c->fq_p, 16 * n))) return rc;
+  if ((rc = dalloc(c->fq_d, 16 * n))) return rc;
+  std::vector<float> tp(4 * n), td(4 * n);
+  for (uint64_t i = 0; i < n; ++i)
+    for (int k = 0; k < 3; ++k) {
+      tp[4 * i + k] = p[3 * i + k];
+      td[4 * i + k] = wi[3 * i + k];
+    }
+  HIP_TRY(hipMemcpy(c->fq_p.p, tp.data(), 16 * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->fq_d.p, td.data(), 16 * n, hipMemcpyHostToDevice));
+  return MTX_OK;
+}
+
+static int field_check(mtx_ctx *c, uint64_t n) {
+  if (!c || !c->has_field) {
+    mtx_set_error("no radiance field uploaded (mtx_field_upload)");
+    return MTX_E_ARG;
+  }
+  if (n >= (1ull << 31)) {
+    mtx_set_error("too many field queries");
+    return MTX_E_ARG;
+  }
+  return MTX_OK;
+}
+
+int mtx_field_features(mtx_ctx *c, uint64_t n, const float *p, const float *wi, uint16_t *feat) {
+  int rc = field_check(c, n);
+  if (rc) return rc;
+  if (n == 0) return MTX_OK;
+  if (!p || !wi || !feat) {
+    mtx_set_error("mtx_field_features: null buffer");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = field_stage_queries(c, n, p, wi))) return rc;
+  if ((rc = dalloc(c->f_feat, 128 * n))) return rc;
+  if ((rc = prim_timer_begin(c))) return rc;
+  mtxd::field_encode(c->field, (const float4 *)c->fq_p.p, (const float4 *)c->fq_d.p, nullptr, (uint32_t)n,
+                     (uint16_t *)c->f_feat.p, c->stream);
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(feat, c->f_feat.p, 128 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
+int mtx_field_mlp(mtx_ctx *c, uint64_t n, const uint16_t *feat, float *out) {
+  int rc = field_check(c, n);
+  if (rc) return rc;
+  if (n == 0) return MTX_OK;
+  if (!feat || !out) {
+    mtx_set_error("mtx_field_mlp: null buffer");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = dalloc(c->f_feat, 128 * n))) return rc;
+  if ((rc = dalloc(c->f_out, 12 * n))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->f_feat.p, feat, 128 * n, hipMemcpyHostToDevice, c->stream));
+  if ((rc = prim_timer_begin(c))) return rc;
+  mtxd::field_mlp((const uint16_t *)c->f_feat.p, nullptr, (uint32_t)n, c->field_frag.p, c->field_hidden,
+                  (float *)c->f_out.p, c->n_cu, c->stream);
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->f_out.p, 12 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
+int mtx_field_eval(mtx_ctx *c, uint64_t n, const float *p, const float *wi, float *out) {
+  int rc = field_check(c, n);
+  if (rc) return rc;
+  if (n == 0) return MTX_OK;
+  if (!p || !wi || !out) {
+    mtx_set_error("mtx_field_eval: null buffer");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = field_stage_queries(c, n, p, wi))) return rc;
+  if ((rc = dalloc(c->f_feat, 128 * n))) return rc;
+  if ((rc = dalloc(c->f_out, 12 * n))) return rc;
+  if ((rc = prim_timer_begin(c))) return rc;
+  mtxd::field_encode(c->field, (const float4 *)c->fq_p.p, (const float4 *)c->fq_d.p, nullptr, (uint32_t)n,
+                     (uint16_t *)c->f_feat.p, c->stream);
+  mtxd::field_mlp((const uint16_t *)c->f_feat.p, nullptr, (uint32_t)n, c->field_frag.p, c->field_hidden,
+                  (float *)c->f_out.p, c->n_cu, c->stream);
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->f_out.p, 12 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
 
 int mtx_prefix_sum_u32(mtx_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, int inclusive) {
   if (!c || (n && (!in || !out))) {

@@ -1,0 +1,199 @@
+// field.hip — fp16 radiance-field inference on the gfx950 matrix cores
+// (nerad.py:54-106 Field: hash-grid + SH encoding, then a 64-wide MLP with
+// LeakyReLU, no bias; SURVEY §8f item 3, the cache NRC queries).
+//
+// k_field_encode  one thread per query: mtx_core/field.h features -> fp16 row
+//                 of 64 (p_norm, hash-grid, wi, SH, zero padding)
+// k_field_mlp     one wave per 64 queries (two 32-query N-tiles), all layers
+//                 fused: activations stay in registers between layers. Every
+//                 layer is  Y[64 x 32q] = W[64 x 64] * X[64 x 32q]  with
+//                 v_mfma_f32_32x32x16_f16 (A = weights from LDS, B = the
+//                 previous accumulator converted to fp16). The accumulator's
+//                 rows (output features) sit in registers, so it is the next
+//                 layer's B operand with no lane movement; the host prepacks
+//                 each weight fragment in that permuted k order
+//                 (cdna_hip_programming.md §3, "accumulator tile as the next
+//                 MFMA's operand"). f32 accumulation, fp16 activations.
+#include <hip/hip_runtime.h>
+
+#include "mtx.h"
+#include "mtx_core/field.h"
+#include "prims.h"
+
+void mtx_set_error(const char *fmt, ...);
+
+namespace mtxd {
+
+using namespace mtx;
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kFieldPad = 64;     // features per query (padded)
+constexpr float kLeakySlope = 0.01f;  // drjit.nn.LeakyReLU default
+
+__global__ void k_field_encode(FieldEncoding e, const float4 *qp, const float4 *qd, const uint32_t *count,
+                               uint32_t n_max, uint16_t *feat) {
+  const uint32_t n = count ? min(*count, n_max) : n_max;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float4 p = qp[i], d = qd[i];
+    field_features(e, V3{p.x, p.y, p.z}, V3{d.x, d.y, d.z}, feat + (size_t)kFieldPad * i, kFieldPad);
+  }
+}
+
+__device__ __forceinline__ half8 leaky_pack(const f32x16 &acc, int s) {
+  half8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = acc[8 * s + j];
+    r[j] = (_Float16)(v >= 0.f ? v : v * kLeakySlope);
+  }
+  return r;
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// wfrag: prepacked fragments [frag][64 lanes] (see field_prepack); n_hidden
+// hidden 64x64 layers after the input layer; out: 3 floats per query
+// (fp16-rounded, the reference's Float16 network output cast to Color3f).
+__global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const uint32_t *count, uint32_t n_max,
+                                                   const half8 *wfrag, uint32_t n_frag, uint32_t n_hidden,
+                                                   float *out) {
+  extern __shared__ half8 w[];
+  for (uint32_t i = threadIdx.x; i < n_frag * 64; i += blockDim.x) w[i] = wfrag[i];
+  __syncthreads();
+  const uint32_t n = count ? min(*count, n_max) : n_max;
+  const uint32_t lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+  const uint32_t waves_per_block = blockDim.x >> 6;
+  const uint32_t wave = blockIdx.x * waves_per_block + (threadIdx.x >> 6);
+  const uint32_t n_waves = gridDim.x * waves_per_block;
+  for (uint32_t tile = wave; tile * 64 < n; tile += n_waves) {
+    const uint32_t q0 = tile * 64;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = zero16();
+    // input layer: B fragments straight from the feature rows (natural k order)
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      half8 b[2];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const uint32_t q = q0 + nt * 32 + col;
+        if (q < n) {
+          b[nt] = *reinterpret_cast<const half8 *>(feat + (size_t)kFieldPad * q + ks * 16 + h * 8);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[nt][j] = (_Float16)0.f;
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const half8 a = w[(mt * 4 + ks) * 64 + lane];
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
+    uint32_t base = 8;
+    for (uint32_t layer = 0; layer < n_hidden; ++layer, base += 8) {
+      half8 bf[2][4];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) bf[nt][2 * mt + s] = leaky_pack(acc[mt][nt], s);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+          const half8 a = w[(base + mt * 4 + ks) * 64 + lane];
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[nt][ks], acc[mt][nt], 0, 0, 0);
+        }
+    }
+    // output layer (3 rows of one 32-row M tile)
+    half8 bf[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) bf[nt][2 * mt + s] = leaky_pack(acc[mt][nt], s);
+    f32x16 o[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const half8 a = w[(base + ks) * 64 + lane];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) o[nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[nt][ks], o[nt], 0, 0, 0);
+    }
+    // C/D rows 0..2 = registers 0..2 of the lanes with h = 0
+    if (h == 0) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const uint32_t q = q0 + nt * 32 + col;
+        if (q < n) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) out[3 * (size_t)q + c] = (float)(_Float16)o[nt][c];
+        }
+      }
+    }
+  }
+}
+
+uint32_t field_frag_count(uint32_t n_hidden) { return 8 * (1 + n_hidden) + 4; }
+
+// Host: weight matrices (fp16 bits, W[out][in] row-major per layer: input
+// n_in -> 64, n_hidden x 64 -> 64, 64 -> 3) -> MFMA A fragments.
+void field_prepack(const uint16_t *weights, uint32_t n_in, uint32_t n_hidden, uint16_t *frag) {
+  const uint32_t n_layers = n_hidden + 2;
+  size_t woff = 0;
+  uint32_t f = 0;
+  for (uint32_t l = 0; l < n_layers; ++l) {
+    const uint32_t in = l == 0 ? n_in : 64, out = l == n_layers - 1 ? 3 : 64;
+    const uint32_t n_mt = l == n_layers - 1 ? 1 : 2;
+    for (uint32_t mt = 0; mt < n_mt; ++mt)
+      for (uint32_t ks = 0; ks < 4; ++ks, ++f)
+        for (uint32_t lane = 0; lane < 64; ++lane)
+          for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t row = 32 * mt + (lane & 31), h = lane >> 5;
+            const uint32_t k = l == 0 ? 16 * ks + 8 * h + j
+                                      : 32 * (ks >> 1) + 16 * (ks & 1) + 8 * (j >> 2) + 4 * h + (j & 3);
+            frag[((size_t)f * 64 + lane) * 8 + j] = (row < out && k < in) ? weights[woff + (size_t)row * in + k] : 0;
+          }
+    woff += (size_t)in * out;
+  }
+}
+
+int field_encode(const FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count, uint32_t n_max,
+                 uint16_t *feat, hipStream_t st) {
+  if (n_max == 0) return MTX_OK;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n_max + 255) / 256, 65535);
+  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(256), 0, st, e, qp, qd, count, n_max, feat);
+  return MTX_OK;
+}
+
+int field_mlp(const uint16_t *feat, const uint32_t *count, uint32_t n_max, const void *wfrag, uint32_t n_hidden,
+              float *out, int n_cu, hipStream_t st) {
+  if (n_max == 0) return MTX_OK;
+  const uint32_t n_frag = field_frag_count(n_hidden);
+  const size_t lds = (size_t)n_frag * 64 * sizeof(half8);
+  const uint64_t tiles = (n_max + 63) / 64;
+  const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((tiles + 3) / 4, (uint64_t)n_cu * 3));
+  hipLaunchKernelGGL(k_field_mlp, dim3(blocks), dim3(256), lds, st, feat, count, n_max, (const half8 *)wfrag, n_frag,
+                     n_hidden, out);
+  return MTX_OK;
+}
+
+}  // namespace mtxd

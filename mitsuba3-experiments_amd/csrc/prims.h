@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mtx_core/field.h"
+
 namespace mtxd {
 
 size_t scan_workspace_bytes(uint64_t n);
@@ -21,5 +23,13 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
 size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value);
 int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
                        uint64_t n_value, void *ws, hipStream_t st);
+
+// Radiance field (field.hip)
+uint32_t field_frag_count(uint32_t n_hidden);
+void field_prepack(const uint16_t *weights, uint32_t n_in, uint32_t n_hidden, uint16_t *frag);
+int field_encode(const mtx::FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count,
+                 uint32_t n_max, uint16_t *feat, hipStream_t st);
+int field_mlp(const uint16_t *feat, const uint32_t *count, uint32_t n_max, const void *wfrag, uint32_t n_hidden,
+              float *out, int n_cu, hipStream_t st);
 
 }  // namespace mtxd

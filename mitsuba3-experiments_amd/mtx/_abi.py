@@ -145,6 +145,22 @@ class RenderArgs(C.Structure):
     ]
 
 
+class FieldDesc(C.Structure):
+    _fields_ = [
+        ("n_levels", C.c_uint32),
+        ("n_features", C.c_uint32),
+        ("log2_table", C.c_uint32),
+        ("base_res", C.c_uint32),
+        ("per_level_scale", C.c_float),
+        ("bbox_min", C.c_float * 3),
+        ("bbox_max", C.c_float * 3),
+        ("n_in", C.c_uint32),
+        ("n_hidden", C.c_uint32),
+        ("table", C.c_void_p),
+        ("weights", C.c_void_p),
+    ]
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("rays_closest", C.c_uint64),
@@ -187,5 +203,9 @@ EXPORTS = [
     "mtx_prefix_sum_f32_hs",
     "mtx_hashgrid_build",
     "mtx_scatter_reduce_f32",
+    "mtx_field_upload",
+    "mtx_field_features",
+    "mtx_field_mlp",
+    "mtx_field_eval",
     "mtx_last_device_ms",
 ]

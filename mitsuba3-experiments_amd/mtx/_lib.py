@@ -56,6 +56,10 @@ def lib() -> C.CDLL:
         "mtx_scene_upload": ([vp, C.POINTER(_abi.SceneDesc)], C.c_int),
         "mtx_render": ([vp, C.POINTER(_abi.RenderArgs), vp, C.c_int, C.POINTER(_abi.Stats)], C.c_int),
         "mtx_last_device_ms": ([vp], C.c_double),
+        "mtx_field_upload": ([vp, C.POINTER(_abi.FieldDesc)], C.c_int),
+        "mtx_field_features": ([vp, u64, vp, vp, vp], C.c_int),
+        "mtx_field_mlp": ([vp, u64, vp, vp], C.c_int),
+        "mtx_field_eval": ([vp, u64, vp, vp, vp], C.c_int),
         "mtx_set_camera": ([vp, C.POINTER(_abi.Camera)], C.c_int),
         "mtx_restir_rows": ([vp, C.c_int, u32, u32, vp, C.c_int], C.c_int),
         "mtx_restir_state": ([vp, C.c_int, vp, u64], C.c_int),

@@ -48,6 +48,7 @@ def lib():
             "orc_dmath": [C.c_int, vp, vp, u64],
             "orc_pssmlt_render": [SD, RA, u32, vp, vp],
             "orc_restir_frame": [SD, RA, C.POINTER(_abi.Camera), vp, vp, vp, vp, vp, vp],
+            "orc_field_features": [C.POINTER(_abi.FieldDesc), u64, vp, vp, vp],
         }
         for k, a in sig.items():
             getattr(L, k).argtypes = a
@@ -216,3 +217,13 @@ class RestirOracle:
         self.prev[...] = self.cur  # restirgi.py:247
         self.prev_cam = _abi.Camera.from_buffer_copy(bytes(scene.camera))
         return f
+
+
+def field_features(field, p, wi):
+    """mtx_core/field.h features of (p, wi) for a mtx.field.Field (fp16 rows of 64)."""
+    p = np.ascontiguousarray(p, np.float32).reshape(-1, 3)
+    wi = np.ascontiguousarray(wi, np.float32).reshape(-1, 3)
+    out = np.zeros((len(p), 64), np.uint16)
+    d = field.desc()
+    lib().orc_field_features(C.byref(d), len(p), p.ctypes.data, wi.ctypes.data, out.ctypes.data)
+    return out.view(np.float16)

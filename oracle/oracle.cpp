@@ -38,6 +38,7 @@
 #include "mtx_core/geometry.h"
 #include "mtx_core/interaction.h"
 #include "mtx_core/restir.h"
+#include "mtx_core/field.h"
 #include "mtx_core/rng.h"
 #include "mtx_core/warp.h"
 
@@ -892,6 +893,31 @@ extern "C" int orc_restir_frame(const mtx_scene_desc *d, const mtx_render_args *
 }
 
 extern "C" {
+
+// ------------------------- nerad.py:86-106 features -------------------------
+// The radiance-field encoder restated in mtx_core/field.h (shared with the
+// device), driven from a mtx_field_desc as mtx_field_upload does.
+int orc_field_features(const mtx_field_desc *f, uint64_t n, const float *p, const float *wi, uint16_t *out) {
+  FieldEncoding e{};
+  e.table = f->table;
+  e.n_levels = f->n_levels;
+  e.n_features = f->n_features;
+  e.log2_table = f->log2_table;
+  for (uint32_t l = 0; l < f->n_levels; ++l) {
+    const double scale = exp2((double)l * log2((double)f->per_level_scale)) * f->base_res - 1.0;
+    e.level_scale[l] = (float)scale;
+    e.level_res[l] = (uint32_t)ceil((double)(float)scale) + 1u;
+  }
+  for (int k = 0; k < 3; ++k) {
+    e.bbox_min[k] = f->bbox_min[k];
+    e.bbox_max[k] = f->bbox_max[k];
+  }
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i)
+    field_features(e, V3{p[3 * i], p[3 * i + 1], p[3 * i + 2]}, V3{wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]},
+                   out + 64 * i, 64);
+  return 0;
+}
 
 // ------------------------------- RNG KATs ----------------------------------
 int orc_rng_stream(uint32_t seed, uint32_t lane0, uint32_t n_lanes, uint32_t n_draws, float *out) {

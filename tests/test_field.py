@@ -1,0 +1,94 @@
+"""Radiance field (nerad.py:54-106) for NRC: shared encoder (oracle vs HIP,
+bit-exact) and the fused fp16 MFMA MLP (vs a plain fp32 reference with fp16
+activation rounding; tolerance stated below)."""
+import numpy as np
+import pytest
+
+
+def _field(**kw):
+    from mtx.field import Field
+
+    return Field(bbox=([-3.0, 0.0, -2.0], [4.0, 3.0, 4.0]), **kw)
+
+
+def _queries(n, seed=1):
+    rng = np.random.default_rng(seed)
+    p = rng.uniform([-3, 0, -2], [4, 3, 4], (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    return p, d
+
+
+def test_sh_basis_orthonormal(oracle):
+    """The 16 SH features (dr.sh_eval order 3) are orthonormal on the sphere."""
+    f = _field()
+    p, d = _queries(200_000, seed=3)
+    feat = oracle.field_features(f, p, d).astype(np.float64)
+    Y = feat[:, 38:54]
+    G = 4 * np.pi * (Y.T @ Y) / len(Y)
+    np.testing.assert_allclose(G, np.eye(16), atol=0.03)
+    assert np.array_equal(feat[:, 35:38], d.astype(np.float16).astype(np.float64))  # wi
+    assert (feat[:, 54:] == 0).all()
+
+
+def test_hashgrid_partition_of_unity_and_vertices(oracle):
+    f = _field()
+    f.table[:] = np.float16(1.0)
+    p, d = _queries(5000)
+    feat = oracle.field_features(f, p, d)
+    assert (feat[:, 3:35] == np.float16(1.0)).all()  # trilinear weights sum to one
+    # a point on a level-0 grid vertex returns that vertex's entry (dense level:
+    # scale 15, resolution 16, index x + 16 y + 256 z)
+    f2 = _field()
+    rng = np.random.default_rng(0)
+    f2.table[0] = rng.uniform(-1, 1, f2.table[0].shape).astype(np.float16)
+    gx, gy, gz = 3, 7, 11
+    pn = (np.array([gx, gy, gz], np.float64) - 0.5) / 15.0
+    pw = (f2.bbox_min + pn * (f2.bbox_max - f2.bbox_min)).astype(np.float32)[None]
+    feat = oracle.field_features(f2, pw, d[:1])
+    idx = gx + 16 * gy + 256 * gz
+    np.testing.assert_allclose(feat[0, 3:5].astype(np.float32), f2.table[0, idx].astype(np.float32), atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_field_features_bit_exact(oracle):
+    f = _field()
+    p, d = _queries(20_000)
+    assert np.array_equal(f.features(p, d).view(np.uint16), oracle.field_features(f, p, d).view(np.uint16))
+
+
+@pytest.mark.gpu
+def test_field_mlp_exact_on_integer_selection_network():
+    """Weights that select one input per output (asymmetric permutations) and
+    small non-negative integer features: every value is exact in fp16 and f32,
+    so any fragment-layout error shows as a wrong integer."""
+    f = _field()
+    n_in = f.n_in
+    for li, w in enumerate(f.weights):
+        w[:] = 0
+        rows, cols = w.shape
+        for o in range(rows):
+            k = (o * 7 + 3) % cols if li == 0 else ((o * 5 + 1) % cols if li < len(f.weights) - 1 else o * 11 + 2)
+            w[o, k] = 1
+    rng = np.random.default_rng(5)
+    n = 1000
+    feat = np.zeros((n, 64), np.float16)
+    feat[:, :n_in] = rng.integers(0, 8, (n, n_in)).astype(np.float16)
+    got = f.mlp(feat)
+    ref = f.mlp_reference(feat)
+    assert np.array_equal(got, ref)
+    assert len(np.unique(got)) > 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 1000, 65_537])
+def test_field_eval_vs_reference(oracle, n):
+    """Field(si) on the GPU vs encoder (oracle) + fp32 reference MLP.
+    Tolerance: fp16 activations and f32 MFMA accumulation in a different
+    order than numpy -> |err| <= 2e-3 + 2e-2 |ref|."""
+    f = _field()
+    p, d = _queries(n, seed=n)
+    got = f(p, d)
+    ref = f.mlp_reference(oracle.field_features(f, p, d))
+    np.testing.assert_allclose(got, ref, rtol=2e-2, atol=2e-3)
+    assert np.isfinite(got).all() and np.abs(got).max() > 0
