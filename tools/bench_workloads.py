@@ -278,5 +278,47 @@ def prims(args):
            "sample": f"same {nv} values ({c:.2f} s), oracle orc_scatter_reduce_f32"})
 
 
+# ------------------------------------------------- radiance field (MFMA) --
+MFMA_F16_PEAK_TFS = 2500.0  # MI355X dense fp16 (MI355X_MICROARCH.md; 2:1-sparse figure excluded)
+
+
+def field(args):
+    from mtx.field import Field
+    from mtx._lib import context, lib
+
+    ctx = context(0)
+    f = Field(bbox=([-3.0, 0.0, -2.0], [4.0, 3.0, 4.0]))
+    f.upload(ctx)
+    n = 1 << 22
+    rng = np.random.default_rng(0)
+    p = rng.uniform([-3, 0, -2], [4, 3, 4], (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    feat = f.features(p, d, ctx)
+    enc_ms = lib().mtx_last_device_ms(ctx.handle)
+    ms = []
+    for _ in range(5):
+        f.mlp(feat, ctx)
+        ms.append(lib().mtx_last_device_ms(ctx.handle))
+    ms = min(ms)
+    flops = f.flops_per_query() * n
+    tfs = flops / (ms / 1e3) / 1e12
+    # CPU: the fp32 numpy reference network on a sample (plain BLAS threads)
+    nc = 1 << 16
+    t0 = time.perf_counter()
+    f.mlp_reference(feat[:nc])
+    c = time.perf_counter() - t0
+    _line("Field MLP inference Mqueries/sec (nerad.py:54-106: 54->64x5->3 fp16, MFMA)", n / (ms / 1e3) / 1e6,
+          "Mqueries/s", 5, 1, ms,
+          {"workload": f"fused 6-layer MLP, {n} queries, v_mfma_f32_32x32x16_f16, f32 accumulate",
+           "flops_per_query": f.flops_per_query(), "encode_ms": round(enc_ms, 3),
+           "encode_Mqueries_s": round(n / (enc_ms / 1e3) / 1e6, 1)},
+          {"bound": "mfma", "kernel": "k_field_mlp", "achieved": round(tfs, 2), "peak": MFMA_F16_PEAK_TFS,
+           "unit": "TFLOP/s", "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "traffic": None,
+           "alg_bytes_per_launch": int(n * (128 + 12))},
+          {"value": round(nc / c / 1e6, 4), "unit": "Mqueries/s", "cores": _threads(), "kind": "port",
+           "sample": f"{nc} queries, numpy fp32 reference network ({c:.2f} s)"}, dtype="f16")
+
+
 def run(args):
-    {"pssmlt": pssmlt, "restir": restir, "nrc": nrc, "prims": prims}[args.workload](args)
+    {"pssmlt": pssmlt, "restir": restir, "nrc": nrc, "prims": prims, "field": field}[args.workload](args)
