@@ -166,7 +166,9 @@ typedef struct mtx_render_args {
   uint32_t y0, y1;       /* film rows [y0, y1) traced by this call */
   uint32_t chunk_paths;  /* wavefront size (0 = default) */
   float nrc_c;           /* NRC spread threshold (nrc.py:123) */
-  uint32_t flags;        /* bit0: collect traversal stats, bit1: per-kernel HIP event timing */
+  uint32_t flags;        /* bit0: collect traversal stats, bit1: per-kernel HIP event timing,
+                            bit2 (NRC): query the uploaded radiance field where the spread
+                            criterion ends a segment (NRC radiance cache) */
   uint32_t iterations;   /* PSSMLT Metropolis iterations (pssmlt.py:208: 200; 0 = 200) */
   uint32_t frame;        /* ReSTIR GI frame index (restirgi.py self.n); 0 resets the reservoirs */
   /* ReSTIR GI properties (restirgi.py:157-166) */

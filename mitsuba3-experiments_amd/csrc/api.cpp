@@ -93,6 +93,7 @@ struct mtx_ctx {
   DevBuf shade_rec;  // per-triangle shading records
   // radiance field (mtx_field_upload)
   DevBuf field_table, field_frag, fq_p, fq_d, f_feat, f_out;
+  DevBuf cq_p, cq_d, cq_t, cq_count;  // NRC cache queries of a chunk
   mtx::FieldEncoding field{};
   uint32_t field_hidden = 0;
   bool has_field = false;
@@ -178,7 +179,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
                     &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
-                    &c->f_feat, &c->f_out, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
+                    &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
   for (DevBuf *b : bufs) dfree(*b);
@@ -411,6 +412,10 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.mlt_prop = (float2 *)c->mlt_prop.p;
   b.vpath = (float4 *)c->vpath.p;
   b.vprop = (float4 *)c->vprop.p;
+  b.cq_p = (float4 *)c->cq_p.p;
+  b.cq_d = (float4 *)c->cq_d.p;
+  b.cq_t = (float4 *)c->cq_t.p;
+  b.cq_count = (uint32_t *)c->cq_count.p;
   return b;
 }
 
@@ -428,6 +433,30 @@ int ensure_mlt(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     c->mlt_depth = max_depth;
   }
   return MTX_OK;
+}
+
+// NRC radiance-cache buffers for `cap` paths (queries <= paths).
+int ensure_cache(mtx_ctx *c, uint32_t cap) {
+  int rc;
+  if (!c->has_field) {
+    mtx_set_error("mtx_render: NRC cache requested but no radiance field uploaded (mtx_field_upload)");
+    return MTX_E_ARG;
+  }
+  if ((rc = dalloc(c->cq_p, 16ull * cap))) return rc;
+  if ((rc = dalloc(c->cq_d, 16ull * cap))) return rc;
+  if ((rc = dalloc(c->cq_t, 16ull * cap))) return rc;
+  if ((rc = dalloc(c->cq_count, 16))) return rc;
+  if ((rc = dalloc(c->f_feat, 128ull * cap))) return rc;
+  if ((rc = dalloc(c->f_out, 12ull * cap))) return rc;
+  return MTX_OK;
+}
+
+// Encode + MLP + L += T * out for the chunk's compacted cache queries.
+void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap) {
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream);
+  mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
+                  (float *)c->f_out.p, c->n_cu, c->stream);
+  mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream);
 }
 
 int check_args(mtx_ctx *c, const mtx_render_args *a) {
@@ -492,7 +521,8 @@ struct Timer {
 void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
                  uint64_t *n_trace, uint64_t *n_shadow) {
   const mtxd::DevScene &s = c->scene;
-  const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1);
+  // an NRC cache query needs one more trace + shade after the last segment
+  const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1) + (p.nrc_cache ? 1u : 0u);
   for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
     hipEvent_t e = tm.begin(0);
     mtxd::launch_trace_closest(s, b, bounce, p.stats, c->trace_grid, c->stream);
@@ -742,6 +772,8 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   px_per_chunk = std::min(px_per_chunk, band_px);
   const uint32_t cap = px_per_chunk * a->spp;
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+  const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
+  if (nrc_cache && (rc = ensure_cache(c, cap))) return rc;
   if ((rc = dalloc(c->contrib, 9ull * 16 * band_px))) return rc;
   const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
   float4 *film_dev = (float4 *)film_rgbw;
@@ -791,6 +823,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;
     p.sample_major = c->sample_major;
+    p.nrc_cache = nrc_cache ? 1u : 0u;
     const size_t cbytes = 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2);
     if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
       // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains
@@ -807,8 +840,10 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       continue;
     }
     HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, c->stream));
+    if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
     run_bounces(c, b, p, tm, &n_trace, &n_shadow);
+    if (nrc_cache) run_cache(c, b, p.n_paths);
     mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, c->stream);
   }
   mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, c->stream);
@@ -917,6 +952,8 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
   const uint32_t chunk = a->chunk_paths ? a->chunk_paths : default_chunk(c, a);
   const uint32_t cap = (uint32_t)std::min<uint64_t>(n, chunk);
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+  const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
+  if (nrc_cache && (rc = ensure_cache(c, cap))) return rc;
   if ((rc = dalloc(c->s0, 24ull * cap))) return rc;
   if ((rc = dalloc(c->s1, 4ull * cap))) return rc;
   if ((rc = dalloc(c->s2, 12ull * cap))) return rc;
@@ -939,9 +976,12 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     p.height = c->scene.camera.height;
     p.n_paths = m;
     p.nrc_c = a->nrc_c;
+    p.nrc_cache = nrc_cache ? 1u : 0u;
     HIP_TRY(hipMemsetAsync(b.counters, 0, 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2), c->stream));
+    if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
     run_bounces(c, b, p, tm, &nt, &ns);
+    if (nrc_cache) run_cache(c, b, m);
     mtxd::launch_collect(b, p, (float *)c->s2.p, (uint8_t *)c->s3.p, c->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));

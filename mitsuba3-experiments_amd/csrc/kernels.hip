@@ -22,6 +22,8 @@
 // CPU restatement in oracle/ bit for bit.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "device_common.h"
 
 using namespace mtx;
@@ -188,6 +190,8 @@ __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const fl
 struct ShadeIO {
   ShadowRec rec;
   bool emit;
+  bool query;  // NRC radiance-cache query at this hit (field.hip)
+  float4 qp, qd, qt;
 };
 
 // Builds the shadow record for an NEE contribution. fma_form: value = (T, X)
@@ -238,6 +242,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   const V3 ray_d = V3{rd.x, rd.y, rd.z};
   const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
   io.emit = false;
+  io.query = false;
 
   // ------------------------------ head ------------------------------------
   bool active_next = true;
@@ -264,6 +269,18 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
       spread = 0.f;
     }
   } else {
+    if (INT == MTX_INT_NRC && (flags & PF_CACHE_QUERY)) {
+      // the segment ended by the spread criterion (nrc.py:70-71): the radiance
+      // cache replaces the rest of the path, queried at the next hit with the
+      // direction back to the previous vertex (nerad.py:86-106 Field(si))
+      if (si.valid) {
+        io.query = true;
+        io.qp = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
+        io.qd = make_float4(-ray_d.x, -ray_d.y, -ray_d.z, 0.f);
+        io.qt = make_float4(T.x, T.y, T.z, __uint_as_float(path));
+      }
+      return false;
+    }
     // path.py:283-300 / nrc.py:79-100: emission of the BSDF-sampled hit
     const bool bsdf_delta = (flags & PF_PREV_DELTA) != 0;
     const V3 rel = si.p - prev_p;
@@ -376,6 +393,10 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     eta *= bs.eta;
     const float a = sqr(spread);  // nrc.py:70-71
     active = a < p.nrc_c * a0;
+    if (!active && p.nrc_cache) {  // trace one more segment to the cache query
+      flags |= PF_CACHE_QUERY;
+      active = true;
+    }
     prev_p = si.p;
     prev_pdf = bs.pdf;
     flags = (bs.type & BF_DELTA) ? (flags | PF_PREV_DELTA) : (flags & ~PF_PREV_DELTA);
@@ -474,6 +495,7 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     const uint32_t i = base + threadIdx.x;
     ShadeIO io;
     io.emit = false;
+    io.query = false;
     bool cont = false;
     uint32_t path = 0;
     if (i < count) {
@@ -487,6 +509,31 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, sh_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path;
     if (io.emit) b.shadow[sslot] = io.rec;
+    if constexpr (INT == MTX_INT_NRC) {
+      if (p.nrc_cache) {
+        const uint32_t q = wave_append(b.cq_count, io.query);
+        if (io.query) {
+          b.cq_p[q] = io.qp;
+          b.cq_d[q] = io.qd;
+          b.cq_t[q] = io.qt;
+        }
+      }
+    }
+  }
+}
+
+// L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
+// plain sum: L = L + T * out, as the oracle-side composition in the tests).
+__global__ void k_cache_apply(WaveBuffers b, const float *out) {
+  const uint32_t n = *b.cq_count;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const float4 t = b.cq_t[q];
+    const uint32_t path = __float_as_uint(t.w);
+    float4 L = b.L[path];
+    L.x = L.x + t.x * out[3 * (size_t)q];
+    L.y = L.y + t.y * out[3 * (size_t)q + 1];
+    L.z = L.z + t.z * out[3 * (size_t)q + 2];
+    b.L[path] = L;
   }
 }
 
@@ -834,6 +881,10 @@ int shade_blocks_per_cu() {
       nb <= 0)
     nb = 2;
   return nb;
+}
+void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st) {
+  const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_cache_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out);
 }
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
   hipLaunchKernelGGL(k_mlt_init, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);

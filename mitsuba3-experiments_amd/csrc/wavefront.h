@@ -27,6 +27,7 @@ enum : uint32_t {
   PF_VALID_RAY = 1u,   // path-mis.py:129-133 valid_ray
   PF_PREV_DELTA = 2u,  // path-mis.py:137 prev_bsdf_delta
   PF_PRIMARY_VALID = 4u,
+  PF_CACHE_QUERY = 8u,  // NRC: the next hit is the radiance-cache query
 };
 
 constexpr int kTraceBlock = 128;     // threads per traversal block
@@ -88,6 +89,9 @@ struct WaveBuffers {
   // by the bounce-0 shade (path order).
   float4 *rs_xs;
   float4 *rs_ns;
+  // NRC radiance-cache queries (compacted): p, -d, (T, path), count
+  float4 *cq_p, *cq_d, *cq_t;
+  uint32_t *cq_count;
 };
 
 // ReSTIR GI frame state (restirgi.py:217-226, 230-231). Sample / reservoir
@@ -127,6 +131,7 @@ struct ChunkParams {
   uint32_t large_step;  // PSSMLT: i % 50 == 0 (pssmlt.py:209)
   uint32_t restir;      // ReSTIR GI secondary paths (path-mis loop, restirgi.py:459-588)
   uint32_t sample_major;  // chunk path order: 1 = s * n_px + q, 0 = q * spp + s
+  uint32_t nrc_cache;     // NRC: query the radiance field where the spread criterion stops
 };
 
 // -------- launch wrappers (kernels.hip) --------
@@ -149,6 +154,7 @@ void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams
 void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st);
+void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st);
 // ReSTIR GI (restir.hip)
 void launch_restir_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
                          hipStream_t st);

@@ -28,6 +28,9 @@ MTX_RESTIR_JACOBIAN = 2
 MTX_RESTIR_BSDF_SAMPLING = 4
 MTX_RESTIR_SPATIAL_SPATIAL = 8
 MTX_RESTIR_STAGE_A = 16
+MTX_RENDER_STATS = 1
+MTX_RENDER_TIMING = 2
+MTX_RENDER_NRC_CACHE = 4
 MTX_RESTIR_STAGE_B = 32
 
 MTX_ROUGH_TRANSMITTANCE_RES = 64

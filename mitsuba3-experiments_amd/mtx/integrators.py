@@ -179,6 +179,26 @@ class NRCIntegrator(SamplingIntegrator):
         self.max_depth = self.props.get("max_depth", 10)  # nrc.py:23
         self.c = self.props.get("c", 0.01)  # nrc.py:123
         self.rr_depth = 0
+        # Radiance cache (nerad.py Field): a segment stopped
+        # by the spread criterion adds T * field(x, -d) at its next hit.
+        self.field = self.props.get("field", None)
+
+    def render_args(self, *args, **kwargs) -> _abi.RenderArgs:
+        a = super().render_args(*args, **kwargs)
+        if self.field is not None:
+            a.flags |= _abi.MTX_RENDER_NRC_CACHE
+        return a
+
+    def render_film(self, scene, *args, ctx=None, device: int | None = None, **kwargs):
+        ctx = ctx or context(device)
+        if self.field is not None:
+            self.field._ensure(ctx)
+        return super().render_film(scene, *args, ctx=ctx, **kwargs)
+
+    def sample(self, scene, sampler: IndependentSampler, ray, medium=None, active=True):
+        if self.field is not None:
+            self.field._ensure(context())
+        return super().sample(scene, sampler, ray, medium, active)
 
 
 class PssmltSimple(SamplingIntegrator):

@@ -38,6 +38,7 @@ def lib():
             "orc_trace": [SD, u64, vp, C.c_int, C.c_int, vp, vp],
             "orc_sample_rays": [SD, RA, u64, vp, vp, u32, vp, vp],
             "orc_render_samples": [SD, RA, vp, vp],
+            "orc_render_samples_q": [SD, RA, vp, vp, vp],
             "orc_film": [u32, u32, u32, u32, vp, vp, vp],
             "orc_render": [SD, RA, vp],
             "orc_rng_stream": [u32, u32, u32, u32, vp],
@@ -73,6 +74,19 @@ def render_samples(scene, args):
     d = scene.desc()
     lib().orc_render_samples(C.byref(d), C.byref(args), L.ctypes.data, pos.ctypes.data)
     return L, pos
+
+
+def render_samples_nrc_cache(scene, args):
+    """NRC with the radiance-cache option (args.flags bit 2): per-sample
+    (L [n,3], pos [n,2], query [n,10]); query rows are {valid, p.xyz, wi.xyz,
+    T.xyz} of the cache lookup the stopped segment makes (zeros: none)."""
+    n = (args.y1 - args.y0) * scene.width * args.spp
+    L = np.zeros((n, 3), np.float32)
+    pos = np.zeros((n, 2), np.float32)
+    q = np.zeros((n, 10), np.float32)
+    d = scene.desc()
+    lib().orc_render_samples_q(C.byref(d), C.byref(args), L.ctypes.data, pos.ctypes.data, q.ctypes.data)
+    return L, pos, q
 
 
 def film(width, y0, y1, spp, L, pos):

@@ -315,7 +315,14 @@ V3 orc_path(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_
 }
 
 // ----------------------------- nrc.py:25-125 -------------------------------
-V3 orc_nrc(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, float c, bool *valid_out) {
+// With `query` (the radiance-cache option, MTX_RENDER_NRC_CACHE, SURVEY §8f
+// item 3) the segment stopped by the spread criterion traces its BSDF ray one
+// more time; a valid hit becomes the cache query (p, -d, f) written as
+// query[0..9] = {1, p.xyz, wi.xyz, f.xyz}. L itself is unchanged.
+V3 orc_nrc(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, float c, bool *valid_out,
+           float *query = nullptr) {
+  if (query)
+    for (int k = 0; k < 10; ++k) query[k] = 0.f;
   SurfaceInteraction si = intersect(s, ray);  // :117
   const bool primary_valid = si.valid;
   bool active = si.valid;  // :119
@@ -344,8 +351,16 @@ V3 orc_nrc(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, float c,
     f = f * bsdf_weight;
     eta *= bs.eta;
     float a = sqr(spread);  // :70-71
+    const bool stopped = active && !(a < c * a0);
     active = active && (a < c * a0);
     Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
+    if (stopped && query) {
+      SurfaceInteraction sq = intersect(s, nray);
+      if (sq.valid) {
+        const float qv[10] = {1.f, sq.p.x, sq.p.y, sq.p.z, -nray.d.x, -nray.d.y, -nray.d.z, f.x, f.y, f.z};
+        for (int k = 0; k < 10; ++k) query[k] = qv[k];
+      }
+    }
     SurfaceInteraction si2 = active ? intersect(s, nray) : compute_si(s, kInf, 0xffffffffu, 0.f, 0.f, nray.d);
     bool bsdf_delta = (bs.type & BF_DELTA) != 0;
     V3 rel = si2.p - si.p;
@@ -416,10 +431,11 @@ V3 orc_pssmlt_sample(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth
   return L;
 }
 
-V3 run_integrator(const SceneView &s, const mtx_render_args &a, Pcg32 &rng, const Ray &ray, bool *valid) {
+V3 run_integrator(const SceneView &s, const mtx_render_args &a, Pcg32 &rng, const Ray &ray, bool *valid,
+                  float *query = nullptr) {
   switch (a.integrator) {
     case MTX_INT_PATH: return orc_path(s, rng, ray, a.max_depth, a.rr_depth, valid);
-    case MTX_INT_NRC: return orc_nrc(s, rng, ray, a.max_depth, a.nrc_c, valid);
+    case MTX_INT_NRC: return orc_nrc(s, rng, ray, a.max_depth, a.nrc_c, valid, (a.flags & 4u) ? query : nullptr);
     default: return orc_path_mis(s, rng, ray, a.max_depth, a.rr_depth, valid);
   }
 }
@@ -480,7 +496,9 @@ int orc_sample_rays(const mtx_scene_desc *d, const mtx_render_args *a, uint64_t 
 // Per-sample radiance for film rows [y0,y1): lane = (y*W + x)*spp_total +
 // sample_offset + s; writes L (3 per sample) and the film position (2 per
 // sample) in (pixel, s) order. Used by the per-lane parity tests.
-int orc_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float *L, float *pos) {
+// `query` (NULL, or 10 floats per sample): NRC radiance-cache queries, see
+// orc_nrc; all zero for samples without one.
+int orc_render_samples_q(const mtx_scene_desc *d, const mtx_render_args *a, float *L, float *pos, float *query) {
   SceneView s = make_view(d);
   const uint32_t W = s.camera.width, H = s.camera.height;
   const uint64_t npx = (uint64_t)(a->y1 - a->y0) * W;
@@ -496,8 +514,11 @@ int orc_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float 
       V2 adj = V2{sx / (float)W, sy / (float)H};
       Ray ray = camera_ray(s.camera, adj);  // path.py:60-62
       bool v = false;
-      V3 res = run_integrator(s, *a, rng, ray, &v);
       uint64_t o = (uint64_t)p * spp + k;
+      float qbuf[10];
+      V3 res = run_integrator(s, *a, rng, ray, &v, qbuf);
+      if (query)
+        for (int j = 0; j < 10; ++j) query[10 * o + j] = (a->integrator == MTX_INT_NRC && (a->flags & 4u)) ? qbuf[j] : 0.f;
       L[3 * o] = res.x;
       L[3 * o + 1] = res.y;
       L[3 * o + 2] = res.z;
@@ -506,6 +527,10 @@ int orc_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float 
     }
   }
   return 0;
+}
+
+int orc_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float *L, float *pos) {
+  return orc_render_samples_q(d, a, L, pos, nullptr);
 }
 
 // Film accumulation in the fixed order documented in DESIGN.md ("Film"):

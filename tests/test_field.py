@@ -92,3 +92,49 @@ def test_field_eval_vs_reference(oracle, n):
     ref = f.mlp_reference(oracle.field_features(f, p, d))
     np.testing.assert_allclose(got, ref, rtol=2e-2, atol=2e-3)
     assert np.isfinite(got).all() and np.abs(got).max() > 0
+
+
+def test_nrc_cache_queries_leave_L_unchanged(small_scene, oracle):
+    """The cache option only adds queries: the oracle's per-sample L and film
+    positions are identical with and without it, and stopped segments that
+    hit a surface produce queries with unit-length wi (CPU)."""
+    from mtx import load_dict
+
+    integ = load_dict({"type": "nrc"})
+    a = integ.render_args(small_scene, 3, 2)
+    L0, pos0 = oracle.render_samples(small_scene, a)
+    a.flags |= 4
+    L1, pos1, q = oracle.render_samples_nrc_cache(small_scene, a)
+    assert np.array_equal(L0, L1) and np.array_equal(pos0, pos1)
+    m = q[:, 0] == 1
+    assert 0.05 < m.mean() < 1.0
+    assert (q[~m] == 0).all()
+    np.testing.assert_allclose(np.linalg.norm(q[m, 4:7], axis=1), 1.0, atol=1e-5)
+    assert (q[m, 7:10] >= 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [0, 1000])
+def test_nrc_cache_film_bit_exact(small_scene, oracle, chunk):
+    """NRC with the radiance cache: the GPU film equals the
+    oracle's per-sample L + T * Field(query) composed on the host (field
+    evaluated by the same fused MFMA kernel through mtx_field_eval), splatted
+    by the oracle film. Bit-exact: every step is the same IEEE sequence."""
+    from mtx import load_dict
+    from mtx.field import Field
+
+    field = Field(small_scene, seed=5, table_scale=1.0)
+    integ = load_dict({"type": "nrc", "field": field})
+    spp = 4
+    film = integ.render_film(small_scene, seed=3, spp=spp, chunk_paths=chunk)
+    a = integ.render_args(small_scene, 3, spp)
+    assert a.flags & 4
+    L, pos, q = oracle.render_samples_nrc_cache(small_scene, a)
+    m = q[:, 0] == 1
+    assert m.any()
+    out = field(q[m, 1:4], q[m, 4:7])
+    L[m] = L[m] + q[m, 7:10] * out
+    ref = oracle.film(small_scene.width, 0, small_scene.height, spp, L, pos)
+    np.testing.assert_array_equal(film, ref)
+    plain = load_dict({"type": "nrc"}).render_film(small_scene, seed=3, spp=spp)
+    assert not np.array_equal(plain, film)
