@@ -205,6 +205,11 @@ typedef struct mtx_stats {
   /* closest-hit traversal wave iterations (node phase, leaf phase): SIMD
    * utilisation = visits / (64 * iterations) */
   uint64_t wave_node_iters, wave_leaf_iters;
+  /* NRC radiance cache (MTX_RENDER_NRC_CACHE): queries answered, HIP-event
+   * time of the feature encoder and of the fused MLP (part of other_ms's
+   * complement: other_ms excludes them) */
+  uint64_t cache_queries;
+  double cache_encode_ms, cache_mlp_ms;
 } mtx_stats;
 
 /* --------------------------- context ------------------------------ */

@@ -64,37 +64,74 @@ MTX_HD uint16_t float_to_half_bits(float f) {
 
 MTX_HD float round_half(float f) { return half_bits_to_float(float_to_half_bits(f)); }
 
-// Hash-grid encoding of one point (p_norm in [0,1]^3): fp16 bits of the
-// n_levels * n_features interpolated features (f32 interpolation, one
+// Hash-grid encoding of level l of one point (p_norm in [0,1]^3): fp16 bits
+// of the level's n_features interpolated features (f32 interpolation, one
 // rounding to fp16 per feature).
-MTX_HD void field_hashgrid(const FieldEncoding &e, V3 pn, uint16_t *out) {
+// Entries (both features, packed) of corners x and x+1 of one (y, z) row.
+MTX_HD void field_fetch_pair(const uint32_t *tab, uint32_t i0, uint32_t i1, uint32_t *a, uint32_t *b) {
+#ifdef MTX_DEVICE_COMPILE
+  // one 8-B gather when the two entries are adjacent (dense levels, and
+  // hashed levels whose x-pair differs in bit 0 only): half the requests
+  if (i1 == i0 + 1u || i0 == i1 + 1u) {
+    const uint32_t lo = i1 == i0 + 1u ? i0 : i1;
+    uint2 v;
+    __builtin_memcpy(&v, __builtin_assume_aligned(tab + lo, 4), 8);
+    *a = i1 == i0 + 1u ? v.x : v.y;
+    *b = i1 == i0 + 1u ? v.y : v.x;
+    return;
+  }
+#endif
+  *a = tab[i0];
+  *b = tab[i1];
+}
+
+// Hash-grid encoding of level l of one point (p_norm in [0,1]^3): fp16 bits
+// of the level's n_features interpolated features (f32 interpolation, one
+// rounding to fp16 per feature).
+MTX_HD void field_hashgrid_level(const FieldEncoding &e, V3 pn, uint32_t l, uint16_t *out) {
   const uint32_t T = 1u << e.log2_table;
-  for (uint32_t l = 0; l < e.n_levels; ++l) {
-    const float scale = e.level_scale[l];
-    const uint32_t res = e.level_res[l];
-    const bool dense = (uint64_t)res * res * res <= (uint64_t)T;
-    const float px = fmaf(pn.x, scale, 0.5f), py = fmaf(pn.y, scale, 0.5f), pz = fmaf(pn.z, scale, 0.5f);
-    const float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
-    const float tx = px - fx, ty = py - fy, tz = pz - fz;
-    const uint32_t gx = (uint32_t)(int32_t)fx, gy = (uint32_t)(int32_t)fy, gz = (uint32_t)(int32_t)fz;
-    float acc0 = 0.f, acc1 = 0.f;
+  const float scale = e.level_scale[l];
+  const uint32_t res = e.level_res[l];
+  const bool dense = (uint64_t)res * res * res <= (uint64_t)T;
+  const float px = fmaf(pn.x, scale, 0.5f), py = fmaf(pn.y, scale, 0.5f), pz = fmaf(pn.z, scale, 0.5f);
+  const float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
+  const float tx = px - fx, ty = py - fy, tz = pz - fz;
+  const uint32_t gx = (uint32_t)(int32_t)fx, gy = (uint32_t)(int32_t)fy, gz = (uint32_t)(int32_t)fz;
+  auto index = [&](uint32_t x, uint32_t y, uint32_t z) -> uint32_t {
+    const uint32_t idx = dense ? x + y * res + z * res * res
+                               : (x * kFieldPrimes[0]) ^ (y * kFieldPrimes[1]) ^ (z * kFieldPrimes[2]);
+    return idx & (T - 1u);  // T is a power of two
+  };
+  float acc0 = 0.f, acc1 = 0.f;
+  if (e.n_features == 2) {
+    const uint32_t *tab = reinterpret_cast<const uint32_t *>(e.table) + (size_t)l * T;
+    uint32_t ent[8];
+    for (uint32_t yz = 0; yz < 4; ++yz) {
+      const uint32_t y = gy + (yz & 1u), z = gz + (yz >> 1);
+      field_fetch_pair(tab, index(gx, y, z), index(gx + 1u, y, z), &ent[2 * yz], &ent[2 * yz + 1]);
+    }
     for (uint32_t c = 0; c < 8; ++c) {
       const uint32_t bx = c & 1u, by = (c >> 1) & 1u, bz = (c >> 2) & 1u;
-      const uint32_t x = gx + bx, y = gy + by, z = gz + bz;
-      uint32_t idx;
-      if (dense)
-        idx = x + y * res + z * res * res;
-      else
-        idx = (x * kFieldPrimes[0]) ^ (y * kFieldPrimes[1]) ^ (z * kFieldPrimes[2]);
-      idx &= T - 1u;  // T is a power of two
       const float w = (bx ? tx : 1.f - tx) * (by ? ty : 1.f - ty) * (bz ? tz : 1.f - tz);
-      const uint16_t *f = e.table + ((size_t)l * T + idx) * e.n_features;
-      acc0 = fmaf(w, half_bits_to_float(f[0]), acc0);
-      if (e.n_features > 1) acc1 = fmaf(w, half_bits_to_float(f[1]), acc1);
+      acc0 = fmaf(w, half_bits_to_float((uint16_t)(ent[c] & 0xffffu)), acc0);
+      acc1 = fmaf(w, half_bits_to_float((uint16_t)(ent[c] >> 16)), acc1);
     }
-    out[e.n_features * l] = float_to_half_bits(acc0);
-    if (e.n_features > 1) out[e.n_features * l + 1] = float_to_half_bits(acc1);
+    out[0] = float_to_half_bits(acc0);
+    out[1] = float_to_half_bits(acc1);
+    return;
   }
+  for (uint32_t c = 0; c < 8; ++c) {
+    const uint32_t bx = c & 1u, by = (c >> 1) & 1u, bz = (c >> 2) & 1u;
+    const float w = (bx ? tx : 1.f - tx) * (by ? ty : 1.f - ty) * (bz ? tz : 1.f - tz);
+    const uint16_t *f = e.table + ((size_t)l * T + index(gx + bx, gy + by, gz + bz)) * e.n_features;
+    acc0 = fmaf(w, half_bits_to_float(f[0]), acc0);
+  }
+  out[0] = float_to_half_bits(acc0);
+}
+
+// All levels of one point: out[n_features * l + k].
+MTX_HD void field_hashgrid(const FieldEncoding &e, V3 pn, uint16_t *out) {
+  for (uint32_t l = 0; l < e.n_levels; ++l) field_hashgrid_level(e, pn, l, out + e.n_features * l);
 }
 
 // Real spherical harmonics, degrees 0..3 (16 coefficients, index l*(l+1)+m).
@@ -128,20 +165,22 @@ MTX_HD void field_sh3(V3 d, float *r) {
   r[9] = tc * s0;
 }
 
-// Feature vector (fp16 bits) of one query: p_norm(3), p_enc(L*F), wi(3),
-// sh(16), zero padding up to n_pad. Returns the number of real features.
-MTX_HD uint32_t field_features(const FieldEncoding &e, V3 p, V3 wi, uint16_t *out, uint32_t n_pad) {
-  const V3 pn = V3{(p.x - e.bbox_min[0]) / (e.bbox_max[0] - e.bbox_min[0]),
-                   (p.y - e.bbox_min[1]) / (e.bbox_max[1] - e.bbox_min[1]),
-                   (p.z - e.bbox_min[2]) / (e.bbox_max[2] - e.bbox_min[2])};
+MTX_HD V3 field_pnorm(const FieldEncoding &e, V3 p) {
+  return V3{(p.x - e.bbox_min[0]) / (e.bbox_max[0] - e.bbox_min[0]),
+            (p.y - e.bbox_min[1]) / (e.bbox_max[1] - e.bbox_min[1]),
+            (p.z - e.bbox_min[2]) / (e.bbox_max[2] - e.bbox_min[2])};
+}
+
+// Everything of the feature row except the hash-grid block: p_norm(3) at
+// 0..2, wi(3) and sh(16) after the L*F grid features, zeros up to n_pad.
+// Returns the number of real features.
+MTX_HD uint32_t field_features_direct(const FieldEncoding &e, V3 pn, V3 wi, uint16_t *out, uint32_t n_pad) {
   float sh[16];
   field_sh3(wi, sh);
-  uint32_t k = 0;
-  out[k++] = float_to_half_bits(pn.x);
-  out[k++] = float_to_half_bits(pn.y);
-  out[k++] = float_to_half_bits(pn.z);
-  field_hashgrid(e, pn, out + k);
-  k += e.n_levels * e.n_features;
+  out[0] = float_to_half_bits(pn.x);
+  out[1] = float_to_half_bits(pn.y);
+  out[2] = float_to_half_bits(pn.z);
+  uint32_t k = 3 + e.n_levels * e.n_features;
   out[k++] = float_to_half_bits(wi.x);
   out[k++] = float_to_half_bits(wi.y);
   out[k++] = float_to_half_bits(wi.z);
@@ -149,6 +188,14 @@ MTX_HD uint32_t field_features(const FieldEncoding &e, V3 p, V3 wi, uint16_t *ou
   const uint32_t n = k;
   while (k < n_pad) out[k++] = 0;
   return n;
+}
+
+// Feature vector (fp16 bits) of one query: p_norm(3), p_enc(L*F), wi(3),
+// sh(16), zero padding up to n_pad. Returns the number of real features.
+MTX_HD uint32_t field_features(const FieldEncoding &e, V3 p, V3 wi, uint16_t *out, uint32_t n_pad) {
+  const V3 pn = field_pnorm(e, p);
+  field_hashgrid(e, pn, out + 3);
+  return field_features_direct(e, pn, wi, out, n_pad);
 }
 
 }  // namespace mtx

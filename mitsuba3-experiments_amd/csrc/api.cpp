@@ -451,13 +451,6 @@ int ensure_cache(mtx_ctx *c, uint32_t cap) {
   return MTX_OK;
 }
 
-// Encode + MLP + L += T * out for the chunk's compacted cache queries.
-void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap) {
-  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream);
-  mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
-                  (float *)c->f_out.p, c->n_cu, c->stream);
-  mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream);
-}
 
 int check_args(mtx_ctx *c, const mtx_render_args *a) {
   if (!c || !a) {
@@ -484,7 +477,8 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
 struct Timer {
   mtx_ctx *c;
   bool on;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs[4];
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs[6];  // trace, shadow, shade, all, encode, mlp
+  uint64_t cache_queries = 0;
   size_t next = 0;
   hipEvent_t get() {
     if (next >= c->events.size()) {
@@ -516,6 +510,24 @@ struct Timer {
     return ms;
   }
 };
+
+// Encode + MLP + L += T * out for the chunk's compacted cache queries.
+void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm) {
+  hipEvent_t e = tm.begin(4);
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream);
+  tm.end(4, e);
+  e = tm.begin(5);
+  mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
+                  (float *)c->f_out.p, c->n_cu, c->stream);
+  tm.end(5, e);
+  mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream);
+  if (tm.on) {
+    uint32_t nq = 0;
+    if (hipMemcpyAsync(&nq, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+        hipStreamSynchronize(c->stream) == hipSuccess)
+      tm.cache_queries += nq;
+  }
+}
 
 // Runs one chunk's bounce loop (rays already generated, counters[0] set).
 void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
@@ -571,7 +583,11 @@ int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_
     stats->trace_ms = tm.total(0);
     stats->shadow_ms = tm.total(1);
     stats->shade_ms = tm.total(2);
-    stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms;
+    stats->cache_encode_ms = tm.total(4);
+    stats->cache_mlp_ms = tm.total(5);
+    stats->cache_queries = tm.cache_queries;
+    stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms - stats->cache_encode_ms -
+                      stats->cache_mlp_ms;
   }
   return MTX_OK;
 }
@@ -843,7 +859,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
     run_bounces(c, b, p, tm, &n_trace, &n_shadow);
-    if (nrc_cache) run_cache(c, b, p.n_paths);
+    if (nrc_cache) run_cache(c, b, p.n_paths, tm);
     mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, c->stream);
   }
   mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, c->stream);
@@ -981,7 +997,7 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
     run_bounces(c, b, p, tm, &nt, &ns);
-    if (nrc_cache) run_cache(c, b, m);
+    if (nrc_cache) run_cache(c, b, m, tm);
     mtxd::launch_collect(b, p, (float *)c->s2.p, (uint8_t *)c->s3.p, c->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));

@@ -32,12 +32,37 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kFieldPad = 64;     // features per query (padded)
 constexpr float kLeakySlope = 0.01f;  // drjit.nn.LeakyReLU default
 
-__global__ void k_field_encode(FieldEncoding e, const float4 *qp, const float4 *qd, const uint32_t *count,
-                               uint32_t n_max, uint16_t *feat) {
+// One thread per (query, level): the 8 corner gathers of a level are
+// independent of the other levels, so a block covers 256 / n_levels queries
+// with every thread issuing its own gathers. The rows are assembled in LDS
+// and written out as 16-B stores (one 128-B row = 8 lanes).
+constexpr uint32_t kEncodeBlock = 256;
+
+__global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, const float4 *qp, const float4 *qd,
+                                                               const uint32_t *count, uint32_t n_max,
+                                                               uint16_t *feat) {
+  extern __shared__ uint4 rows[];  // 256 / n_levels rows of 128 B
   const uint32_t n = count ? min(*count, n_max) : n_max;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float4 p = qp[i], d = qd[i];
-    field_features(e, V3{p.x, p.y, p.z}, V3{d.x, d.y, d.z}, feat + (size_t)kFieldPad * i, kFieldPad);
+  const uint32_t L = e.n_levels, qpb = kEncodeBlock / L;
+  uint16_t *row_h = reinterpret_cast<uint16_t *>(rows);
+  const uint32_t ql = threadIdx.x / L, l = threadIdx.x - ql * L;
+  for (uint32_t q0 = blockIdx.x * qpb; q0 < n; q0 += gridDim.x * qpb) {
+    const uint32_t q = q0 + ql;
+    if (ql < qpb && q < n) {
+      const float4 p = qp[q];
+      const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
+      uint16_t *row = row_h + (size_t)kFieldPad * ql;
+      field_hashgrid_level(e, pn, l, row + 3 + e.n_features * l);
+      if (l == 0) {
+        const float4 d = qd[q];
+        field_features_direct(e, pn, V3{d.x, d.y, d.z}, row, kFieldPad);
+      }
+    }
+    __syncthreads();
+    const uint32_t nq = min(qpb, n - q0);
+    for (uint32_t c = threadIdx.x; c < nq * (kFieldPad / 8); c += kEncodeBlock)
+      reinterpret_cast<uint4 *>(feat + (size_t)kFieldPad * q0)[c] = rows[c];
+    __syncthreads();
   }
 }
 
@@ -179,8 +204,13 @@ void field_prepack(const uint16_t *weights, uint32_t n_in, uint32_t n_hidden, ui
 int field_encode(const FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count, uint32_t n_max,
                  uint16_t *feat, hipStream_t st) {
   if (n_max == 0) return MTX_OK;
-  const unsigned blocks = (unsigned)std::min<uint64_t>((n_max + 255) / 256, 65535);
-  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(256), 0, st, e, qp, qd, count, n_max, feat);
+  if (e.n_levels == 0 || e.n_levels > kEncodeBlock) {
+    mtx_set_error("field_encode: unsupported n_levels %u", e.n_levels);
+    return MTX_E_ARG;
+  }
+  const uint32_t qpb = kEncodeBlock / e.n_levels;
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n_max + qpb - 1) / qpb, 256ull * 64);
+  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(kEncodeBlock), (size_t)qpb * kFieldPad * 2, st, e, qp, qd, count, n_max, feat);
   return MTX_OK;
 }
 

@@ -181,6 +181,9 @@ class Stats(C.Structure):
         ("paths", C.c_uint64),
         ("wave_node_iters", C.c_uint64),
         ("wave_leaf_iters", C.c_uint64),
+        ("cache_queries", C.c_uint64),
+        ("cache_encode_ms", C.c_double),
+        ("cache_mlp_ms", C.c_double),
     ]
 
     def as_dict(self) -> dict:

@@ -188,6 +188,32 @@ def nrc(args):
     _line("NRC Mpaths/sec on bedroom@1280x720 spp=4 (C5)", n / dt / 1e6, "Mpaths/s", reps, 1, dt * 1e3,
           {"workload": "nrc.py NRCIntegrator.sample: NEE+MIS segments, spread heuristic c=0.01, max_depth 10",
            "paths_per_step": n}, _trace_roofline(cnt, agg["trace_ms"] / reps, "step"), cpu)
+    # the same with the radiance cache: stopped segments
+    # trace one more segment and query the fused fp16 MFMA field there
+    from mtx.field import Field
+
+    cached = NRCIntegrator({"field": Field(sc)})
+    cached.render_film(sc, seed=99, spp=spp, out=film)
+    _sync()
+    agg = None
+    t0 = time.perf_counter()
+    for k in range(reps):
+        st = cached.render_film(sc, seed=k, spp=spp, out=film, stats=True)[1]
+        agg = dict(st) if agg is None else {x: agg[x] + st[x] for x in st}
+    _sync()
+    dtc = (time.perf_counter() - t0) / reps
+    cnt = cached.render_film(sc, seed=0, spp=spp, out=film, stats=True, counters=True)[1]
+    _line("NRC + radiance cache Mpaths/sec on bedroom@1280x720 spp=4 (C5, nerad.py Field queries)", n / dtc / 1e6,
+          "Mpaths/s", reps, 1, dtc * 1e3,
+          {"workload": "nrc.py segments + one cache query per stopped segment: hash-grid/SH encode + fused "
+                       "54->64x5->3 fp16 MLP (v_mfma_f32_32x32x16_f16) + L += T * out",
+           "paths_per_step": n, "extra_ms_per_step": round((dtc - dt) * 1e3, 3),
+           "cache_queries_per_step": int(agg["cache_queries"] / reps),
+           "cache_encode_ms": round(agg["cache_encode_ms"] / reps, 3),
+           "cache_mlp_ms": round(agg["cache_mlp_ms"] / reps, 3),
+           "trace_ms": round(agg["trace_ms"] / reps, 3), "shadow_ms": round(agg["shadow_ms"] / reps, 3),
+           "shade_ms": round(agg["shade_ms"] / reps, 3)},
+          _trace_roofline(cnt, agg["trace_ms"] / reps, "step"), cpu)
 
 
 # ------------------------------------------------------------- primitives --
@@ -295,7 +321,22 @@ def field(args):
     d = rng.normal(size=(n, 3))
     d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
     feat = f.features(p, d, ctx)
-    enc_ms = lib().mtx_last_device_ms(ctx.handle)
+    enc_ms = min(lib().mtx_last_device_ms(ctx.handle), (f.features(p, d, ctx), lib().mtx_last_device_ms(ctx.handle))[1])
+    # the same queries in Morton order: hash-grid gathers of neighbouring
+    # lanes then share cache lines (the locality the table's L2/MALL sees)
+    g = np.clip(((p - p.min(0)) / (p.max(0) - p.min(0)) * 1023).astype(np.uint64), 0, 1023)
+
+    def spread3(x):
+        x = (x | (x << 16)) & 0x030000FF
+        x = (x | (x << 8)) & 0x0300F00F
+        x = (x | (x << 4)) & 0x030C30C3
+        return (x | (x << 2)) & 0x09249249
+
+    order = np.argsort(spread3(g[:, 0]) | (spread3(g[:, 1]) << 1) | (spread3(g[:, 2]) << 2), kind="stable")
+    ps, ds = np.ascontiguousarray(p[order]), np.ascontiguousarray(d[order])
+    f.features(ps, ds, ctx)
+    enc_sorted_ms = min(lib().mtx_last_device_ms(ctx.handle),
+                        (f.features(ps, ds, ctx), lib().mtx_last_device_ms(ctx.handle))[1])
     ms = []
     for _ in range(5):
         f.mlp(feat, ctx)
@@ -312,7 +353,8 @@ def field(args):
           "Mqueries/s", 5, 1, ms,
           {"workload": f"fused 6-layer MLP, {n} queries, v_mfma_f32_32x32x16_f16, f32 accumulate",
            "flops_per_query": f.flops_per_query(), "encode_ms": round(enc_ms, 3),
-           "encode_Mqueries_s": round(n / (enc_ms / 1e3) / 1e6, 1)},
+           "encode_Mqueries_s": round(n / (enc_ms / 1e3) / 1e6, 1), "encode_morton_ms": round(enc_sorted_ms, 3),
+           "encode_morton_Mqueries_s": round(n / (enc_sorted_ms / 1e3) / 1e6, 1)},
           {"bound": "mfma", "kernel": "k_field_mlp", "achieved": round(tfs, 2), "peak": MFMA_F16_PEAK_TFS,
            "unit": "TFLOP/s", "frac": round(tfs / MFMA_F16_PEAK_TFS, 4), "traffic": None,
            "alg_bytes_per_launch": int(n * (128 + 12))},
