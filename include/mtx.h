@@ -152,7 +152,8 @@ enum {
   MTX_INT_PATH_MIS = 2,      /* path-mis.py:24-155 ("path_test") */
   MTX_INT_NRC = 3,           /* nrc.py:25-125 */
   MTX_INT_PSSMLT_SIMPLE = 4, /* pssmlt.py:167-228 + pssmltsimple.py:16-142 */
-  MTX_INT_RESTIR_GI = 5      /* restirgi.py:182-588 */
+  MTX_INT_RESTIR_GI = 5,     /* restirgi.py:182-588 */
+  MTX_INT_PSSMLT_PATH = 6    /* pssmlt.py:167-228 + pssmltpath.py:17-190 ("pssmlt") */
 };
 
 typedef struct mtx_render_args {

@@ -103,7 +103,8 @@ struct mtx_ctx {
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
   uint32_t capacity = 0;
   DevBuf mlt_cur, mlt_L, mlt_prop, vpath, vprop;  // PSSMLT chain state
-  uint32_t mlt_capacity = 0, mlt_depth = 0;
+  DevBuf vpath_es, vprop_es;                       // pssmltpath emitter samples
+  uint32_t mlt_capacity = 0, mlt_depth = 0, mlt_es_capacity = 0, mlt_es_depth = 0;
   // ReSTIR GI frame state (restirgi.py:217-226): kept across mtx_render calls
   DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM, rs_xs, rs_ns;
   uint32_t rs_n = 0, rs_cur = 0, rs_pending_frame = 0;
@@ -177,7 +178,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
-                    &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop,
+                    &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop, &c->vpath_es, &c->vprop_es,
                     &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
@@ -364,7 +365,9 @@ uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
   // PSSMLT chains also keep the current and proposed path vertices
   const size_t per_path =
-      kPathStateBytes + (a->integrator == MTX_INT_PSSMLT_SIMPLE ? 32ull * std::max<uint32_t>(a->max_depth, 1) + 48 : 0);
+      kPathStateBytes + (a->integrator == MTX_INT_PSSMLT_SIMPLE ? 32ull * std::max<uint32_t>(a->max_depth, 1) + 48
+                         : a->integrator == MTX_INT_PSSMLT_PATH ? 48ull * std::max<uint32_t>(a->max_depth, 1) + 48
+                                                                : 0);
   // buffers this context already holds count as available
   const size_t fit = std::max<size_t>((size_t)((double)free_b * 0.4) / per_path, c->capacity);
   return (uint32_t)std::max<size_t>(1u << 20, std::min<size_t>(kDefaultChunk, fit));
@@ -412,6 +415,8 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.mlt_prop = (float2 *)c->mlt_prop.p;
   b.vpath = (float4 *)c->vpath.p;
   b.vprop = (float4 *)c->vprop.p;
+  b.vpath_es = (float2 *)c->vpath_es.p;
+  b.vprop_es = (float2 *)c->vprop_es.p;
   b.cq_p = (float4 *)c->cq_p.p;
   b.cq_d = (float4 *)c->cq_d.p;
   b.cq_t = (float4 *)c->cq_t.p;
@@ -419,8 +424,15 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   return b;
 }
 
-int ensure_mlt(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
+int ensure_mlt(mtx_ctx *c, uint32_t cap, uint32_t max_depth, bool emitter_samples) {
   int rc;
+  if (emitter_samples && (!c->vpath_es.p || c->mlt_es_capacity != c->capacity || max_depth > c->mlt_es_depth)) {
+    const size_t wc = c->capacity;
+    if ((rc = dalloc(c->vpath_es, 8 * wc * max_depth))) return rc;
+    if ((rc = dalloc(c->vprop_es, 8 * wc * max_depth))) return rc;
+    c->mlt_es_capacity = c->capacity;
+    c->mlt_es_depth = max_depth;
+  }
   if (cap > c->mlt_capacity || max_depth > c->mlt_depth || c->mlt_capacity != c->capacity) {
     // vertex buffers are indexed [depth * wavefront capacity + chain]
     const size_t wc = c->capacity;
@@ -462,7 +474,8 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
     return MTX_E_NOSCENE;
   }
   if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC &&
-      a->integrator != MTX_INT_PSSMLT_SIMPLE && a->integrator != MTX_INT_RESTIR_GI) {
+      a->integrator != MTX_INT_PSSMLT_SIMPLE && a->integrator != MTX_INT_RESTIR_GI &&
+      a->integrator != MTX_INT_PSSMLT_PATH) {
     mtx_set_error("integrator %u is not supported by this entry point", a->integrator);
     return MTX_E_UNSUPPORTED;
   }
@@ -809,12 +822,14 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     HIP_TRY(hipStreamSynchronize(c->stream));
     return fill_stats(c, stats, want_stats, tm, n_trace, n_shadow, (uint64_t)W * H * a->spp);
   }
-  if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
+  const bool mlt = a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH;
+  if (mlt) {
     if (a->sample_offset != 0 || a->spp_total != a->spp) {
       mtx_set_error("mtx_render: PSSMLT chains cannot be split by sample range (use row bands)");
       return MTX_E_ARG;
     }
-    if ((rc = ensure_mlt(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+    if ((rc = ensure_mlt(c, cap, std::max<uint32_t>(a->max_depth, 1), a->integrator == MTX_INT_PSSMLT_PATH)))
+      return rc;
     HIP_TRY(hipMemsetAsync(c->contrib.p, 0, 9ull * 16 * band_px, c->stream));
   }
   mtxd::WaveBuffers b = buffers(c);
@@ -841,7 +856,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.sample_major = c->sample_major;
     p.nrc_cache = nrc_cache ? 1u : 0u;
     const size_t cbytes = 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2);
-    if (a->integrator == MTX_INT_PSSMLT_SIMPLE) {
+    if (mlt) {
       // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains
       const uint32_t iters = a->iterations ? a->iterations : 200;
       mtxd::launch_mlt_init(b, p, c->stream);
@@ -955,7 +970,8 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
                     uint32_t rng_skip, float *L, uint8_t *valid) {
   int rc = check_args(c, a);
   if (rc) return rc;
-  if (a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_RESTIR_GI) {
+  if (a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH ||
+      a->integrator == MTX_INT_RESTIR_GI) {
     mtx_set_error("mtx_sample_rays: PSSMLT / ReSTIR GI are render-level algorithms (use mtx_render)");
     return MTX_E_UNSUPPORTED;
   }

@@ -481,6 +481,108 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   return active;
 }
 
+// pssmltpath.py:17-168 — one bounce of a PSSMLT proposal with NEE + MIS:
+// emission at the hit weighted against the previous BSDF sample (:71-82),
+// unmasked BSDF sample (:99-101), mutation of the local direction AND of the
+// emitter sample against the current path's vertex (:103-105, mutate
+// :170-190), re-evaluation (:107-110), NEE from the mutated emitter sample
+// (:118-134, shadow ray), proposed vertex write (:138), RR (:154-166).
+// Draws per bounce: 1 + 2 (BSDF) + 2 (mutation) + 1 (RR).
+__device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
+                                                  const ChunkParams &p, uint32_t path, ShadeIO &io) {
+  const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
+  const uint4 mi = b.misc[path];
+  const float4 h = b.hit[path];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  uint32_t depth = mi.w & 0xffffu, flags = mi.w >> 16;
+  V3 T = V3{th.x, th.y, th.z};
+  float eta = th.w;
+  V3 L = V3{Lr.x, Lr.y, Lr.z};
+  float prev_pdf = Lr.w;
+  const V3 prev_p = V3{pv.x, pv.y, pv.z};
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{rd.x, rd.y, rd.z});
+  io.emit = false;
+  io.query = false;
+  // direct emission (:71-82)
+  const bool prev_delta = (flags & PF_PREV_DELTA) != 0;
+  const V3 rel = si.p - prev_p;
+  const float dist = norm(rel);
+  const float em_pdf = prev_delta ? 0.f : pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+  const float mis_bsdf = mis_weight_b(prev_pdf, em_pdf);
+  const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
+  L = fma3v(T, le * mis_bsdf, L);
+  const bool active_next = (depth + 1 < p.max_depth) && si.valid;  // :84
+  // BSDF sampling (:99-101), not masked
+  const float s1 = rng.next_1d();
+  const V2 s2 = rng.next_2d();
+  BSDFSample bs;
+  bs.wo = v3s(0.f);
+  bs.pdf = 0.f;
+  bs.eta = 0.f;
+  bs.type = 0;
+  V3 w = v3s(0.f);
+  mtx_material mat;
+  if (si.valid) {
+    mat = sv.materials[si.material];
+    w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+  }
+  // mutate (:170-190): a = 0.01 on the direction, sqrt(0.01) on the emitter sample
+  const V2 um = rng.next_2d();
+  const size_t vi = (size_t)depth * b.capacity + path;
+  const float4 o4 = b.vpath[vi];
+  const float2 oes = b.vpath_es[vi];
+  V3 vwo;
+  V2 es;
+  if (p.large_step) {
+    vwo = bs.wo;
+    es = um;
+  } else {
+    vwo = normalize(V3{o4.x, o4.y, o4.z} * 0.99f + bs.wo * 0.01f);
+    const V2 g = square_to_std_normal(um);
+    es = V2{dr_clamp(g.x * 0.1f + oes.x, 0.f, 1.f), dr_clamp(g.y * 0.1f + oes.y, 0.f, 1.f)};
+  }
+  V3 val = v3s(0.f);
+  float pdf = 0.f;
+  if (si.valid) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, vwo, &val, &pdf);  // :107
+  if (pdf <= 0.f) vwo = bs.wo;                                                // :109
+  if (pdf > 0.f) w = val / pdf;                                               // :110
+  const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, vwo));               // :114
+  // emitter sampling from the mutated sample (:118-134)
+  const bool active_em = active_next && (bsdf_flags(mat) & BF_SMOOTH) != 0;
+  if (active_em) {
+    DirectionSample ds;
+    const V3 em_weight = sample_emitter_direction(sv, si.p, es, &ds);
+    const V3 wo = to_local(si.sh, ds.d);
+    V3 ev;
+    float epdf;
+    bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &ev, &epdf);
+    const float mi_em = mis_weight_b(ds.pdf, epdf);
+    make_shadow(io, si, ds, path, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true);
+  }
+  b.vprop[vi] = make_float4(vwo.x, vwo.y, vwo.z, 0.f);  // :138
+  b.vprop_es[vi] = make_float2(es.x, es.y);
+  T = T * w;
+  eta *= bs.eta;
+  prev_pdf = bs.pdf;
+  flags = (bs.type & BF_DELTA) ? (flags | PF_PREV_DELTA) : (flags & ~PF_PREV_DELTA);
+  if (si.valid) depth += 1;  // :154
+  const float fmax_ = hmax(T);
+  const float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+  const bool rr_active = depth >= p.rr_depth;
+  const bool rr_continue = rng.next_1d() < rr_prob;
+  if (rr_active) T = T * rcp(rr_prob);
+  const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
+  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+  b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
+  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  return active;
+}
+
 template <int INT>
 __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
@@ -502,6 +604,8 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
       path = in_q[i];
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
         cont = shade_pssmlt(s, sv, b, p, path);
+      else if constexpr (INT == MTX_INT_PSSMLT_PATH)
+        cont = shade_pssmlt_path(s, sv, b, p, path, io);
       else
         cont = shade_path<INT>(s, sv, b, p, bounce, path, io);
     }
@@ -722,6 +826,10 @@ __global__ void k_mlt_init(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   for (uint32_t d = 0; d < max_depth; ++d) {
     b.vpath[(size_t)d * b.capacity + i] = make_float4(0.f, 0.f, 0.f, 0.f);
     b.vprop[(size_t)d * b.capacity + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.integrator == MTX_INT_PSSMLT_PATH) {
+      b.vpath_es[(size_t)d * b.capacity + i] = make_float2(0.f, 0.f);
+      b.vprop_es[(size_t)d * b.capacity + i] = make_float2(0.f, 0.f);
+    }
   }
 }
 
@@ -753,7 +861,10 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   b.ray_d[i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
   b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
-  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+  // pssmltpath.py:42-44: prev_si zero, prev_bsdf_delta = True
+  const uint32_t fl = p.integrator == MTX_INT_PSSMLT_PATH ? (PF_PREV_DELTA << 16) : 0u;
+  if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
   b.queue[0][i] = i;
 }
 
@@ -783,6 +894,9 @@ __global__ void k_mlt_end(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
     b.mlt_L[i] = make_float4(Lp.x, Lp.y, Lp.z, 0.f);
     for (uint32_t d = 0; d < max_depth; ++d)
       b.vpath[(size_t)d * b.capacity + i] = b.vprop[(size_t)d * b.capacity + i];
+    if (p.integrator == MTX_INT_PSSMLT_PATH)
+      for (uint32_t d = 0; d < max_depth; ++d)
+        b.vpath_es[(size_t)d * b.capacity + i] = b.vprop_es[(size_t)d * b.capacity + i];
   }
   b.mlt_cur[i] = cur;
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
@@ -861,6 +975,9 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
       break;
     case MTX_INT_PSSMLT_SIMPLE:
       hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_SIMPLE>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
+    case MTX_INT_PSSMLT_PATH:
+      hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
     default:
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);

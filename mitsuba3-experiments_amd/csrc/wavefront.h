@@ -85,6 +85,8 @@ struct WaveBuffers {
   float2 *mlt_prop;
   float4 *vpath;
   float4 *vprop;
+  float2 *vpath_es;  // pssmltpath.py PathVert.emitter_sample (current / proposed)
+  float2 *vprop_es;
   // ReSTIR GI: first hit of the secondary path (restirgi.py:452-455), written
   // by the bounce-0 shade (path order).
   float4 *rs_xs;

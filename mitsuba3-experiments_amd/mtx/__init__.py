@@ -12,6 +12,7 @@ from .integrators import (  # noqa: F401
     NRCIntegrator,
     Path,
     PathIntegrator,
+    PssmltPath,
     PssmltSimple,
     RestirIntegrator,
     develop,

@@ -22,6 +22,7 @@ MTX_INT_PATH_MIS = 2
 MTX_INT_NRC = 3
 MTX_INT_PSSMLT_SIMPLE = 4
 MTX_INT_RESTIR_GI = 5
+MTX_INT_PSSMLT_PATH = 6
 
 MTX_RESTIR_BIAS_CORRECTION = 1
 MTX_RESTIR_JACOBIAN = 2

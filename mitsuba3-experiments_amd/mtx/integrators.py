@@ -222,6 +222,17 @@ class PssmltSimple(SamplingIntegrator):
         raise MtxError("PssmltSimple.sample() needs the Metropolis chain state; use render()")
 
 
+class PssmltPath(PssmltSimple):
+    """pssmlt.py:96-255 + pssmltpath.py:12-193 ("pssmlt"): the same chains
+    and Metropolis schedule as PssmltSimple, with an NEE + MIS proposal
+    tracer; each path vertex holds the local direction and the emitter
+    sample, mutated as normalize(0.99 old + 0.01 new) and
+    clamp(old + 0.1 N(0,1)) (pssmltpath.py:170-190)."""
+
+    integrator_id = _abi.MTX_INT_PSSMLT_PATH
+    name = "pssmlt"
+
+
 class RestirIntegrator(SamplingIntegrator):
     """restirgi.py:151-588 ("restirgi"): ReSTIR GI. Each render() call is one
     frame: an initial sample per lane (camera hit x_v + a path-mis secondary
@@ -331,6 +342,7 @@ class RestirIntegrator(SamplingIntegrator):
 register_integrator("restirgi", lambda props: RestirIntegrator(props))
 register_integrator("mypath", lambda props: Path(props))
 register_integrator("pssmlt_simple", lambda props: PssmltSimple(props))
+register_integrator("pssmlt", lambda props: PssmltPath(props))  # pssmltpath.py:193
 register_integrator("path_test", lambda props: PathIntegrator(props))
 register_integrator("nrc", lambda props: NRCIntegrator(props))
 

@@ -13,6 +13,7 @@
 //   * path.py:27-192       transcribed SamplingIntegrator.render/render_sample
 //                          (lane -> pixel, film jitter, camera ray, block.put)
 //   * pssmlt.py / pssmltsimple.py Pssmlt.render      -> orc_pssmlt_render()
+//   * pssmltpath.py:17-190 PssmltPath.sample          -> orc_pssmlt_path_sample()
 //   * restirgi.py:182-457 RestirIntegrator.render    -> orc_restir_frame()
 //   * prefix_sum.py:9-36, hashgrid.py:8-90, reductions.py:12-54
 // The upstream per-lane primitives these loops call (Scene.ray_intersect,
@@ -431,6 +432,80 @@ V3 orc_pssmlt_sample(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth
   return L;
 }
 
+// --------------------------- pssmltpath.py:17-190 ---------------------------
+// One proposal with NEE + MIS. Vertex = (local wo, emitter sample); both are
+// mutated against the current path's vertex and written to the proposal.
+V3 orc_pssmlt_path_sample(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_t rr_depth,
+                          bool large_step, const V3 *path_v, const V2 *path_es, V3 *prop_v, V2 *prop_es) {
+  V3 f = v3s(1.f), L = v3s(0.f);
+  float eta = 1.f;
+  uint32_t depth = 0;
+  V3 prev_p = v3s(0.f);  // prev_si = zeros (:42)
+  float prev_bsdf_pdf = 1.f;
+  bool prev_bsdf_delta = true;
+  bool active = true;
+  while (active) {
+    SurfaceInteraction si = intersect(s, ray);  // :67
+    V3 rel = si.p - prev_p;                      // :71-82
+    float dist = norm(rel);
+    V3 ds_d = si.valid ? rel / dist : to_world(si.sh, si.wi) * -1.f;
+    float em_pdf = prev_bsdf_delta ? 0.f : pdf_emitter_direction(s, si.emitter, ds_d, dist, si.sh.n);
+    float mis_bsdf = mis_weight_b(prev_bsdf_pdf, em_pdf);
+    V3 le = (prev_bsdf_pdf > 0.f) ? emitter_eval(s, si.emitter, si.wi) : v3s(0.f);
+    L = fma3v(f, le * mis_bsdf, L);
+    bool active_next = (depth + 1 < max_depth) && si.valid;  // :84
+    float s1 = rng.next_1d();                                 // :99-101
+    V2 s2 = rng.next_2d();
+    BSDFSample bs{};
+    V3 w = v3s(0.f);
+    const mtx_material *mat = si.valid ? &s.materials[si.material] : nullptr;
+    if (mat) w = bsdf_sample(s.bsdf, *mat, si.uv, si.wi, s1, s2, &bs);
+    V2 um = rng.next_2d();  // :104 mutate(path[depth], wo, next_2d, large_step)
+    V3 vwo;
+    V2 es;
+    if (large_step) {
+      vwo = bs.wo;
+      es = um;
+    } else {  // :176-188
+      vwo = normalize(path_v[depth] * 0.99f + bs.wo * 0.01f);
+      V2 g = square_to_std_normal(um);
+      es = V2{dr_clamp(g.x * 0.1f + path_es[depth].x, 0.f, 1.f), dr_clamp(g.y * 0.1f + path_es[depth].y, 0.f, 1.f)};
+    }
+    V3 val = v3s(0.f);
+    float pdf = 0.f;
+    if (mat) bsdf_eval_pdf(s.bsdf, *mat, si.uv, si.wi, vwo, &val, &pdf);  // :107
+    if (pdf <= 0.f) vwo = bs.wo;                                          // :109
+    if (pdf > 0.f) w = val / pdf;                                         // :110
+    ray = spawn_ray(si.p, si.n, to_world(si.sh, vwo));                    // :114
+    bool active_em = active_next && smooth(s, si);                        // :118
+    if (active_em) {                                                      // :120-134
+      DirectionSample ds{};
+      V3 em_weight = sample_emitter_visible(s, si, es, &ds);
+      V3 wo = to_local(si.sh, ds.d);
+      V3 ev;
+      float epdf;
+      bsdf_eval_pdf(s.bsdf, *mat, si.uv, si.wi, wo, &ev, &epdf);
+      float mi_em = mis_weight_b(ds.pdf, epdf);
+      L = fma3v(f, ev * em_weight * mi_em, L);
+    }
+    prop_v[depth] = vwo;  // :138
+    prop_es[depth] = es;
+    f = f * w;
+    eta *= bs.eta;
+    prev_p = si.p;
+    prev_bsdf_pdf = bs.pdf;
+    prev_bsdf_delta = (bs.type & BF_DELTA) != 0;
+    if (si.valid) depth += 1;  // :154
+    float fmax_ = hmax(f);
+    float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+    bool rr_active = depth >= rr_depth;
+    bool rr_continue = rng.next_1d() < rr_prob;
+    if (rr_active) f = f * rcp(rr_prob);
+    active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
+  }
+  return L;
+}
+
 V3 run_integrator(const SceneView &s, const mtx_render_args &a, Pcg32 &rng, const Ray &ray, bool *valid,
                   float *query = nullptr) {
   switch (a.integrator) {
@@ -611,6 +686,8 @@ int orc_pssmlt_render(const mtx_scene_desc *d, const mtx_render_args *a, uint32_
   for (int64_t p = 0; p < (int64_t)npx; ++p) {
     const uint32_t y = a->y0 + (uint32_t)(p / W), x = (uint32_t)(p % W);
     std::vector<V3> path_v((size_t)spp * D, v3s(0.f)), prop_v((size_t)spp * D, v3s(0.f));
+    const bool with_nee = a->integrator == MTX_INT_PSSMLT_PATH;  // pssmltpath.py
+    std::vector<V2> path_es(with_nee ? (size_t)spp * D : 0, V2{0.f, 0.f}), prop_es(path_es);
     std::vector<Pcg32> rng(spp);
     std::vector<V2> off(spp, V2{0.5f, 0.5f});
     std::vector<V3> Lc(spp, v3s(0.f));
@@ -631,7 +708,11 @@ int orc_pssmlt_render(const mtx_scene_desc *d, const mtx_render_args *a, uint32_
         }
         V2 sp = V2{((float)x + po.x) / (float)W, ((float)y + po.y) / (float)H};  // :128
         Ray ray = camera_ray(s.camera, sp);
-        V3 Lp = orc_pssmlt_sample(s, r, ray, D, a->rr_depth, large, &path_v[(size_t)k * D], &prop_v[(size_t)k * D]);
+        V3 Lp = with_nee ? orc_pssmlt_path_sample(s, r, ray, D, a->rr_depth, large, &path_v[(size_t)k * D],
+                                                   &path_es[(size_t)k * D], &prop_v[(size_t)k * D],
+                                                   &prop_es[(size_t)k * D])
+                         : orc_pssmlt_sample(s, r, ray, D, a->rr_depth, large, &path_v[(size_t)k * D],
+                                             &prop_v[(size_t)k * D]);
         float acc_a = dr_clamp(luminance(Lp) / luminance(Lc[k]), 0.f, 1.f);  // :137
         bool accept = r.next_1d() < acc_a;                                  // :138-140
         if (accept) cw[k] = acc_a; else cw[k] += 1.f - acc_a;               // :143-144
@@ -639,6 +720,8 @@ int orc_pssmlt_render(const mtx_scene_desc *d, const mtx_render_args *a, uint32_
           off[k] = po;
           Lc[k] = Lp;
           for (uint32_t dd = 0; dd < D; ++dd) path_v[(size_t)k * D + dd] = prop_v[(size_t)k * D + dd];  // :155-158
+          if (with_nee)
+            for (uint32_t dd = 0; dd < D; ++dd) path_es[(size_t)k * D + dd] = prop_es[(size_t)k * D + dd];
         }
       }
       if (agg) {  // block.put(pos, L / cw) at the integer pixel position (:161-165)

@@ -8,6 +8,7 @@ the reference's sources. Vectors:
   trace_rays / trace_hits 4096 rays on the 2 %-budget bedroom proxy
   film_<integrator>       64x36, spp 16, seed 0 films (path_test, mypath, nrc)
   film_pssmlt_simple      32x18, spp 2, seed 2, 60 Metropolis iterations
+  film_pssmlt             the same for pssmltpath.py (NEE + MIS proposals)
   film_restirgi_f<k>      64x36 ReSTIR GI frames 0..2 (test-restir-spatial.py
                           "unbiased" properties)
   hs_scan_sha             sha256 of the Hillis-Steele scan of 10^6 floats
@@ -73,7 +74,8 @@ def compute():
         integ = load_dict({"type": name})
         out[f"film_{name}"] = oracle.render(s, integ.render_args(s, 0, 16))
     sp = s.with_film(32, 18)
-    out["film_pssmlt_simple"] = oracle.pssmlt_render(sp, load_dict({"type": "pssmlt_simple"}).render_args(sp, 2, 2), 60)
+    for name in ("pssmlt_simple", "pssmlt"):
+        out[f"film_{name}"] = oracle.pssmlt_render(sp, load_dict({"type": name}).render_args(sp, 2, 2), 60)
     for k, f in enumerate(restir_frames(s)):
         out[f"film_restirgi_f{k}"] = f
     x = oracle.rng_stream(0, 0, 1_000_000, 1)[:, 0].copy()

@@ -54,8 +54,9 @@ def test_golden_pssmlt_and_restir_oracle(golden, oracle, small_scene):
     from mtx import load_dict
 
     sp = small_scene.with_film(32, 18)
-    f = oracle.pssmlt_render(sp, load_dict({"type": "pssmlt_simple"}).render_args(sp, 2, 2), 60)
-    assert np.array_equal(f, golden["film_pssmlt_simple"])
+    for name in ("pssmlt_simple", "pssmlt"):
+        f = oracle.pssmlt_render(sp, load_dict({"type": name}).render_args(sp, 2, 2), 60)
+        assert np.array_equal(f, golden[f"film_{name}"])
     for k, f in enumerate(make_golden.restir_frames(small_scene)):
         assert np.array_equal(f, golden[f"film_restirgi_f{k}"])
 
@@ -66,8 +67,9 @@ def test_golden_pssmlt_and_restir_gpu(golden, small_scene):
     import make_golden
 
     sp = small_scene.with_film(32, 18)
-    integ = load_dict({"type": "pssmlt_simple", "iterations": 60})
-    assert np.array_equal(integ.render_film(sp, seed=2, spp=2), golden["film_pssmlt_simple"])
+    for name in ("pssmlt_simple", "pssmlt"):
+        integ = load_dict({"type": name, "iterations": 60})
+        assert np.array_equal(integ.render_film(sp, seed=2, spp=2), golden[f"film_{name}"])
     integ = load_dict({"type": "restirgi", **make_golden.RESTIR_PROPS})
     for k in range(3):
         assert np.array_equal(integ.render_film(small_scene, seed=k, spp=1), golden[f"film_restirgi_f{k}"])

@@ -221,14 +221,16 @@ def test_scatter_reduce(oracle):
         assert np.array_equal(g, c)
 
 
+@pytest.mark.parametrize("name", ["pssmlt_simple", "pssmlt"])
 @pytest.mark.parametrize("iterations", [1, 60])
-def test_pssmlt_film_bit_exact(small_scene, oracle, iterations):
+def test_pssmlt_film_bit_exact(small_scene, oracle, iterations, name):
     """Pssmlt.render: the film after `iterations` Metropolis steps (60 covers a
     large-step reset at 50 and the aggregation window 41-49) is bit-identical
-    to the CPU restatement; chunks of 700 chains exercise the chunking."""
+    to the CPU restatement; chunks of 700 chains exercise the chunking.
+    "pssmlt" is pssmltpath.py (NEE + MIS proposals, mutated emitter samples)."""
     from mtx import load_dict
 
-    integ = load_dict({"type": "pssmlt_simple", "iterations": iterations})
+    integ = load_dict({"type": name, "iterations": iterations})
     sc = small_scene.with_film(32, 18)
     film = integ.render_film(sc, seed=2, spp=2, chunk_paths=700)
     ref = oracle.pssmlt_render(sc, integ.render_args(sc, 2, 2), iterations)
