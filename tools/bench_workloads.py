@@ -4,6 +4,7 @@ module is imported by bench.py, which sets up sys.path):
 
   pssmlt  C3  pssmltsimple.py PSSMLT, bedroom 1280x720, 256 chains/pixel,
               --iterations Metropolis iterations (20 = the SURVEY's CI variant)
+  pssmltpath  the same chains with pssmltpath.py's NEE + MIS proposals
   restir  C4  restirgi.py ReSTIR GI, bedroom 1920x1080, props of
               restirgi.py:610-620, --frames timed frames
   nrc     C5  nrc.py NRC path segments, bedroom 1280x720 spp 4
@@ -60,17 +61,18 @@ def _sync():
 
 
 # --------------------------------------------------------------- PSSMLT (C3) --
-def pssmlt(args):
+def pssmlt(args, with_nee=False):
     import binding as oracle
     import torch
-    from mtx import PssmltSimple, scene
+    from mtx import PssmltPath, PssmltSimple, scene
 
     torch.cuda.set_device(0)
     sc = scene.bedroom(1280, 720)
     spp, it = args.spp, args.iterations
-    integ = PssmltSimple({"iterations": it})
+    cls = PssmltPath if with_nee else PssmltSimple
+    integ = cls({"iterations": it})
     film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
-    PssmltSimple({"iterations": 1}).render_film(sc, seed=99, spp=spp, out=film)  # allocation warm-up
+    cls({"iterations": 1}).render_film(sc, seed=99, spp=spp, out=film)  # allocation warm-up
     _sync()
     t0 = time.perf_counter()
     st = None
@@ -95,13 +97,14 @@ def pssmlt(args):
            "cores": _threads(), "kind": "port",
            "sample": f"{rows} of {sc.height} rows x {sc.width} px x {spp} chains x {it} iterations ({c:.1f} s); "
                      "oracle/oracle.cpp orc_pssmlt_render (OpenMP)"}
-    _line("PSSMLT Mchain-iterations/sec on bedroom@1280x720, 256 chains/pixel (C3)", chains * it / dt / 1e6,
-          "Mchain-iterations/s", args.steps, 1, dt * 1e3,
-          {"workload": f"pssmltsimple.py + pssmlt.py render, {it} iterations (large step every 50, aggregate "
+    script = "pssmltpath.py (NEE + MIS)" if with_nee else "pssmltsimple.py"
+    _line(f"PSSMLT{'-path' if with_nee else ''} Mchain-iterations/sec on bedroom@1280x720, {spp} chains/pixel (C3)",
+          chains * it / dt / 1e6, "Mchain-iterations/s", args.steps, 1, dt * 1e3,
+          {"workload": f"{script} + pssmlt.py render, {it} iterations (large step every 50, aggregate "
                        f"i%50>40), max_depth 16, rr_depth 4, {chains} chains", "chains": chains, "iterations": it},
           _trace_roofline(cnt, st["trace_ms"], "step"), cpu,
           {"kernels_ms_per_step": {"trace_closest": round(st["trace_ms"], 3), "shade": round(st["shade_ms"], 3),
-                                   "other": round(st["other_ms"], 3)}})
+                                   "trace_shadow": round(st["shadow_ms"], 3), "other": round(st["other_ms"], 3)}})
 
 
 # -------------------------------------------------------------- ReSTIR (C4) --
@@ -363,4 +366,5 @@ def field(args):
 
 
 def run(args):
-    {"pssmlt": pssmlt, "restir": restir, "nrc": nrc, "prims": prims, "field": field}[args.workload](args)
+    {"pssmlt": pssmlt, "pssmltpath": lambda a: pssmlt(a, with_nee=True), "restir": restir, "nrc": nrc,
+     "prims": prims, "field": field}[args.workload](args)
