@@ -119,6 +119,8 @@ struct mtx_ctx {
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
   uint32_t trace_batch = 256;
+  uint32_t refill_lanes = 16;
+  uint32_t speculate = 1;
   uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -166,6 +168,8 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
+  if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
+  if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   *out = c;
   return MTX_OK;
 }
@@ -340,6 +344,8 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.camera = d->camera;
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
   s.trace_batch = c->trace_batch;
+  s.refill_lanes = c->refill_lanes;
+  s.speculate = c->speculate;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {

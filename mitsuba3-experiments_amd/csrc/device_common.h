@@ -222,12 +222,14 @@ namespace mtxd {
 // (each lane descends until it reaches a leaf or runs out of nodes) with a
 // leaf phase (one leaf per lane), so inner-node and triangle code do not
 // serialise against each other inside one iteration. When at least
-// kRefillLanes lanes of the wave have finished, their slots are refilled from
-// the ray queue with one atomic per wave (ballot + mbcnt). The visit order
-// of each ray is exactly that of `traverse` above (same results and counts).
+// s.refill_lanes lanes of the wave have finished, their slots are refilled from
+// the ray queue with one atomic per wave (ballot + mbcnt). In the STATS
+// kernels the visit order of each ray is exactly that of `traverse` above
+// (same results and counts, the oracle's order); the production kernels
+// speculate (below) and return the same hits with a wave-dependent order.
 // ---------------------------------------------------------------------------
-constexpr int32_t kTravDone = INT32_MIN;  // never a valid leaf reference
-constexpr uint32_t kRefillLanes = 16;
+constexpr int32_t kTravDone = INT32_MIN;           // never a valid leaf reference
+constexpr int32_t kTravLeafTaken = INT32_MIN + 1;  // leaf moved to the leaf phase, pop next
 
 // Src provides: load(k, TraceRay&, float &tmax, uint32_t &payload) and
 // finish(payload, bool any_hit, float t, uint32_t prim, float u, float v).
@@ -243,8 +245,15 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   uint32_t payload = 0, prim = 0xffffffffu;
   TraceRay r;
   float tbest = 0.f, bu = 0.f, bv = 0.f;
-  int32_t node = kTravDone;
+  int32_t node = kTravDone, leaf = 0;
+  bool has_leaf = false;
   int sp = 0;
+  const bool spec = !STATS && s.speculate;
+  auto pop = [&](int &spr) -> int32_t {
+    if (spr == 0) return kTravDone;
+    --spr;
+    return spr < lds_n ? stk[spr * kTraceBlock] : ovf[(size_t)(spr - lds_n) * s.ovf_threads];
+  };
   while (true) {
     if (!exhausted) {
       // Idle lanes take rays from the wave's reservoir of claimed queue
@@ -294,6 +303,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
           hit = false;
           node = 0;
           sp = 0;
+          has_leaf = false;
           has = true;
         }
         exhausted = drained && res_lo >= res_hi;
@@ -301,7 +311,17 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     }
     if (__ballot(has) == 0) break;
     while (true) {
-      // inner-node phase
+      // inner-node phase. With speculation (Aila & Laine 2009), a lane that
+      // reaches a leaf postpones it and keeps descending until every lane
+      // still in the phase holds a postponed leaf: the leaf phase then runs
+      // with more lanes busy. The hit is unchanged (inclusive culling and the
+      // smaller-index tie rule make it order independent); the visit sequence
+      // is not, so the STATS kernels (visit counters, tests) do not speculate.
+      if (spec && has && !has_leaf && node < 0 && node != kTravDone) {
+        leaf = node;
+        has_leaf = true;
+        node = pop(sp);
+      }
       while (has && node >= 0) {
         if (STATS) {
           const uint64_t m = __ballot(true);
@@ -323,21 +343,34 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
               ++sp;
             }
           node = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
-        } else if (sp > 0) {
-          --sp;
-          node = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];
         } else {
-          node = kTravDone;
+          node = pop(sp);
+        }
+        if (spec) {
+          if (!has_leaf && node < 0 && node != kTravDone) {
+            leaf = node;
+            has_leaf = true;
+            node = pop(sp);
+          }
+          if (__ballot(!has_leaf) == 0) break;
         }
       }
-      // leaf phase: one leaf per lane
-      if (has && node != kTravDone) {
+      // leaf phase: one leaf per lane (the postponed one first)
+      if (has && (has_leaf || (node < 0 && node != kTravDone))) {
         if (STATS) {
           const uint64_t m = __ballot(true);
           if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
         }
+        int32_t lf;
+        if (has_leaf) {
+          lf = leaf;
+          has_leaf = false;
+        } else {
+          lf = node;
+          node = kTravLeafTaken;
+        }
         uint32_t first, cnt;
-        leaf_decode(node, &first, &cnt);
+        leaf_decode(lf, &first, &cnt);
         for (uint32_t k = 0; k < cnt; ++k) {
           const uint32_t pr = first + k;
           const float4 g0 = s.tri[3 * pr + 0], g1 = s.tri[3 * pr + 1], g2 = s.tri[3 * pr + 2];
@@ -358,11 +391,8 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
         }
         if (ANY && hit) {
           node = kTravDone;
-        } else if (sp > 0) {
-          --sp;
-          node = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];
-        } else {
-          node = kTravDone;
+        } else if (node == kTravLeafTaken) {
+          node = pop(sp);
         }
       }
       if (has && node == kTravDone) {
@@ -371,7 +401,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
         ++nr;
       }
       const uint64_t idle = __ballot(!has);
-      if (idle == ~0ull || (!exhausted && (uint32_t)__popcll(idle) >= kRefillLanes)) break;
+      if (idle == ~0ull || (!exhausted && (uint32_t)__popcll(idle) >= s.refill_lanes)) break;
     }
   }
 }

@@ -54,6 +54,8 @@ struct DevScene {
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
   int32_t *stack_ovf;      // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
+  uint32_t refill_lanes;   // persistent kernels: refill a wave once this many lanes are idle
+  uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
   mtx_camera camera;
 };
 
