@@ -110,8 +110,10 @@ MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint
 
 // Child reference of the slot encoded in a sort key.
 MTX_HD int32_t wide_ref(uint32_t key, int32_t r0, int32_t r1, int32_t r2, int32_t r3) {
-  const uint32_t k = key & 3u;
-  return k == 0u ? r0 : (k == 1u ? r1 : (k == 2u ? r2 : r3));
+  // two bit selects (no branches on the device)
+  const bool b0 = (key & 1u) != 0u, b1 = (key & 2u) != 0u;
+  const int32_t lo = b0 ? r1 : r0, hi = b0 ? r3 : r2;
+  return b1 ? hi : lo;
 }
 
 MTX_HD void leaf_decode(int32_t c, uint32_t *first, uint32_t *count) {

@@ -228,6 +228,9 @@ namespace mtxd {
 // (same results and counts, the oracle's order); the production kernels
 // speculate (below) and return the same hits with a wave-dependent order.
 // ---------------------------------------------------------------------------
+#ifndef MTX_PUSH_BRANCHY
+#define MTX_PUSH_BRANCHY 0  // A/B: 1 = per-entry conditional pushes only
+#endif
 constexpr int32_t kTravDone = INT32_MIN;           // never a valid leaf reference
 constexpr int32_t kTravLeafTaken = INT32_MIN + 1;  // leaf moved to the leaf phase, pop next
 
@@ -332,16 +335,30 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
         ++nv;
         const int n = wide_visit(s, r, node, tbest, rf, key);
         if (n > 0) {
+          // far children pushed farthest first: entries sp .. sp+n-2 hold
+          // key[n-1] .. key[1]. Branch-free: three stores, the ones beyond
+          // the new top are dead (capacity 3*depth+1 covers them).
+          const int32_t c1 = wide_ref(key[1], rf.x, rf.y, rf.z, rf.w);
+          const int32_t c2 = wide_ref(key[2], rf.x, rf.y, rf.z, rf.w);
+          const int32_t c3 = wide_ref(key[3], rf.x, rf.y, rf.z, rf.w);
+          const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
+          if (!MTX_PUSH_BRANCHY && sp + 3 <= lds_n) {
+            stk[sp * kTraceBlock] = e0;
+            stk[(sp + 1) * kTraceBlock] = e1;
+            stk[(sp + 2) * kTraceBlock] = c1;
+          } else {
+            const int32_t e[3] = {e0, e1, c1};
 #pragma unroll
-          for (int rr = 3; rr >= 1; --rr)
-            if (rr < n) {
-              const int32_t far = wide_ref(key[rr], rf.x, rf.y, rf.z, rf.w);
-              if (sp < lds_n)
-                stk[sp * kTraceBlock] = far;
-              else
-                ovf[(size_t)(sp - lds_n) * s.ovf_threads] = far;
-              ++sp;
-            }
+            for (int j = 0; j < 3; ++j)
+              if (j < n - 1) {
+                const int q = sp + j;
+                if (q < lds_n)
+                  stk[q * kTraceBlock] = e[j];
+                else
+                  ovf[(size_t)(q - lds_n) * s.ovf_threads] = e[j];
+              }
+          }
+          sp += n - 1;
           node = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
         } else {
           node = pop(sp);
