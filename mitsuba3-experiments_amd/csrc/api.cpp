@@ -101,6 +101,7 @@ struct mtx_ctx {
   mtxd::DevScene scene{};
   // wavefront
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
+  DevBuf xheads, rs_heads;  // per-XCD claim cursors of the persistent trace kernels
   uint32_t capacity = 0;
   DevBuf mlt_cur, mlt_L, mlt_prop, vpath, vprop;  // PSSMLT chain state
   DevBuf vpath_es, vprop_es;                       // pssmltpath emitter samples
@@ -121,6 +122,7 @@ struct mtx_ctx {
   uint32_t trace_batch = 256;
   uint32_t refill_lanes = 16;
   uint32_t speculate = 1;
+  uint32_t xcd_claim = 1;
   uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -170,6 +172,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
+  if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   *out = c;
   return MTX_OK;
 }
@@ -181,7 +184,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   DevBuf *bufs[] = {&c->nodes,  &c->tri,     &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
-                    &c->q0,     &c->q1,      &c->shadow,   &c->counters,  &c->stats,    &c->contrib, &c->film,
+                    &c->q0,     &c->q1,      &c->shadow,   &c->counters, &c->xheads, &c->rs_heads,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop, &c->vpath_es, &c->vprop_es,
                     &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
@@ -346,6 +349,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.trace_batch = c->trace_batch;
   s.refill_lanes = c->refill_lanes;
   s.speculate = c->speculate;
+  s.xcd_claim = c->xcd_claim;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {
@@ -396,6 +400,7 @@ int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     c->capacity = cap;
   }
   if ((rc = dalloc(c->counters, 16ull * (max_depth + 2)))) return rc;
+  if ((rc = dalloc(c->xheads, 8ull * mtxd::kXSlotWords * (max_depth + 2)))) return rc;
   if ((rc = dalloc(c->stats, 8 * 8))) return rc;
   return MTX_OK;
 }
@@ -414,6 +419,7 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.queue[1] = (uint32_t *)c->q1.p;
   b.shadow = (mtxd::ShadowRec *)c->shadow.p;
   b.counters = (uint32_t *)c->counters.p;
+  b.xheads = (uint32_t *)c->xheads.p;
   b.stats = (unsigned long long *)c->stats.p;
   b.capacity = c->capacity;
   b.mlt_cur = (float4 *)c->mlt_cur.p;
@@ -428,6 +434,13 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.cq_t = (float4 *)c->cq_t.p;
   b.cq_count = (uint32_t *)c->cq_count.p;
   return b;
+}
+
+// Zeroes a chunk's queue counters and the per-XCD claim cursors.
+hipError_t reset_counters(const mtxd::WaveBuffers &b, uint32_t depth, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(b.counters, 0, 16ull * (depth + 2), st);
+  if (e != hipSuccess) return e;
+  return hipMemsetAsync(b.xheads, 0, 8ull * mtxd::kXSlotWords * (depth + 2), st);
 }
 
 int ensure_mlt(mtx_ctx *c, uint32_t cap, uint32_t max_depth, bool emitter_samples) {
@@ -627,6 +640,7 @@ int ensure_restir(mtx_ctx *c, uint32_t n) {
     if ((rc = dalloc(c->rs_rng, 16 * N))) return rc;
     if ((rc = dalloc(c->rs_rays, 9 * 32 * N))) return rc;
     if ((rc = dalloc(c->rs_count, 16))) return rc;
+    if ((rc = dalloc(c->rs_heads, 4ull * mtxd::kXSlotWords))) return rc;
     if ((rc = dalloc(c->rs_occ, 18 * N))) return rc;
     if ((rc = dalloc(c->rs_qM, 10 * 4 * N))) return rc;
     if ((rc = dalloc(c->rs_xs, 16 * N))) return rc;
@@ -698,6 +712,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   r.rng = (uint4 *)c->rs_rng.p;
   r.test_rays = (float4 *)c->rs_rays.p;
   r.test_count = (uint32_t *)c->rs_count.p;
+  r.test_heads = (uint32_t *)c->rs_heads.p;
   r.occ = (uint8_t *)c->rs_occ.p;
   r.qM = (uint32_t *)c->rs_qM.p;
   r.n = n;
@@ -730,17 +745,16 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   p.sample_major = c->sample_major;
   p.stats = want_stats ? 1 : 0;
   if (want_stats) HIP_TRY(hipMemsetAsync(c->stats.p, 0, 64, c->stream));
-  const size_t cbytes = 16ull * (depth + 2);
   hipEvent_t e;
   if (run_a) {
     // sample_initial: primary rays and their closest hits
-    HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
+    HIP_TRY(reset_counters(b, depth, st));
     mtxd::launch_raygen_camera(c->scene, b, p, st);
     e = tm.begin(0);
     mtxd::launch_trace_closest(c->scene, b, 0, p.stats, c->trace_grid, st);
     tm.end(0, e);
     ++*n_trace;
-    HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, st));
+    HIP_TRY(reset_counters(b, depth, st));
     mtxd::launch_restir_begin(c->scene, b, p, r, st);
     run_bounces(c, b, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
     mtxd::launch_restir_collect(b, p, r, st);
@@ -750,12 +764,14 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // spatial_resampling (reads samples / temporal reservoirs of rows outside
     // the band: a row-banded caller imports them between stage A and B)
     HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
+    HIP_TRY(hipMemsetAsync(r.test_heads, 0, 4ull * mtxd::kXSlotWords, st));
     mtxd::launch_restir_spatial_rays(r, p, st);
     e = tm.begin(1);
     mtxd::launch_trace_test(c->scene, r, 0, c->trace_grid, st);
     tm.end(1, e);
     ++*n_shadow;
     HIP_TRY(hipMemsetAsync(r.test_count, 0, 16, st));
+    HIP_TRY(hipMemsetAsync(r.test_heads, 0, 4ull * mtxd::kXSlotWords, st));
     mtxd::launch_restir_spatial_merge(r, p, st);
     if (a->restir_flags & MTX_RESTIR_BIAS_CORRECTION) {
       e = tm.begin(1);
@@ -861,14 +877,13 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.stats = want_stats ? 1 : 0;
     p.sample_major = c->sample_major;
     p.nrc_cache = nrc_cache ? 1u : 0u;
-    const size_t cbytes = 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2);
     if (mlt) {
       // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains
       const uint32_t iters = a->iterations ? a->iterations : 200;
       mtxd::launch_mlt_init(b, p, c->stream);
       for (uint32_t it = 0; it < iters; ++it) {
         p.large_step = (it % 50 == 0) ? 1u : 0u;  // reset_interval = 50 (:206)
-        HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, c->stream));
+        HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
         mtxd::launch_mlt_begin(c->scene, b, p, c->stream);
         run_bounces(c, b, p, tm, &n_trace, &n_shadow);
         mtxd::launch_mlt_end(b, p, c->stream);
@@ -876,7 +891,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       }
       continue;
     }
-    HIP_TRY(hipMemsetAsync(b.counters, 0, cbytes, c->stream));
+    HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
     if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
     run_bounces(c, b, p, tm, &n_trace, &n_shadow);
@@ -1015,7 +1030,7 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     p.n_paths = m;
     p.nrc_c = a->nrc_c;
     p.nrc_cache = nrc_cache ? 1u : 0u;
-    HIP_TRY(hipMemsetAsync(b.counters, 0, 16ull * (std::max<uint32_t>(a->max_depth, 1) + 2), c->stream));
+    HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
     if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
     run_bounces(c, b, p, tm, &nt, &ns);

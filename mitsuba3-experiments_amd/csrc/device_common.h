@@ -236,8 +236,25 @@ constexpr int32_t kTravLeafTaken = INT32_MIN + 1;  // leaf moved to the leaf pha
 
 // Src provides: load(k, TraceRay&, float &tmax, uint32_t &payload) and
 // finish(payload, bool any_hit, float t, uint32_t prim, float u, float v).
+// XCD of the executing wave (0-7): speed only (which L2 the wave fills).
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & (kXcds - 1u);
+}
+
+// Queue segment k of 8: [count*k/8, count*(k+1)/8).
+__device__ __forceinline__ uint32_t xseg_bound(uint32_t count, uint32_t k) {
+  return (uint32_t)(((uint64_t)count * k) >> 3);
+}
+
+// heads: kXcds claim cursors (kXHeadStride words apart), zeroed before the
+// launch. A wave claims rays from the queue segment of its own XCD first,
+// so the rays an XCD traces come from one band of the (pixel-ordered)
+// queue and share BVH nodes in that XCD's L2; exhausted segments send the
+// wave on to the next XCD's segment.
 template <bool ANY, bool STATS = false, class Src>
-__device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *fetch,
+__device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                            int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
                                            uint32_t *wave_iters = nullptr) {
   const uint32_t lane = lane_id();
@@ -252,6 +269,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   bool has_leaf = false;
   int sp = 0;
   const bool spec = !STATS && s.speculate;
+  uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
   auto pop = [&](int &spr) -> int32_t {
     if (spr == 0) return kTravDone;
     --spr;
@@ -270,15 +288,24 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
         uint32_t base2 = 0, got2 = 0;
         if (left < n && !drained) {
           const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
-          uint32_t b = 0;
-          if (lane == leader) b = atomicAdd(fetch, s.trace_batch);
-          b = __builtin_amdgcn_readlane(b, leader);
-          if (b >= count) {
-            drained = true;
-          } else {
-            base2 = b;
-            got2 = min(s.trace_batch, count - b);
-            if (count - b <= s.trace_batch) drained = true;
+          while (true) {  // wave-uniform
+            const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
+            const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
+            uint32_t b = 0xffffffffu;
+            if (hi > lo) {
+              if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, s.trace_batch);
+              b = __builtin_amdgcn_readlane(b, leader);
+            }
+            if (hi > lo && b < hi - lo) {
+              base2 = lo + b;
+              got2 = min(s.trace_batch, hi - lo - b);
+              break;
+            }
+            if (++tries >= kXcds) {
+              drained = true;
+              break;
+            }
+            seg = (seg + 1) & (kXcds - 1u);
           }
         }
         const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveB
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   const ClosestSrc src{b, b.queue[bounce & 1]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
-  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], &b.counters[4 * bounce + 2], stack + threadIdx.x, nv,
+  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, stack + threadIdx.x, nv,
                            tv, nr, wi);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene s, WaveBu
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   const ShadowSrc src{b};
   uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop<true>(s, src, b.counters[4 * bounce + 1], &b.counters[4 * bounce + 3], stack + threadIdx.x, nv, tv, nr);
+  trace_loop<true>(s, src, b.counters[4 * bounce + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, stack + threadIdx.x, nv, tv, nr);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
     if ((threadIdx.x & 63) == 0) {

@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_test(DevScene s, RestirBu
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   const TestSrc src{r, occ_base};
   uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop<true>(s, src, r.test_count[0], &r.test_count[1], stack + threadIdx.x, nv, tv, nr);
+  trace_loop<true>(s, src, r.test_count[0], r.test_heads, stack + threadIdx.x, nv, tv, nr);
 }
 
 static inline unsigned rs_blocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }

@@ -33,6 +33,12 @@ enum : uint32_t {
 constexpr int kTraceBlock = 128;     // threads per traversal block
 constexpr uint32_t kLdsStack = 16;   // default LDS part of the persistent traversal stack (entries per lane)
 
+// Per-XCD claim cursors of the persistent trace kernels: kXcds words,
+// kXHeadStride words (128 B) apart; one slot per trace launch of a chunk.
+constexpr uint32_t kXcds = 8;
+constexpr uint32_t kXHeadStride = 32;
+constexpr uint32_t kXSlotWords = kXcds * kXHeadStride;
+
 struct DevScene {
   const int4 *nodes;  // 4 x int4 per node
   const float4 *tri;  // 3 x float4 per triangle
@@ -56,6 +62,7 @@ struct DevScene {
   uint32_t ovf_threads;    // threads of the persistent trace grid
   uint32_t refill_lanes;   // persistent kernels: refill a wave once this many lanes are idle
   uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
+  uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
 };
 
@@ -77,7 +84,8 @@ struct WaveBuffers {
   float4 *hit;
   uint32_t *queue[2];
   ShadowRec *shadow;
-  uint32_t *counters;   // per bounce b: [4b+0] rays, [4b+1] shadow rays, [4b+2] ray fetch, [4b+3] shadow fetch
+  uint32_t *counters;   // per bounce b: [4b+0] rays, [4b+1] shadow rays, [4b+2], [4b+3] unused
+  uint32_t *xheads;     // per bounce b: slot 2b closest-hit, 2b+1 shadow claim cursors (kXSlotWords each)
   unsigned long long *stats;  // nodes_c, tris_c, nodes_s, tris_s, rays_c, rays_s
   uint32_t capacity;
   // PSSMLT chain state (pssmlt.py:196-200): offset.xy, cumulative weight | L | proposed offset,
@@ -111,7 +119,8 @@ struct RestirBuffers {
   float4 *emit;       // emittance at the primary hit (:421-423)
   uint4 *rng;         // sampler state between the phases
   float4 *test_rays;  // compacted visibility tests: (o, maxt), (d, slot)
-  uint32_t *test_count;  // [0] count, [1] fetch cursor
+  uint32_t *test_count;  // [0] count
+  uint32_t *test_heads;  // per-XCD claim cursors of k_trace_test (kXSlotWords)
   uint8_t *occ;       // 18 per lane: spatial tests [0,9), bias-correction tests [9,18)
   uint32_t *qM;       // 10 per lane: Q.M with bit 31 = active, [9] = Z before the loop
   uint32_t n;      // lanes of the whole frame (state arrays)
