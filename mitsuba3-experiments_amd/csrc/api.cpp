@@ -123,6 +123,7 @@ struct mtx_ctx {
   uint32_t refill_lanes = 16;
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
+  uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
   uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -173,6 +174,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
+  if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
   *out = c;
   return MTX_OK;
 }
@@ -316,7 +318,11 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
           r[24 + 2 * k + 1] = d->vuv[2 * (size_t)vi + 1];
         }
       }
-      const uint32_t mat = sh.material, fl = use_n | use_uv;
+      // bits 8..12: shading class of the material (k_shade sorts a block's
+      // paths by it: lanes of a wave then run the same BSDF code)
+      const mtx_material &m = d->materials[sh.material];
+      const uint32_t cls = 1u + ((m.type & 7u) << 2 | (m.tex >= 0 ? 2u : 0u) | ((m.flags & MTX_MF_MASK) ? 1u : 0u));
+      const uint32_t mat = sh.material, fl = use_n | use_uv | (cls << 8);
       const int32_t em = sh.emitter;
       memcpy(&r[3], &mat, 4);
       memcpy(&r[7], &em, 4);
@@ -350,6 +356,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.refill_lanes = c->refill_lanes;
   s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
+  s.shade_sort = c->shade_sort;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {

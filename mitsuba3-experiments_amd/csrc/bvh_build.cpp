@@ -14,6 +14,7 @@
 // traversal's fixed LDS stack can never overflow.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -54,6 +55,7 @@ struct Box {
 };
 
 constexpr int kBins = 32;
+constexpr float kDefaultCt = 1.f;  // SAH cost of a traversal step, in triangle tests
 
 struct Builder {
   const float *vpos;
@@ -64,6 +66,8 @@ struct Builder {
   std::vector<uint32_t> idx;
   std::vector<int32_t> nodes;  // 16 words per node
   std::vector<uint32_t> order; // leaf order -> input tri
+  float ct = kDefaultCt;
+  int layout = 0;
   uint32_t max_depth_seen = 0;
 
   static int ceil_log2(uint32_t c) {
@@ -139,7 +143,7 @@ struct Builder {
           acc.grow(bins[b]);
           c += counts[b];
           if (c == 0 || right_cnt[b + 1] == 0) continue;
-          float cost = 1.f + (acc.area() * (float)c + right_area[b + 1] * (float)right_cnt[b + 1]) / pa;
+          float cost = ct + (acc.area() * (float)c + right_area[b + 1] * (float)right_cnt[b + 1]) / pa;
           if (cost < best_cost) {
             best_cost = cost;
             best_axis = a;
@@ -230,6 +234,45 @@ struct Builder {
 
   // Opens the inner child with the largest surface area (ties: first) until
   // the node has 4 children or only leaves remain.
+  std::vector<Child> open_children(uint32_t node2) const {
+    std::vector<Child> ch = {{nodes[16 * (size_t)node2 + 12], child_box2(node2, 0)},
+                             {nodes[16 * (size_t)node2 + 13], child_box2(node2, 1)}};
+    while (ch.size() < MTX_BVH_WIDTH) {
+      int best = -1;
+      float best_area = -1.f;
+      for (int i = 0; i < (int)ch.size(); ++i)
+        if (ch[i].ref >= 0 && ch[i].box.area() > best_area) {
+          best_area = ch[i].box.area();
+          best = i;
+        }
+      if (best < 0) break;
+      const uint32_t n2 = (uint32_t)ch[best].ref;
+      Child a{nodes[16 * (size_t)n2 + 12], child_box2(n2, 0)}, b{nodes[16 * (size_t)n2 + 13], child_box2(n2, 1)};
+      ch[best] = a;
+      ch.insert(ch.begin() + best + 1, b);
+    }
+    return ch;
+  }
+
+  // Sibling-contiguous layout: the inner children of a wide node get
+  // consecutive indices (two 64-B nodes per 128-B line), allocated before
+  // their subtrees.
+  void collapse_siblings(uint32_t w, uint32_t node2, uint32_t depth) {
+    const std::vector<Child> ch = open_children(node2);
+    wide_depth = std::max(wide_depth, depth + 1);
+    int32_t refs[MTX_BVH_WIDTH] = {0, 0, 0, 0};
+    uint32_t n_inner = 0;
+    for (const Child &c : ch) n_inner += c.ref >= 0 ? 1u : 0u;
+    const uint32_t base = (uint32_t)(wnodes.size() / 16);
+    wnodes.resize(wnodes.size() + 16 * (size_t)n_inner, 0);
+    uint32_t j = 0;
+    for (size_t k = 0; k < ch.size(); ++k) refs[k] = ch[k].ref >= 0 ? (int32_t)(base + j++) : ch[k].ref;
+    encode(w, ch, refs);
+    j = 0;
+    for (size_t k = 0; k < ch.size(); ++k)
+      if (ch[k].ref >= 0) collapse_siblings(base + j++, (uint32_t)ch[k].ref, depth + 1);
+  }
+
   int32_t collapse(uint32_t node2, uint32_t depth) {
     std::vector<Child> ch = {{nodes[16 * (size_t)node2 + 12], child_box2(node2, 0)},
                              {nodes[16 * (size_t)node2 + 13], child_box2(node2, 1)}};
@@ -357,6 +400,11 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
       return MTX_E_ARG;
     }
   Builder b;
+  // build knobs (tuning experiments): SAH traversal cost relative to one
+  // triangle test, and the wide-node layout (0 depth-first, 1 siblings
+  // contiguous)
+  if (const char *e = getenv("MTX_BVH_CT")) b.ct = std::max(0.05f, (float)atof(e));
+  if (const char *e = getenv("MTX_BVH_LAYOUT")) b.layout = atoi(e);
   b.vpos = vpos;
   b.vidx = tri_vidx;
   b.n = n_tris;
@@ -366,7 +414,12 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     return MTX_E_ARG;
   }
   b.wnodes.reserve(b.nodes.size() / 2 + 16);
-  b.collapse(0, 0);
+  if (b.layout == 1) {
+    b.wnodes.resize(16, 0);
+    b.collapse_siblings(0, 0, 0);
+  } else {
+    b.collapse(0, 0);
+  }
   if (!b.quant_ok) {
     mtx_set_error("mtx_bvh_build: child box quantisation failed (non-finite or huge coordinates?)");
     return MTX_E_ARG;

@@ -136,6 +136,48 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c0, ui
   s1 = o1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
 }
 
+// Stable block-wide counting sort of one value per thread by a key in
+// [0, kShadeClasses): returns the value of rank threadIdx.x. Deterministic
+// (ranks from ballots, no LDS atomics). Every thread of the block calls it.
+constexpr uint32_t kShadeClasses = 32;
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_sort_by_key(uint32_t key, uint32_t value) {
+  constexpr int W = BLOCK / 64;
+  __shared__ uint32_t cnt[W][kShadeClasses];
+  __shared__ uint32_t off[kShadeClasses];
+  __shared__ uint32_t vals[BLOCK];
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t j = threadIdx.x; j < W * kShadeClasses; j += BLOCK) (&cnt[0][0])[j] = 0u;
+  __syncthreads();
+  uint32_t rank = 0;
+  uint64_t pending = __ballot(true);
+  while (pending) {  // one round per distinct key in the wave
+    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)pending) - 1);
+    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
+    const uint64_t m = __ballot(key == k);
+    if (key == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == leader) cnt[wave][k] = (uint32_t)__popcll(m);
+    pending &= ~m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < kShadeClasses; ++k) {
+      off[k] = t;
+#pragma unroll
+      for (int w = 0; w < W; ++w) t += cnt[w][k];
+    }
+  }
+  __syncthreads();
+  uint32_t dst = off[key] + rank;
+  for (uint32_t w = 0; w < wave; ++w) dst += cnt[w][key];
+  vals[dst] = value;
+  __syncthreads();
+  const uint32_t out = vals[threadIdx.x];
+  __syncthreads();
+  return out;
+}
+
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;

@@ -600,8 +600,20 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     io.query = false;
     bool cont = false;
     uint32_t path = 0;
-    if (i < count) {
-      path = in_q[i];
+    if (i < count) path = in_q[i];
+    bool valid = i < count;
+    if (s.shade_sort) {
+      // the block's paths ordered by the shading class of their hit: waves
+      // then run one or two BSDF branches instead of all of them
+      uint32_t key = kShadeClasses - 1;  // slots past the queue end sort last
+      if (valid) {
+        const uint32_t prim = __float_as_uint(b.hit[path].y);
+        key = prim == 0xffffffffu ? 0u : (__float_as_uint(s.shade_rec[8 * (size_t)prim + 2].w) >> 8) & 31u;
+      }
+      path = block_sort_by_key<kShadeBlock>(key, path);
+      valid = threadIdx.x < min(count - base, (uint32_t)kShadeBlock);
+    }
+    if (valid) {
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
         cont = shade_pssmlt(s, sv, b, p, path);
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
