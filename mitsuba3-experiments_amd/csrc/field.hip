@@ -13,7 +13,11 @@
 //                 layer's B operand with no lane movement; the host prepacks
 //                 each weight fragment in that permuted k order
 //                 (cdna_hip_programming.md §3, "accumulator tile as the next
-//                 MFMA's operand"). f32 accumulation, fp16 activations.
+//                 MFMA's operand"). f32 accumulation, fp16 activations:
+//                 each accumulator pair is rounded with v_cvt_pk_f16_f32 and
+//                 LeakyReLU runs packed in fp16 (v_pk_mul_f16 + v_pk_max_f16);
+//                 MFMA results stay in VGPRs (-amdgpu-mfma-vgpr-form), so a
+//                 layer costs 16 MFMAs + 48 VALU per wave (MFMA-bound).
 #include <hip/hip_runtime.h>
 
 #include "mtx.h"
@@ -30,6 +34,9 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kFieldPad = 64;     // features per query (padded)
+#ifndef MTX_MLP_PREFETCH
+#define MTX_MLP_PREFETCH 0  // A/B: 1 = load the next tile's input at the top of the tile (180 VGPRs: slower)
+#endif
 constexpr float kLeakySlope = 0.01f;  // drjit.nn.LeakyReLU default
 
 // One thread per (query, level): the 8 corner gathers of a level are
@@ -66,12 +73,20 @@ __global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, 
   }
 }
 
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+
+// Accumulator -> next layer's B operand: round to fp16, then LeakyReLU in
+// fp16 as max(h, h * 0.01) (the activation of a Float16 network; packed
+// v_cvt_pk_f16_f32 / v_pk_mul_f16 / v_pk_max_f16, 1.5 VALU per element).
 __device__ __forceinline__ half8 leaky_pack(const f32x16 &acc, int s) {
   half8 r;
+  const half2v slope = {(_Float16)kLeakySlope, (_Float16)kLeakySlope};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float v = acc[8 * s + j];
-    r[j] = (_Float16)(v >= 0.f ? v : v * kLeakySlope);
+  for (int j = 0; j < 4; ++j) {
+    half2v h = {(_Float16)acc[8 * s + 2 * j], (_Float16)acc[8 * s + 2 * j + 1]};
+    h = __builtin_elementwise_max(h, h * slope);
+    r[2 * j] = h.x;
+    r[2 * j + 1] = h.y;
   }
   return r;
 }
@@ -97,34 +112,40 @@ __global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const u
   const uint32_t waves_per_block = blockDim.x >> 6;
   const uint32_t wave = blockIdx.x * waves_per_block + (threadIdx.x >> 6);
   const uint32_t n_waves = gridDim.x * waves_per_block;
-  for (uint32_t tile = wave; tile * 64 < n; tile += n_waves) {
-    const uint32_t q0 = tile * 64;
-    f32x16 acc[2][2];
+  // input-layer B fragments of a tile (natural k order), zero past n
+  auto load_in = [&](uint32_t tile, half8 (&b)[2][4]) {
 #pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
+    for (int nt = 0; nt < 2; ++nt) {
+      const uint32_t q = tile * 64 + nt * 32 + col;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = zero16();
-    // input layer: B fragments straight from the feature rows (natural k order)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      half8 b[2];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const uint32_t q = q0 + nt * 32 + col;
+      for (int ks = 0; ks < 4; ++ks) {
         if (q < n) {
-          b[nt] = *reinterpret_cast<const half8 *>(feat + (size_t)kFieldPad * q + ks * 16 + h * 8);
+          b[nt][ks] = *reinterpret_cast<const half8 *>(feat + (size_t)kFieldPad * q + ks * 16 + h * 8);
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) b[nt][j] = (_Float16)0.f;
+          for (int j = 0; j < 8; ++j) b[nt][ks][j] = (_Float16)0.f;
         }
       }
+    }
+  };
+  half8 bin[2][4];
+  if (wave * 64 < n) load_in(wave, bin);
+  for (uint32_t tile = wave; tile * 64 < n; tile += n_waves) {
+    const uint32_t q0 = tile * 64;
+    half8 bnext[2][4];
+    // the next tile's features load while this tile's layers run
+    if (MTX_MLP_PREFETCH && (tile + n_waves) * 64 < n) load_in(tile + n_waves, bnext);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt) {
         const half8 a = w[(mt * 4 + ks) * 64 + lane];
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b[nt], acc[mt][nt], 0, 0, 0);
+        for (int nt = 0; nt < 2; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bin[nt][ks], ks == 0 ? zero16() : acc[mt][nt], 0, 0,
+                                                                0);
       }
-    }
     uint32_t base = 8;
     for (uint32_t layer = 0; layer < n_hidden; ++layer, base += 8) {
       half8 bf[2][4];
@@ -135,17 +156,14 @@ __global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const u
 #pragma unroll
           for (int s = 0; s < 2; ++s) bf[nt][2 * mt + s] = leaky_pack(acc[mt][nt], s);
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = zero16();
-#pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
           const half8 a = w[(base + mt * 4 + ks) * 64 + lane];
 #pragma unroll
           for (int nt = 0; nt < 2; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[nt][ks], acc[mt][nt], 0, 0, 0);
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bf[nt][ks], ks == 0 ? zero16() : acc[mt][nt], 0,
+                                                                  0, 0);
         }
     }
     // output layer (3 rows of one 32-row M tile)
@@ -173,6 +191,14 @@ __global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const u
           for (int c = 0; c < 3; ++c) out[3 * (size_t)q + c] = (float)(_Float16)o[nt][c];
         }
       }
+    }
+    if (MTX_MLP_PREFETCH) {
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) bin[nt][ks] = bnext[nt][ks];
+    } else if ((tile + n_waves) * 64 < n) {
+      load_in(tile + n_waves, bin);
     }
   }
 }

@@ -97,13 +97,15 @@ class Field:
 
     # ------------------------------------------------------ CPU reference --
     def mlp_reference(self, feat) -> np.ndarray:
-        """Plain fp32 reference of the network (fp16 weights, activations
-        rounded to fp16 between layers as the device does); test use only."""
+        """Plain fp32 reference of the network (fp16 weights, f32 layer
+        products, activations rounded to fp16 and LeakyReLU(0.01) evaluated
+        in fp16 as the device does); test use only."""
         x = np.asarray(feat, np.float16).astype(np.float32)[:, : self.n_in]
         for i, w in enumerate(self.weights):
             x = x @ w.astype(np.float32).T
             if i < len(self.weights) - 1:
-                x = np.where(x >= 0, x, x * np.float32(0.01)).astype(np.float16).astype(np.float32)
+                h = x.astype(np.float16)
+                x = np.maximum(h, h * np.float16(0.01)).astype(np.float32)
         return x.astype(np.float16).astype(np.float32)
 
     def flops_per_query(self) -> int:
