@@ -98,6 +98,40 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
   return base + prefix;
 }
 
+// Block-level reservation of `cnt` consecutive slots per thread: one
+// device-scope atomic per block (same-address atomics from every wave of
+// the chip serialise at ~90 per microsecond). Returns this thread's first
+// slot; every thread of the block must call it.
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t *counter) {
+  constexpr int W = BLOCK / 64;
+  __shared__ uint32_t wsum[W];
+  __shared__ uint32_t bbase;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t x = cnt;  // inclusive prefix inside the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= (uint32_t)off) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const uint32_t v = wsum[w];
+      wsum[w] = t;
+      t += v;
+    }
+    bbase = t ? atomicAdd(counter, t) : 0u;
+  }
+  __syncthreads();
+  const uint32_t r = bbase + wsum[wave] + x - cnt;
+  __syncthreads();
+  return r;
+}
+
 // Block-level stream compaction into two queues: one device-scope atomic
 // per queue per block step (instead of one per wave) -- same-address atomics
 // from every wave of the chip serialise. All threads of the block must call
@@ -311,6 +345,9 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   bool has_leaf = false;
   int sp = 0;
   const bool spec = !STATS && s.speculate;
+  // more waves than batches: the surplus exits at once (a near-empty queue
+  // would otherwise cost every wave of the grid its claim atomics)
+  if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + s.trace_batch - 1) / s.trace_batch) return;
   uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
   auto pop = [&](int &spr) -> int32_t {
     if (spr == 0) return kTravDone;

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveB
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
     unsigned long long w0 = wave_sum_u64(wi[0]), w1 = wave_sum_u64(wi[1]);
-    if ((threadIdx.x & 63) == 0) {
+    if ((threadIdx.x & 63) == 0 && n) {
       atomicAdd(&b.stats[0], a);
       atomicAdd(&b.stats[1], c);
       atomicAdd(&b.stats[4], n);
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene s, WaveBu
   trace_loop<true>(s, src, b.counters[4 * bounce + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, stack + threadIdx.x, nv, tv, nr);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
-    if ((threadIdx.x & 63) == 0) {
+    if ((threadIdx.x & 63) == 0 && n) {
       atomicAdd(&b.stats[2], a);
       atomicAdd(&b.stats[3], c);
       atomicAdd(&b.stats[5], n);
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     if (io.emit) b.shadow[sslot] = io.rec;
     if constexpr (INT == MTX_INT_NRC) {
       if (p.nrc_cache) {
-        const uint32_t q = wave_append(b.cq_count, io.query);
+        const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);
         if (io.query) {
           b.cq_p[q] = io.qp;
           b.cq_d[q] = io.qd;

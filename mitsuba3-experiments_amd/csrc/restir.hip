@@ -26,6 +26,8 @@ namespace mtxd {
 
 namespace {
 
+constexpr int kRsBlock = 256;  // block size of the k_rs_* kernels (block_reserve)
+
 __device__ __forceinline__ RSample ld_sample(const float4 *b, uint32_t n, uint32_t i) {
   const float4 p0 = b[i], p1 = b[(size_t)n + i], p2 = b[2 * (size_t)n + i], p3 = b[3 * (size_t)n + i],
                p4 = b[4 * (size_t)n + i];
@@ -137,7 +139,7 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
       b.rs_ns[path] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  const uint32_t slot = wave_append(&b.counters[0], enq);
+  const uint32_t slot = block_reserve<kRsBlock>(enq ? 1u : 0u, &b.counters[0]);
   if (enq) b.queue[0][slot] = path;
 }
 
@@ -204,12 +206,9 @@ __device__ __forceinline__ int spatial_max_iter(const RestirBuffers &r, uint32_t
   return (r.max_M_spatial == 0 || (double)M < (double)r.max_M_spatial / 2.0) ? 9 : 3;  // :297
 }
 
-__device__ __forceinline__ void emit_test(const RestirBuffers &r, bool pred, const Ray &ray, uint32_t slot) {
-  const uint32_t o = wave_append(&r.test_count[0], pred);
-  if (pred) {
-    r.test_rays[2 * (size_t)o] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
-    r.test_rays[2 * (size_t)o + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(slot));
-  }
+__device__ __forceinline__ void put_test(const RestirBuffers &r, uint32_t o, const Ray &ray, uint32_t slot) {
+  r.test_rays[2 * (size_t)o] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
+  r.test_rays[2 * (size_t)o + 1] = make_float4(ray.d.x, ray.d.y, ray.d.z, __uint_as_float(slot));
 }
 
 // spatial_resampling, pass 1: the visibility rays of :316-318.
@@ -225,17 +224,23 @@ __global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
   const int max_iter = spatial_max_iter(r, Ms);
   const RSample q = ld_sample(r.cur, r.n, ii);
   const float rad = r.radius[ii];
+  // candidates first, then one block-wide reservation for all of the lane's
+  // tests (test order is irrelevant: results are addressed by slot)
+  uint32_t idx[9], mask = 0;
+#pragma unroll
   for (int k = 0; k < 9; ++k) {
     const Neighbour nb = neighbour(r, p, rng, k, max_iter, rad, x, y, smp, q);
-    const bool act = live && nb.active;
-    Ray ray{v3s(0.f), v3s(0.f), 0.f};
-    if (act) {
-      const float4 xs = r.tres[2 * (size_t)r.n + nb.idx];
-      ray = spawn_ray_to(q.x_v, q.n_v, V3{xs.x, xs.y, xs.z});
-    }
-    emit_test(r, act, ray, 9 * ii + (uint32_t)k);
+    idx[k] = nb.idx;
+    if (live && nb.active) mask |= 1u << k;
     rng.next_1d();  // merge draw (:328)
   }
+  uint32_t o = block_reserve<kRsBlock>((uint32_t)__popc(mask), &r.test_count[0]);
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+    if ((mask >> k) & 1u) {
+      const float4 xs = r.tres[2 * (size_t)r.n + idx[k]];
+      put_test(r, o++, spawn_ray_to(q.x_v, q.n_v, V3{xs.x, xs.y, xs.z}), 9 * ii + (uint32_t)k);
+    }
 }
 
 // spatial_resampling, pass 2: replays the lane's draws with the visibility
@@ -291,13 +296,11 @@ __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
       for (int k = 0; k < 9; ++k) r.qM[10 * (size_t)ii + k] = qM[k] | (((qa >> k) & 1u) << 31);
       r.qM[10 * (size_t)ii + 9] = Z;
     }
+    const uint32_t m = live ? (qa & 0x1ffu) : 0u;
+    uint32_t o = block_reserve<kRsBlock>((uint32_t)__popc(m), &r.test_count[0]);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) {
-      const bool act = live && ((qa >> k) & 1u);
-      Ray ray{v3s(0.f), v3s(0.f), 0.f};
-      if (act) ray = spawn_ray_to(Rn.z.x_s, Rn.z.n_s, qp[k]);
-      emit_test(r, act, ray, 9 * ii + (uint32_t)k);
-    }
+    for (int k = 0; k < 9; ++k)
+      if ((m >> k) & 1u) put_test(r, o++, spawn_ray_to(Rn.z.x_s, Rn.z.n_s, qp[k]), 9 * ii + (uint32_t)k);
   }
 }
 
