@@ -347,7 +347,12 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   const bool spec = !STATS && s.speculate;
   // more waves than batches: the surplus exits at once (a near-empty queue
   // would otherwise cost every wave of the grid its claim atomics)
-  if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + s.trace_batch - 1) / s.trace_batch) return;
+  // Claim size: s.trace_batch, cut down (to >= 64) when the queue is too
+  // short to give every wave of the grid a batch: a small queue then still
+  // spreads over the chip instead of running a few long per-lane chains.
+  const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
+  const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
+  if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + batch - 1) / batch) return;
   uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
   auto pop = [&](int &spr) -> int32_t {
     if (spr == 0) return kTravDone;
@@ -372,12 +377,12 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
             const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
             uint32_t b = 0xffffffffu;
             if (hi > lo) {
-              if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, s.trace_batch);
+              if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
               b = __builtin_amdgcn_readlane(b, leader);
             }
             if (hi > lo && b < hi - lo) {
               base2 = lo + b;
-              got2 = min(s.trace_batch, hi - lo - b);
+              got2 = min(batch, hi - lo - b);
               break;
             }
             if (++tries >= kXcds) {
