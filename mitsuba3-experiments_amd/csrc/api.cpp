@@ -727,6 +727,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   r.nb = nb;
   r.prev_cam = c->rs_prev_cam;
   r.flags = a->restir_flags;
+  r.xcd_remap = c->xcd_claim;
   r.max_M_temporal = a->max_M_temporal;
   r.max_M_spatial = a->max_M_spatial;
   r.initial_radius = a->initial_search_radius;

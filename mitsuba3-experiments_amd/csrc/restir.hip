@@ -28,6 +28,19 @@ namespace {
 
 constexpr int kRsBlock = 256;  // block size of the k_rs_* kernels (block_reserve)
 
+// Lane of this thread with the grid's blocks regrouped so that the blocks
+// sharing an XCD (b, b+8, ...) take one contiguous band of pixels: the
+// neighbour reads of the temporal / spatial passes then hit that XCD's L2.
+// A bijection for any grid size (speed only).
+__device__ __forceinline__ uint32_t rs_thread(const RestirBuffers &r) {
+  uint32_t b = blockIdx.x;
+  if (r.xcd_remap) {
+    const uint32_t n = gridDim.x, q = n / 8u, rem = n % 8u, x = b % 8u, k = b / 8u;
+    b = x * q + min(x, rem) + k;
+  }
+  return b * blockDim.x + threadIdx.x;
+}
+
 __device__ __forceinline__ RSample ld_sample(const float4 *b, uint32_t n, uint32_t i) {
   const float4 p0 = b[i], p1 = b[(size_t)n + i], p2 = b[2 * (size_t)n + i], p3 = b[3 * (size_t)n + i],
                p4 = b[4 * (size_t)n + i];
@@ -159,7 +172,7 @@ __global__ void k_rs_collect(WaveBuffers b, ChunkParams p, RestirBuffers r) {
 
 // temporal_resampling (:365-410)
 __global__ void k_rs_temporal(RestirBuffers r, ChunkParams p) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = rs_thread(r);
   if (t >= r.nb) return;
   const uint32_t i = r.lane0 + t;
   const uint32_t smp = i % p.spp;
@@ -213,7 +226,7 @@ __device__ __forceinline__ void put_test(const RestirBuffers &r, uint32_t o, con
 
 // spatial_resampling, pass 1: the visibility rays of :316-318.
 __global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = rs_thread(r);
   const bool live = t < r.nb;
   const uint32_t ii = r.lane0 + (live ? t : 0u);
   const uint32_t smp = ii % p.spp;
@@ -247,7 +260,7 @@ __global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
 // results, merges (:320-332), and either finishes W (:350) or emits the
 // bias-correction rays (:334-346).
 __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = rs_thread(r);
   const bool live = t < r.nb;
   const uint32_t ii = r.lane0 + (live ? t : 0u);
   const uint32_t smp = ii % p.spp;

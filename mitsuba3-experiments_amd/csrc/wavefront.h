@@ -129,6 +129,7 @@ struct RestirBuffers {
   uint32_t nb;     // lanes this call computes (row band)
   mtx_camera prev_cam;
   uint32_t flags, max_M_temporal, max_M_spatial;
+  uint32_t xcd_remap;  // k_rs_* neighbour passes: XCD-banded block order
   float initial_radius, minimal_radius;
   uint32_t frame;
 };
