@@ -32,8 +32,10 @@ namespace mtxd {
 
 namespace {
 
-constexpr int kScanBlock = 256;
-constexpr int kScanItems = 16;
+// Large tiles: the tile ticket is one same-address atomic per tile (~90 per
+// microsecond chip-wide), so 16K-element tiles keep it off the critical path.
+constexpr int kScanBlock = 512;
+constexpr int kScanItems = 32;
 constexpr uint32_t kScanTile = kScanBlock * kScanItems;
 
 
@@ -61,22 +63,34 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_u32(const uint32_t *__restr
   __syncthreads();
   const uint32_t tile = s_tile;
   unsigned long long *status = ws + 2;
-  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
-  uint32_t v[kScanItems];
-  if (base + kScanItems <= n) {
-    const uint4 *p = reinterpret_cast<const uint4 *>(in + base);
+  const uint64_t tile0 = (uint64_t)tile * kScanTile;
+  const bool full = tile0 + kScanTile <= n;
+  // Coalesced 16-B loads (consecutive lanes, consecutive 16 B), transposed
+  // through LDS to kScanItems consecutive items per thread. One padding
+  // dword per kScanItems keeps the blocked accesses conflict-free.
+  __shared__ uint32_t s_x[kScanTile + kScanTile / kScanItems];
 #pragma unroll
-    for (int q = 0; q < kScanItems / 4; ++q) {
-      uint4 x = p[q];
-      v[4 * q] = x.x;
-      v[4 * q + 1] = x.y;
-      v[4 * q + 2] = x.z;
-      v[4 * q + 3] = x.w;
+  for (int q = 0; q < kScanItems / 4; ++q) {
+    const uint32_t i = (uint32_t)q * (kScanBlock * 4) + tid * 4;
+    uint4 x;
+    if (full) {
+      x = *reinterpret_cast<const uint4 *>(in + tile0 + i);
+    } else {
+      x.x = tile0 + i < n ? in[tile0 + i] : 0u;
+      x.y = tile0 + i + 1 < n ? in[tile0 + i + 1] : 0u;
+      x.z = tile0 + i + 2 < n ? in[tile0 + i + 2] : 0u;
+      x.w = tile0 + i + 3 < n ? in[tile0 + i + 3] : 0u;
     }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) v[k] = (base + k < n) ? in[base + k] : 0u;
+    const uint32_t pi = i + i / kScanItems;
+    s_x[pi] = x.x;
+    s_x[pi + 1] = x.y;
+    s_x[pi + 2] = x.z;
+    s_x[pi + 3] = x.w;
   }
+  __syncthreads();
+  uint32_t v[kScanItems];
+#pragma unroll
+  for (int k = 0; k < kScanItems; ++k) v[k] = s_x[tid * (kScanItems + 1) + k];
 #pragma unroll
   for (int k = 1; k < kScanItems; ++k) v[k] += v[k - 1];
   const uint32_t total = v[kScanItems - 1];
@@ -134,17 +148,24 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_u32(const uint32_t *__restr
   }
   __syncthreads();
   const uint32_t off = s_prefix + wave_prefix + thread_excl;
-  uint32_t o[kScanItems];
+  // results back through LDS (each thread rewrites only its own slots, so
+  // no barrier is needed before the writes), then coalesced 16-B stores
 #pragma unroll
-  for (int k = 0; k < kScanItems; ++k) o[k] = (inclusive ? v[k] : (k ? v[k - 1] : 0u)) + off;
-  if (base + kScanItems <= n) {
-    uint4 *p = reinterpret_cast<uint4 *>(out + base);
+  for (int k = 0; k < kScanItems; ++k) s_x[tid * (kScanItems + 1) + k] = (inclusive ? v[k] : (k ? v[k - 1] : 0u)) + off;
+  __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kScanItems / 4; ++q) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k)
-      if (base + k < n) out[base + k] = o[k];
+  for (int q = 0; q < kScanItems / 4; ++q) {
+    const uint32_t i = (uint32_t)q * (kScanBlock * 4) + tid * 4;
+    const uint32_t pi = i + i / kScanItems;
+    const uint4 x = make_uint4(s_x[pi], s_x[pi + 1], s_x[pi + 2], s_x[pi + 3]);
+    if (full) {
+      *reinterpret_cast<uint4 *>(out + tile0 + i) = x;
+    } else {
+      if (tile0 + i < n) out[tile0 + i] = x.x;
+      if (tile0 + i + 1 < n) out[tile0 + i + 1] = x.y;
+      if (tile0 + i + 2 < n) out[tile0 + i + 2] = x.z;
+      if (tile0 + i + 3 < n) out[tile0 + i + 3] = x.w;
+    }
   }
 }
 

@@ -1,0 +1,103 @@
+"""Edge cases of the GPU primitives (prefix_sum.py, hashgrid.py,
+reductions.py): empty inputs, sizes one past a power of two, a single hot
+target / cell, hash collisions, points on the bounding-box maximum, invalid
+arguments. HIP results are compared with the oracle or exact numpy."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_prefix_sum_empty_and_sizes():
+    from mtx import primitives
+
+    assert primitives.prefix_sum(np.zeros(0, np.uint32)).size == 0
+    assert primitives.prefix_sum(np.zeros(0, np.float32)).size == 0
+    for n in (2, 63, 64, 65, (1 << 20) + 1):
+        x = np.arange(n, dtype=np.uint32) % 7
+        assert np.array_equal(primitives.prefix_sum(x), np.cumsum(x, dtype=np.uint64).astype(np.uint32))
+
+
+def test_prefix_sum_f32_power_of_two_boundaries(oracle):
+    from mtx import primitives
+
+    for n in (2047, 2048, 2049, (1 << 20) + 1):
+        x = oracle.rng_stream(3, 0, n, 1)[:, 0].copy()
+        assert np.array_equal(primitives.prefix_sum(x), oracle.prefix_sum_f32_hs(x))
+
+
+def test_prefix_sum_rejects_exclusive_f32_and_other_dtypes():
+    from mtx import primitives
+
+    with pytest.raises(ValueError):
+        primitives.prefix_sum(np.ones(4, np.float32), inclusive=False)
+    with pytest.raises(TypeError):
+        primitives.prefix_sum(np.ones(4, np.int64))
+
+
+def _grid_vs_oracle(oracle, p, res, n_cells):
+    from mtx import primitives
+
+    n = p.shape[1]
+    g = primitives.HashGrid(p, res, n_cells)
+    cell, size, off, idx = oracle.hashgrid(p, res, n_cells)
+    assert np.array_equal(g.cell, cell)
+    assert np.array_equal(g.cell_size, size)
+    assert np.array_equal(g.cell_offset, off)
+    order = np.lexsort((g.sample_idx, np.repeat(np.arange(n_cells), size)))
+    assert np.array_equal(g.sample_idx[order], idx)
+    assert int(size.sum()) == n
+    return g
+
+
+def test_hashgrid_single_cell_collisions_and_bbox_max(oracle):
+    rng = np.random.default_rng(11)
+    p = rng.random((3, 5000), dtype=np.float32)
+    # every sample in one cell (maximal contention on one counter)
+    g = _grid_vs_oracle(oracle, p, 100, 1)
+    assert g.cell_size.tolist() == [5000]
+    # fewer cells than occupied grid cells: hash collisions
+    _grid_vs_oracle(oracle, p, 100, 97)
+    # samples exactly on the bounding-box maximum (q = resolution)
+    p[:, :100] = p.max()
+    _grid_vs_oracle(oracle, p, 16, 4096)
+
+
+def test_hashgrid_rejects_empty():
+    from mtx import MtxError, primitives
+
+    with pytest.raises(MtxError):
+        primitives.HashGrid(np.zeros((3, 0), np.float32), 10, 4)
+    with pytest.raises(MtxError):
+        primitives.HashGrid(np.random.default_rng(0).random((3, 10), dtype=np.float32), 10, 0)
+
+
+@pytest.mark.parametrize("op", ["add", "min", "max"])
+def test_scatter_reduce_one_hot_target(oracle, op):
+    """Every value into target 0: one long ordered fold (ascending index)."""
+    from mtx import primitives
+
+    rng = np.random.default_rng(12)
+    nv = 1 << 16
+    val = rng.random(nv, dtype=np.float32) - 0.5
+    idx = np.zeros(nv, np.uint32)
+    tgt = rng.random(8, dtype=np.float32)
+    o = {"add": 0, "min": 1, "max": 2}[op]
+    g = primitives.scatter_reduce_with(op, tgt, val, idx)
+    assert np.array_equal(g, oracle.scatter_reduce(o, tgt, val, idx))
+    assert np.array_equal(g[1:], tgt[1:])
+    if op == "add":  # left fold in ascending index order, as the oracle
+        acc = np.float32(tgt[0])
+        for v in val:
+            acc = np.float32(acc + v)
+        assert g[0] == acc
+
+
+def test_scatter_reduce_empty_and_invalid():
+    from mtx import MtxError, primitives
+
+    t = np.arange(5, dtype=np.float32)
+    assert np.array_equal(primitives.scatter_reduce_with("add", t, np.zeros(0, np.float32),
+                                                         np.zeros(0, np.uint32)), t)
+    with pytest.raises(MtxError):
+        primitives.scatter_reduce_with("add", t, np.ones(3, np.float32), np.array([0, 5, 1], np.uint32))
