@@ -264,12 +264,16 @@ def prims(args):
     c = cpu_time(lambda: oracle.prefix_sum_f32_hs(xf[: 1 << 22]))
     passes = int(np.floor(np.log2(n))) + 1
     ach = 8 * n / (ms / 1e3) / 1e9
+    hs_bytes = 12 * n * (1 + max(0, passes - 11))
     _line("prefix_sum f32 Hillis-Steele Gelem/sec (prefix_sum.py:9-36), n=2^24", n / (ms / 1e3) / 1e9, "Gelem/s", 3,
           1, ms, {"workload": f"{passes} Hillis-Steele passes in the reference's summation order (bit-exact)",
                   "n": n},
           {"bound": "hbm", "kernel": "scan_f32_hs (LDS passes + global passes)", "achieved": round(ach, 1),
            "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
-           "alg_bytes_per_launch": 8 * n, "note": "algorithmic bytes = one read + one write per element"},
+           "alg_bytes_per_launch": 8 * n, "note": "algorithmic bytes = one read + one write per element",
+           "hs_pass_bytes_per_launch": hs_bytes, "hs_pass_GBs": round(hs_bytes / (ms / 1e3) / 1e9, 1),
+           "hs_note": "bytes the reference's Hillis-Steele order needs with 11 passes fused in LDS "
+                      "(12 B/element) + one 2-read/1-write pass per remaining level (12 B/element each)"},
           {"value": round((1 << 22) / c / 1e9, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
            "sample": f"2^22 elements ({c:.2f} s), oracle orc_prefix_sum_f32_hs"})
     # hash grid, n = 2^24 points, res 100, n_cells = n (hashgrid.py:16-84)
