@@ -82,14 +82,33 @@ MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint
   const float ax = wide_scale(eb) * r.idir.x, bx = (ox - r.o.x) * r.idir.x;
   const float ay = wide_scale(eb >> 8) * r.idir.y, by = (oy - r.o.y) * r.idir.y;
   const float az = wide_scale(eb >> 16) * r.idir.z, bz = (oz - r.o.z) * r.idir.z;
+  // near / far bound of each axis from the direction's sign: fma(q, a, b)
+  // is monotonic in q, so this equals min / max of the two planes (NaN
+  // planes of a zero direction component are ignored either way)
+  const bool nx_ = r.idir.x < 0.f, ny_ = r.idir.y < 0.f, nz_ = r.idir.z < 0.f;
+  const uint32_t qnx = nx_ ? qhx : qlx, qfx = nx_ ? qlx : qhx;
+  const uint32_t qny = ny_ ? qhy : qly, qfy = ny_ ? qly : qhy;
+  const uint32_t qnz = nz_ ? qhz : qlz, qfz = nz_ ? qlz : qhz;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int sh = 8 * k;
-    const float lx = fmaf((float)((qlx >> sh) & 255u), ax, bx), hx = fmaf((float)((qhx >> sh) & 255u), ax, bx);
-    const float ly = fmaf((float)((qly >> sh) & 255u), ay, by), hy = fmaf((float)((qhy >> sh) & 255u), ay, by);
-    const float lz = fmaf((float)((qlz >> sh) & 255u), az, bz), hz = fmaf((float)((qhz >> sh) & 255u), az, bz);
-    const float tmin = fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fmaxf(fminf(lz, hz), 0.f));
-    const float tmax = fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fminf(fmaxf(lz, hz), tfar));
+#ifdef MTX_DEVICE_COMPILE
+    // the same six fmas, issued as three packed v_pk_fma_f32
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v tx = __builtin_elementwise_fma(f2v{(float)((qnx >> sh) & 255u), (float)((qfx >> sh) & 255u)},
+                                             f2v{ax, ax}, f2v{bx, bx});
+    const f2v ty = __builtin_elementwise_fma(f2v{(float)((qny >> sh) & 255u), (float)((qfy >> sh) & 255u)},
+                                             f2v{ay, ay}, f2v{by, by});
+    const f2v tz = __builtin_elementwise_fma(f2v{(float)((qnz >> sh) & 255u), (float)((qfz >> sh) & 255u)},
+                                             f2v{az, az}, f2v{bz, bz});
+    const float nx = tx.x, fx = tx.y, ny = ty.x, fy = ty.y, nz = tz.x, fz = tz.y;
+#else
+    const float nx = fmaf((float)((qnx >> sh) & 255u), ax, bx), fx = fmaf((float)((qfx >> sh) & 255u), ax, bx);
+    const float ny = fmaf((float)((qny >> sh) & 255u), ay, by), fy = fmaf((float)((qfy >> sh) & 255u), ay, by);
+    const float nz = fmaf((float)((qnz >> sh) & 255u), az, bz), fz = fmaf((float)((qfz >> sh) & 255u), az, bz);
+#endif
+    const float tmin = fmaxf(fmaxf(fmaxf(nx, ny), nz), 0.f);
+    const float tmax = fminf(fminf(fminf(fx, fy), fz), tfar);
     const bool hit = k < nch && tmin <= tmax;
     key[k] = hit ? ((f2u(tmin) & 0x7ffffffcu) | (uint32_t)k) : (0x7f800000u | (uint32_t)k);
   }
