@@ -47,6 +47,9 @@ def parse():
                         "SURVEY §8 configurations on one GPU (C3 PSSMLT, C4 ReSTIR GI, C5 NRC, primitives)")
     p.add_argument("--iterations", type=int, default=20, help="PSSMLT Metropolis iterations (C3 short variant)")
     p.add_argument("--frames", type=int, default=10, help="ReSTIR GI timed frames")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="--workload pssmlt/pssmltpath/restir with N>1 ranks: nccl (RCCL) or gloo (host-staged; "
+                        "lets several ranks share one GPU in a rehearsal)")
     return p.parse_args()
 
 

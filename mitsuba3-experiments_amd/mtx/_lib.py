@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 from . import _abi
 
@@ -125,9 +126,14 @@ _contexts: dict[int, Context] = {}
 
 
 def context(device: int | None = None) -> Context:
-    """Process-wide context per device (default: LOCAL_RANK or 0)."""
+    """Process-wide context per device (default: torch's current device once
+    torch has initialised HIP, else LOCAL_RANK or 0)."""
     if device is None:
-        device = int(os.environ.get("LOCAL_RANK", "0"))
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            device = torch.cuda.current_device()
+        else:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
     if device not in _contexts:
         _contexts[device] = Context(device)
     return _contexts[device]

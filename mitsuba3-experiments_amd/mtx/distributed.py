@@ -37,6 +37,20 @@ def _to_tensor(film, like_device=None):
     return film
 
 
+def _host_staged(group=None) -> bool:
+    """gloo moves host memory only: device tensors are staged through the
+    host (used when several ranks share one GPU, e.g. a 1-GPU rehearsal of
+    the N>1 path). RCCL (backend "nccl") sends device memory directly."""
+    import torch.distributed as dist
+
+    return dist.get_backend(group) == "gloo"
+
+
+def _comm(t, group=None):
+    """The tensor handed to the collective: `t` itself, or its host copy."""
+    return t.cpu() if (t.is_cuda and _host_staged(group)) else t
+
+
 def gather_sum(film, group=None):
     """Sum of every rank's film in rank order, returned on rank 0 (None elsewhere).
     `film` is a torch tensor (device for nccl, cpu for gloo) or numpy array."""
@@ -44,15 +58,16 @@ def gather_sum(film, group=None):
     import torch.distributed as dist
 
     t = _to_tensor(film)
+    c = _comm(t, group)
     world = dist.get_world_size(group)
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t, group=group)
+    parts = [torch.empty_like(c) for _ in range(world)]
+    dist.all_gather(parts, c, group=group)
     if dist.get_rank(group) != 0:
         return None
-    total = torch.zeros_like(t)
+    total = torch.zeros_like(c)
     for p in parts:
         total.add_(p)
-    return total
+    return total.to(t.device)
 
 
 def gather_bands(band, y0: int, y1: int, height: int, group=None):
@@ -64,6 +79,8 @@ def gather_bands(band, y0: int, y1: int, height: int, group=None):
     world = dist.get_world_size(group)
     W2 = t.shape[1]
     maxrows = max(b1 - b0 for b0, b1 in row_bands(height, world)) + 2
+    dev = t.device
+    t = _comm(t, group)
     buf = torch.zeros((maxrows, W2, t.shape[2]), dtype=t.dtype, device=t.device)
     buf[: t.shape[0]] = t
     meta = torch.tensor([y0, y1], dtype=torch.int64, device=t.device)
@@ -77,7 +94,7 @@ def gather_bands(band, y0: int, y1: int, height: int, group=None):
     for p, m in zip(parts, metas):
         a, b = int(m[0]), int(m[1])
         full[a: b + 2] += p[: b - a + 2]
-    return full
+    return full.to(dev)
 
 
 def render_sharded(render, height: int, spp: int, mode: str = "samples", group=None):
@@ -124,6 +141,7 @@ def exchange_halos(export_rows, import_rows, y0: int, y1: int, height: int, halo
     export_rows(which, row0, nrows) -> contiguous tensor; import_rows(which,
     row0, tensor). which in ('sample', 'temporal'). Bands must be at least
     `halo` rows tall so the neighbours own every halo row."""
+    import torch
     import torch.distributed as dist
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
@@ -133,22 +151,20 @@ def exchange_halos(export_rows, import_rows, y0: int, y1: int, height: int, halo
     for which in ("sample", "temporal"):
         ops, recvs = [], []
         if rank > 0 and send_up[1]:
-            ops.append(dist.P2POp(dist.isend, export_rows(which, *send_up), rank - 1, group))
+            ops.append(dist.P2POp(dist.isend, _comm(export_rows(which, *send_up), group), rank - 1, group))
         if rank < world - 1 and send_down[1]:
-            ops.append(dist.P2POp(dist.isend, export_rows(which, *send_down), rank + 1, group))
-        if rank > 0 and recv_up[1]:
-            t = export_rows(which, recv_up[0], recv_up[1]).clone()  # shape / dtype / device template
-            ops.append(dist.P2POp(dist.irecv, t, rank - 1, group))
-            recvs.append((recv_up[0], t))
-        if rank < world - 1 and recv_down[1]:
-            t = export_rows(which, recv_down[0], recv_down[1]).clone()
-            ops.append(dist.P2POp(dist.irecv, t, rank + 1, group))
-            recvs.append((recv_down[0], t))
+            ops.append(dist.P2POp(dist.isend, _comm(export_rows(which, *send_down), group), rank + 1, group))
+        for peer, (row0, nrows) in ((rank - 1, recv_up), (rank + 1, recv_down)):
+            if 0 <= peer < world and nrows:
+                tmpl = export_rows(which, row0, nrows)  # shape / dtype / device template
+                t = torch.empty_like(_comm(tmpl, group))
+                ops.append(dist.P2POp(dist.irecv, t, peer, group))
+                recvs.append((row0, t, tmpl.device))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        for row0, t in recvs:
-            import_rows(which, row0, t)
+        for row0, t, dev in recvs:
+            import_rows(which, row0, t.to(dev))
 
 
 def restir_band_frame(integ, scene, seed: int, y0: int, y1: int, exchange, spp: int = 1, out=None, ctx=None):

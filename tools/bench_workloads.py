@@ -60,51 +60,130 @@ def _sync():
     torch.cuda.synchronize()
 
 
+# ------------------------------------------------------- ranks (C3, C4) --
+class Ranks:
+    """One process per GPU (torchrun env) or a single process. C3 and C4 are
+    strong-scaling row bands of one film: each rank owns rows
+    [y0, y1); the timed region is bracketed by barrier + synchronize and the
+    elapsed time is the max over ranks. backend "nccl" is RCCL; "gloo"
+    (--backend gloo) stages device tensors through the host so that several
+    ranks can share one GPU in a rehearsal."""
+
+    def __init__(self, args, height):
+        import torch
+        import torch.distributed as dist
+
+        from mtx import distributed
+
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(self.dev)
+        if self.world > 1:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.dev))
+            else:
+                dist.init_process_group(args.backend)
+        self.y0, self.y1 = distributed.row_bands(height, self.world)[self.rank]
+
+    def barrier(self):
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_elapsed(self, t):
+        import torch
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return t
+        x = torch.tensor([t], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            x = x.cuda()
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        return float(x.item())
+
+    def gather(self, band, height):
+        from mtx import distributed
+
+        if self.world > 1:
+            distributed.gather_bands(band, self.y0, self.y1, height)
+
+    def parallelism(self):
+        return f"row bands x{self.world}" + (", RCCL all_gather of band films" if self.world > 1 else "")
+
+    def close(self):
+        import torch.distributed as dist
+
+        if self.world > 1:
+            dist.destroy_process_group()
+
+
+def _sum_stats(a, b):
+    return dict(b) if a is None else {x: a[x] + b[x] for x in b}
+
+
 # --------------------------------------------------------------- PSSMLT (C3) --
 def pssmlt(args, with_nee=False):
     import binding as oracle
     import torch
     from mtx import PssmltPath, PssmltSimple, scene
 
-    torch.cuda.set_device(0)
     sc = scene.bedroom(1280, 720)
+    rk = Ranks(args, sc.height)
+    y0, y1 = rk.y0, rk.y1
     spp, it = args.spp, args.iterations
     cls = PssmltPath if with_nee else PssmltSimple
     integ = cls({"iterations": it})
-    film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
-    cls({"iterations": 1}).render_film(sc, seed=99, spp=spp, out=film)  # allocation warm-up
-    _sync()
+    film = torch.empty((y1 - y0 + 2, sc.width + 2, 4), dtype=torch.float32, device=f"cuda:{rk.dev}")
+    cls({"iterations": 1}).render_film(sc, seed=99, spp=spp, y0=y0, y1=y1, out=film, device=rk.dev)  # warm-up
+    rk.barrier()
     t0 = time.perf_counter()
     st = None
     for k in range(args.steps):
-        st = integ.render_film(sc, seed=k, spp=spp, out=film, stats=True)[1]
-    _sync()
-    dt = (time.perf_counter() - t0) / args.steps
-    cnt = integ.render_film(sc, seed=0, spp=spp, out=film, stats=True, counters=True)[1]
+        st = _sum_stats(st, integ.render_film(sc, seed=k, spp=spp, y0=y0, y1=y1, out=film, stats=True,
+                                              device=rk.dev)[1])
+        rk.gather(film, sc.height)
+    rk.barrier()
+    dt = rk.max_elapsed(time.perf_counter() - t0) / args.steps
+    st = {x: v / args.steps for x, v in st.items()}
+    cnt = integ.render_film(sc, seed=0, spp=spp, y0=y0, y1=y1, out=film, stats=True, counters=True,
+                            device=rk.dev)[1]
     chains = sc.width * sc.height * spp
-    # CPU: the oracle on a band of rows, same chains per pixel and iterations
-    oracle.build()
-    a1 = integ.render_args(sc, 0, spp, 0, 1)
-    t1 = time.perf_counter()
-    oracle.pssmlt_render(sc, a1, it)
-    c1 = time.perf_counter() - t1
-    rows = max(1, min(sc.height, int(args.cpu_seconds / max(c1, 1e-3))))
-    a = integ.render_args(sc, 0, spp, 0, rows)
-    t1 = time.perf_counter()
-    oracle.pssmlt_render(sc, a, it)
-    c = time.perf_counter() - t1
-    cpu = {"value": round(sc.width * rows * spp * it / c / 1e6, 4), "unit": "Mchain-iterations/s",
-           "cores": _threads(), "kind": "port",
-           "sample": f"{rows} of {sc.height} rows x {sc.width} px x {spp} chains x {it} iterations ({c:.1f} s); "
-                     "oracle/oracle.cpp orc_pssmlt_render (OpenMP)"}
-    script = "pssmltpath.py (NEE + MIS)" if with_nee else "pssmltsimple.py"
-    _line(f"PSSMLT{'-path' if with_nee else ''} Mchain-iterations/sec on bedroom@1280x720, {spp} chains/pixel (C3)",
-          chains * it / dt / 1e6, "Mchain-iterations/s", args.steps, 1, dt * 1e3,
-          {"workload": f"{script} + pssmlt.py render, {it} iterations (large step every 50, aggregate "
-                       f"i%50>40), max_depth 16, rr_depth 4, {chains} chains", "chains": chains, "iterations": it},
-          _trace_roofline(cnt, st["trace_ms"], "step"), cpu,
-          {"kernels_ms_per_step": {"trace_closest": round(st["trace_ms"], 3), "shade": round(st["shade_ms"], 3),
-                                   "trace_shadow": round(st["shadow_ms"], 3), "other": round(st["other_ms"], 3)}})
+    cpu = None
+    if rk.world == 1:
+        # CPU: the oracle on a band of rows, same chains per pixel and iterations
+        oracle.build()
+        a1 = integ.render_args(sc, 0, spp, 0, 1)
+        t1 = time.perf_counter()
+        oracle.pssmlt_render(sc, a1, it)
+        c1 = time.perf_counter() - t1
+        rows = max(1, min(sc.height, int(args.cpu_seconds / max(c1, 1e-3))))
+        a = integ.render_args(sc, 0, spp, 0, rows)
+        t1 = time.perf_counter()
+        oracle.pssmlt_render(sc, a, it)
+        c = time.perf_counter() - t1
+        cpu = {"value": round(sc.width * rows * spp * it / c / 1e6, 4), "unit": "Mchain-iterations/s",
+               "cores": _threads(), "kind": "port",
+               "sample": f"{rows} of {sc.height} rows x {sc.width} px x {spp} chains x {it} iterations ({c:.1f} s); "
+                         "oracle/oracle.cpp orc_pssmlt_render (OpenMP)"}
+    if rk.rank == 0:
+        script = "pssmltpath.py (NEE + MIS)" if with_nee else "pssmltsimple.py"
+        _line(f"PSSMLT{'-path' if with_nee else ''} Mchain-iterations/sec on bedroom@1280x720, {spp} chains/pixel (C3)",
+              chains * it / dt / 1e6, "Mchain-iterations/s", args.steps, 1, dt * 1e3,
+              {"workload": f"{script} + pssmlt.py render, {it} iterations (large step every 50, aggregate "
+                           f"i%50>40), max_depth 16, rr_depth 4, {chains} chains", "chains": chains,
+               "iterations": it, "parallelism": rk.parallelism()},
+              _trace_roofline(cnt, st["trace_ms"], "step"), cpu,
+              {"kernels_ms_per_step": {"trace_closest": round(st["trace_ms"], 3), "shade": round(st["shade_ms"], 3),
+                                       "trace_shadow": round(st["shadow_ms"], 3), "other": round(st["other_ms"], 3)},
+               "n_gpus": rk.world, "scaling": "strong" if rk.world > 1 else "weak"})
+    rk.close()
 
 
 # -------------------------------------------------------------- ReSTIR (C4) --
@@ -115,50 +194,76 @@ RESTIR_C4 = {"jacobian": False, "bias_correction": False, "bsdf_sampling": True,
 def restir(args):
     import binding as oracle
     import torch
-    from mtx import RestirIntegrator, scene
+    from mtx import RestirIntegrator, distributed, scene
+    from mtx._lib import context
 
-    torch.cuda.set_device(0)
     sc = scene.bedroom(1920, 1080)
+    rk = Ranks(args, sc.height)
+    y0, y1 = rk.y0, rk.y1
     integ = RestirIntegrator(RESTIR_C4)
-    film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
+    film = torch.empty((y1 - y0 + 2, sc.width + 2, 4), dtype=torch.float32, device=f"cuda:{rk.dev}")
+    halo = distributed.restir_halo(integ)
+    ctx = context(rk.dev)
+    ex, im = distributed.device_row_io(integ, sc, 1, ctx)
+
+    def frame(seed, stats=False, counters=False):
+        """One frame of this rank's band: stage A, halo swap, stage B, film
+        gather (a single-rank frame is one call)."""
+        if rk.world == 1:
+            r = integ.render_film(sc, seed=seed, spp=1, out=film, stats=stats, counters=counters, ctx=ctx)
+            return r[1] if stats else None
+        a = integ.render_film(sc, seed=seed, spp=1, y0=y0, y1=y1, stage="A", stats=stats, counters=counters,
+                              ctx=ctx)
+        distributed.exchange_halos(ex, im, y0, y1, sc.height, halo)
+        b = integ.render_film(sc, seed=seed, spp=1, y0=y0, y1=y1, stage="B", out=film, stats=stats,
+                              counters=counters, ctx=ctx)
+        rk.gather(film, sc.height)
+        return _sum_stats(a[1], b[1]) if stats else None
+
     W = max(1, args.warmup)
     for k in range(W):
-        integ.render_film(sc, seed=k, spp=1, out=film)
-    _sync()
+        frame(k)
+    rk.barrier()
     agg = None
     t0 = time.perf_counter()
     for k in range(args.frames):
-        st = integ.render_film(sc, seed=W + k, spp=1, out=film, stats=True)[1]
-        agg = dict(st) if agg is None else {x: agg[x] + st[x] for x in st}
-    _sync()
-    dt = (time.perf_counter() - t0) / args.frames
-    cnt = integ.render_film(sc, seed=W + args.frames, spp=1, out=film, stats=True, counters=True)[1]
+        agg = _sum_stats(agg, frame(W + k, stats=True))
+    rk.barrier()
+    dt = rk.max_elapsed(time.perf_counter() - t0) / args.frames
+    cnt = frame(W + args.frames, stats=True, counters=True)
     px = sc.width * sc.height
-    # CPU: the oracle's frame loop on a reduced film
-    oracle.build()
-    small = sc.with_film(240, 135)
-    orc = oracle.RestirOracle(small)
-    ci = RestirIntegrator(RESTIR_C4)
-    t1 = time.perf_counter()
-    nf = 0
-    while nf < 3 and (nf == 0 or time.perf_counter() - t1 < args.cpu_seconds):
-        ci.n = nf
-        orc.frame(small, ci.render_args(small, nf, 1))
-        nf += 1
-    c = time.perf_counter() - t1
-    cpu = {"value": round(240 * 135 * nf / c / 1e6, 4), "unit": "Mpixel-frames/s", "cores": _threads(),
-           "kind": "port", "sample": f"{nf} frames at 240x135 ({c:.1f} s), same properties; oracle/oracle.cpp "
-                                     "orc_restir_frame (OpenMP)"}
-    _line("ReSTIR GI Mpixel-frames/sec on bedroom@1920x1080 (C4, 1 GPU)", px / dt / 1e6, "Mpixel-frames/s",
-          args.frames, W, dt * 1e3,
-          {"workload": "restirgi.py render per frame: initial sample + path-mis secondary path (max_depth 8), "
-                       "temporal + 9-tap spatial reuse with visibility, props restirgi.py:610-620",
-           "frames_per_s": round(1.0 / dt, 2), "pixels": px},
-          _trace_roofline(cnt, agg["trace_ms"] / args.frames, "frame"), cpu,
-          {"kernels_ms_per_frame": {"trace_closest": round(agg["trace_ms"] / args.frames, 3),
-                                    "trace_shadow_and_visibility": round(agg["shadow_ms"] / args.frames, 3),
-                                    "shade": round(agg["shade_ms"] / args.frames, 3),
-                                    "other": round(agg["other_ms"] / args.frames, 3)}})
+    cpu = None
+    if rk.world == 1:
+        # CPU: the oracle's frame loop on a reduced film
+        oracle.build()
+        small = sc.with_film(240, 135)
+        orc = oracle.RestirOracle(small)
+        ci = RestirIntegrator(RESTIR_C4)
+        t1 = time.perf_counter()
+        nf = 0
+        while nf < 3 and (nf == 0 or time.perf_counter() - t1 < args.cpu_seconds):
+            ci.n = nf
+            orc.frame(small, ci.render_args(small, nf, 1))
+            nf += 1
+        c = time.perf_counter() - t1
+        cpu = {"value": round(240 * 135 * nf / c / 1e6, 4), "unit": "Mpixel-frames/s", "cores": _threads(),
+               "kind": "port", "sample": f"{nf} frames at 240x135 ({c:.1f} s), same properties; oracle/oracle.cpp "
+                                         "orc_restir_frame (OpenMP)"}
+    if rk.rank == 0:
+        _line(f"ReSTIR GI Mpixel-frames/sec on bedroom@1920x1080 (C4, {rk.world} GPU)", px / dt / 1e6,
+              "Mpixel-frames/s", args.frames, W, dt * 1e3,
+              {"workload": "restirgi.py render per frame: initial sample + path-mis secondary path (max_depth 8), "
+                           "temporal + 9-tap spatial reuse with visibility, props restirgi.py:610-620",
+               "frames_per_s": round(1.0 / dt, 2), "pixels": px,
+               "parallelism": rk.parallelism() + (f", P2P halo of {halo} rows (samples + temporal reservoirs)"
+                                                  if rk.world > 1 else "")},
+              _trace_roofline(cnt, agg["trace_ms"] / args.frames, "frame"), cpu,
+              {"kernels_ms_per_frame": {"trace_closest": round(agg["trace_ms"] / args.frames, 3),
+                                        "trace_shadow_and_visibility": round(agg["shadow_ms"] / args.frames, 3),
+                                        "shade": round(agg["shade_ms"] / args.frames, 3),
+                                        "other": round(agg["other_ms"] / args.frames, 3)},
+               "n_gpus": rk.world, "scaling": "strong" if rk.world > 1 else "weak"})
+    rk.close()
 
 
 # ----------------------------------------------------------------- NRC (C5) --
