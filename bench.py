@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--chunk", type=int, default=0, help="wavefront paths per chunk (0 = library default)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU time of the baseline sample")
-    p.add_argument("--workload", default="path_mis", choices=["path_mis", "pssmlt", "pssmltpath", "restir", "nrc", "prims", "field"],
+    p.add_argument("--workload", default="path_mis", choices=["path_mis", "pssmlt", "pssmltpath", "restir", "nrc", "prims", "field", "nerad"],
                    help="path_mis = the driver's headline line (default); the others measure the remaining "
                         "SURVEY §8 configurations on one GPU (C3 PSSMLT, C4 ReSTIR GI, C5 NRC, primitives)")
     p.add_argument("--iterations", type=int, default=20, help="PSSMLT Metropolis iterations (C3 short variant)")

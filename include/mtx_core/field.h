@@ -129,6 +129,28 @@ MTX_HD void field_hashgrid_level(const FieldEncoding &e, V3 pn, uint32_t l, uint
   out[0] = float_to_half_bits(acc0);
 }
 
+// Corner table indices (within level l) and trilinear weights of one point:
+// the same arithmetic as field_hashgrid_level (the backward pass scatters
+// d(feature) * weight to these entries).
+MTX_HD void field_level_corners(const FieldEncoding &e, V3 pn, uint32_t l, uint32_t idx[8], float w[8]) {
+  const uint32_t T = 1u << e.log2_table;
+  const float scale = e.level_scale[l];
+  const uint32_t res = e.level_res[l];
+  const bool dense = (uint64_t)res * res * res <= (uint64_t)T;
+  const float px = fmaf(pn.x, scale, 0.5f), py = fmaf(pn.y, scale, 0.5f), pz = fmaf(pn.z, scale, 0.5f);
+  const float fx = floorf(px), fy = floorf(py), fz = floorf(pz);
+  const float tx = px - fx, ty = py - fy, tz = pz - fz;
+  const uint32_t gx = (uint32_t)(int32_t)fx, gy = (uint32_t)(int32_t)fy, gz = (uint32_t)(int32_t)fz;
+  for (uint32_t c = 0; c < 8; ++c) {
+    const uint32_t bx = c & 1u, by = (c >> 1) & 1u, bz = (c >> 2) & 1u;
+    const uint32_t x = gx + bx, y = gy + by, z = gz + bz;
+    const uint32_t i = dense ? x + y * res + z * res * res
+                             : (x * kFieldPrimes[0]) ^ (y * kFieldPrimes[1]) ^ (z * kFieldPrimes[2]);
+    idx[c] = i & (T - 1u);
+    w[c] = (bx ? tx : 1.f - tx) * (by ? ty : 1.f - ty) * (bz ? tz : 1.f - tz);
+  }
+}
+
 // All levels of one point: out[n_features * l + k].
 MTX_HD void field_hashgrid(const FieldEncoding &e, V3 pn, uint16_t *out) {
   for (uint32_t l = 0; l < e.n_levels; ++l) field_hashgrid_level(e, pn, l, out + e.n_features * l);

@@ -97,6 +97,22 @@ struct mtx_ctx {
   mtx::FieldEncoding field{};
   uint32_t field_hidden = 0;
   bool has_field = false;
+  DevBuf field_w16;  // plain fp16 weights (training forward / backward)
+  uint32_t field_n_in = 0, field_n_w = 0;
+  uint64_t field_n_table = 0;  // fp16 table entries
+  // field training (mtx_field_train_init): fp32 master parameters [table |
+  // weights], Adam moments, gradients, per-batch scratch
+  DevBuf tr_p, tr_m, tr_v, tr_g, tr_wpart, tr_loss, tr_out, tr_dfeat, tr_feat, tr_flag, tr_target;
+  mtx_field_opt opt{};
+  bool training = false;
+  uint32_t adam_t = 0, good_steps = 0;
+  float scale = 1.f;
+  // neural radiosity surface tables (mtx_nerad_upload) and batch buffers
+  DevBuf nr_shape_pmf, nr_shape_cdf, nr_tri_off, nr_tri_pmf, nr_tri_cdf, nr_tri_prim, nr_dists;
+  mtx::NeradTables nr{};
+  bool has_nerad = false;
+  uint32_t scene_n_shapes = 0;
+  DevBuf nr_lhs, nr_qp, nr_qd, nr_Lrhs, nr_lanes;
   DevBuf nodes, tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
@@ -191,7 +207,11 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
-                    &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5};
+                    &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5,
+                    &c->field_w16, &c->tr_p, &c->tr_m, &c->tr_v, &c->tr_g, &c->tr_wpart, &c->tr_loss, &c->tr_out,
+                    &c->tr_dfeat, &c->tr_feat, &c->tr_flag, &c->tr_target, &c->nr_shape_pmf, &c->nr_shape_cdf,
+                    &c->nr_tri_off, &c->nr_tri_pmf, &c->nr_tri_cdf, &c->nr_tri_prim, &c->nr_dists, &c->nr_lhs,
+                    &c->nr_qp, &c->nr_qd, &c->nr_Lrhs, &c->nr_lanes};
   for (DevBuf *b : bufs) dfree(*b);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
   for (hipEvent_t ev : c->prim_ev)
@@ -295,6 +315,8 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   if ((rc = upload(c->vnormal, d->vnormal, d->vnormal ? 3ull * d->n_verts : 0, st))) return rc;
   if ((rc = upload(c->vuv, d->vuv, d->vuv ? 2ull * d->n_verts : 0, st))) return rc;
   if ((rc = upload(c->shapes, d->shapes, d->n_shapes, st))) return rc;
+  c->scene_n_shapes = d->n_shapes;
+  c->has_nerad = false;  // surface tables belong to the previous scene
   if ((rc = upload(c->materials, d->materials, d->n_materials, st))) return rc;
   if ((rc = upload(c->emitters, d->emitters, d->n_emitters, st))) return rc;
   if ((rc = upload(c->textures, d->textures, d->n_textures, st))) return rc;
@@ -574,15 +596,21 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
   const mtxd::DevScene &s = c->scene;
   // an NRC cache query needs one more trace + shade after the last segment
   const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1) + (p.nrc_cache ? 1u : 0u);
+  // nerad RHS lanes start at their surface point (no bounce-0 trace) and
+  // trace NEE rays at that point only
+  const bool nerad = p.integrator == MTX_INT_NERAD_RHS;
   for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
-    hipEvent_t e = tm.begin(0);
-    mtxd::launch_trace_closest(s, b, bounce, p.stats, c->trace_grid, c->stream);
-    tm.end(0, e);
-    ++*n_trace;
+    hipEvent_t e;
+    if (!(nerad && bounce == 0)) {
+      e = tm.begin(0);
+      mtxd::launch_trace_closest(s, b, bounce, p.stats, c->trace_grid, c->stream);
+      tm.end(0, e);
+      ++*n_trace;
+    }
     e = tm.begin(2);
     mtxd::launch_shade(s, b, p, bounce, c->shade_grid, c->stream);
     tm.end(2, e);
-    if (p.integrator != MTX_INT_PSSMLT_SIMPLE) {  // PSSMLT traces no NEE rays
+    if (p.integrator != MTX_INT_PSSMLT_SIMPLE && !(nerad && bounce > 0)) {  // PSSMLT traces no NEE rays
       e = tm.begin(1);
       mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
       tm.end(1, e);
@@ -1122,7 +1150,13 @@ int mtx_field_upload(mtx_ctx *c, const mtx_field_desc *f) {
   std::vector<uint16_t> frag((size_t)n_frag * 64 * 8);
   mtxd::field_prepack(f->weights, f->n_in, f->n_hidden, frag.data());
   if ((rc = upload(c->field_frag, frag.data(), frag.size(), c->stream))) return rc;
+  const uint32_t n_w = 64u * f->n_in + f->n_hidden * 4096u + 3u * 64u;
+  if ((rc = upload(c->field_w16, f->weights, n_w, c->stream))) return rc;
   HIP_TRY(hipStreamSynchronize(c->stream));
+  c->field_n_in = f->n_in;
+  c->field_n_w = n_w;
+  c->field_n_table = table_halfs;
+  c->training = false;  // a new field: mtx_field_train_init starts over
   mtx::FieldEncoding &e = c->field;
   e.table = (const uint16_t *)c->field_table.p;
   e.n_levels = f->n_levels;
@@ -1357,6 +1391,417 @@ int mtx_scatter_reduce_f32(mtx_ctx *c, int op, float *target, uint64_t n_target,
   HIP_TRY(hipMemcpyAsync(target, c->s0.p, 4 * n_target, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   prim_timer_read(c);
+  return MTX_OK;
+}
+
+}  // extern "C"
+
+// ============================================================================
+// Radiance-field training and neural radiosity samples (nerad.py:121-375)
+// ============================================================================
+static int train_check(mtx_ctx *c) {
+  if (!c || !c->has_field) {
+    mtx_set_error("no radiance field uploaded (mtx_field_upload)");
+    return MTX_E_ARG;
+  }
+  if (!c->training) {
+    mtx_set_error("field training not initialised (mtx_field_train_init)");
+    return MTX_E_ARG;
+  }
+  return MTX_OK;
+}
+
+// Forward + backward of the field for n points (queries qp / qd on the
+// device, targets 3n floats on the device): gradients of scale * loss in
+// tr_g = [table | weights], network outputs in tr_out, loss (unscaled) on
+// the host.
+static int field_backward(mtx_ctx *c, const float4 *qp, const float4 *qd, const float *target, uint32_t n,
+                          float scale, double *loss) {
+  int rc;
+  const uint32_t LF = c->field.n_levels * c->field.n_features;
+  const uint32_t blocks = (n + 63) / 64;
+  const uint64_t n_params = c->field_n_table + c->field_n_w;
+  if ((rc = dalloc(c->tr_feat, 128ull * n))) return rc;
+  if ((rc = dalloc(c->tr_out, 12ull * n))) return rc;
+  if ((rc = dalloc(c->tr_loss, 4ull * blocks))) return rc;
+  if ((rc = dalloc(c->tr_wpart, 4ull * blocks * c->field_n_w))) return rc;
+  if ((rc = dalloc(c->tr_dfeat, 4ull * n * LF))) return rc;
+  if ((rc = dalloc(c->tr_g, 4 * n_params))) return rc;
+  mtxd::field_encode(c->field, qp, qd, nullptr, n, (uint16_t *)c->tr_feat.p, c->stream);
+  HIP_TRY(hipMemsetAsync(c->tr_g.p, 0, 4 * c->field_n_table, c->stream));
+  float *g = (float *)c->tr_g.p;
+  mtxd::field_train_launch((const uint16_t *)c->tr_feat.p, n, (const uint16_t *)c->field_w16.p, c->field_n_in,
+                           c->field_hidden, target, (float)(2.0 * scale / (3.0 * n)), (float *)c->tr_out.p,
+                           (float *)c->tr_loss.p, (float *)c->tr_wpart.p, g + c->field_n_table,
+                           (float *)c->tr_dfeat.p, LF, c->stream);
+  mtxd::field_encode_bwd_launch(c->field, qp, n, (const float *)c->tr_dfeat.p, g, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (loss) {
+    std::vector<float> part(blocks);
+    HIP_TRY(hipMemcpyAsync(part.data(), c->tr_loss.p, 4ull * blocks, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    double sq = 0.0;
+    for (float x : part) sq += x;
+    *loss = sq / (3.0 * n);
+  }
+  return MTX_OK;
+}
+
+// GradScaler.step(opt): finite check of the scaled gradients, Adam on the
+// unscaled ones (skipped on inf / NaN), scale update; the fp16 table and
+// weights are rewritten by the Adam kernel and re-packed for the MFMA MLP.
+static int field_opt_step(mtx_ctx *c, mtx_train_stats *st) {
+  const uint64_t n_params = c->field_n_table + c->field_n_w;
+  int rc;
+  if ((rc = dalloc(c->tr_flag, 16))) return rc;
+  HIP_TRY(hipMemsetAsync(c->tr_flag.p, 0, 4, c->stream));
+  mtxd::grad_check_launch((const float *)c->tr_g.p, n_params, (uint32_t *)c->tr_flag.p, c->stream);
+  uint32_t found = 0;
+  HIP_TRY(hipMemcpyAsync(&found, c->tr_flag.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const mtx_field_opt &o = c->opt;
+  if (!found) {
+    ++c->adam_t;
+    const double t = c->adam_t;
+    const float lr_t = (float)(o.lr * std::sqrt(1.0 - std::pow((double)o.beta_2, t)) /
+                               (1.0 - std::pow((double)o.beta_1, t)));
+    mtxd::adam_launch((float *)c->tr_p.p, (float *)c->tr_m.p, (float *)c->tr_v.p, (const float *)c->tr_g.p, n_params,
+                      lr_t, o.beta_1, o.beta_2, o.epsilon, 1.f / c->scale, (const uint32_t *)c->tr_flag.p,
+                      (uint16_t *)c->field_table.p, c->field_n_table, (uint16_t *)c->field_w16.p, c->stream);
+    mtxd::field_prepack_launch((const uint16_t *)c->field_w16.p, c->field_n_in, c->field_hidden,
+                               (uint16_t *)c->field_frag.p, c->stream);
+    HIP_TRY(hipGetLastError());
+    if (++c->good_steps >= o.growth_interval) {
+      c->scale *= o.growth_factor;
+      c->good_steps = 0;
+    }
+  } else {
+    c->scale *= o.backoff_factor;
+    c->good_steps = 0;
+  }
+  if (st) {
+    st->found_inf = found;
+    st->scale = c->scale;
+    st->step = c->adam_t;
+  }
+  return MTX_OK;
+}
+
+struct PhaseTimer {
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipStream_t st;
+  explicit PhaseTimer(hipStream_t s) : st(s) {
+    for (auto &e : ev) hipEventCreate(&e);
+  }
+  ~PhaseTimer() {
+    for (auto &e : ev) hipEventDestroy(e);
+  }
+  void mark(int i) { hipEventRecord(ev[i], st); }
+  double ms(int a, int b) {
+    float t = 0.f;
+    hipEventElapsedTime(&t, ev[a], ev[b]);
+    return t;
+  }
+};
+
+static int nerad_check(mtx_ctx *c, const mtx_nerad_args *a, bool need_field = true) {
+  if (!c || !a) {
+    mtx_set_error("null context or args");
+    return MTX_E_ARG;
+  }
+  if (!c->has_scene || !c->has_nerad) {
+    mtx_set_error("nerad: upload a scene and its surface tables (mtx_nerad_upload) first");
+    return MTX_E_NOSCENE;
+  }
+  if (need_field && !c->has_field) {
+    mtx_set_error("nerad: no radiance field uploaded (mtx_field_upload)");
+    return MTX_E_ARG;
+  }
+  if (a->batch == 0 || a->M == 0 || (uint64_t)a->batch * a->M >= (1ull << 31)) {
+    mtx_set_error("nerad: bad batch %u / M %u", a->batch, a->M);
+    return MTX_E_ARG;
+  }
+  return MTX_OK;
+}
+
+static int nerad_lhs_dev(mtx_ctx *c, const mtx_nerad_args *a) {
+  int rc;
+  if ((rc = dalloc(c->nr_lhs, 48ull * a->batch))) return rc;
+  if ((rc = dalloc(c->nr_qp, 16ull * a->batch))) return rc;
+  if ((rc = dalloc(c->nr_qd, 16ull * a->batch))) return rc;
+  mtxd::launch_nerad_lhs(c->scene, c->nr, a->lhs_seed, a->batch, (float4 *)c->nr_lhs.p, (float4 *)c->nr_qp.p,
+                         (float4 *)c->nr_qd.p, c->stream);
+  HIP_TRY(hipGetLastError());
+  return MTX_OK;
+}
+
+// sample_rhs (nerad.py:175-238) for the points in nr_lhs: L_rhs in nr_Lrhs.
+static int nerad_rhs_dev(mtx_ctx *c, const mtx_nerad_args *a, float *lanes_dev, uint32_t *queries,
+                         mtx_train_stats *st = nullptr) {
+  int rc;
+  const uint32_t n = a->batch * a->M;
+  const uint32_t bounces = 12;  // first vertex, its BSDF hit, <= 10 next_smooth_si traces (:150)
+  if ((rc = ensure_wavefront(c, n, bounces))) return rc;
+  if ((rc = ensure_cache(c, n))) return rc;
+  if ((rc = dalloc(c->nr_Lrhs, 12ull * a->batch))) return rc;
+  mtxd::WaveBuffers b = buffers(c);
+  mtxd::ChunkParams p{};
+  p.integrator = MTX_INT_NERAD_RHS;
+  p.max_depth = bounces;
+  p.seed = a->rhs_seed;
+  p.spp = p.spp_total = 1;
+  p.n_paths = n;
+  p.n_px = n;
+  const bool counters = st && (a->flags & 1u);
+  p.stats = counters ? 1u : 0u;
+  HIP_TRY(reset_counters(b, bounces, c->stream));
+  HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
+  if (counters) HIP_TRY(hipMemsetAsync(b.stats, 0, 64, c->stream));
+  mtxd::launch_nerad_raygen(b, p, (const float4 *)c->nr_lhs.p, a->M, c->stream);
+  Timer tm{c, st != nullptr};
+  uint64_t nt = 0, ns = 0;
+  run_bounces(c, b, p, tm, &nt, &ns);
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, n, (uint16_t *)c->f_feat.p, c->stream);
+  mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, n, c->field_frag.p, c->field_hidden,
+                  (float *)c->f_out.p, c->n_cu, c->stream);
+  mtxd::launch_nerad_apply(b, (const float *)c->f_out.p, n, c->stream);
+  mtxd::launch_nerad_mean(b, a->batch, a->M, (float *)c->nr_Lrhs.p, lanes_dev, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (queries) HIP_TRY(hipMemcpyAsync(queries, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream));
+  if (st) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    st->ms_trace = tm.total(0);
+    if (counters) {
+      unsigned long long h[8];
+      HIP_TRY(hipMemcpy(h, b.stats, 64, hipMemcpyDeviceToHost));
+      st->nodes_closest = h[0];
+      st->tris_closest = h[1];
+      st->rays_closest = h[4];
+    }
+  }
+  return MTX_OK;
+}
+
+extern "C" {
+
+int mtx_field_train_init(mtx_ctx *c, const mtx_field_opt *opt) {
+  if (!c || !opt || !c->has_field) {
+    mtx_set_error("mtx_field_train_init: null argument or no field uploaded");
+    return MTX_E_ARG;
+  }
+  if (!(opt->lr > 0.f) || !(opt->init_scale > 0.f) || opt->growth_interval == 0) {
+    mtx_set_error("mtx_field_train_init: bad optimiser settings");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  const uint64_t n_params = c->field_n_table + c->field_n_w;
+  int rc;
+  if ((rc = dalloc(c->tr_p, 4 * n_params))) return rc;
+  if ((rc = dalloc(c->tr_m, 4 * n_params))) return rc;
+  if ((rc = dalloc(c->tr_v, 4 * n_params))) return rc;
+  mtxd::half_to_float_launch((const uint16_t *)c->field_table.p, c->field_n_table, (float *)c->tr_p.p, c->stream);
+  mtxd::half_to_float_launch((const uint16_t *)c->field_w16.p, c->field_n_w, (float *)c->tr_p.p + c->field_n_table,
+                             c->stream);
+  HIP_TRY(hipMemsetAsync(c->tr_m.p, 0, 4 * n_params, c->stream));
+  HIP_TRY(hipMemsetAsync(c->tr_v.p, 0, 4 * n_params, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->opt = *opt;
+  c->adam_t = 0;
+  c->good_steps = 0;
+  c->scale = opt->init_scale;
+  c->training = true;
+  return MTX_OK;
+}
+
+int mtx_field_grad(mtx_ctx *c, uint64_t n, const float *p, const float *wi, const float *target, float scale,
+                   float *out, double *loss, float *grad_table, float *grad_weights) {
+  int rc = field_check(c, n);
+  if (rc) return rc;
+  if (n == 0 || !p || !wi || !target) {
+    mtx_set_error("mtx_field_grad: empty batch or null input");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = field_stage_queries(c, n, p, wi))) return rc;
+  if ((rc = upload(c->tr_target, target, 3 * n, c->stream))) return rc;
+  if ((rc = field_backward(c, (const float4 *)c->fq_p.p, (const float4 *)c->fq_d.p, (const float *)c->tr_target.p,
+                           (uint32_t)n, scale, loss)))
+    return rc;
+  const float *g = (const float *)c->tr_g.p;
+  if (out) HIP_TRY(hipMemcpyAsync(out, c->tr_out.p, 12 * n, hipMemcpyDeviceToHost, c->stream));
+  if (grad_table) HIP_TRY(hipMemcpyAsync(grad_table, g, 4 * c->field_n_table, hipMemcpyDeviceToHost, c->stream));
+  if (grad_weights)
+    HIP_TRY(hipMemcpyAsync(grad_weights, g + c->field_n_table, 4ull * c->field_n_w, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+int mtx_field_train_step(mtx_ctx *c, uint64_t n, const float *p, const float *wi, const float *target,
+                         mtx_train_stats *stats) {
+  int rc = field_check(c, n);
+  if (rc || (rc = train_check(c))) return rc;
+  if (n == 0 || !p || !wi || !target) {
+    mtx_set_error("mtx_field_train_step: empty batch or null input");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = field_stage_queries(c, n, p, wi))) return rc;
+  if ((rc = upload(c->tr_target, target, 3 * n, c->stream))) return rc;
+  double loss = 0.0;
+  if ((rc = field_backward(c, (const float4 *)c->fq_p.p, (const float4 *)c->fq_d.p, (const float *)c->tr_target.p,
+                           (uint32_t)n, c->scale, &loss)))
+    return rc;
+  mtx_train_stats st{};
+  st.loss = loss;
+  if ((rc = field_opt_step(c, &st))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (stats) *stats = st;
+  return MTX_OK;
+}
+
+int mtx_field_params(mtx_ctx *c, float *table, float *weights, float *m, float *v) {
+  int rc = train_check(c);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  const uint64_t nt = c->field_n_table, nw = c->field_n_w;
+  if (table) HIP_TRY(hipMemcpy(table, c->tr_p.p, 4 * nt, hipMemcpyDeviceToHost));
+  if (weights) HIP_TRY(hipMemcpy(weights, (const float *)c->tr_p.p + nt, 4 * nw, hipMemcpyDeviceToHost));
+  if (m) HIP_TRY(hipMemcpy(m, c->tr_m.p, 4 * (nt + nw), hipMemcpyDeviceToHost));
+  if (v) HIP_TRY(hipMemcpy(v, c->tr_v.p, 4 * (nt + nw), hipMemcpyDeviceToHost));
+  return MTX_OK;
+}
+
+int mtx_nerad_upload(mtx_ctx *c, const mtx_nerad_tables *t) {
+  if (!c || !t || !c->has_scene) {
+    mtx_set_error("mtx_nerad_upload: null argument or no scene");
+    return MTX_E_ARG;
+  }
+  const uint32_t S = t->n_shapes, E = t->n_entries;
+  if (S != c->scene_n_shapes || !t->shape_pmf || !t->shape_cdf || !t->tri_off || !t->tri_pmf || !t->tri_cdf ||
+      !t->tri_prim || !t->tri_sum || !t->tri_norm || !t->tri_valid || t->tri_off[S] != E ||
+      t->shape_valid[0] > t->shape_valid[1] || t->shape_valid[1] >= S) {
+    mtx_set_error("mtx_nerad_upload: tables do not match the scene (%u shapes)", c->scene_n_shapes);
+    return MTX_E_ARG;
+  }
+  for (uint32_t k = 0; k < S; ++k) {
+    const uint32_t cnt = t->tri_off[k + 1] - t->tri_off[k];
+    if (t->tri_off[k + 1] < t->tri_off[k] || cnt == 0 || t->tri_valid[2 * k] > t->tri_valid[2 * k + 1] ||
+        t->tri_valid[2 * k + 1] >= cnt) {
+      mtx_set_error("mtx_nerad_upload: bad triangle range of shape %u", k);
+      return MTX_E_ARG;
+    }
+  }
+  for (uint32_t i = 0; i < E; ++i)
+    if (t->tri_prim[i] >= c->scene.n_tris) {
+      mtx_set_error("mtx_nerad_upload: tri_prim[%u] out of range", i);
+      return MTX_E_ARG;
+    }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = upload(c->nr_shape_pmf, t->shape_pmf, S, c->stream))) return rc;
+  if ((rc = upload(c->nr_shape_cdf, t->shape_cdf, S, c->stream))) return rc;
+  if ((rc = upload(c->nr_tri_off, t->tri_off, S + 1, c->stream))) return rc;
+  if ((rc = upload(c->nr_tri_pmf, t->tri_pmf, E, c->stream))) return rc;
+  if ((rc = upload(c->nr_tri_cdf, t->tri_cdf, E, c->stream))) return rc;
+  if ((rc = upload(c->nr_tri_prim, t->tri_prim, E, c->stream))) return rc;
+  std::vector<mtx::DiscreteDist> d(S);
+  for (uint32_t k = 0; k < S; ++k) {
+    const uint32_t off = t->tri_off[k];
+    d[k].pmf = (const float *)c->nr_tri_pmf.p + off;
+    d[k].cdf = (const float *)c->nr_tri_cdf.p + off;
+    d[k].n = t->tri_off[k + 1] - off;
+    d[k].valid_lo = t->tri_valid[2 * k];
+    d[k].valid_hi = t->tri_valid[2 * k + 1];
+    d[k].sum = t->tri_sum[k];
+    d[k].normalization = t->tri_norm[k];
+  }
+  if ((rc = upload(c->nr_dists, d.data(), S, c->stream))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  mtx::NeradTables &n = c->nr;
+  n.shape.pmf = (const float *)c->nr_shape_pmf.p;
+  n.shape.cdf = (const float *)c->nr_shape_cdf.p;
+  n.shape.n = S;
+  n.shape.valid_lo = t->shape_valid[0];
+  n.shape.valid_hi = t->shape_valid[1];
+  n.shape.sum = t->shape_sum;
+  n.shape.normalization = t->shape_norm;
+  n.tri_dist = (const mtx::DiscreteDist *)c->nr_dists.p;
+  n.tri_off = (const uint32_t *)c->nr_tri_off.p;
+  n.tri_prim = (const uint32_t *)c->nr_tri_prim.p;
+  c->has_nerad = true;
+  return MTX_OK;
+}
+
+int mtx_nerad_lhs(mtx_ctx *c, const mtx_nerad_args *a, float *out) {
+  int rc = nerad_check(c, a, false);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = nerad_lhs_dev(c, a))) return rc;
+  if (out) {
+    std::vector<float> raw(12ull * a->batch);
+    HIP_TRY(hipMemcpyAsync(raw.data(), c->nr_lhs.p, 48ull * a->batch, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (uint64_t i = 0; i < a->batch; ++i) {
+      const float *r = raw.data() + 12 * i;
+      float *o = out + 9 * i;
+      o[0] = r[3];  // prim bits
+      o[1] = r[7];
+      o[2] = r[8];
+      o[3] = r[0];
+      o[4] = r[1];
+      o[5] = r[2];
+      o[6] = r[4];
+      o[7] = r[5];
+      o[8] = r[6];
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+int mtx_nerad_rhs(mtx_ctx *c, const mtx_nerad_args *a, float *L_rhs, float *lanes) {
+  int rc = nerad_check(c, a);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  if ((rc = nerad_lhs_dev(c, a))) return rc;
+  float *lanes_dev = nullptr;
+  if (lanes) {
+    if ((rc = dalloc(c->nr_lanes, 12ull * a->batch * a->M))) return rc;
+    lanes_dev = (float *)c->nr_lanes.p;
+  }
+  if ((rc = nerad_rhs_dev(c, a, lanes_dev, nullptr))) return rc;
+  if (L_rhs) HIP_TRY(hipMemcpyAsync(L_rhs, c->nr_Lrhs.p, 12ull * a->batch, hipMemcpyDeviceToHost, c->stream));
+  if (lanes) HIP_TRY(hipMemcpyAsync(lanes, lanes_dev, 12ull * a->batch * a->M, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return MTX_OK;
+}
+
+int mtx_nerad_step(mtx_ctx *c, const mtx_nerad_args *a, mtx_train_stats *stats) {
+  int rc = nerad_check(c, a);
+  if (rc || (rc = train_check(c))) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  PhaseTimer pt(c->stream);
+  pt.mark(0);
+  if ((rc = nerad_lhs_dev(c, a))) return rc;  // si_lhs = isampler.sample(sampler_lhs) (:338)
+  pt.mark(1);
+  uint32_t nq = 0;
+  mtx_train_stats st{};
+  if ((rc = nerad_rhs_dev(c, a, nullptr, &nq, &st))) return rc;  // L_rhs = sample_rhs(si_lhs) (:341)
+  pt.mark(2);
+  double loss = 0.0;  // L_lhs = Field(si_lhs), loss, backward (:340-344)
+  if ((rc = field_backward(c, (const float4 *)c->nr_qp.p, (const float4 *)c->nr_qd.p, (const float *)c->nr_Lrhs.p,
+                           a->batch, c->scale, &loss)))
+    return rc;
+  st.loss = loss;
+  if ((rc = field_opt_step(c, &st))) return rc;  // scaler.step(opt) (:345)
+  pt.mark(3);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  st.rhs_queries = nq;
+  st.ms_lhs = pt.ms(0, 1);
+  st.ms_rhs = pt.ms(1, 2);
+  st.ms_train = pt.ms(2, 3);
+  st.ms_total = pt.ms(0, 3);
+  if (stats) *stats = st;
   return MTX_OK;
 }
 

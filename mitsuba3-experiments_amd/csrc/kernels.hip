@@ -583,6 +583,105 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   return active;
 }
 
+// nerad.py:175-238 Integrator.sample_rhs, one lane = one of the M samples of a
+// training point (nerad.py:178-180 dr.repeat). Bounce 0 is the sampled
+// surface point itself (hit record written by k_nerad_raygen): NEE with a
+// visibility test (:193-197, mis_weight of mitsuba.ad.integrators.common =
+// variant B) and a BSDF sample (:201-203). Bounce 1 is the BSDF ray's hit:
+// f = mis_weight(bs.pdf, emitter pdf) * bsdf_weight (:205-214), then
+// next_smooth_si (:131-166) follows delta / null vertices (bounces 2..11,
+// f2 in prev.xyz). At the stop vertex: f *= f2, zero if invalid (:216-219);
+// a valid vertex becomes a field query (Le kept in prev.xyz), L += f * (Le +
+// field) is applied after the field evaluation (k_nerad_apply, :222-226).
+// State: thr.xyz = f, L.w = bs.pdf of bounce 0, prev.xyz = si.p (bounce 0)
+// then f2, misc.w = chain depth.
+__device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
+                                            uint32_t bounce, uint32_t path, ShadeIO &io) {
+  const float4 rd = b.ray_d[path], Lr = b.L[path], pv = b.prev[path], th = b.thr[path];
+  const uint4 mi = b.misc[path];
+  const float4 h = b.hit[path];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  uint32_t depth = mi.w & 0xffffu;
+  const V3 ray_d = V3{rd.x, rd.y, rd.z};
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
+  io.emit = false;
+  io.query = false;
+  V3 L = V3{Lr.x, Lr.y, Lr.z};
+  V3 f = V3{th.x, th.y, th.z};
+  V3 f2 = V3{pv.x, pv.y, pv.z};
+  if (bounce == 0) {
+    const mtx_material mat = sv.materials[si.material];
+    DirectionSample ds;
+    const V3 em = sample_emitter_direction(sv, si.p, rng.next_2d(), &ds);  // :193
+    V3 val;
+    float pdf;
+    bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :194
+    const float mis = mis_weight_b(ds.pdf, pdf);
+    make_shadow(io, si, ds, path, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :196
+    const float s1 = rng.next_1d();
+    const V2 s2 = rng.next_2d();
+    BSDFSample bs;
+    const V3 w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);  // :201-203
+    const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));   // :205
+    b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+    b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+    b.thr[path] = make_float4(w.x, w.y, w.z, 1.f);
+    b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
+    b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
+    b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+    return true;  // traced unconditionally (:206)
+  }
+  if (bounce == 1) {
+    // emitter pdf of the BSDF-sampled hit (:210-213), f (:214)
+    const V3 prev_p = f2;
+    const V3 rel = si.p - prev_p;
+    const float dist = norm(rel);
+    const float em_pdf = pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    f = f * mis_weight_b(Lr.w, em_pdf);
+    f2 = v3s(1.f);
+  }
+  // next_smooth_si (:131-166): sample at this vertex; continue while delta
+  BSDFSample bs;
+  bs.type = 0;
+  V3 w = v3s(0.f);
+  const float s1 = rng.next_1d();
+  const V2 s2 = rng.next_2d();
+  if (si.valid) {
+    const mtx_material mat = sv.materials[si.material];
+    w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+  }
+  if (bounce >= 2) depth += 1;  // :162
+  const bool chain = (bs.type & BF_DELTA) != 0 && depth < 10;
+  if (chain) {
+    f2 = f2 * w;  // :157
+    const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
+    b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+    b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+    b.thr[path] = make_float4(f.x, f.y, f.z, 1.f);
+    b.prev[path] = make_float4(f2.x, f2.y, f2.z, 0.f);
+    b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
+    return true;
+  }
+  // stop vertex (:216-226)
+  f = f * f2;
+  if (!si.valid) f = f * 0.f;
+  const V3 le = emitter_eval(sv, si.emitter, si.wi);
+  if (si.valid) {
+    io.query = true;
+    const V3 wi = to_world(si.sh, si.wi);  // Field.__call__ wi (nerad.py:100)
+    io.qp = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
+    io.qd = make_float4(wi.x, wi.y, wi.z, 0.f);
+    io.qt = make_float4(f.x, f.y, f.z, __uint_as_float(path));
+    b.prev[path] = make_float4(le.x, le.y, le.z, 0.f);
+  } else {
+    L = L + f * (le + v3s(0.f));
+    b.L[path] = make_float4(L.x, L.y, L.z, Lr.w);
+  }
+  return false;
+}
+
 template <int INT>
 __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
@@ -618,6 +717,8 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
         cont = shade_pssmlt(s, sv, b, p, path);
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
         cont = shade_pssmlt_path(s, sv, b, p, path, io);
+      else if constexpr (INT == MTX_INT_NERAD_RHS)
+        cont = shade_nerad(s, sv, b, bounce, path, io);
       else
         cont = shade_path<INT>(s, sv, b, p, bounce, path, io);
     }
@@ -625,8 +726,8 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, sh_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path;
     if (io.emit) b.shadow[sslot] = io.rec;
-    if constexpr (INT == MTX_INT_NRC) {
-      if (p.nrc_cache) {
+    if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS) {
+      if (INT == MTX_INT_NERAD_RHS || p.nrc_cache) {
         const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);
         if (io.query) {
           b.cq_p[q] = io.qp;
@@ -990,6 +1091,9 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
       break;
     case MTX_INT_PSSMLT_PATH:
       hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
+    case MTX_INT_NERAD_RHS:
+      hipLaunchKernelGGL(k_shade<MTX_INT_NERAD_RHS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
     default:
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);

@@ -32,4 +32,18 @@ int field_encode(const mtx::FieldEncoding &e, const float4 *qp, const float4 *qd
 int field_mlp(const uint16_t *feat, const uint32_t *count, uint32_t n_max, const void *wfrag, uint32_t n_hidden,
               float *out, int n_cu, hipStream_t st);
 
+// Radiance-field training (field_train.hip)
+size_t field_train_lds(uint32_t n_hidden);
+int field_train_launch(const uint16_t *feat, uint32_t n, const uint16_t *w16, uint32_t n_in, uint32_t n_hidden,
+                       const float *target, float gscale, float *out, float *wave_loss, float *wpart, float *grad_w,
+                       float *dfeat, uint32_t n_grid, hipStream_t st);
+void field_encode_bwd_launch(const mtx::FieldEncoding &e, const float4 *qp, uint32_t n, const float *dfeat,
+                             float *gtab, hipStream_t st);
+void grad_check_launch(const float *g, uint64_t n, uint32_t *flag, hipStream_t st);
+void adam_launch(float *p, float *m, float *v, const float *g, uint64_t n, float lr_t, float b1, float b2, float eps,
+                 float inv_scale, const uint32_t *flag, uint16_t *tab16, uint64_t n_tab, uint16_t *w16,
+                 hipStream_t st);
+void half_to_float_launch(const uint16_t *h, uint64_t n, float *f, hipStream_t st);
+void field_prepack_launch(const uint16_t *w16, uint32_t n_in, uint32_t n_hidden, uint16_t *frag, hipStream_t st);
+
 }  // namespace mtxd

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 2
+MTX_ABI_VERSION = 3
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -23,6 +23,7 @@ MTX_INT_NRC = 3
 MTX_INT_PSSMLT_SIMPLE = 4
 MTX_INT_RESTIR_GI = 5
 MTX_INT_PSSMLT_PATH = 6
+MTX_INT_NERAD_RHS = 7
 
 MTX_RESTIR_BIAS_CORRECTION = 1
 MTX_RESTIR_JACOBIAN = 2
@@ -191,6 +192,64 @@ class Stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class FieldOpt(C.Structure):
+    _fields_ = [
+        ("lr", C.c_float),
+        ("beta_1", C.c_float),
+        ("beta_2", C.c_float),
+        ("epsilon", C.c_float),
+        ("init_scale", C.c_float),
+        ("growth_factor", C.c_float),
+        ("backoff_factor", C.c_float),
+        ("growth_interval", C.c_uint32),
+    ]
+
+
+class TrainStats(C.Structure):
+    _fields_ = [
+        ("loss", C.c_double),
+        ("scale", C.c_float),
+        ("found_inf", C.c_uint32),
+        ("step", C.c_uint32),
+        ("rhs_queries", C.c_uint32),
+        ("ms_lhs", C.c_double),
+        ("ms_rhs", C.c_double),
+        ("ms_train", C.c_double),
+        ("ms_total", C.c_double),
+        ("ms_trace", C.c_double),
+        ("rays_closest", C.c_uint64),
+        ("nodes_closest", C.c_uint64),
+        ("tris_closest", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class NeradTables(C.Structure):
+    _fields_ = [
+        ("n_shapes", C.c_uint32),
+        ("n_entries", C.c_uint32),
+        ("shape_pmf", C.c_void_p),
+        ("shape_cdf", C.c_void_p),
+        ("shape_sum", C.c_float),
+        ("shape_norm", C.c_float),
+        ("shape_valid", C.c_uint32 * 2),
+        ("tri_off", C.c_void_p),
+        ("tri_pmf", C.c_void_p),
+        ("tri_cdf", C.c_void_p),
+        ("tri_prim", C.c_void_p),
+        ("tri_sum", C.c_void_p),
+        ("tri_norm", C.c_void_p),
+        ("tri_valid", C.c_void_p),
+    ]
+
+
+class NeradArgs(C.Structure):
+    _fields_ = [("lhs_seed", C.c_uint32), ("rhs_seed", C.c_uint32), ("batch", C.c_uint32), ("M", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
 # Every symbol include/mtx.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "mtx_abi_version",
@@ -215,4 +274,12 @@ EXPORTS = [
     "mtx_field_mlp",
     "mtx_field_eval",
     "mtx_last_device_ms",
+    "mtx_field_train_init",
+    "mtx_field_grad",
+    "mtx_field_train_step",
+    "mtx_field_params",
+    "mtx_nerad_upload",
+    "mtx_nerad_lhs",
+    "mtx_nerad_rhs",
+    "mtx_nerad_step",
 ]

@@ -355,6 +355,7 @@ def _bind_scene(ctx, scene) -> None:
     d = scene.desc()
     check(lib().mtx_scene_upload(ctx.handle, C.byref(d)), "mtx_scene_upload")
     ctx._scene_key = key
+    ctx._nerad_key = None  # surface tables (mtx_nerad_upload) belong to the previous scene
     ctx.scene = scene  # keep the host arrays alive while bound
 
 

@@ -50,6 +50,8 @@ def lib():
             "orc_pssmlt_render": [SD, RA, u32, vp, vp],
             "orc_restir_frame": [SD, RA, C.POINTER(_abi.Camera), vp, vp, vp, vp, vp, vp],
             "orc_field_features": [C.POINTER(_abi.FieldDesc), u64, vp, vp, vp],
+            "orc_nerad_lhs": [SD, C.POINTER(_abi.NeradTables), u32, u32, vp],
+            "orc_nerad_rhs": [SD, C.POINTER(_abi.NeradTables), u32, u32, u32, u32, vp],
         }
         for k, a in sig.items():
             getattr(L, k).argtypes = a
@@ -241,3 +243,39 @@ def field_features(field, p, wi):
     d = field.desc()
     lib().orc_field_features(C.byref(d), len(p), p.ctypes.data, wi.ctypes.data, out.ctypes.data)
     return out.view(np.float16)
+
+
+def nerad_lhs(scene, tables, seed, n):
+    """IntersectionSampler.sample restated (nerad.py:270-285): (n, 9) rows as mtx_nerad_lhs."""
+    from mtx.nerad import tables_struct
+
+    out = np.zeros((n, 9), np.float32)
+    d = scene.desc()
+    t = tables_struct(tables)
+    lib().orc_nerad_lhs(C.byref(d), C.byref(t), seed, n, out.ctypes.data)
+    return out
+
+
+def nerad_rhs(scene, tables, lhs_seed, rhs_seed, batch, M):
+    """sample_rhs lanes without the field term (nerad.py:175-238): (batch*M, 16) rows =
+    L_nee(3), f(3), Le(3), stop-vertex valid, query p(3), query wi(3)."""
+    from mtx.nerad import tables_struct
+
+    out = np.zeros((batch * M, 16), np.float32)
+    d = scene.desc()
+    t = tables_struct(tables)
+    lib().orc_nerad_rhs(C.byref(d), C.byref(t), lhs_seed, rhs_seed, batch, M, out.ctypes.data)
+    return out
+
+
+def nerad_compose(lanes, field_out, M):
+    """L = L_nee + f * (Le + Field) per lane (field 0 at invalid stop vertices),
+    then dr.block_sum(L, M) / M with the samples added in order (float32)."""
+    f32 = np.float32
+    L = lanes[:, 0:3] + lanes[:, 3:6] * (lanes[:, 6:9] + field_out.astype(f32))
+    n = len(lanes) // M
+    acc = np.zeros((n, 3), f32)
+    Lm = L.reshape(n, M, 3)
+    for j in range(M):
+        acc = acc + Lm[:, j]
+    return L, acc / f32(M)

@@ -16,6 +16,8 @@
 //   * pssmltpath.py:17-190 PssmltPath.sample          -> orc_pssmlt_path_sample()
 //   * restirgi.py:182-457 RestirIntegrator.render    -> orc_restir_frame()
 //   * prefix_sum.py:9-36, hashgrid.py:8-90, reductions.py:12-54
+//   * nerad.py:121-285 IntersectionSampler.sample / Integrator.sample_rhs
+//                          (training samples)      -> orc_nerad_lhs/_rhs()
 // The upstream per-lane primitives these loops call (Scene.ray_intersect,
 // BSDF, emitter, sampler) come from include/mtx_core;
 // the BVH traversal below is an independent scalar re-implementation over
@@ -42,6 +44,7 @@
 #include "mtx_core/field.h"
 #include "mtx_core/rng.h"
 #include "mtx_core/warp.h"
+#include "mtx_core/nerad.h"
 
 using namespace mtx;
 
@@ -1189,6 +1192,151 @@ int orc_warp(int op, const float *u, float *out, uint64_t n) {
       default: return -1;
     }
     o[0] = v.x; o[1] = v.y; o[2] = v.z;
+  }
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+// ------------------------ nerad.py:121-285 (training samples) ----------------
+struct NeradHost {
+  std::vector<DiscreteDist> dists;
+  NeradTables t;
+};
+
+NeradHost nerad_tables(const mtx_nerad_tables *h) {
+  NeradHost r;
+  r.dists.resize(h->n_shapes);
+  for (uint32_t k = 0; k < h->n_shapes; ++k) {
+    const uint32_t off = h->tri_off[k];
+    r.dists[k] = DiscreteDist{h->tri_pmf + off, h->tri_cdf + off, h->tri_off[k + 1] - off, h->tri_valid[2 * k],
+                              h->tri_valid[2 * k + 1], h->tri_sum[k], h->tri_norm[k]};
+  }
+  r.t.shape = DiscreteDist{h->shape_pmf, h->shape_cdf, h->n_shapes, h->shape_valid[0], h->shape_valid[1],
+                           h->shape_sum, h->shape_norm};
+  r.t.tri_dist = r.dists.data();
+  r.t.tri_off = h->tri_off;
+  r.t.tri_prim = h->tri_prim;
+  return r;
+}
+
+// IntersectionSampler.sample (:270-285) of point i: the surface interaction
+// of the sampled (triangle, barycentrics), seen along -wi_world.
+SurfaceInteraction nerad_point(const SceneView &s, const NeradTables &t, uint32_t seed, uint32_t i, V3 *wi_world,
+                               SurfaceSample *ss) {
+  Pcg32 rng = sampler_lane(seed, i);
+  *ss = nerad_surface_sample(t, s.shapes, s.materials, rng);
+  const SurfaceInteraction f = compute_si(s, 1.f, ss->prim, ss->b1, ss->b2, V3{0.f, 0.f, 1.f});
+  *wi_world = to_world(f.sh, ss->wi_local);
+  return compute_si(s, 1.f, ss->prim, ss->b1, ss->b2, *wi_world * -1.f);
+}
+
+// bsdf.sample on si (null BSDF for an invalid interaction)
+V3 sample_or_null(const SceneView &s, const SurfaceInteraction &si, float u1, V2 u2, BSDFSample *bs) {
+  if (!si.valid) {
+    bs->wo = v3s(0.f);
+    bs->pdf = 0.f;
+    bs->eta = 0.f;
+    bs->type = 0;
+    return v3s(0.f);
+  }
+  return bsdf_sample(s.bsdf, s.materials[si.material], si.uv, si.wi, u1, u2, bs);
+}
+
+// Integrator.sample_rhs (:175-238) for one lane, without the field term:
+// L_nee (:193-197), the path weight f of the stop vertex (zero if invalid,
+// :214-219), its emission Le and its field query (p, si.to_world(si.wi)).
+// The caller forms L = L_nee + f * (Le + Field(query)) (:222-226).
+void orc_nerad_lane(const SceneView &s, const SurfaceInteraction &si, Pcg32 &rng, float *o) {
+  V3 L = v3s(0.f);
+  DirectionSample ds{};
+  const V3 em = sample_emitter_visible(s, si, rng.next_2d(), &ds);  // :193
+  const mtx_material &m = s.materials[si.material];
+  V3 val;
+  float pdf;
+  bsdf_eval_pdf(s.bsdf, m, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :194
+  L = L + val * mis_weight_b(ds.pdf, pdf) * em;                              // :196
+  const float u1 = rng.next_1d();
+  const V2 u2 = rng.next_2d();
+  BSDFSample bs;
+  const V3 w = bsdf_sample(s.bsdf, m, si.uv, si.wi, u1, u2, &bs);  // :201-203
+  SurfaceInteraction si2 = intersect(s, spawn_ray(si.p, si.n, to_world(si.sh, bs.wo)));  // :205-206
+  bool active = si2.valid;
+  const V3 rel = si2.p - si.p;
+  const float dist = norm(rel);
+  const float em_pdf = pdf_emitter_direction(s, si2.emitter, rel / dist, dist, si2.sh.n);  // :210-213
+  V3 f = w * mis_weight_b(bs.pdf, em_pdf);                                                // :214
+  // next_smooth_si (:131-166)
+  V3 f2 = v3s(1.f);
+  float t1 = rng.next_1d();
+  V2 t2 = rng.next_2d();
+  BSDFSample b2;
+  V3 w2 = sample_or_null(s, si2, t1, t2, &b2);
+  bool chain = (b2.type & BF_DELTA) != 0;
+  uint32_t depth = 0;
+  while (chain) {
+    f2 = f2 * w2;
+    si2 = intersect(s, spawn_ray(si2.p, si2.n, to_world(si2.sh, b2.wo)));
+    t1 = rng.next_1d();
+    t2 = rng.next_2d();
+    w2 = sample_or_null(s, si2, t1, t2, &b2);
+    depth += 1;
+    chain = (b2.type & BF_DELTA) != 0 && depth < 10;
+  }
+  active = active && si2.valid;  // :217
+  f = f * f2;                    // :218
+  if (!active) f = f * 0.f;      // :219
+  const V3 le = emitter_eval(s, si2.emitter, si2.wi);
+  const V3 wi = to_world(si2.sh, si2.wi);
+  const float vals[16] = {L.x, L.y, L.z, f.x, f.y, f.z, le.x, le.y, le.z, si2.valid ? 1.f : 0.f,
+                          si2.p.x, si2.p.y, si2.p.z, wi.x, wi.y, wi.z};
+  for (int k = 0; k < 16; ++k) o[k] = vals[k];
+}
+
+}  // namespace
+
+extern "C" {
+
+// IntersectionSampler.sample for n points: 9 floats each (prim bits, b1, b2,
+// p, wi_world), as mtx_nerad_lhs.
+int orc_nerad_lhs(const mtx_scene_desc *d, const mtx_nerad_tables *h, uint32_t seed, uint32_t n, float *out) {
+  SceneView s = make_view(d);
+  NeradHost nt = nerad_tables(h);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    V3 wi;
+    SurfaceSample ss;
+    const SurfaceInteraction si = nerad_point(s, nt.t, seed, (uint32_t)i, &wi, &ss);
+    float *o = out + 9 * i;
+    uint32_t pb = ss.prim;
+    memcpy(o, &pb, 4);
+    o[1] = ss.b1;
+    o[2] = ss.b2;
+    o[3] = si.p.x;
+    o[4] = si.p.y;
+    o[5] = si.p.z;
+    o[6] = wi.x;
+    o[7] = wi.y;
+    o[8] = wi.z;
+  }
+  return 0;
+}
+
+// sample_rhs lanes (batch * M, lane = point * M + j): 16 floats per lane, see
+// orc_nerad_lane.
+int orc_nerad_rhs(const mtx_scene_desc *d, const mtx_nerad_tables *h, uint32_t lhs_seed, uint32_t rhs_seed,
+                  uint32_t batch, uint32_t M, float *lanes) {
+  SceneView s = make_view(d);
+  NeradHost nt = nerad_tables(h);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t i = 0; i < (int64_t)batch * M; ++i) {
+    V3 wi;
+    SurfaceSample ss;
+    const SurfaceInteraction si = nerad_point(s, nt.t, lhs_seed, (uint32_t)(i / M), &wi, &ss);
+    Pcg32 rng = sampler_lane(rhs_seed, (uint32_t)i);
+    orc_nerad_lane(s, si, rng, lanes + 16 * i);
   }
   return 0;
 }

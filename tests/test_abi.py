@@ -26,7 +26,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 2
+    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 3
 
 
 def test_struct_sizes_match_header():
@@ -37,6 +37,10 @@ def test_struct_sizes_match_header():
     assert C.sizeof(_abi.Shape) == 16
     assert C.sizeof(_abi.Camera) == 112
     assert C.sizeof(_abi.RenderArgs) == 80
+    assert C.sizeof(_abi.FieldOpt) == 32
+    assert C.sizeof(_abi.TrainStats) == 88
+    assert C.sizeof(_abi.NeradTables) == 96
+    assert C.sizeof(_abi.NeradArgs) == 20
 
 
 def test_ctx_create_without_gpu_fails_cleanly():

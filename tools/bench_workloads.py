@@ -474,6 +474,68 @@ def field(args):
            "sample": f"{nc} queries, numpy fp32 reference network ({c:.2f} s)"}, dtype="f16")
 
 
+# ---------------------------------------------------- nerad training (f3) --
+def nerad(args):
+    """nerad.py training_step on the bedroom proxy at the script's sizes
+    (batch_size 2^14 LHS points, M = 32 RHS samples each, :244-245)."""
+    import binding as oracle
+    import torch
+    from mtx import scene
+    from mtx.field import Field
+    from mtx.nerad import FieldTrainer
+
+    torch.cuda.set_device(0)
+    sc = scene.bedroom(1280, 720)
+    field = Field(sc)
+    batch, M = 2 ** 14, 32
+    tr = FieldTrainer(sc, field, batch_size=batch, M=M)
+    for _ in range(max(1, args.warmup)):
+        tr.step()
+    _sync()
+    reps = max(args.steps, 10)
+    agg = None
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        st = tr.step()
+        agg = _sum_stats(agg, st)
+    _sync()
+    dt = (time.perf_counter() - t0) / reps
+    lanes = batch * M
+    cnt = tr.step(counters=True)  # untimed: RHS visit counts
+    alg = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
+           + cnt["tris_closest"] * TRI_BYTES)
+    tms = agg["ms_trace"] / reps
+    ach = alg / (tms / 1e3) / 1e9 if tms > 0 else 0.0
+    roof = {"bound": "hbm", "kernel": "k_trace_closest (RHS BSDF rays + next_smooth_si chain)",
+            "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None, "trace_ms_per_step": round(tms, 3),
+            "alg_bytes_per_step": int(alg), "rays_per_step": int(cnt["rays_closest"]),
+            "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
+            "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2)}
+    # CPU: the oracle's RHS lanes (the dominant part) on a reduced batch
+    oracle.build()
+    nb = 64
+    t1 = time.perf_counter()
+    oracle.nerad_rhs(sc, tr.isampler.tables, 1, 2, nb, M)
+    c = time.perf_counter() - t1
+    nb = max(nb, min(2 ** 20, int(nb * args.cpu_seconds / max(c, 1e-3))))
+    t1 = time.perf_counter()
+    oracle.nerad_rhs(sc, tr.isampler.tables, 1, 2, nb, M)
+    c = time.perf_counter() - t1
+    cpu = {"value": round(nb * M / c / 1e6, 4), "unit": "M RHS samples/s", "cores": _threads(), "kind": "port",
+           "sample": f"{nb} points x {M} RHS samples without the field term ({c:.1f} s); oracle/oracle.cpp "
+                     "orc_nerad_rhs (OpenMP)"}
+    ms = {k: round(agg[k] / reps, 3) for k in ("ms_lhs", "ms_rhs", "ms_trace", "ms_train", "ms_total")}
+    _line("nerad training steps/sec on bedroom (batch 2^14 x M=32, f3)", 1.0 / dt, "steps/s", reps,
+          max(1, args.warmup), dt * 1e3,
+          {"workload": "nerad.py training_step: IntersectionSampler LHS, sample_rhs (NEE + BSDF sample + "
+                       "next_smooth_si + field query) on the wavefront, fp16 field forward/backward, hash-grid "
+                       "gradient scatter, GradScaler + Adam", "batch_size": batch, "M": M,
+           "rhs_samples_per_s": round(lanes / dt / 1e6, 3), "phase_ms": ms,
+           "rhs_field_queries_per_step": int(agg["rhs_queries"] / reps), "final_loss": round(st["loss"], 6)},
+          roof, cpu)
+
+
 def run(args):
     {"pssmlt": pssmlt, "pssmltpath": lambda a: pssmlt(a, with_nee=True), "restir": restir, "nrc": nrc,
-     "prims": prims, "field": field}[args.workload](args)
+     "prims": prims, "field": field, "nerad": nerad}[args.workload](args)
