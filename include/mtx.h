@@ -154,7 +154,7 @@ enum {
   MTX_INT_PSSMLT_SIMPLE = 4, /* pssmlt.py:167-228 + pssmltsimple.py:16-142 */
   MTX_INT_RESTIR_GI = 5,     /* restirgi.py:182-588 */
   MTX_INT_PSSMLT_PATH = 6,   /* pssmlt.py:167-228 + pssmltpath.py:17-190 ("pssmlt") */
-  MTX_INT_NERAD_RHS = 7      /* nerad.py:175-238 Integrator.sample_rhs (internal: mtx_nerad_*) */
+  MTX_INT_NERAD_RHS = 7      /* nerad.py:174-233 Integrator.sample_rhs (internal: mtx_nerad_*) */
 };
 
 typedef struct mtx_render_args {
@@ -327,17 +327,17 @@ int mtx_field_mlp(mtx_ctx *ctx, uint64_t n, const uint16_t *feat, float *out);
 int mtx_field_eval(mtx_ctx *ctx, uint64_t n, const float *p, const float *wi, float *out);
 
 /* ------------------ radiance-field training (nerad.py) ------------------ */
-/* nerad.py:318-375: the field above trained by neural radiosity. The fp16
+/* nerad.py:336-400: the field above trained by neural radiosity. The fp16
  * table / weights uploaded with mtx_field_upload are the network; training
  * keeps fp32 master copies + Adam moments in the context and re-casts the
- * fp16 field after every step (:365-366). */
+ * fp16 field after every step (:389-390). */
 typedef struct mtx_field_opt {
-  float lr, beta_1, beta_2, epsilon;     /* drjit.opt.Adam(lr=1e-3) defaults (:351-357) */
+  float lr, beta_1, beta_2, epsilon;     /* drjit.opt.Adam(lr=1e-3) defaults (:336-342) */
   float init_scale, growth_factor, backoff_factor;
-  uint32_t growth_interval;              /* drjit.opt.GradScaler (:362) */
+  uint32_t growth_interval;              /* drjit.opt.GradScaler (:347) */
 } mtx_field_opt;
 typedef struct mtx_train_stats {
-  double loss;        /* mean((L_lhs - L_rhs)^2) of the step, unscaled (:342) */
+  double loss;        /* mean((L_lhs - L_rhs)^2) of the step, unscaled (:370) */
   float scale;        /* GradScaler scale after the step */
   uint32_t found_inf; /* 1: non-finite gradient, step skipped */
   uint32_t step;      /* Adam steps taken */
@@ -359,7 +359,7 @@ int mtx_field_train_step(mtx_ctx *ctx, uint64_t n, const float *p, const float *
 /* fp32 master parameters (table, weights) and Adam moments; any pointer may be NULL. */
 int mtx_field_params(mtx_ctx *ctx, float *table, float *weights, float *m, float *v);
 
-/* Surface-area tables of the uploaded scene (IntersectionSampler, nerad.py:254-266): the
+/* Surface-area tables of the uploaded scene (IntersectionSampler, nerad.py:281-289): the
  * shape distribution and per shape the distribution over its triangles (entries
  * [tri_off[s], tri_off[s+1]) of tri_pmf / tri_cdf / tri_prim; leaf-order triangles).
  * cdf = double-accumulated inclusive prefix stored as float; *_valid = first / last
@@ -377,19 +377,19 @@ typedef struct mtx_nerad_tables {
 } mtx_nerad_tables;
 int mtx_nerad_upload(mtx_ctx *ctx, const mtx_nerad_tables *t);
 typedef struct mtx_nerad_args {
-  uint32_t lhs_seed;  /* sampler_lhs.seed(seed(), batch_size) (:371) */
-  uint32_t rhs_seed;  /* sampler.seed(seed(), batch_size * M) in sample_rhs (:183) */
-  uint32_t batch;     /* batch_size (:244: 2^14) */
-  uint32_t M;         /* RHS samples per point (:245: 32) */
+  uint32_t lhs_seed;  /* sampler_lhs.seed(seed(), batch_size) (:387) */
+  uint32_t rhs_seed;  /* sampler.seed(seed(), batch_size * M) in sample_rhs (:189) */
+  uint32_t batch;     /* batch_size (:258: 2^14) */
+  uint32_t M;         /* RHS samples per point (:259: 32) */
   uint32_t flags;     /* bit 0: count traversal visits (slower STATS kernels) */
 } mtx_nerad_args;
-/* IntersectionSampler.sample for `batch` points (:270-285): 9 floats per point
+/* IntersectionSampler.sample for `batch` points (:291-310): 9 floats per point
  * (prim as uint32 bits, b1, b2, p.xyz, wi_world.xyz). */
 int mtx_nerad_lhs(mtx_ctx *ctx, const mtx_nerad_args *a, float *out);
-/* Integrator.sample_rhs (:175-238) at the mtx_nerad_lhs(a) points with the current field:
+/* Integrator.sample_rhs (:174-233) at the mtx_nerad_lhs(a) points with the current field:
  * L_rhs (3 per point); lanes (NULL or 3 * batch * M): every sample's L before the mean. */
 int mtx_nerad_rhs(mtx_ctx *ctx, const mtx_nerad_args *a, float *L_rhs, float *lanes);
-/* training_step (:336-348) on the device: LHS points, L_lhs = Field(si), L_rhs, loss,
+/* training_step (:363-375) on the device: LHS points, L_lhs = Field(si), L_rhs, loss,
  * backward, GradScaler + Adam, fp16 refresh of the field. */
 int mtx_nerad_step(mtx_ctx *ctx, const mtx_nerad_args *a, mtx_train_stats *stats);
 

@@ -1,10 +1,10 @@
 // mtx_core/nerad.h — neural radiosity training samples (nerad.py), shared by
 // the device kernels and the CPU restatement in oracle/.
 //
-//   IntersectionSampler.sample (nerad.py:270-285): a shape by surface area
-//     (DiscreteDistribution over shape areas, :262-266), a direction sample,
+//   IntersectionSampler.sample (nerad.py:291-310): a shape by surface area
+//     (DiscreteDistribution over shape areas, :284-289), a direction sample,
 //     then shape.sample_position(0, u2) and a uniform sphere / hemisphere
-//     direction for two-sided / one-sided BSDFs (:276-283).
+//     direction for two-sided / one-sided BSDFs (:297-308).
 //   Upstream pieces restated (Mitsuba 3 core, unverifiable offline; parity
 //   unpinned): DiscreteDistribution::sample / sample_reuse (cdf accumulated
 //   in double, stored as float; search restricted to the non-zero range),
@@ -93,7 +93,7 @@ struct SurfaceSample {
   V3 wi_local;    // incident direction in the shading frame
 };
 
-// IntersectionSampler.sample (nerad.py:270-285), draws in the reference
+// IntersectionSampler.sample (nerad.py:291-310), draws in the reference
 // order: shape (next_1d), direction (next_2d), position (next_2d).
 MTX_HD SurfaceSample nerad_surface_sample(const NeradTables &t, const mtx_shape *shapes,
                                           const mtx_material *materials, Pcg32 &rng) {

@@ -918,7 +918,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       const uint32_t iters = a->iterations ? a->iterations : 200;
       mtxd::launch_mlt_init(b, p, c->stream);
       for (uint32_t it = 0; it < iters; ++it) {
-        p.large_step = (it % 50 == 0) ? 1u : 0u;  // reset_interval = 50 (:206)
+        p.large_step = (it % 50 == 0) ? 1u : 0u;  // reset_interval = 50 (:209)
         HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
         mtxd::launch_mlt_begin(c->scene, b, p, c->stream);
         run_bounces(c, b, p, tm, &n_trace, &n_shadow);
@@ -1535,12 +1535,12 @@ static int nerad_lhs_dev(mtx_ctx *c, const mtx_nerad_args *a) {
   return MTX_OK;
 }
 
-// sample_rhs (nerad.py:175-238) for the points in nr_lhs: L_rhs in nr_Lrhs.
+// sample_rhs (nerad.py:174-233) for the points in nr_lhs: L_rhs in nr_Lrhs.
 static int nerad_rhs_dev(mtx_ctx *c, const mtx_nerad_args *a, float *lanes_dev, uint32_t *queries,
                          mtx_train_stats *st = nullptr) {
   int rc;
   const uint32_t n = a->batch * a->M;
-  const uint32_t bounces = 12;  // first vertex, its BSDF hit, <= 10 next_smooth_si traces (:150)
+  const uint32_t bounces = 12;  // first vertex, its BSDF hit, <= 10 next_smooth_si traces (:146)
   if ((rc = ensure_wavefront(c, n, bounces))) return rc;
   if ((rc = ensure_cache(c, n))) return rc;
   if ((rc = dalloc(c->nr_Lrhs, 12ull * a->batch))) return rc;
@@ -1782,18 +1782,18 @@ int mtx_nerad_step(mtx_ctx *c, const mtx_nerad_args *a, mtx_train_stats *stats) 
   HIP_TRY(hipSetDevice(c->device));
   PhaseTimer pt(c->stream);
   pt.mark(0);
-  if ((rc = nerad_lhs_dev(c, a))) return rc;  // si_lhs = isampler.sample(sampler_lhs) (:338)
+  if ((rc = nerad_lhs_dev(c, a))) return rc;  // si_lhs = isampler.sample(sampler_lhs) (:365)
   pt.mark(1);
   uint32_t nq = 0;
   mtx_train_stats st{};
-  if ((rc = nerad_rhs_dev(c, a, nullptr, &nq, &st))) return rc;  // L_rhs = sample_rhs(si_lhs) (:341)
+  if ((rc = nerad_rhs_dev(c, a, nullptr, &nq, &st))) return rc;  // L_rhs = sample_rhs(si_lhs) (:368)
   pt.mark(2);
-  double loss = 0.0;  // L_lhs = Field(si_lhs), loss, backward (:340-344)
+  double loss = 0.0;  // L_lhs = Field(si_lhs), loss, backward (:367-372)
   if ((rc = field_backward(c, (const float4 *)c->nr_qp.p, (const float4 *)c->nr_qd.p, (const float *)c->nr_Lrhs.p,
                            a->batch, c->scale, &loss)))
     return rc;
   st.loss = loss;
-  if ((rc = field_opt_step(c, &st))) return rc;  // scaler.step(opt) (:345)
+  if ((rc = field_opt_step(c, &st))) return rc;  // scaler.step(opt) (:373)
   pt.mark(3);
   HIP_TRY(hipStreamSynchronize(c->stream));
   st.rhs_queries = nq;

@@ -1,8 +1,8 @@
-// field_train.hip — training of the radiance field (nerad.py:318-375):
-// loss = mean((L_lhs - detach(L_rhs))^2) (:342), dr.backward(scaler.scale(
-// loss)) through the fp16 MLP and the hash-grid table (:344), then
+// field_train.hip — training of the radiance field (nerad.py:336-400):
+// loss = mean((L_lhs - detach(L_rhs))^2) (:370), dr.backward(scaler.scale(
+// loss)) through the fp16 MLP and the hash-grid table (:372), then
 // scaler.step(opt) -- GradScaler + Adam on fp32 master copies of the table
-// and the weights, re-cast to the fp16 field after the step (:365-366).
+// and the weights, re-cast to the fp16 field after the step (:389-390).
 //
 // k_field_train     one block per 64 training points (lane = point). The
 //                   forward keeps every layer's fp16 input tile in LDS

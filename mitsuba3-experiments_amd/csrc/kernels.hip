@@ -583,16 +583,16 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   return active;
 }
 
-// nerad.py:175-238 Integrator.sample_rhs, one lane = one of the M samples of a
-// training point (nerad.py:178-180 dr.repeat). Bounce 0 is the sampled
+// nerad.py:174-233 Integrator.sample_rhs, one lane = one of the M samples of a
+// training point (nerad.py:182-184 dr.repeat). Bounce 0 is the sampled
 // surface point itself (hit record written by k_nerad_raygen): NEE with a
-// visibility test (:193-197, mis_weight of mitsuba.ad.integrators.common =
-// variant B) and a BSDF sample (:201-203). Bounce 1 is the BSDF ray's hit:
-// f = mis_weight(bs.pdf, emitter pdf) * bsdf_weight (:205-214), then
-// next_smooth_si (:131-166) follows delta / null vertices (bounces 2..11,
-// f2 in prev.xyz). At the stop vertex: f *= f2, zero if invalid (:216-219);
+// visibility test (:197-200, mis_weight of mitsuba.ad.integrators.common =
+// variant B) and a BSDF sample (:204-206). Bounce 1 is the BSDF ray's hit:
+// f = mis_weight(bs.pdf, emitter pdf) * bsdf_weight (:208-217), then
+// next_smooth_si (:124-164) follows delta / null vertices (bounces 2..11,
+// f2 in prev.xyz). At the stop vertex: f *= f2, zero if invalid (:219-222);
 // a valid vertex becomes a field query (Le kept in prev.xyz), L += f * (Le +
-// field) is applied after the field evaluation (k_nerad_apply, :222-226).
+// field) is applied after the field evaluation (k_nerad_apply, :226-229).
 // State: thr.xyz = f, L.w = bs.pdf of bounce 0, prev.xyz = si.p (bounce 0)
 // then f2, misc.w = chain depth.
 __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
@@ -614,27 +614,27 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   if (bounce == 0) {
     const mtx_material mat = sv.materials[si.material];
     DirectionSample ds;
-    const V3 em = sample_emitter_direction(sv, si.p, rng.next_2d(), &ds);  // :193
+    const V3 em = sample_emitter_direction(sv, si.p, rng.next_2d(), &ds);  // :197
     V3 val;
     float pdf;
-    bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :194
+    bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :198
     const float mis = mis_weight_b(ds.pdf, pdf);
-    make_shadow(io, si, ds, path, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :196
+    make_shadow(io, si, ds, path, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :200
     const float s1 = rng.next_1d();
     const V2 s2 = rng.next_2d();
     BSDFSample bs;
-    const V3 w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);  // :201-203
-    const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));   // :205
+    const V3 w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);  // :204-206
+    const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));   // :208
     b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
     b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
     b.thr[path] = make_float4(w.x, w.y, w.z, 1.f);
     b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
     b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
-    return true;  // traced unconditionally (:206)
+    return true;  // traced unconditionally (:209)
   }
   if (bounce == 1) {
-    // emitter pdf of the BSDF-sampled hit (:210-213), f (:214)
+    // emitter pdf of the BSDF-sampled hit (:213-216), f (:217)
     const V3 prev_p = f2;
     const V3 rel = si.p - prev_p;
     const float dist = norm(rel);
@@ -642,7 +642,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     f = f * mis_weight_b(Lr.w, em_pdf);
     f2 = v3s(1.f);
   }
-  // next_smooth_si (:131-166): sample at this vertex; continue while delta
+  // next_smooth_si (:124-164): sample at this vertex; continue while delta
   BSDFSample bs;
   bs.type = 0;
   V3 w = v3s(0.f);
@@ -652,10 +652,10 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     const mtx_material mat = sv.materials[si.material];
     w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
   }
-  if (bounce >= 2) depth += 1;  // :162
+  if (bounce >= 2) depth += 1;  // :160
   const bool chain = (bs.type & BF_DELTA) != 0 && depth < 10;
   if (chain) {
-    f2 = f2 * w;  // :157
+    f2 = f2 * w;  // :150
     const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
     b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
     b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
@@ -664,7 +664,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
     return true;
   }
-  // stop vertex (:216-226)
+  // stop vertex (:219-229)
   f = f * f2;
   if (!si.valid) f = f * 0.f;
   const V3 le = emitter_eval(sv, si.emitter, si.wi);

@@ -1,8 +1,8 @@
 // nerad.hip — training samples of the neural radiosity field (nerad.py,
 // SURVEY §8f item 3): the left-hand side points (IntersectionSampler.sample,
-// nerad.py:270-285) and the right-hand side estimate (Integrator.sample_rhs,
-// nerad.py:175-238) on the wavefront. The RHS lanes (M per point, dr.repeat
-// at :178) run k_shade<MTX_INT_NERAD_RHS> (kernels.hip, shade_nerad) over
+// nerad.py:291-310) and the right-hand side estimate (Integrator.sample_rhs,
+// nerad.py:174-233) on the wavefront. The RHS lanes (M per point, dr.repeat
+// at :182) run k_shade<MTX_INT_NERAD_RHS> (kernels.hip, shade_nerad) over
 // the same persistent trace kernels as the path tracers; their stop
 // vertices query the fp16 MFMA field (field.hip) through the NRC cache
 // queue, then k_nerad_apply and k_nerad_mean form L_rhs.
@@ -32,7 +32,7 @@ __global__ void k_nerad_lhs(DevScene s, NeradTables t, uint32_t seed, uint32_t n
   qd[i] = make_float4(wi.x, wi.y, wi.z, 0.f);
 }
 
-// RHS lane i = point * M + j (sampler lane i, nerad.py:182-183): the hit
+// RHS lane i = point * M + j (sampler lane i, nerad.py:182-189): the hit
 // record is the point itself, seen from the ray direction -wi_world.
 __global__ void k_nerad_raygen(WaveBuffers b, ChunkParams p, const float4 *lhs, uint32_t M) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -51,7 +51,7 @@ __global__ void k_nerad_raygen(WaveBuffers b, ChunkParams p, const float4 *lhs, 
   b.queue[0][i] = i;
 }
 
-// L += f * (Le + Field(si)) at the stop vertices (nerad.py:222-226).
+// L += f * (Le + Field(si)) at the stop vertices (nerad.py:226-229).
 __global__ void k_nerad_apply(WaveBuffers b, const float *out) {
   const uint32_t n = *b.cq_count;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
@@ -66,7 +66,7 @@ __global__ void k_nerad_apply(WaveBuffers b, const float *out) {
   }
 }
 
-// dr.block_sum(L, M) / M (nerad.py:228), samples summed in order.
+// dr.block_sum(L, M) / M (nerad.py:231), samples summed in order.
 __global__ void k_nerad_mean(WaveBuffers b, uint32_t n, uint32_t M, float *L_rhs, float *lanes) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -1,5 +1,5 @@
 """Neural radiosity training of the radiance field (nerad.py; SURVEY §8f
-item 3: "training (Adam, GradScaler, nerad.py:336-375) after" inference).
+item 3: "training (Adam, GradScaler, nerad.py:336-400) after" inference).
 
 The reference trains ``Field`` (hash grid + fp16 MLP, nerad.py:54-106) by
 minimising the radiosity residual ``mean((L_lhs - detach(L_rhs))^2)``
@@ -30,7 +30,7 @@ from .integrators import _bind_scene
 
 
 class SeedGenerator:
-    """The reference's global ``seed()`` counter (nerad.py:30-38)."""
+    """The reference's global ``seed()`` counter (nerad.py:33-40)."""
 
     def __init__(self, start: int = 0):
         self.next = int(start)
@@ -43,7 +43,7 @@ class SeedGenerator:
 
 # ---------------------------------------------------------------- tables --
 def surface_tables(scene) -> dict:
-    """Surface-area distributions of IntersectionSampler (nerad.py:258-266):
+    """Surface-area distributions of IntersectionSampler (nerad.py:281-289):
     the shapes weighted by area, and per shape its triangles by area (upstream
     Mesh::m_area_pmf; triangles in BVH leaf order). cdf = float(double
     prefix sum), normalization = float(1 / double(sum))."""
@@ -78,8 +78,8 @@ def surface_tables(scene) -> dict:
             raise MtxError(f"shape {s} has zero surface area")
         tri_norm[s] = np.float32(1.0 / np.float64(tri_sum[s]))
         tri_valid[2 * s], tri_valid[2 * s + 1] = nz[0], nz[-1]
-        shape_area[s] = float(tri_sum[s])  # shape.surface_area() (:262)
-    w = (shape_area / shape_area.sum()).astype(np.float32)  # weights /= dr.sum(weights) (:264)
+        shape_area[s] = float(tri_sum[s])  # shape.surface_area() (:285)
+    w = (shape_area / shape_area.sum()).astype(np.float32)  # weights /= dr.sum(weights) (:287)
     shape_cdf = np.cumsum(w.astype(np.float64))
     nz = np.nonzero(w > 0)[0]
     return {
@@ -107,7 +107,7 @@ def tables_struct(t: dict) -> _abi.NeradTables:
 
 # ------------------------------------------------------- reference names --
 class IntersectionSampler:
-    """nerad.py:254-285: surface points by area and incident directions
+    """nerad.py:275-310: surface points by area and incident directions
     (uniform sphere for two-sided BSDFs, hemisphere otherwise)."""
 
     def __init__(self, scene):
@@ -132,14 +132,14 @@ class IntersectionSampler:
 
 
 class Adam:
-    """drjit.opt.Adam settings (nerad.py:351-357; upstream defaults)."""
+    """drjit.opt.Adam settings (nerad.py:336-342; upstream defaults)."""
 
     def __init__(self, lr: float = 1e-3, beta_1: float = 0.9, beta_2: float = 0.999, epsilon: float = 1e-8):
         self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
 
 
 class GradScaler:
-    """drjit.opt.GradScaler settings (nerad.py:362): dynamic loss scaling
+    """drjit.opt.GradScaler settings (nerad.py:347): dynamic loss scaling
     (upstream defaults unverifiable offline: torch.amp's are used)."""
 
     def __init__(self, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0, backoff_factor: float = 0.5,
@@ -149,7 +149,7 @@ class GradScaler:
 
 
 class Integrator:
-    """nerad.py:121-238: sample_lhs = Field(si); sample_rhs = one bounce of
+    """nerad.py:118-255: sample_lhs = Field(si); sample_rhs = one bounce of
     the rendering equation with M samples per point, continued by the field."""
 
     def __init__(self, field: Field, batch_size: int = 2 ** 14, M: int = 32):
@@ -173,9 +173,9 @@ class Integrator:
 
 
 class FieldTrainer:
-    """The training loop of nerad.py:368-385 on one device context: each
+    """The training loop of nerad.py:383-400 on one device context: each
     step seeds the LHS sampler and the RHS sampler from the reference's
-    seed() counter and runs training_step (:336-348) on the GPU."""
+    seed() counter and runs training_step (:363-375) on the GPU."""
 
     def __init__(self, scene, field: Field, batch_size: int = 2 ** 14, M: int = 32, opt: Adam | None = None,
                  scaler: GradScaler | None = None, seed_start: int = 1, ctx=None):
@@ -183,7 +183,7 @@ class FieldTrainer:
         self.isampler = IntersectionSampler(scene)
         self.integrator = Integrator(field, batch_size, M)
         self.opt, self.scaler = opt or Adam(), scaler or GradScaler()
-        self.seed = SeedGenerator(seed_start)  # seed 0 renders img_ref in the script (:296)
+        self.seed = SeedGenerator(seed_start)  # seed 0 renders img_ref in the script (:329)
         self.ctx = self.isampler.bind(field._ensure(ctx or context()))
         o = _abi.FieldOpt(lr=self.opt.lr, beta_1=self.opt.beta_1, beta_2=self.opt.beta_2,
                           epsilon=self.opt.epsilon, init_scale=self.scaler.init_scale,

@@ -246,7 +246,7 @@ def field_features(field, p, wi):
 
 
 def nerad_lhs(scene, tables, seed, n):
-    """IntersectionSampler.sample restated (nerad.py:270-285): (n, 9) rows as mtx_nerad_lhs."""
+    """IntersectionSampler.sample restated (nerad.py:291-310): (n, 9) rows as mtx_nerad_lhs."""
     from mtx.nerad import tables_struct
 
     out = np.zeros((n, 9), np.float32)
@@ -257,7 +257,7 @@ def nerad_lhs(scene, tables, seed, n):
 
 
 def nerad_rhs(scene, tables, lhs_seed, rhs_seed, batch, M):
-    """sample_rhs lanes without the field term (nerad.py:175-238): (batch*M, 16) rows =
+    """sample_rhs lanes without the field term (nerad.py:174-233): (batch*M, 16) rows =
     L_nee(3), f(3), Le(3), stop-vertex valid, query p(3), query wi(3)."""
     from mtx.nerad import tables_struct
 

@@ -16,7 +16,7 @@
 //   * pssmltpath.py:17-190 PssmltPath.sample          -> orc_pssmlt_path_sample()
 //   * restirgi.py:182-457 RestirIntegrator.render    -> orc_restir_frame()
 //   * prefix_sum.py:9-36, hashgrid.py:8-90, reductions.py:12-54
-//   * nerad.py:121-285 IntersectionSampler.sample / Integrator.sample_rhs
+//   * nerad.py:118-310 IntersectionSampler.sample / Integrator.sample_rhs
 //                          (training samples)      -> orc_nerad_lhs/_rhs()
 // The upstream per-lane primitives these loops call (Scene.ray_intersect,
 // BSDF, emitter, sampler) come from include/mtx_core;
@@ -1200,7 +1200,7 @@ int orc_warp(int op, const float *u, float *out, uint64_t n) {
 
 namespace {
 
-// ------------------------ nerad.py:121-285 (training samples) ----------------
+// ------------------------ nerad.py:118-310 (training samples) ----------------
 struct NeradHost {
   std::vector<DiscreteDist> dists;
   NeradTables t;
@@ -1222,7 +1222,7 @@ NeradHost nerad_tables(const mtx_nerad_tables *h) {
   return r;
 }
 
-// IntersectionSampler.sample (:270-285) of point i: the surface interaction
+// IntersectionSampler.sample (:291-310) of point i: the surface interaction
 // of the sampled (triangle, barycentrics), seen along -wi_world.
 SurfaceInteraction nerad_point(const SceneView &s, const NeradTables &t, uint32_t seed, uint32_t i, V3 *wi_world,
                                SurfaceSample *ss) {
@@ -1245,30 +1245,30 @@ V3 sample_or_null(const SceneView &s, const SurfaceInteraction &si, float u1, V2
   return bsdf_sample(s.bsdf, s.materials[si.material], si.uv, si.wi, u1, u2, bs);
 }
 
-// Integrator.sample_rhs (:175-238) for one lane, without the field term:
-// L_nee (:193-197), the path weight f of the stop vertex (zero if invalid,
+// Integrator.sample_rhs (:174-233) for one lane, without the field term:
+// L_nee (:197-200), the path weight f of the stop vertex (zero if invalid,
 // :214-219), its emission Le and its field query (p, si.to_world(si.wi)).
-// The caller forms L = L_nee + f * (Le + Field(query)) (:222-226).
+// The caller forms L = L_nee + f * (Le + Field(query)) (:226-229).
 void orc_nerad_lane(const SceneView &s, const SurfaceInteraction &si, Pcg32 &rng, float *o) {
   V3 L = v3s(0.f);
   DirectionSample ds{};
-  const V3 em = sample_emitter_visible(s, si, rng.next_2d(), &ds);  // :193
+  const V3 em = sample_emitter_visible(s, si, rng.next_2d(), &ds);  // :197
   const mtx_material &m = s.materials[si.material];
   V3 val;
   float pdf;
-  bsdf_eval_pdf(s.bsdf, m, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :194
-  L = L + val * mis_weight_b(ds.pdf, pdf) * em;                              // :196
+  bsdf_eval_pdf(s.bsdf, m, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :198
+  L = L + val * mis_weight_b(ds.pdf, pdf) * em;                              // :200
   const float u1 = rng.next_1d();
   const V2 u2 = rng.next_2d();
   BSDFSample bs;
-  const V3 w = bsdf_sample(s.bsdf, m, si.uv, si.wi, u1, u2, &bs);  // :201-203
-  SurfaceInteraction si2 = intersect(s, spawn_ray(si.p, si.n, to_world(si.sh, bs.wo)));  // :205-206
+  const V3 w = bsdf_sample(s.bsdf, m, si.uv, si.wi, u1, u2, &bs);  // :204-206
+  SurfaceInteraction si2 = intersect(s, spawn_ray(si.p, si.n, to_world(si.sh, bs.wo)));  // :208-209
   bool active = si2.valid;
   const V3 rel = si2.p - si.p;
   const float dist = norm(rel);
-  const float em_pdf = pdf_emitter_direction(s, si2.emitter, rel / dist, dist, si2.sh.n);  // :210-213
-  V3 f = w * mis_weight_b(bs.pdf, em_pdf);                                                // :214
-  // next_smooth_si (:131-166)
+  const float em_pdf = pdf_emitter_direction(s, si2.emitter, rel / dist, dist, si2.sh.n);  // :213-216
+  V3 f = w * mis_weight_b(bs.pdf, em_pdf);                                                // :217
+  // next_smooth_si (:124-164)
   V3 f2 = v3s(1.f);
   float t1 = rng.next_1d();
   V2 t2 = rng.next_2d();

@@ -70,7 +70,7 @@ def test_oracle_rhs_lanes(nscene, tables, oracle):
     assert np.all(lanes[:, 0:3] >= 0) and np.all(lanes[:, 3:6] >= 0)
     valid = lanes[:, 9] > 0
     assert 0.2 < valid.mean() <= 1.0
-    assert np.all(lanes[~valid, 3:6] == 0)  # f *= select(active, 1, 0) (nerad.py:219)
+    assert np.all(lanes[~valid, 3:6] == 0)  # f *= select(active, 1, 0) (nerad.py:222)
     # a different RHS seed gives different samples, the same seed the same ones
     assert np.array_equal(lanes, oracle.nerad_rhs(nscene, tables, 3, 4, 128, 8))
     assert not np.array_equal(lanes, oracle.nerad_rhs(nscene, tables, 3, 5, 128, 8))
@@ -261,7 +261,7 @@ def test_adam_and_grad_scaler(nscene):
 
 @pytest.mark.gpu
 def test_training_reduces_loss(nscene):
-    """training_step (nerad.py:336-348) on the device lowers the radiosity
+    """training_step (nerad.py:363-375) on the device lowers the radiosity
     residual of a fixed validation batch (same LHS / RHS seeds, M = 64, so
     the residual is deterministic given the field), and the fp16 field the
     renderer sees is the cast of the fp32 master weights."""
