@@ -523,7 +523,7 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
   }
   if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC &&
       a->integrator != MTX_INT_PSSMLT_SIMPLE && a->integrator != MTX_INT_RESTIR_GI &&
-      a->integrator != MTX_INT_PSSMLT_PATH) {
+      a->integrator != MTX_INT_PSSMLT_PATH && a->integrator != MTX_INT_NERAD) {
     mtx_set_error("integrator %u is not supported by this entry point", a->integrator);
     return MTX_E_UNSUPPORTED;
   }
@@ -573,7 +573,7 @@ struct Timer {
 };
 
 // Encode + MLP + L += T * out for the chunk's compacted cache queries.
-void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm) {
+void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false) {
   hipEvent_t e = tm.begin(4);
   mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream);
   tm.end(4, e);
@@ -581,7 +581,10 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm) 
   mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
                   (float *)c->f_out.p, c->n_cu, c->stream);
   tm.end(5, e);
-  mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream);
+  if (nerad_render)
+    mtxd::launch_nerad_apply(b, (const float *)c->f_out.p, cap, 1, c->stream);
+  else
+    mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream);
   if (tm.on) {
     uint32_t nq = 0;
     if (hipMemcpyAsync(&nq, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
@@ -598,7 +601,7 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
   const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1) + (p.nrc_cache ? 1u : 0u);
   // nerad RHS lanes start at their surface point (no bounce-0 trace) and
   // trace NEE rays at that point only
-  const bool nerad = p.integrator == MTX_INT_NERAD_RHS;
+  const bool nerad = p.integrator == MTX_INT_NERAD_RHS, nerad_render = p.integrator == MTX_INT_NERAD;
   for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
     hipEvent_t e;
     if (!(nerad && bounce == 0)) {
@@ -610,7 +613,8 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     e = tm.begin(2);
     mtxd::launch_shade(s, b, p, bounce, c->shade_grid, c->stream);
     tm.end(2, e);
-    if (p.integrator != MTX_INT_PSSMLT_SIMPLE && !(nerad && bounce > 0)) {  // PSSMLT traces no NEE rays
+    if (p.integrator != MTX_INT_PSSMLT_SIMPLE && !nerad_render &&
+        !(nerad && bounce > 0)) {  // PSSMLT and the nerad render trace no NEE rays
       e = tm.begin(1);
       mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
       tm.end(1, e);
@@ -860,7 +864,8 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   const uint32_t cap = px_per_chunk * a->spp;
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
-  if (nrc_cache && (rc = ensure_cache(c, cap))) return rc;
+  const bool nerad_render = a->integrator == MTX_INT_NERAD;
+  if ((nrc_cache || nerad_render) && (rc = ensure_cache(c, cap))) return rc;
   if ((rc = dalloc(c->contrib, 9ull * 16 * band_px))) return rc;
   const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
   float4 *film_dev = (float4 *)film_rgbw;
@@ -928,10 +933,11 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       continue;
     }
     HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
-    if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
+    if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
     run_bounces(c, b, p, tm, &n_trace, &n_shadow);
     if (nrc_cache) run_cache(c, b, p.n_paths, tm);
+    if (nerad_render) run_cache(c, b, p.n_paths, tm, true);
     mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, c->stream);
   }
   mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, c->stream);
@@ -1042,7 +1048,8 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
   const uint32_t cap = (uint32_t)std::min<uint64_t>(n, chunk);
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
-  if (nrc_cache && (rc = ensure_cache(c, cap))) return rc;
+  const bool nerad_render = a->integrator == MTX_INT_NERAD;
+  if ((nrc_cache || nerad_render) && (rc = ensure_cache(c, cap))) return rc;
   if ((rc = dalloc(c->s0, 24ull * cap))) return rc;
   if ((rc = dalloc(c->s1, 4ull * cap))) return rc;
   if ((rc = dalloc(c->s2, 12ull * cap))) return rc;
@@ -1067,10 +1074,11 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     p.nrc_c = a->nrc_c;
     p.nrc_cache = nrc_cache ? 1u : 0u;
     HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
-    if (nrc_cache) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
+    if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
     run_bounces(c, b, p, tm, &nt, &ns);
     if (nrc_cache) run_cache(c, b, m, tm);
+    if (nerad_render) run_cache(c, b, m, tm, true);
     mtxd::launch_collect(b, p, (float *)c->s2.p, (uint8_t *)c->s3.p, c->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));
@@ -1564,7 +1572,7 @@ static int nerad_rhs_dev(mtx_ctx *c, const mtx_nerad_args *a, float *lanes_dev, 
   mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, n, (uint16_t *)c->f_feat.p, c->stream);
   mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, n, c->field_frag.p, c->field_hidden,
                   (float *)c->f_out.p, c->n_cu, c->stream);
-  mtxd::launch_nerad_apply(b, (const float *)c->f_out.p, n, c->stream);
+  mtxd::launch_nerad_apply(b, (const float *)c->f_out.p, n, 0, c->stream);
   mtxd::launch_nerad_mean(b, a->batch, a->M, (float *)c->nr_Lrhs.p, lanes_dev, c->stream);
   HIP_TRY(hipGetLastError());
   if (queries) HIP_TRY(hipMemcpyAsync(queries, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream));

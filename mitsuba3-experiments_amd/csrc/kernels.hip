@@ -595,6 +595,10 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
 // field) is applied after the field evaluation (k_nerad_apply, :226-229).
 // State: thr.xyz = f, L.w = bs.pdf of bounce 0, prev.xyz = si.p (bounce 0)
 // then f2, misc.w = chain depth.
+// RENDER: Integrator.sample (nerad.py:235-254) -- a camera lane runs
+// next_smooth_si from its first hit (bounce 0 = chain start, no NEE), then
+// L = Field(si) * f + Le(si) (applied by k_nerad_apply after the field).
+template <bool RENDER>
 __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                             uint32_t bounce, uint32_t path, ShadeIO &io) {
   const float4 rd = b.ray_d[path], Lr = b.L[path], pv = b.prev[path], th = b.thr[path];
@@ -611,7 +615,12 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   V3 L = V3{Lr.x, Lr.y, Lr.z};
   V3 f = V3{th.x, th.y, th.z};
   V3 f2 = V3{pv.x, pv.y, pv.z};
-  if (bounce == 0) {
+  if (RENDER && bounce == 0) {  // next_smooth_si's f = Spectrum(1) (:135)
+    f = v3s(1.f);
+    f2 = v3s(1.f);
+    depth = 0;
+  }
+  if (!RENDER && bounce == 0) {
     const mtx_material mat = sv.materials[si.material];
     DirectionSample ds;
     const V3 em = sample_emitter_direction(sv, si.p, rng.next_2d(), &ds);  // :197
@@ -633,7 +642,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
     return true;  // traced unconditionally (:209)
   }
-  if (bounce == 1) {
+  if (!RENDER && bounce == 1) {
     // emitter pdf of the BSDF-sampled hit (:213-216), f (:217)
     const V3 prev_p = f2;
     const V3 rel = si.p - prev_p;
@@ -652,7 +661,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     const mtx_material mat = sv.materials[si.material];
     w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
   }
-  if (bounce >= 2) depth += 1;  // :160
+  if (bounce > (RENDER ? 0u : 1u)) depth += 1;  // :160
   const bool chain = (bs.type & BF_DELTA) != 0 && depth < 10;
   if (chain) {
     f2 = f2 * w;  // :150
@@ -664,11 +673,14 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
     return true;
   }
-  // stop vertex (:219-229)
+  // stop vertex (:219-229; render: :250-252)
   f = f * f2;
   if (!si.valid) f = f * 0.f;
   const V3 le = emitter_eval(sv, si.emitter, si.wi);
-  if (si.valid) {
+  if (RENDER && !si.valid) {
+    L = v3s(0.f) * f + le;
+    b.L[path] = make_float4(L.x, L.y, L.z, Lr.w);
+  } else if (si.valid) {
     io.query = true;
     const V3 wi = to_world(si.sh, si.wi);  // Field.__call__ wi (nerad.py:100)
     io.qp = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
@@ -718,7 +730,9 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
         cont = shade_pssmlt_path(s, sv, b, p, path, io);
       else if constexpr (INT == MTX_INT_NERAD_RHS)
-        cont = shade_nerad(s, sv, b, bounce, path, io);
+        cont = shade_nerad<false>(s, sv, b, bounce, path, io);
+      else if constexpr (INT == MTX_INT_NERAD)
+        cont = shade_nerad<true>(s, sv, b, bounce, path, io);
       else
         cont = shade_path<INT>(s, sv, b, p, bounce, path, io);
     }
@@ -726,8 +740,8 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, sh_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path;
     if (io.emit) b.shadow[sslot] = io.rec;
-    if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS) {
-      if (INT == MTX_INT_NERAD_RHS || p.nrc_cache) {
+    if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
+      if (INT != MTX_INT_NRC || p.nrc_cache) {
         const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);
         if (io.query) {
           b.cq_p[q] = io.qp;
@@ -1094,6 +1108,9 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
       break;
     case MTX_INT_NERAD_RHS:
       hipLaunchKernelGGL(k_shade<MTX_INT_NERAD_RHS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
+    case MTX_INT_NERAD:
+      hipLaunchKernelGGL(k_shade<MTX_INT_NERAD>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
     default:
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);

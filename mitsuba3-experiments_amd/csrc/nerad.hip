@@ -51,17 +51,24 @@ __global__ void k_nerad_raygen(WaveBuffers b, ChunkParams p, const float4 *lhs, 
   b.queue[0][i] = i;
 }
 
-// L += f * (Le + Field(si)) at the stop vertices (nerad.py:226-229).
-__global__ void k_nerad_apply(WaveBuffers b, const float *out) {
+// L += f * (Le + Field(si)) at the stop vertices (nerad.py:226-229), or for
+// a rendered lane L = Field(si) * f + Le(si) (:251-252).
+__global__ void k_nerad_apply(WaveBuffers b, const float *out, uint32_t render) {
   const uint32_t n = *b.cq_count;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
     const float4 t = b.cq_t[q];
     const uint32_t path = __float_as_uint(t.w);
     const float4 le = b.prev[path];
     float4 L = b.L[path];
-    L.x = L.x + t.x * (le.x + out[3 * (size_t)q]);
-    L.y = L.y + t.y * (le.y + out[3 * (size_t)q + 1]);
-    L.z = L.z + t.z * (le.z + out[3 * (size_t)q + 2]);
+    if (render) {
+      L.x = out[3 * (size_t)q] * t.x + le.x;
+      L.y = out[3 * (size_t)q + 1] * t.y + le.y;
+      L.z = out[3 * (size_t)q + 2] * t.z + le.z;
+    } else {
+      L.x = L.x + t.x * (le.x + out[3 * (size_t)q]);
+      L.y = L.y + t.y * (le.y + out[3 * (size_t)q + 1]);
+      L.z = L.z + t.z * (le.z + out[3 * (size_t)q + 2]);
+    }
     b.L[path] = L;
   }
 }
@@ -99,9 +106,9 @@ void launch_nerad_raygen(const WaveBuffers &b, const ChunkParams &p, const float
                          hipStream_t st) {
   hipLaunchKernelGGL(k_nerad_raygen, dim3(nblocks(p.n_paths, 256)), dim3(256), 0, st, b, p, lhs, M);
 }
-void launch_nerad_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st) {
+void launch_nerad_apply(const WaveBuffers &b, const float *out, uint32_t capacity, uint32_t render, hipStream_t st) {
   const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 16384);
-  hipLaunchKernelGGL(k_nerad_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out);
+  hipLaunchKernelGGL(k_nerad_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out, render);
 }
 void launch_nerad_mean(const WaveBuffers &b, uint32_t n, uint32_t M, float *L_rhs, float *lanes, hipStream_t st) {
   hipLaunchKernelGGL(k_nerad_mean, dim3(nblocks(n, 256)), dim3(256), 0, st, b, n, M, L_rhs, lanes);

@@ -188,7 +188,8 @@ void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any
 void launch_nerad_lhs(const DevScene &s, const mtx::NeradTables &t, uint32_t seed, uint32_t n, float4 *lhs,
                       float4 *qp, float4 *qd, hipStream_t st);
 void launch_nerad_raygen(const WaveBuffers &b, const ChunkParams &p, const float4 *lhs, uint32_t M, hipStream_t st);
-void launch_nerad_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st);
+void launch_nerad_apply(const WaveBuffers &b, const float *out, uint32_t capacity, uint32_t render,
+                        hipStream_t st);
 void launch_nerad_mean(const WaveBuffers &b, uint32_t n, uint32_t M, float *L_rhs, float *lanes, hipStream_t st);
 
 }  // namespace mtxd

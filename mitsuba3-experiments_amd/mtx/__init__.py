@@ -9,6 +9,7 @@ through the C ABI declared in include/mtx.h.
 from ._lib import MtxError, context, lib  # noqa: F401
 from .integrators import (  # noqa: F401
     IndependentSampler,
+    NeradIntegrator,
     NRCIntegrator,
     Path,
     PathIntegrator,

@@ -24,6 +24,7 @@ MTX_INT_PSSMLT_SIMPLE = 4
 MTX_INT_RESTIR_GI = 5
 MTX_INT_PSSMLT_PATH = 6
 MTX_INT_NERAD_RHS = 7
+MTX_INT_NERAD = 8
 
 MTX_RESTIR_BIAS_CORRECTION = 1
 MTX_RESTIR_JACOBIAN = 2

@@ -201,6 +201,33 @@ class NRCIntegrator(SamplingIntegrator):
         return super().sample(scene, sampler, ray, medium, active)
 
 
+class NeradIntegrator(SamplingIntegrator):
+    """nerad.py:118-254 Integrator used as a renderer (sample(), :235-254):
+    a camera ray's first hit is followed through delta / null vertices
+    (next_smooth_si, :124-164, at most 10 more traces) and L = Field(si) * f
+    + Le(si). Needs the trained (or any) radiance field: props["field"]."""
+
+    integrator_id = _abi.MTX_INT_NERAD
+    name = "nerad"
+
+    def __init__(self, props=None):
+        super().__init__(props)
+        self.field = self.props.get("field", None)
+        if self.field is None:
+            raise MtxError('"nerad" needs a radiance field: load_dict({"type": "nerad", "field": Field(scene)})')
+        self.max_depth = 11  # the first hit + next_smooth_si's max_depth = 10 (:146)
+        self.rr_depth = 0
+
+    def render_film(self, scene, *args, ctx=None, device: int | None = None, **kwargs):
+        ctx = ctx or context(device)
+        self.field._ensure(ctx)
+        return super().render_film(scene, *args, ctx=ctx, **kwargs)
+
+    def sample(self, scene, sampler: IndependentSampler, ray, medium=None, active=True):
+        self.field._ensure(context())
+        return super().sample(scene, sampler, ray, medium, active)
+
+
 class PssmltSimple(SamplingIntegrator):
     """pssmlt.py:96-255 + pssmltsimple.py:11-145 ("pssmlt_simple"): per-pixel
     primary-sample-space MLT over W*H*spp chains; 200 Metropolis iterations
@@ -345,6 +372,7 @@ register_integrator("pssmlt_simple", lambda props: PssmltSimple(props))
 register_integrator("pssmlt", lambda props: PssmltPath(props))  # pssmltpath.py:193
 register_integrator("path_test", lambda props: PathIntegrator(props))
 register_integrator("nrc", lambda props: NRCIntegrator(props))
+register_integrator("nerad", lambda props: NeradIntegrator(props))
 
 
 def _bind_scene(ctx, scene) -> None:

@@ -155,6 +155,13 @@ class Integrator:
     def __init__(self, field: Field, batch_size: int = 2 ** 14, M: int = 32):
         self.field, self.batch_size, self.M = field, int(batch_size), int(M)
 
+    def render(self, scene, sensor=None, seed: int = 0, spp: int = 1, develop: bool = True, evaluate: bool = True):
+        """integrator.render(scene, sensor, seed, spp) (nerad.py:399): sample()
+        (:235-254) for every camera lane, on the wavefront (MTX_INT_NERAD)."""
+        from .integrators import NeradIntegrator
+
+        return NeradIntegrator({"field": self.field}).render(scene, seed=seed, spp=spp, develop=develop)
+
     def sample_lhs(self, scene, si: np.ndarray, ctx=None) -> np.ndarray:
         """Field(si) at IntersectionSampler points ((n, 9) rows)."""
         return self.field(si[:, 3:6], si[:, 6:9], ctx=ctx)

@@ -52,6 +52,7 @@ def lib():
             "orc_field_features": [C.POINTER(_abi.FieldDesc), u64, vp, vp, vp],
             "orc_nerad_lhs": [SD, C.POINTER(_abi.NeradTables), u32, u32, vp],
             "orc_nerad_rhs": [SD, C.POINTER(_abi.NeradTables), u32, u32, u32, u32, vp],
+            "orc_nerad_render_samples": [SD, RA, vp, vp],
         }
         for k, a in sig.items():
             getattr(L, k).argtypes = a
@@ -279,3 +280,14 @@ def nerad_compose(lanes, field_out, M):
     for j in range(M):
         acc = acc + Lm[:, j]
     return L, acc / f32(M)
+
+
+def nerad_render_samples(scene, args):
+    """Integrator.sample lanes of a render (nerad.py:235-254): (n, 16) rows as
+    nerad_rhs (L_nee = 0) and the film positions (n, 2), (pixel, sample) order."""
+    n = (args.y1 - args.y0) * scene.width * args.spp
+    lanes = np.zeros((n, 16), np.float32)
+    pos = np.zeros((n, 2), np.float32)
+    d = scene.desc()
+    lib().orc_nerad_render_samples(C.byref(d), C.byref(args), lanes.ctypes.data, pos.ctypes.data)
+    return lanes, pos

@@ -1295,6 +1295,35 @@ void orc_nerad_lane(const SceneView &s, const SurfaceInteraction &si, Pcg32 &rng
   for (int k = 0; k < 16; ++k) o[k] = vals[k];
 }
 
+// Integrator.sample (nerad.py:235-254) for one camera lane, without the
+// field term: next_smooth_si from the first hit, f (zero if invalid, :250),
+// Le and the field query; the caller forms L = Field * f + Le (:251-252).
+void orc_nerad_render_lane(const SceneView &s, Pcg32 &rng, const Ray &ray, float *o) {
+  SurfaceInteraction si = intersect(s, ray);  // :247
+  V3 f = v3s(1.f);
+  float t1 = rng.next_1d();
+  V2 t2 = rng.next_2d();
+  BSDFSample bs;
+  V3 w = sample_or_null(s, si, t1, t2, &bs);
+  bool chain = (bs.type & BF_DELTA) != 0;
+  uint32_t depth = 0;
+  while (chain) {
+    f = f * w;
+    si = intersect(s, spawn_ray(si.p, si.n, to_world(si.sh, bs.wo)));
+    t1 = rng.next_1d();
+    t2 = rng.next_2d();
+    w = sample_or_null(s, si, t1, t2, &bs);
+    depth += 1;
+    chain = (bs.type & BF_DELTA) != 0 && depth < 10;
+  }
+  f = f * (si.valid ? 1.f : 0.f);
+  const V3 le = emitter_eval(s, si.emitter, si.wi);
+  const V3 wi = to_world(si.sh, si.wi);
+  const float vals[16] = {0.f, 0.f, 0.f, f.x, f.y, f.z, le.x, le.y, le.z, si.valid ? 1.f : 0.f,
+                          si.p.x, si.p.y, si.p.z, wi.x, wi.y, wi.z};
+  for (int k = 0; k < 16; ++k) o[k] = vals[k];
+}
+
 }  // namespace
 
 extern "C" {
@@ -1337,6 +1366,30 @@ int orc_nerad_rhs(const mtx_scene_desc *d, const mtx_nerad_tables *h, uint32_t l
     const SurfaceInteraction si = nerad_point(s, nt.t, lhs_seed, (uint32_t)(i / M), &wi, &ss);
     Pcg32 rng = sampler_lane(rhs_seed, (uint32_t)i);
     orc_nerad_lane(s, si, rng, lanes + 16 * i);
+  }
+  return 0;
+}
+
+// Integrator.sample lanes of a render (camera lanes as orc_render_samples):
+// 16 floats per sample (see orc_nerad_render_lane) and the film position.
+int orc_nerad_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float *lanes, float *pos) {
+  SceneView s = make_view(d);
+  const uint32_t W = s.camera.width, H = s.camera.height;
+  const uint64_t npx = (uint64_t)(a->y1 - a->y0) * W;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t p = 0; p < (int64_t)npx; ++p) {
+    const uint32_t y = a->y0 + (uint32_t)(p / W), x = (uint32_t)(p % W);
+    for (uint32_t k = 0; k < a->spp; ++k) {
+      const uint32_t lane = (uint32_t)(((uint64_t)y * W + x) * a->spp_total + a->sample_offset + k);
+      Pcg32 rng = sampler_lane(a->seed, lane);
+      const V2 u = rng.next_2d();
+      const float sx = (float)x + u.x, sy = (float)y + u.y;
+      const Ray ray = camera_ray(s.camera, V2{sx / (float)W, sy / (float)H});
+      const uint64_t o = (uint64_t)p * a->spp + k;
+      orc_nerad_render_lane(s, rng, ray, lanes + 16 * o);
+      pos[2 * o] = sx;
+      pos[2 * o + 1] = sy;
+    }
   }
   return 0;
 }

@@ -291,3 +291,25 @@ def test_training_reduces_loss(nscene):
     assert np.array_equal(field.weights[0], ws[0].astype(np.float16))
     feat = field.features(p, wi, ctx=tr.ctx)
     np.testing.assert_allclose(live, field.mlp_reference(feat), atol=2e-2 * max(1.0, np.abs(live).max()))
+
+
+@pytest.mark.gpu
+def test_nerad_render_bit_exact(nscene, oracle):
+    """Integrator.sample as a renderer (nerad.py:235-254): every sample's
+    L = Field(si) * f + Le and the film bit-exact against the oracle's lanes
+    composed with the same field evaluation."""
+    from mtx import load_dict
+
+    field = _field(nscene, seed=4)
+    integ = load_dict({"type": "nerad", "field": field})
+    spp = 3
+    film = integ.render_film(nscene, seed=2, spp=spp)
+    a = integ.render_args(nscene, 2, spp)
+    lanes, pos = oracle.nerad_render_samples(nscene, a)
+    valid = lanes[:, 9] > 0
+    fv = np.zeros((len(lanes), 3), np.float32)
+    fv[valid] = field(lanes[valid, 10:13], lanes[valid, 13:16])
+    L = fv * lanes[:, 3:6] + lanes[:, 6:9]
+    ref = oracle.film(nscene.width, 0, nscene.height, spp, np.ascontiguousarray(L, np.float32), pos)
+    assert np.array_equal(film, ref), int((film != ref).sum())
+    assert valid.mean() > 0.5 and film[..., 3].sum() > 0
