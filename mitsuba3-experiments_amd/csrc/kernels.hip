@@ -136,11 +136,10 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   } else {
     depth = 1;  // path.py:230, nrc.py:39
   }
+  // throughput = 1, eta = 1, L = 0, prev_bsdf_pdf = 1 (path-mis.py:45), prev_p = 0 are
+  // not stored: the bounce-0 shade uses these constants (kInitThr / kInitL / kInitPrev)
   b.ray_o[i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
   b.ray_d[i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
-  b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
-  b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1 (path-mis.py:45)
-  b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   b.pos[i] = pos;
   b.queue[0][i] = i;
@@ -187,6 +186,12 @@ __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const fl
 // ---------------------------------------------------------------------------
 // Shading: one bounce of the integrator for one path.
 // ---------------------------------------------------------------------------
+// Initial path state (init_path, k_rs_begin): throughput 1 / eta 1, L 0 /
+// prev_bsdf_pdf 1, prev_p 0 / spread 0. Never stored: bounce-0 shades use it.
+__device__ constexpr float4 kInitThr = {1.f, 1.f, 1.f, 1.f};
+__device__ constexpr float4 kInitL = {0.f, 0.f, 0.f, 1.f};
+__device__ constexpr float4 kInitPrev = {0.f, 0.f, 0.f, 0.f};
+
 struct ShadeIO {
   ShadowRec rec;
   bool emit;
@@ -226,7 +231,10 @@ template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p,
                                            uint32_t bounce, uint32_t path, ShadeIO &io) {
-  const float4 ro = b.ray_o[path], rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
+  const float4 ro = b.ray_o[path], rd = b.ray_d[path];
+  // bounce 0: the state init_path / k_rs_begin would have stored (not read)
+  const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
+  const float4 pv = bounce == 0 ? kInitPrev : b.prev[path];
   const uint4 mi = b.misc[path];
   const float4 h = b.hit[path];
   Pcg32 rng;
@@ -601,7 +609,11 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
 template <bool RENDER>
 __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                             uint32_t bounce, uint32_t path, ShadeIO &io) {
-  const float4 rd = b.ray_d[path], Lr = b.L[path], pv = b.prev[path], th = b.thr[path];
+  const float4 rd = b.ray_d[path];
+  // a rendered lane's bounce-0 state is the camera raygen's (nothing stored)
+  const float4 Lr = (RENDER && bounce == 0) ? kInitL : b.L[path];
+  const float4 pv = (RENDER && bounce == 0) ? kInitPrev : b.prev[path];
+  const float4 th = (RENDER && bounce == 0) ? kInitThr : b.thr[path];
   const uint4 mi = b.misc[path];
   const float4 h = b.hit[path];
   Pcg32 rng;

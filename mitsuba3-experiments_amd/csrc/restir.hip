@@ -139,9 +139,7 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
       const Ray nr = spawn_ray(si.p, si.n, to_world(si.sh, wo));
       b.ray_o[path] = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
       b.ray_d[path] = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
-      b.thr[path] = make_float4(1.f, 1.f, 1.f, 1.f);
-      b.L[path] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
-      b.prev[path] = make_float4(0.f, 0.f, 0.f, 0.f);
+      // throughput 1, L 0, prev_bsdf_pdf 1, prev_p 0: the bounce-0 shade's constants
       b.misc[path] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
       enq = true;
     } else {
