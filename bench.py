@@ -48,8 +48,8 @@ def parse():
     p.add_argument("--iterations", type=int, default=20, help="PSSMLT Metropolis iterations (C3 short variant)")
     p.add_argument("--frames", type=int, default=10, help="ReSTIR GI timed frames")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                   help="--workload pssmlt/pssmltpath/restir with N>1 ranks: nccl (RCCL) or gloo (host-staged; "
-                        "lets several ranks share one GPU in a rehearsal)")
+                   help="N>1 ranks: nccl (RCCL, the measurement) or gloo (host-staged device tensors; lets "
+                        "several ranks share one GPU in a rehearsal of the N>1 code path)")
     return p.parse_args()
 
 
@@ -67,9 +67,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU (--backend gloo)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from mtx import PathIntegrator, scene
 
@@ -107,7 +111,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # visit counters (deterministic): one untimed step, same seed as step 0
