@@ -780,6 +780,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   p.px0 = a->y0 * W;
   p.n_px = (a->y1 - a->y0) * W;
   p.band_y0 = a->y0;
+  p.band_px = (a->y1 - a->y0) * W;
   p.n_paths = nb;
   p.restir = 1;
   p.sample_major = c->sample_major;
@@ -913,6 +914,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.px0 = px0;
     p.n_px = std::min(px_per_chunk, a->y1 * W - px0);
     p.band_y0 = a->y0;
+    p.band_px = (a->y1 - a->y0) * W;
     p.n_paths = p.n_px * a->spp;
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;

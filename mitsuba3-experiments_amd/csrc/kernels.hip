@@ -851,9 +851,9 @@ __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkPara
     __syncthreads();
   }
   if (q >= p.n_px) return;
-  const size_t o = 9 * ((size_t)(pix - p.band_y0 * p.width));
+  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: 9 planes of band_px
 #pragma unroll
-  for (int k = 0; k < 9; ++k) contrib[o + k] = acc[k];
+  for (int k = 0; k < 9; ++k) contrib[(size_t)k * p.band_px + o] = acc[k];
 }
 
 __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
@@ -883,13 +883,14 @@ __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
       }
     }
   }
-  const size_t o = 9 * ((size_t)(pix - p.band_y0 * p.width));
+  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: 9 planes of band_px
 #pragma unroll
-  for (int k = 0; k < 9; ++k) contrib[o + k] = acc[k];
+  for (int k = 0; k < 9; ++k) contrib[(size_t)k * p.band_px + o] = acc[k];
 }
 
 __global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, uint32_t y0, uint32_t y1) {
   const uint32_t FW = W + 2, FH = (y1 - y0) + 2;
+  const size_t P = (size_t)(y1 - y0) * W;  // contrib: 9 planes of the band's pixels
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= FW * FH) return;
   const int px = (int)(q % FW) - 1, py = (int)(y0 + q / FW) - 1;
@@ -900,7 +901,7 @@ __global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, u
     for (int dx = 0; dx < 3; ++dx) {
       const int sxp = px - dx + 1, syp = py - dy + 1;
       if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
-      const float4 c = contrib[9 * ((size_t)(syp - (int)y0) * W + sxp) + dy * 3 + dx];
+      const float4 c = contrib[(size_t)(dy * 3 + dx) * P + (size_t)(syp - (int)y0) * W + sxp];
       r = r + c.x;
       g = g + c.y;
       bl = bl + c.z;
@@ -1048,10 +1049,10 @@ __global__ void k_mlt_film(WaveBuffers b, ChunkParams p, float4 *contrib) {
   if (q >= p.n_px) return;
   const uint32_t pix = p.px0 + q;
   const int y = (int)(pix / p.width), x = (int)(pix - (uint32_t)y * p.width);
-  const size_t o = 9 * ((size_t)(pix - p.band_y0 * p.width));
+  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: 9 planes of band_px
   float4 acc[9];
 #pragma unroll
-  for (int k = 0; k < 9; ++k) acc[k] = contrib[o + k];
+  for (int k = 0; k < 9; ++k) acc[k] = contrib[(size_t)k * p.band_px + o];
   for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
     const uint32_t c = q * p.spp + sidx;
     const float4 lc = b.mlt_L[c];
@@ -1073,7 +1074,7 @@ __global__ void k_mlt_film(WaveBuffers b, ChunkParams p, float4 *contrib) {
     }
   }
 #pragma unroll
-  for (int k = 0; k < 9; ++k) contrib[o + k] = acc[k];
+  for (int k = 0; k < 9; ++k) contrib[(size_t)k * p.band_px + o] = acc[k];
 }
 
 // ---------------------------------------------------------------------------

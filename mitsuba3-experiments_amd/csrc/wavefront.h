@@ -141,6 +141,7 @@ struct ChunkParams {
   uint32_t width, height;
   uint32_t px0, n_px;   // first film pixel (y*W+x) of the chunk and pixel count
   uint32_t band_y0;     // first row of the rendered band (film/contrib origin)
+  uint32_t band_px;     // pixels of the band (contrib: 9 planes of band_px float4)
   uint32_t n_paths;
   float nrc_c;
   uint32_t stats;
