@@ -106,6 +106,38 @@ MTX_HD Microfacet mat_distr(const mtx_material &m) {
 // One-sided base BSDFs. `wi` and `wo` are in the local shading frame.
 // ---------------------------------------------------------------------------
 
+// roughplastic eval + pdf (one copy, shared by eval_pdf and sample)
+MTX_HD void roughplastic_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val,
+                                  float *pdf) {
+  float ci = wi.z, co = wo.z;
+  if (!(ci > 0.f && co > 0.f)) return;
+  Microfacet distr = mat_distr(m);
+  const float *tab = d.tables + m.table;
+  // --- eval ---
+  V3 H = normalize(wo + wi);
+  float D = distr.eval(H);
+  float F = fresnel_dielectric(dot(wi, H), m.eta).r;
+  float G = distr.G(wi, wo, H);
+  float spec = F * D * G / (4.f * ci);
+  V3 result = v3s(spec);
+  float t_i = lerp_table(tab, ci), t_o = lerp_table(tab, co);
+  V3 diff = mat_color(d, m, uv);
+  V3 denom = (m.flags & MTX_MF_NONLINEAR) ? (v3s(1.f) - diff * m.internal_refl) : v3s(1.f - m.internal_refl);
+  diff = diff / denom;
+  float inv_eta_2 = 1.f / sqr(m.eta);
+  diff = diff * (kInvPi * inv_eta_2 * co * t_i * t_o);
+  *val = result + diff;
+  // --- pdf ---
+  float prob_specular = (1.f - t_i) * m.spec_weight;
+  float prob_diffuse = t_i * (1.f - m.spec_weight);
+  prob_specular = prob_specular / (prob_specular + prob_diffuse);
+  prob_diffuse = 1.f - prob_specular;
+  float p = distr.eval(H) * distr.smith_g1(wi, H) / (4.f * ci);
+  p *= prob_specular;
+  p = p + prob_diffuse * square_to_cosine_hemisphere_pdf(wo);
+  *pdf = p;
+}
+
 // eval + pdf together (upstream eval_pdf)
 MTX_HD void base_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
   float ci = wi.z, co = wo.z;
@@ -120,35 +152,9 @@ MTX_HD void base_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
       }
       break;
     }
-    case MTX_MAT_ROUGHPLASTIC: {
-      if (!(ci > 0.f && co > 0.f)) break;
-      Microfacet distr = mat_distr(m);
-      const float *tab = d.tables + m.table;
-      // --- eval ---
-      V3 H = normalize(wo + wi);
-      float D = distr.eval(H);
-      float F = fresnel_dielectric(dot(wi, H), m.eta).r;
-      float G = distr.G(wi, wo, H);
-      float spec = F * D * G / (4.f * ci);
-      V3 result = v3s(spec);
-      float t_i = lerp_table(tab, ci), t_o = lerp_table(tab, co);
-      V3 diff = mat_color(d, m, uv);
-      V3 denom = (m.flags & MTX_MF_NONLINEAR) ? (v3s(1.f) - diff * m.internal_refl) : v3s(1.f - m.internal_refl);
-      diff = diff / denom;
-      float inv_eta_2 = 1.f / sqr(m.eta);
-      diff = diff * (kInvPi * inv_eta_2 * co * t_i * t_o);
-      *val = result + diff;
-      // --- pdf ---
-      float prob_specular = (1.f - t_i) * m.spec_weight;
-      float prob_diffuse = t_i * (1.f - m.spec_weight);
-      prob_specular = prob_specular / (prob_specular + prob_diffuse);
-      prob_diffuse = 1.f - prob_specular;
-      float p = distr.eval(H) * distr.smith_g1(wi, H) / (4.f * ci);
-      p *= prob_specular;
-      p = p + prob_diffuse * square_to_cosine_hemisphere_pdf(wo);
-      *pdf = p;
+    case MTX_MAT_ROUGHPLASTIC:
+      roughplastic_eval_pdf(d, m, uv, wi, wo, val, pdf);
       break;
-    }
     case MTX_MAT_ROUGHCONDUCTOR: {
       if (!(ci > 0.f && co > 0.f)) break;
       Microfacet distr = mat_distr(m);
@@ -305,9 +311,9 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
         bs->wo = square_to_cosine_hemisphere(u2);
         bs->type = BF_DIFFUSE_REFLECTION;
       }
-      V3 val;
-      float pdf;
-      base_eval_pdf(d, m, uv, wi, bs->wo, &val, &pdf);
+      V3 val = v3s(0.f);
+      float pdf = 0.f;
+      roughplastic_eval_pdf(d, m, uv, wi, bs->wo, &val, &pdf);
       bs->pdf = pdf;
       if (pdf > 0.f) weight = val / pdf;
       break;
@@ -322,37 +328,40 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
 // ---------------------------------------------------------------------------
 
 MTX_HD void twosided_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
-  if (!(m.flags & MTX_MF_TWOSIDED)) {
-    base_eval_pdf(d, m, uv, wi, wo, val, pdf);
-    return;
-  }
-  if (wi.z > 0.f) {
-    base_eval_pdf(d, m, uv, wi, wo, val, pdf);
-  } else if (wi.z < 0.f) {
-    base_eval_pdf(d, m, uv, V3{wi.x, wi.y, -wi.z}, V3{wo.x, wo.y, -wo.z}, val, pdf);
-  } else {
+  // one call of the base BSDF (flipped to the front side when wi.z < 0)
+  const bool two = (m.flags & MTX_MF_TWOSIDED) != 0, flip = two && wi.z < 0.f;
+  if (two && !(wi.z > 0.f) && !flip) {
     *val = v3s(0.f);
     *pdf = 0.f;
+    return;
   }
+  base_eval_pdf(d, m, uv, flip ? V3{wi.x, wi.y, -wi.z} : wi, flip ? V3{wo.x, wo.y, -wo.z} : wo, val, pdf);
 }
 
 MTX_HD V3 twosided_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
-  if (!(m.flags & MTX_MF_TWOSIDED)) return base_sample(d, m, uv, wi, u1, u2, bs);
-  if (wi.z > 0.f) return base_sample(d, m, uv, wi, u1, u2, bs);
-  if (wi.z < 0.f) {
-    V3 w = base_sample(d, m, uv, V3{wi.x, wi.y, -wi.z}, u1, u2, bs);
-    bs->wo.z = -bs->wo.z;
-    return w;
+  const bool two = (m.flags & MTX_MF_TWOSIDED) != 0, flip = two && wi.z < 0.f;
+  if (two && !(wi.z > 0.f) && !flip) {
+    bs->wo = v3s(0.f);
+    bs->pdf = 0.f;
+    bs->eta = 0.f;
+    bs->type = 0;
+    return v3s(0.f);
   }
-  bs->wo = v3s(0.f);
-  bs->pdf = 0.f;
-  bs->eta = 0.f;
-  bs->type = 0;
-  return v3s(0.f);
+  const V3 w = base_sample(d, m, uv, flip ? V3{wi.x, wi.y, -wi.z} : wi, u1, u2, bs);
+  if (flip) bs->wo.z = -bs->wo.z;
+  return w;
 }
 
 // BSDF::eval_pdf (value includes the cosine foreshortening, as upstream)
-MTX_HD void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
+// A/B knob (device only): MTX_BSDF_NOINLINE=1 keeps the two BSDF entry points
+// out of line (one copy of each material's code instead of one per call site).
+#if defined(MTX_DEVICE_COMPILE) && defined(MTX_BSDF_NOINLINE) && MTX_BSDF_NOINLINE
+#define MTX_BSDF_ENTRY __host__ __device__ __noinline__
+#else
+#define MTX_BSDF_ENTRY MTX_HD
+#endif
+
+MTX_BSDF_ENTRY void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
   twosided_eval_pdf(d, m, uv, wi, wo, val, pdf);
   if (m.flags & MTX_MF_MASK) {
     *val = *val * m.opacity;
@@ -361,15 +370,12 @@ MTX_HD void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
 }
 
 // BSDF::sample -> (BSDFSample, weight = value/pdf)
-MTX_HD V3 bsdf_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
-  if (!(m.flags & MTX_MF_MASK)) return twosided_sample(d, m, uv, wi, u1, u2, bs);
+MTX_BSDF_ENTRY V3 bsdf_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
   // mask: nested lobe with probability `opacity`, else a Null pass-through.
   // The factors opacity / (1 - opacity) cancel in the weight and are not
   // included in bs.pdf (upstream mask.cpp).
-  float opacity = m.opacity;
-  if (u1 < opacity) {
-    return twosided_sample(d, m, uv, wi, u1 / opacity, u2, bs);
-  }
+  const bool mask = (m.flags & MTX_MF_MASK) != 0;
+  if (!mask || u1 < m.opacity) return twosided_sample(d, m, uv, wi, mask ? u1 / m.opacity : u1, u2, bs);
   bs->wo = -wi;
   bs->eta = 1.f;
   bs->pdf = 1.f;
