@@ -212,6 +212,25 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
   bs->eta = 1.f;
   bs->type = 0;
   V3 weight = v3s(0.f);
+  // The rough materials draw their microfacet normal in one shared call (one
+  // inlined copy of the visible-normal sampler instead of three); same inputs,
+  // same arithmetic as calling it inside each case.
+  bool need_mf = m.type == MTX_MAT_ROUGHCONDUCTOR || m.type == MTX_MAT_ROUGHDIELECTRIC;
+  V3 wi_mf = m.type == MTX_MAT_ROUGHDIELECTRIC ? mulsign3(wi, ci) : wi;
+  float rp_prob_specular = 0.f;
+  bool rp_specular = false;
+  if (m.type == MTX_MAT_ROUGHPLASTIC && ci > 0.f) {
+    const float *tab = d.tables + m.table;
+    float t_i = lerp_table(tab, ci);
+    float prob_specular = (1.f - t_i) * m.spec_weight;
+    float prob_diffuse = t_i * (1.f - m.spec_weight);
+    rp_prob_specular = prob_specular / (prob_specular + prob_diffuse);
+    rp_specular = u1 < rp_prob_specular;
+    need_mf = rp_specular;
+  }
+  float mf_pdf = 0.f;
+  V3 mf_n = v3s(0.f);
+  if (need_mf) mf_n = mat_distr(m).sample(wi_mf, u2, &mf_pdf);
   switch (m.type) {
     case MTX_MAT_DIFFUSE: {
       bs->wo = square_to_cosine_hemisphere(u2);
@@ -248,8 +267,8 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
     }
     case MTX_MAT_ROUGHCONDUCTOR: {
       Microfacet distr = mat_distr(m);
-      float pdf;
-      V3 mn = distr.sample(wi, u2, &pdf);
+      float pdf = mf_pdf;
+      V3 mn = mf_n;
       bs->wo = reflect_m(wi, mn);
       bs->eta = 1.f;
       bs->type = BF_GLOSSY_REFLECTION;
@@ -265,8 +284,8 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
     }
     case MTX_MAT_ROUGHDIELECTRIC: {
       Microfacet distr = mat_distr(m);
-      float pdf;
-      V3 mn = distr.sample(mulsign3(wi, ci), u2, &pdf);
+      float pdf = mf_pdf;
+      V3 mn = mf_n;
       bool active = pdf != 0.f;
       FresnelResult fr = fresnel_dielectric(dot(wi, mn), m.eta);
       float F = fr.r;
@@ -294,18 +313,9 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
     }
     case MTX_MAT_ROUGHPLASTIC: {
       if (!(ci > 0.f)) break;
-      const float *tab = d.tables + m.table;
-      float t_i = lerp_table(tab, ci);
-      float prob_specular = (1.f - t_i) * m.spec_weight;
-      float prob_diffuse = t_i * (1.f - m.spec_weight);
-      prob_specular = prob_specular / (prob_specular + prob_diffuse);
-      bool sample_specular = u1 < prob_specular;
       bs->eta = 1.f;
-      if (sample_specular) {
-        Microfacet distr = mat_distr(m);
-        float unused;
-        V3 mn = distr.sample(wi, u2, &unused);
-        bs->wo = reflect_m(wi, mn);
+      if (rp_specular) {
+        bs->wo = reflect_m(wi, mf_n);
         bs->type = BF_GLOSSY_REFLECTION;
       } else {
         bs->wo = square_to_cosine_hemisphere(u2);
