@@ -75,13 +75,24 @@ MTX_HD float wide_decode(float origin, float scale, uint32_t q) { return origin 
 // four keys are sorted ascending (5 compare-exchanges), so the visit order is
 // by entry distance, near-ties by slot. Returns the number of hits.
 // qlx.. hold the four children's 8-bit bounds, child k in bits [8k, 8k+8).
+// 2^e * x for the int8 exponent in bits [shift, shift + 8) of eb: exact
+// scaling (= wide_scale(e) * x), one v_bfe_i32 + v_ldexp_f32 on the device.
+MTX_HD float wide_axis_scale(uint32_t eb, int shift, float x) {
+  const int e = (int)(int8_t)(uint8_t)((eb >> shift) & 0xffu);
+#ifdef MTX_DEVICE_COMPILE
+  return __builtin_amdgcn_ldexpf(x, e);
+#else
+  return ldexpf(x, e);
+#endif
+}
+
 MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint32_t eb, uint32_t qlx,
                            uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz, float tfar,
                            uint32_t key[4]) {
   const int nch = (int)(eb >> 24);
-  const float ax = wide_scale(eb) * r.idir.x, bx = (ox - r.o.x) * r.idir.x;
-  const float ay = wide_scale(eb >> 8) * r.idir.y, by = (oy - r.o.y) * r.idir.y;
-  const float az = wide_scale(eb >> 16) * r.idir.z, bz = (oz - r.o.z) * r.idir.z;
+  const float ax = wide_axis_scale(eb, 0, r.idir.x), bx = (ox - r.o.x) * r.idir.x;
+  const float ay = wide_axis_scale(eb, 8, r.idir.y), by = (oy - r.o.y) * r.idir.y;
+  const float az = wide_axis_scale(eb, 16, r.idir.z), bz = (oz - r.o.z) * r.idir.z;
   // near / far bound of each axis from the direction's sign: fma(q, a, b)
   // is monotonic in q, so this equals min / max of the two planes (NaN
   // planes of a zero direction component are ignored either way)
