@@ -10,8 +10,13 @@
 //   passes run in LDS on a tile plus its 2047-element halo, the remaining
 //   passes (offsets >= 2048) as coalesced full-array passes.
 // * hashgrid_build: hashgrid.py:16-90 — scalar bbox reduction, cell hash,
-//   atomic per-cell rank (the reference's winner election, :52-63), exclusive
-//   scan (:65-76), scatter of sample indices (:79-84).
+//   then the cell grouping as one stable radix sort of (cell, sample index)
+//   pairs: sample_idx is the sorted index column, so within a cell the
+//   samples come in ascending index order (one valid outcome of the
+//   reference's race-defined winner election, :52-63, and the exact order of
+//   the CPU restatement); cell_offset (:65-76) and cell_size come from the
+//   run boundaries of the sorted cells. Sequential passes replace the
+//   random-address rank atomics and scatter.
 // * scatter_reduce_f32: reductions.py:12-54 — the reference serialises each
 //   target with host-synchronised winner-election rounds (race-defined
 //   order). Here: one stable radix sort of (index, value) pairs (rocPRIM,
@@ -22,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "mtx.h"
 #include "prims.h"
@@ -212,7 +218,14 @@ __global__ void k_hs_pass(const float *__restrict__ x, float *__restrict__ y, ui
 __global__ void k_minmax(const float *__restrict__ p, uint64_t n3, float2 *partial) {
   __shared__ float smin[256], smax[256];
   float lo = INFINITY, hi = -INFINITY;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n3; i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float4 *p4 = reinterpret_cast<const float4 *>(p);  // 256-B aligned device buffer
+  for (uint64_t i = t0; i < n3 / 4; i += stride) {
+    const float4 v = p4[i];
+    lo = fminf(lo, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
+    hi = fmaxf(hi, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+  }
+  for (uint64_t i = n3 / 4 * 4 + t0; i < n3; i += stride) {
     lo = fminf(lo, p[i]);
     hi = fmaxf(hi, p[i]);
   }
@@ -250,7 +263,7 @@ __global__ void k_minmax_final(float2 *partial, int m) {
 }
 
 __global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t res, uint32_t n_cells,
-                             const float2 *bbox, uint32_t *cell, uint32_t *cell_size, uint32_t *rank) {
+                             const float2 *bbox, uint32_t *cell) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float2 bb = *bbox;
@@ -258,16 +271,89 @@ __global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t r
   const uint32_t x = (uint32_t)((p[i] - bbmin) / ext * fres);
   const uint32_t y = (uint32_t)((p[n + i] - bbmin) / ext * fres);
   const uint32_t z = (uint32_t)((p[2 * n + i] - bbmin) / ext * fres);
-  const uint32_t h = ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
-  cell[i] = h;
-  rank[i] = atomicAdd(&cell_size[h], 1u);
+  cell[i] = ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
 }
 
-__global__ void k_hash_fill(uint64_t n, const uint32_t *cell, const uint32_t *rank, const uint32_t *cell_offset,
-                            uint32_t *sample_idx) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  sample_idx[cell_offset[cell[i]] + rank[i]] = (uint32_t)i;
+// cell_offset[c] = number of samples with cell < c and cell_size[c], from
+// the sorted cells. Block b holds keys [i0, i1) (kHashTile of them) in LDS
+// and owns the cells (key[i0-1], key[i1-1]] (the first block from cell 0,
+// the last up to n_cells - 1): each cell is written once, coalesced, with a
+// binary search in LDS for its first position in the tile, a short walk to
+// the run's end (and a search in global memory for a run that continues
+// past the tile).
+constexpr int kHashTile = 2048;
+__global__ __launch_bounds__(256) void k_hash_ranges(const uint32_t *__restrict__ key, uint64_t n, uint32_t n_cells,
+                                                      uint32_t *__restrict__ cell_offset,
+                                                      uint32_t *__restrict__ cell_size) {
+  __shared__ uint32_t tk[kHashTile];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kHashTile;
+  const uint32_t cnt = (uint32_t)min((uint64_t)kHashTile, n - i0);
+  {  // eight independent loads in flight (clamped index: no branch between them)
+    uint32_t v[kHashTile / 256];
+#pragma unroll
+    for (int r = 0; r < kHashTile / 256; ++r) v[r] = key[i0 + min(threadIdx.x + 256u * r, cnt - 1u)];
+#pragma unroll
+    for (int r = 0; r < kHashTile / 256; ++r) tk[threadIdx.x + 256u * r] = v[r];
+  }
+  __syncthreads();
+  // cells are < n_cells <= 2^32 - 1, so c + 1 fits in 32 bits
+  const uint32_t lo = i0 == 0 ? 0u : key[i0 - 1] + 1u;
+  const uint32_t hi = i0 + cnt == n ? n_cells - 1u : tk[cnt - 1];
+  if (hi < lo) return;
+  for (uint32_t c = lo + threadIdx.x; c <= hi && c >= lo; c += 256) {
+    uint32_t l = 0, h = cnt;  // first tile position with key >= c
+    while (l < h) {
+      const uint32_t m = (l + h) >> 1;
+      if (tk[m] < c)
+        l = m + 1;
+      else
+        h = m;
+    }
+    uint32_t e = l;
+    while (e < cnt && tk[e] == c) ++e;
+    uint64_t ge = i0 + e;
+    if (e == cnt && ge < n && key[ge] == c) {  // the run of c continues past the tile:
+      uint64_t last = ge, step = 1, probe = ge + 1;  // gallop, then bisect: O(log run) loads
+      while (probe < n && key[probe] == c) {
+        last = probe;
+        step *= 2;
+        probe = last + step;
+      }
+      uint64_t gl = last + 1, gh = min(probe, (uint64_t)n);  // first key > c in [gl, gh]
+      while (gl < gh) {
+        const uint64_t m = (gl + gh) >> 1;
+        if (key[m] <= c)
+          gl = m + 1;
+        else
+          gh = m;
+      }
+      ge = gl;
+    }
+    cell_offset[c] = (uint32_t)(i0 + l);
+    cell_size[c] = (uint32_t)(ge - (i0 + l));
+  }
+}
+
+// Sparse case (n_cells > 4 n): lower bounds of c and c + 1 in the sorted
+// cells, one thread per cell.
+__global__ void k_hash_offsets_search(const uint32_t *__restrict__ key, uint64_t n, uint32_t n_cells,
+                                      uint32_t *__restrict__ cell_offset, uint32_t *__restrict__ cell_size) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n_cells) return;
+  auto lower = [&](uint64_t v) -> uint64_t {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if ((uint64_t)key[mid] < v)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  const uint64_t b = lower(c);
+  cell_offset[c] = (uint32_t)b;
+  cell_size[c] = (uint32_t)(lower(c + 1) - b);
 }
 
 // --------------------------- scatter reduce -------------------------------
@@ -335,28 +421,42 @@ int scan_f32_hs(float *a, float *b, uint64_t n, float **result, hipStream_t st) 
   return MTX_OK;
 }
 
+static unsigned key_bits(uint64_t n_target);
+
+static size_t hash_sort_temp_bytes(uint64_t n, uint32_t n_cells) {
+  size_t bytes = 0;
+  rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                            rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)nullptr, (size_t)n, 0u,
+                            key_bits(n_cells));
+  return bytes;
+}
+
 size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells) {
-  return 8ull * 1025 + 4ull * n + scan_workspace_bytes(n_cells) + 16;
+  return 8ull * 1025 + 4ull * n + hash_sort_temp_bytes(n, n_cells) + 512;
 }
 
 int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
                    uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st) {
   char *w = (char *)ws;
   float2 *partial = (float2 *)w;
-  uint32_t *rank = (uint32_t *)(w + 8 * 1025);
-  void *scan_ws = (void *)(w + ((8 * 1025 + 4 * n + 7) & ~(uint64_t)7));
+  uint32_t *keys = (uint32_t *)(w + 8 * 1025);
+  void *temp = (void *)(((uintptr_t)(keys + n) + 255) & ~(uintptr_t)255);
+  size_t temp_bytes = hash_sort_temp_bytes(n, n_cells);
   const int m = 1024;
   hipLaunchKernelGGL(k_minmax, dim3(m), dim3(256), 0, st, p, 3 * n, partial);
   hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(256), 0, st, partial, m);
-  if (hipMemsetAsync(cell_size, 0, 4ull * n_cells, st) != hipSuccess) {
-    mtx_set_error("hashgrid: memset failed");
+  hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell);
+  if (rocprim::radix_sort_pairs(temp, temp_bytes, cell, keys, rocprim::counting_iterator<uint32_t>(0u), sample_idx,
+                                (size_t)n, 0u, key_bits(n_cells), st) != hipSuccess) {
+    mtx_set_error("hashgrid: radix sort failed");
     return MTX_E_HIP;
   }
-  hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell,
-                     cell_size, rank);
-  int rc = scan_u32(cell_size, cell_offset, n_cells, 0, scan_ws, st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_hash_fill, dim3(nblk(n, 256)), dim3(256), 0, st, n, cell, rank, cell_offset, sample_idx);
+  if ((uint64_t)n_cells > 4 * n)
+    hipLaunchKernelGGL(k_hash_offsets_search, dim3(nblk(n_cells, 256)), dim3(256), 0, st, keys, n, n_cells,
+                       cell_offset, cell_size);
+  else
+    hipLaunchKernelGGL(k_hash_ranges, dim3(nblk(n, kHashTile)), dim3(256), 0, st, keys, n, n_cells, cell_offset,
+                       cell_size);
   return MTX_OK;
 }
 

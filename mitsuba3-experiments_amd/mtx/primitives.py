@@ -41,8 +41,9 @@ def hash_cells(p, resolution: int, n_cells: int):
 class HashGrid:
     """hashgrid.py:15-90: build a 3-D spatial hash grid over `sample` points
     (Point3f as a [3, n] array). Attributes: cell_size, cell_offset (exclusive
-    scan), sample_idx (samples grouped by cell; order within a cell is
-    race-defined, as in the reference), cell (per-sample cell index)."""
+    scan), sample_idx (samples grouped by cell, ascending sample index within
+    a cell: one of the orders the reference's race-defined election can
+    produce, and a deterministic one), cell (per-sample cell index)."""
 
     def __init__(self, sample, resolution: int, n_cells: int | None = None, device: int | None = None):
         p = np.ascontiguousarray(np.asarray(sample, np.float32).reshape(3, -1))
