@@ -70,10 +70,19 @@ MTX_HD void res_update(RReservoir &r, const RSample &snew, float wnew, bool acti
 }
 
 // RestirReservoir.merge: weight p * W * M (left to right, M as float).
-MTX_HD void res_merge(RReservoir &r, const RReservoir &o, float p, bool active, float u) {
+// res_merge_w does the weight / count update of o = (W, M) and returns
+// whether o's sample replaces r.z (so a caller can fetch that sample only
+// when it is taken); res_merge is exactly res_update + the count fix-up.
+MTX_HD bool res_merge_w(RReservoir &r, float oW, uint32_t oM, float p, bool active, float u) {
   const uint32_t M0 = r.M;
-  res_update(r, o.z, p * o.W * (float)o.M, active, u);
-  r.M = active ? M0 + o.M : M0;
+  const float wnew = p * oW * (float)oM;
+  r.w = r.w + (active ? wnew : 0.f);
+  r.M = active ? M0 + oM : M0;
+  return active && (u < wnew / r.w);
+}
+
+MTX_HD void res_merge(RReservoir &r, const RReservoir &o, float p, bool active, float u) {
+  if (res_merge_w(r, o.W, o.M, p, active, u)) r.z = o.z;
 }
 
 MTX_HD float dr_clampf(float x, float lo, float hi) { return fmaxf(fminf(x, hi), lo); }

@@ -280,20 +280,42 @@ __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
   uint32_t qM[9];
   V3 qp[9];
   uint32_t qa = 0;
+  // Neighbour reservoirs: per candidate only the planes the merge weight
+  // reads (L_o, then W and M; x_v / x_s / n_s with bias correction or the
+  // Jacobian); the sample planes of the one that ends up selected are read
+  // once after the loop (res_merge_w: same arithmetic as res_merge).
+  uint32_t sel = 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
     const Neighbour nb = neighbour(r, p, rng, k, max_iter, rad, x, y, smp, q);
     const bool active = nb.active;
-    const RReservoir Rk = active ? ld_res(r.tres, r.n, nb.idx) : rres_zero();
+    RReservoir Rk = rres_zero();
+    if (active) {
+      const float4 p4 = r.tres[4 * (size_t)r.n + nb.idx], p5 = r.tres[5 * (size_t)r.n + nb.idx];
+      Rk.z.L_o = V3{p4.x, p4.y, p4.z};
+      Rk.w = p5.x;
+      Rk.W = p5.y;
+      Rk.M = __float_as_uint(p5.z);
+      if (bias || jac) {
+        const float4 p0 = r.tres[nb.idx];
+        Rk.z.x_v = V3{p0.x, p0.y, p0.z};
+      }
+      if (jac) {
+        const float4 p2 = r.tres[2 * (size_t)r.n + nb.idx], p3 = r.tres[3 * (size_t)r.n + nb.idx];
+        Rk.z.x_s = V3{p2.x, p2.y, p2.z};
+        Rk.z.n_s = V3{p3.x, p3.y, p3.z};
+      }
+    }
     const bool shadowed = active && r.occ[9 * (size_t)ii + k] != 0;
     const float jf = jac ? dr_clampf(jacobian_J(q.x_v, Rk), 0.f, 1000.f) : 1.0f;
     const float phat = (!active || shadowed) ? 0.f : p_hat(Rk.z.L_o) * jf;
-    res_merge(Rn, Rk, phat, active, rng.next_1d());
+    if (res_merge_w(Rn, Rk.W, Rk.M, phat, active, rng.next_1d())) sel = nb.idx;
     qM[k] = Rk.M;
     qp[k] = Rk.z.x_v;
     qa |= active ? (1u << k) : 0u;
     any_reused = any_reused || active;
   }
+  if (sel != 0xffffffffu) Rn.z = ld_sample(r.tres, r.n, sel);
   const float phat = p_hat(Rn.z.L_o);
   if (!bias) Rn.W = (phat * (float)Rn.M > 0.f) ? Rn.w / ((float)Rn.M * phat) : 0.f;
   if (live) {
