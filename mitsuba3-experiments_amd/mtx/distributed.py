@@ -11,6 +11,12 @@ naturally (§8e):
 One collective per render (an all_gather of ~15 MB films for 1280x720);
 no data-path exchange during tracing.
 
+prefix_sum (prefix_sum.py:9-36) on a u32 array split into contiguous
+per-rank slices shards with one exchange: a local scan on
+each rank's GPU, an all_gather of the slice totals, then the lower ranks'
+total added (mod 2^32, exact). hashgrid / scatter_reduce build small global
+tables and run as replicas (each rank builds its own).
+
 ReSTIR GI (restirgi.py) is the one path with an exchange step: its spatial
 reuse reads samples and temporal reservoirs up to `initial_search_radius`
 rows away (:301-313) and its temporal reuse reprojects into the previous
@@ -206,3 +212,33 @@ def render_restir_sharded(integ, scene, seed: int, spp: int = 1, group=None):
     film = restir_band_frame(integ, scene, seed, y0, y1,
                              lambda: exchange_halos(ex, im, y0, y1, scene.height, halo, group), spp)
     return gather_bands(film, y0, y1, scene.height, group)
+
+
+def prefix_sum_sharded(x, inclusive: bool = True, group=None, scan=None):
+    """prefix_sum.py:9-36 over a u32 array whose contiguous slices live on the
+    ranks in rank order (`x` is this rank's slice, possibly empty). The local
+    scan runs on this rank's GPU (`scan`, default mtx.primitives.prefix_sum);
+    one all_gather of the per-rank totals gives the offset, the sum of the
+    lower ranks' totals, added mod 2^32. Bit-identical to the scan of the
+    concatenated array: u32 addition is associative mod 2^32. (The f32
+    Hillis-Steele order is not shard-invariant and has no sharded form.)"""
+    import torch
+    import torch.distributed as dist
+
+    x = np.ascontiguousarray(x, dtype=np.uint32)
+    if scan is None:
+        from . import primitives
+
+        scan = primitives.prefix_sum
+    local = scan(x, inclusive=inclusive) if x.size else np.zeros(0, np.uint32)
+    total = 0
+    if x.size:
+        total = int(local[-1]) if inclusive else (int(local[-1]) + int(x[-1])) & 0xFFFFFFFF
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([total], dtype=torch.int64, device=dev)
+    world = dist.get_world_size(group)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    rank = dist.get_rank(group)
+    offset = sum(int(p.item()) for p in parts[:rank]) & 0xFFFFFFFF
+    return (local + np.uint32(offset)).astype(np.uint32)

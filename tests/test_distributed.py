@@ -128,3 +128,44 @@ def test_halo_plan_edges():
     assert ru == (0, 0) and sd == (6, 4) and rd == (10, 4)
     su, sd, ru, rd = distributed.halo_plan(20, 30, 30, 4)
     assert rd == (30, 0) and su == (20, 4) and ru == (16, 4)
+
+
+def _scan_worker(rank, world, port, sizes, out_path):
+    import sys
+
+    sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd"), os.path.join(ROOT, "oracle")]
+    import torch.distributed as dist
+
+    import binding as oracle
+    from mtx import distributed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    x = _scan_input(sum(sizes))
+    lo = sum(sizes[:rank])
+    part = x[lo: lo + sizes[rank]]
+    res = [distributed.prefix_sum_sharded(part, inclusive=inc, scan=oracle.prefix_sum_u32) for inc in (True, False)]
+    np.savez(out_path + f".{rank}.npz", inc=res[0], exc=res[1])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _scan_input(n):
+    # values near 2^32 so the running sum wraps several times
+    rng = np.random.default_rng(11)
+    return (rng.integers(0, 1 << 32, n, dtype=np.uint64)).astype(np.uint32)
+
+
+@pytest.mark.parametrize("sizes", [(5000, 3001), (0, 777), (4096, 0, 123)])
+def test_prefix_sum_sharded(tmp_path, oracle, sizes):
+    """u32 scan sharded as local scan + all_gather of totals +
+    offset equals the single-array scan bit for bit (ragged and empty slices)."""
+    world = len(sizes)
+    out = os.path.join(tmp_path, "scan")
+    mp.start_processes(_scan_worker, args=(world, _free_port(), sizes, out), nprocs=world, join=True,
+                       start_method="spawn")
+    x = _scan_input(sum(sizes))
+    for inc in (True, False):
+        got = np.concatenate([np.load(out + f".{r}.npz")["inc" if inc else "exc"] for r in range(world)])
+        assert got.dtype == np.uint32
+        assert np.array_equal(got, oracle.prefix_sum_u32(x, inclusive=inc))

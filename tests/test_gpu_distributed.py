@@ -60,6 +60,22 @@ def _worker(rank, world, port, kind, out_dir):
         out = torch.empty((y1 - y0 + 2, sc.width + 2, 4), dtype=torch.float32, device="cuda:0")
         integ.render_film(sc, seed=5, spp=2, y0=y0, y1=y1, out=out)
         films.append(distributed.gather_bands(out, y0, y1, sc.height))
+    elif kind == "scan":
+        from mtx import primitives
+
+        x = _scan_input()
+        h = len(x) // 3
+        part = x[:h] if rank == 0 else x[h:]
+        films = [torch.from_numpy(distributed.prefix_sum_sharded(part, inclusive=inc).astype(np.int64))
+                 for inc in (True, False)]
+        res = [torch.empty(len(x) - len(part), dtype=torch.int64) for _ in films]
+        for f, r in zip(films, res):  # gather the two slices on rank 0 (gloo, host)
+            if rank == 0:
+                dist.recv(r, src=1)
+            else:
+                dist.send(f, dst=0)
+        if rank == 0:
+            films = [torch.cat([f, r]) for f, r in zip(films, res)]
     elif kind == "restir":
         integ = load_dict({"type": "restirgi", **RESTIR_PROPS})
         for fr in range(3):
@@ -68,6 +84,11 @@ def _worker(rank, world, port, kind, out_dir):
         np.save(os.path.join(out_dir, "films.npy"), np.stack([f.cpu().numpy() for f in films]))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _scan_input():
+    rng = np.random.default_rng(11)
+    return rng.integers(0, 1 << 32, 300001, dtype=np.uint64).astype(np.uint32)
 
 
 def _run(kind, tmp_path):
@@ -119,3 +140,13 @@ def test_two_rank_restir_frames(tmp_path):
     for fr in range(3):
         ref = integ.render_film(sc, seed=fr, spp=1)
         np.testing.assert_allclose(got[fr], ref, rtol=2e-6, atol=1e-6, err_msg=f"frame {fr}")
+
+
+@pytest.mark.gpu
+def test_two_rank_prefix_sum_u32(tmp_path, oracle):
+    """prefix_sum.py u32 scan sharded over two ranks (local HIP scans + one
+    all_gather of totals) == the single-array scan, bit for bit."""
+    got = _run("scan", tmp_path)
+    x = _scan_input()
+    for g, inc in zip(got, (True, False)):
+        assert np.array_equal(g.astype(np.uint32), oracle.prefix_sum_u32(x, inclusive=inc))
