@@ -55,7 +55,7 @@ struct Box {
   }
 };
 
-constexpr int kBins = 32;
+constexpr int kMaxBins = 256;  // SAH bins: Builder::bins (default 32, MTX_BVH_BINS)
 constexpr float kDefaultCt = 1.f;  // SAH cost of a traversal step, in triangle tests
 
 struct Builder {
@@ -68,6 +68,7 @@ struct Builder {
   std::vector<int32_t> nodes;  // 16 words per node
   std::vector<uint32_t> order; // leaf order -> input tri
   float ct = kDefaultCt;
+  int n_bins = 32;
   int layout = 0;
   uint32_t max_depth_seen = 0;
 
@@ -94,6 +95,7 @@ struct Builder {
   // Partition [s,e) and return the split position; uses binned SAH unless the
   // depth budget forces an object-median split. Returns 0 when a leaf is best.
   uint32_t choose_split(uint32_t s, uint32_t e, uint32_t depth) {
+    const int nb = n_bins;
     const uint32_t cnt = e - s;
     Box cb;
     cb.reset();
@@ -116,23 +118,23 @@ struct Builder {
       for (int a = 0; a < 3; ++a) {
         float ext = cb.hi[a] - cb.lo[a];
         if (!(ext > 0.f)) continue;
-        Box bins[kBins];
-        uint32_t counts[kBins] = {0};
-        for (int b = 0; b < kBins; ++b) bins[b].reset();
-        const float k = (float)kBins / ext;
+        Box bins[kMaxBins];
+        uint32_t counts[kMaxBins] = {0};
+        for (int b = 0; b < nb; ++b) bins[b].reset();
+        const float k = (float)nb / ext;
         for (uint32_t i = s; i < e; ++i) {
           uint32_t t = idx[i];
           int b = (int)((cen[3 * t + a] - cb.lo[a]) * k);
-          b = std::min(std::max(b, 0), kBins - 1);
+          b = std::min(std::max(b, 0), nb - 1);
           counts[b]++;
           bins[b].grow(tbox[t]);
         }
-        float right_area[kBins];
-        uint32_t right_cnt[kBins];
+        float right_area[kMaxBins];
+        uint32_t right_cnt[kMaxBins];
         Box acc;
         acc.reset();
         uint32_t c = 0;
-        for (int b = kBins - 1; b > 0; --b) {
+        for (int b = nb - 1; b > 0; --b) {
           acc.grow(bins[b]);
           c += counts[b];
           right_area[b] = acc.area();
@@ -140,7 +142,7 @@ struct Builder {
         }
         acc.reset();
         c = 0;
-        for (int b = 0; b < kBins - 1; ++b) {
+        for (int b = 0; b < nb - 1; ++b) {
           acc.grow(bins[b]);
           c += counts[b];
           if (c == 0 || right_cnt[b + 1] == 0) continue;
@@ -155,10 +157,10 @@ struct Builder {
       if (cnt <= MTX_BVH_MAX_LEAF && (best_axis < 0 || (float)cnt <= best_cost)) return 0;
       if (best_axis >= 0) {
         const float ext = cb.hi[best_axis] - cb.lo[best_axis];
-        const float k = (float)kBins / ext;
+        const float k = (float)nb / ext;
         uint32_t *mid = std::partition(idx.data() + s, idx.data() + e, [&](uint32_t t) {
           int b = (int)((cen[3 * t + best_axis] - cb.lo[best_axis]) * k);
-          b = std::min(std::max(b, 0), kBins - 1);
+          b = std::min(std::max(b, 0), nb - 1);
           return b <= best_bin;
         });
         uint32_t m = (uint32_t)(mid - idx.data());
@@ -308,6 +310,7 @@ struct Builder {
   // c_tri * count; BVH2 subtrees are contiguous in leaf order). Replaces the
   // greedy largest-area opening (Ylitie et al. 2017, wide-BVH collapse).
   float c_node = 1.0f, c_tri = 1.0f;  // tuned on the bedroom proxy (A/B: +1.8 % vs greedy)
+  float c_leaf = 0.f;                 // per-leaf visit cost (leaf-phase overhead)
   std::vector<float> dp_cost;      // 5 per BVH2 node (index j = 1..4)
   std::vector<uint8_t> dp_split;   // 5 per node: 0 = use j-1 slots, k = k slots left
   std::vector<uint8_t> dp_leaf;    // 1: the subtree as one leaf (j = 1)
@@ -323,7 +326,7 @@ struct Builder {
       const uint32_t code = ~(uint32_t)ref;
       *first = code >> 3;
       *count = (code & 7u) + 1u;
-      for (int j = 1; j <= 4; ++j) cost[j] = area * c_tri * (float)*count;
+      for (int j = 1; j <= 4; ++j) cost[j] = area * (c_leaf + c_tri * (float)*count);
     }
   }
 
@@ -364,10 +367,10 @@ struct Builder {
       }
       const float area = box2[n].area();
       const float c_inner = area * c_node + dist[4];
-      const float c_leaf = sub_count[n] <= MTX_BVH_MAX_LEAF ? area * c_tri * (float)sub_count[n] : INFINITY;
+      const float c_lf = sub_count[n] <= MTX_BVH_MAX_LEAF ? area * (c_leaf + c_tri * (float)sub_count[n]) : INFINITY;
       float *C = &dp_cost[5 * n];
-      dp_leaf[n] = c_leaf <= c_inner ? 1 : 0;
-      C[1] = std::min(c_leaf, c_inner);
+      dp_leaf[n] = c_lf <= c_inner ? 1 : 0;
+      C[1] = std::min(c_lf, c_inner);
       for (int j = 2; j <= 4; ++j) {
         if (dist[j] < C[j - 1]) {
           C[j] = dist[j];
@@ -531,6 +534,7 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
   // its node / triangle costs
   if (const char *e = getenv("MTX_BVH_CT")) b.ct = std::max(0.05f, (float)atof(e));
   if (const char *e = getenv("MTX_BVH_LAYOUT")) b.layout = atoi(e);
+  if (const char *e = getenv("MTX_BVH_BINS")) b.n_bins = std::max(2, std::min(kMaxBins, atoi(e)));
   b.vpos = vpos;
   b.vidx = tri_vidx;
   b.n = n_tris;
@@ -542,6 +546,7 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
   b.wnodes.reserve(b.nodes.size() / 2 + 16);
   if (const char *e = getenv("MTX_BVH_CNODE")) b.c_node = (float)atof(e);
   if (const char *e = getenv("MTX_BVH_CTRI")) b.c_tri = (float)atof(e);
+  if (const char *e = getenv("MTX_BVH_CLEAF")) b.c_leaf = (float)atof(e);
   const char *col = getenv("MTX_BVH_COLLAPSE");
   if (b.layout == 1) {
     b.wnodes.resize(16, 0);
