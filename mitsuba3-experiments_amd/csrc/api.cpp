@@ -604,14 +604,19 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
   const bool nerad = p.integrator == MTX_INT_NERAD_RHS, nerad_render = p.integrator == MTX_INT_NERAD;
   for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
     hipEvent_t e;
+    // past its second vertex the nerad RHS chain only continues through
+    // delta surfaces (next_smooth_si): a small queue, traced and shaded by
+    // an eighth of the persistent grid (dispatching the full grid of
+    // immediately-exiting blocks costs more than the work)
+    const int div = (nerad && bounce >= 2) ? 8 : 1;
     if (!(nerad && bounce == 0)) {
       e = tm.begin(0);
-      mtxd::launch_trace_closest(s, b, bounce, p.stats, c->trace_grid, c->stream);
+      mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), c->stream);
       tm.end(0, e);
       ++*n_trace;
     }
     e = tm.begin(2);
-    mtxd::launch_shade(s, b, p, bounce, c->shade_grid, c->stream);
+    mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), c->stream);
     tm.end(2, e);
     if (p.integrator != MTX_INT_PSSMLT_SIMPLE && !nerad_render &&
         !(nerad && bounce > 0)) {  // PSSMLT and the nerad render trace no NEE rays
