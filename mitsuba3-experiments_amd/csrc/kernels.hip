@@ -346,10 +346,11 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   const V3 wo = to_local(si.sh, ds.d);
   const float s1 = rng.next_1d();
   const V2 s2 = rng.next_2d();
-  V3 bsdf_val;
-  float bsdf_pdf;
+  V3 bsdf_val = v3s(0.f);
+  float bsdf_pdf = 0.f;
   BSDFSample bs;
-  bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
+  // eval / pdf only feed the NEE contribution (no draws, no side effects)
+  if (active_em) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
   const V3 bsdf_weight = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
 
   if (INT == MTX_INT_PATH_MIS) {
