@@ -798,7 +798,10 @@ __device__ __forceinline__ V3 final_L(const WaveBuffers &b, const ChunkParams &p
 // Pixel-major chunks: a pixel's samples are contiguous, so one wave stages
 // 64 pixels x kFilmStage samples through LDS with coalesced loads, then each
 // lane accumulates its own pixel in sample order (same order as below).
-constexpr int kFilmStage = 16;
+#ifndef MTX_FILM_STAGE
+#define MTX_FILM_STAGE 8  // A/B: 8 (11.5 KB of LDS per wave, twice the waves per CU) beats 16 by 0.8 ms and 4
+#endif
+constexpr int kFilmStage = MTX_FILM_STAGE;
 
 __device__ __forceinline__ void film_accumulate(float4 acc[9], int x, int y, float2 ps, V3 L) {
 #pragma unroll
