@@ -5,6 +5,7 @@ import math
 import os
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
@@ -71,11 +72,15 @@ def test_bvh_invariants(small_scene):
     at most 8, children's decoded boxes contain their triangles / subtrees,
     depth as reported."""
     s = small_scene
-    nodes = s.nodes.reshape(-1, 16)
+    _check_bvh(s.nodes, s.tri_geom, s.n_tris, s.bvh_depth)
+
+
+def _check_bvh(nodes, tri_geom, n_tris, bvh_depth):
+    nodes = nodes.reshape(-1, 16)
     f = nodes.view(np.float32)
     u = nodes.view(np.uint32)
-    seen = np.zeros(s.n_tris, np.int32)
-    geom = s.tri_geom.reshape(-1, 12)
+    seen = np.zeros(n_tris, np.int32)
+    geom = tri_geom.reshape(-1, 12)
     v0 = geom[:, 0:3]
     v1 = v0 + geom[:, 4:7]
     v2 = v0 + geom[:, 8:11]
@@ -121,8 +126,8 @@ def test_bvh_invariants(small_scene):
                 assert _decode(f[i, a], e[a], qlo) <= clo[a] and _decode(f[i, a], e[a], qhi) >= chi[a]
             blo, bhi = np.minimum(blo, clo), np.maximum(bhi, chi)
         boxes[i] = (blo, bhi)
-    assert (seen == 1).all() or ((seen >= 1).all() and s.n_tris == 1)
-    assert max_depth <= 40 and max_depth == s.bvh_depth
+    assert (seen == 1).all() or ((seen >= 1).all() and n_tris == 1)
+    assert max_depth <= 40 and max_depth == bvh_depth
 
 
 def test_bvh_closest_hit_equals_brute_force(small_scene, oracle):
@@ -147,3 +152,42 @@ def test_scene_save_load_roundtrip(small_scene, tmp_path):
     assert np.array_equal(t.nodes, small_scene.nodes) and bytes(t.materials) == bytes(small_scene.materials)
     assert bytes(t.camera) == bytes(small_scene.camera)
     assert json.dumps(t.meta, sort_keys=True) == json.dumps(small_scene.meta, sort_keys=True)
+
+
+def _tiny_mesh(kind):
+    rng = np.random.default_rng(5)
+    if kind == "one":
+        v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
+        return v, np.array([[0, 1, 2]], np.uint32)
+    if kind == "identical":  # 20 copies of one triangle: zero-extent splits
+        v = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float32)
+        return v, np.tile(np.array([[0, 1, 2]], np.uint32), (20, 1))
+    n = {"two": 2, "nine": 9, "random": 400, "planar": 300}[kind]
+    v = rng.uniform(-1, 1, (3 * n, 3)).astype(np.float32)
+    if kind == "planar":
+        v[:, 2] = 0.5  # every box flat in z
+    return v, np.arange(3 * n, dtype=np.uint32).reshape(n, 3)
+
+
+@pytest.mark.parametrize("collapse", ["0", "1"])
+@pytest.mark.parametrize("kind", ["one", "two", "nine", "identical", "planar", "random"])
+def test_bvh_build_small_and_degenerate_meshes(kind, collapse, monkeypatch):
+    """Greedy (MTX_BVH_COLLAPSE=0) and dynamic-programming collapses keep the
+    node invariants on tiny, coplanar and coincident-triangle meshes."""
+    import ctypes as C
+
+    from mtx import _lib
+
+    monkeypatch.setenv("MTX_BVH_COLLAPSE", collapse)
+    v, idx = _tiny_mesh(kind)
+    n = len(idx)
+    nodes = np.zeros((2 * n + 2) * 16, np.int32)
+    geom = np.zeros(12 * n, np.float32)
+    perm = np.zeros(n, np.uint32)
+    nn, dep = C.c_uint32(), C.c_uint32()
+    L = _lib.lib()
+    rc = L.mtx_bvh_build(v.ctypes.data, len(v), np.ascontiguousarray(idx).ctypes.data, n, nodes.ctypes.data,
+                         C.byref(nn), geom.ctypes.data, perm.ctypes.data, C.byref(dep))
+    assert rc == 0, L.mtx_last_error()
+    assert sorted(perm.tolist()) == list(range(n))
+    _check_bvh(nodes[: 16 * nn.value], geom, n, dep.value)
