@@ -40,6 +40,19 @@ def test_golden_films_oracle(golden, oracle, small_scene, name):
     assert np.array_equal(oracle.render(small_scene, integ.render_args(small_scene, 0, 16)), golden[f"film_{name}"])
 
 
+def test_golden_independent_of_bvh_collapse(golden, oracle, monkeypatch):
+    """Closest hits do not depend on the tree (inclusive culling + the
+    smaller-index tie rule): the greedy collapse (MTX_BVH_COLLAPSE=0) gives
+    other nodes, and the same hits and film bit for bit."""
+    from mtx import load_dict, scene
+
+    monkeypatch.setenv("MTX_BVH_COLLAPSE", "0")
+    sc = scene.Scene.bedroom(width=64, height=36, scale=0.02, tex_res=64)
+    assert oracle.trace(sc, golden["trace_rays"])[0].tobytes() == golden["trace_hits"].tobytes()
+    integ = load_dict({"type": "path_test"})
+    assert np.array_equal(oracle.render(sc, integ.render_args(sc, 0, 16)), golden["film_path_test"])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["path_test", "mypath", "nrc"])
 def test_golden_films_gpu(golden, small_scene, name):
