@@ -123,7 +123,7 @@ struct mtx_ctx {
   DevBuf vpath_es, vprop_es;                       // pssmltpath emitter samples
   uint32_t mlt_capacity = 0, mlt_depth = 0, mlt_es_capacity = 0, mlt_es_depth = 0;
   // ReSTIR GI frame state (restirgi.py:217-226): kept across mtx_render calls
-  DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM, rs_xs, rs_ns;
+  DevBuf rs_samp[2], rs_tres, rs_sres, rs_radius, rs_hit, rs_dir, rs_emit, rs_rng, rs_rays, rs_count, rs_occ, rs_qM, rs_nbr, rs_xs, rs_ns;
   uint32_t rs_n = 0, rs_cur = 0, rs_pending_frame = 0;
   bool rs_valid = false, rs_pending_b = false;
   mtx_camera rs_prev_cam{};
@@ -206,7 +206,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop, &c->vpath_es, &c->vprop_es,
                     &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
-                    &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_xs, &c->rs_ns,
+                    &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_nbr, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5,
                     &c->field_w16, &c->tr_p, &c->tr_m, &c->tr_v, &c->tr_g, &c->tr_wpart, &c->tr_loss, &c->tr_out,
                     &c->tr_dfeat, &c->tr_feat, &c->tr_flag, &c->tr_target, &c->nr_shape_pmf, &c->nr_shape_cdf,
@@ -687,6 +687,7 @@ int ensure_restir(mtx_ctx *c, uint32_t n) {
     if ((rc = dalloc(c->rs_heads, 4ull * mtxd::kXSlotWords))) return rc;
     if ((rc = dalloc(c->rs_occ, 18 * N))) return rc;
     if ((rc = dalloc(c->rs_qM, 10 * 4 * N))) return rc;
+    if ((rc = dalloc(c->rs_nbr, 10 * 4 * N))) return rc;
     if ((rc = dalloc(c->rs_xs, 16 * N))) return rc;
     if ((rc = dalloc(c->rs_ns, 16 * N))) return rc;
     c->rs_n = n;
@@ -759,6 +760,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   r.test_heads = (uint32_t *)c->rs_heads.p;
   r.occ = (uint8_t *)c->rs_occ.p;
   r.qM = (uint32_t *)c->rs_qM.p;
+  r.nbr = (uint32_t *)c->rs_nbr.p;
   r.n = n;
   r.lane0 = lane0;
   r.nb = nb;

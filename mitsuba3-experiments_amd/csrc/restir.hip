@@ -245,6 +245,11 @@ __global__ void k_rs_spatial_rays(RestirBuffers r, ChunkParams p) {
     if (live && nb.active) mask |= 1u << k;
     rng.next_1d();  // merge draw (:328)
   }
+  if (live) {  // the candidates, for k_rs_spatial_merge (instead of re-deriving them)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r.nbr[10 * (size_t)ii + k] = idx[k];
+    r.nbr[10 * (size_t)ii + 9] = mask;
+  }
   uint32_t o = block_reserve<kRsBlock>((uint32_t)__popc(mask), &r.test_count[0]);
 #pragma unroll
   for (int k = 0; k < 9; ++k)
@@ -261,8 +266,6 @@ __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
   const uint32_t t = rs_thread(r);
   const bool live = t < r.nb;
   const uint32_t ii = r.lane0 + (live ? t : 0u);
-  const uint32_t smp = ii % p.spp;
-  const int64_t x = (int64_t)(ii / p.spp % p.width), y = (int64_t)(ii / p.width / p.spp);
   const bool bias = (r.flags & MTX_RESTIR_BIAS_CORRECTION) != 0;
   const bool jac = (r.flags & MTX_RESTIR_JACOBIAN) != 0;
   Pcg32 rng = ld_rng(r.rng[ii]);
@@ -274,9 +277,11 @@ __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
     res_merge(Rn, Rs, p_hat(Rs.z.L_o), true, rng.next_1d());
     Z += Rs.M;
   }
-  const int max_iter = spatial_max_iter(r, Rs.M);
   const float rad = r.radius[ii];
   bool any_reused = false;
+  // the 9 candidates k_rs_spatial_rays drew (same draws: each disk sample's
+  // two draws are consumed unused)
+  const uint32_t nmask = live ? r.nbr[10 * (size_t)ii + 9] : 0u;
   uint32_t qM[9];
   V3 qp[9];
   uint32_t qa = 0;
@@ -287,7 +292,11 @@ __global__ void k_rs_spatial_merge(RestirBuffers r, ChunkParams p) {
   uint32_t sel = 0xffffffffu;
 #pragma unroll
   for (int k = 0; k < 9; ++k) {
-    const Neighbour nb = neighbour(r, p, rng, k, max_iter, rad, x, y, smp, q);
+    rng.next_u32();  // the candidate's disk sample (next_2d)
+    rng.next_u32();
+    Neighbour nb;
+    nb.idx = live ? r.nbr[10 * (size_t)ii + k] : 0u;
+    nb.active = ((nmask >> k) & 1u) != 0;
     const bool active = nb.active;
     RReservoir Rk = rres_zero();
     if (active) {

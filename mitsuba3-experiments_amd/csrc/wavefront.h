@@ -125,6 +125,7 @@ struct RestirBuffers {
   uint32_t *test_heads;  // per-XCD claim cursors of k_trace_test (kXSlotWords)
   uint8_t *occ;       // 18 per lane: spatial tests [0,9), bias-correction tests [9,18)
   uint32_t *qM;       // 10 per lane: Q.M with bit 31 = active, [9] = Z before the loop
+  uint32_t *nbr;      // 10 per lane: the 9 spatial candidates' lanes, [9] = active mask (rays -> merge)
   uint32_t n;      // lanes of the whole frame (state arrays)
   uint32_t lane0;  // first lane of the rows this call computes
   uint32_t nb;     // lanes this call computes (row band)
