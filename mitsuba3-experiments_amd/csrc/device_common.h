@@ -137,9 +137,11 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t *counte
 // from every wave of the chip serialise. All threads of the block must call
 // it once per step; `parity` alternates between consecutive steps so that the
 // LDS slots of one step are not overwritten while a slow wave still reads them.
+// The two counters are one 8-byte-aligned pair (c[0], c[1]): a single 64-bit
+// atomic reserves both (the low count never carries: it stays below 2^32).
 template <int BLOCK>
-__device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c0, uint32_t *c1, uint32_t parity,
-                                              uint32_t &s0, uint32_t &s1) {
+__device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c, uint32_t parity, uint32_t &s0,
+                                              uint32_t &s1) {
   constexpr int W = BLOCK / 64;
   __shared__ uint32_t wcnt[2][2][W];
   __shared__ uint32_t bbase[2][2];
@@ -157,8 +159,11 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c0, ui
       t0 += wcnt[parity][0][w];
       t1 += wcnt[parity][1][w];
     }
-    bbase[parity][0] = t0 ? atomicAdd(c0, t0) : 0u;
-    bbase[parity][1] = t1 ? atomicAdd(c1, t1) : 0u;
+    uint64_t base = 0;
+    if (t0 | t1)
+      base = atomicAdd(reinterpret_cast<unsigned long long *>(c), ((unsigned long long)t1 << 32) | t0);
+    bbase[parity][0] = (uint32_t)base;
+    bbase[parity][1] = (uint32_t)(base >> 32);
   }
   __syncthreads();
   uint32_t o0 = bbase[parity][0], o1 = bbase[parity][1];

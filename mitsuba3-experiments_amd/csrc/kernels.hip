@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene s, WaveBu
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   const ShadowSrc src{b};
   uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop<true>(s, src, b.counters[4 * bounce + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, stack + threadIdx.x, nv, tv, nr);
+  trace_loop<true>(s, src, b.counters[4 * (bounce + 1) + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, stack + threadIdx.x, nv, tv, nr);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
     if ((threadIdx.x & 63) == 0 && n) {
@@ -713,8 +713,9 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
   const uint32_t count = b.counters[4 * bounce + 0];
   const uint32_t *in_q = b.queue[bounce & 1];
   uint32_t *out_q = b.queue[(bounce + 1) & 1];
+  // [4(bounce+1)] next queue count, [4(bounce+1)+1] this bounce's shadow
+  // rays: one 64-bit pair, reserved by one atomic per block step
   uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
-  uint32_t *sh_cnt = &b.counters[4 * bounce + 1];
   const uint32_t stride = gridDim.x * kShadeBlock;
   uint32_t parity = 0;
   for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += stride, parity ^= 1u) {
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
         cont = shade_path<INT>(s, sv, b, p, bounce, path, io);
     }
     uint32_t slot, sslot;
-    block_append2<kShadeBlock>(cont, io.emit, out_cnt, sh_cnt, parity, slot, sslot);
+    block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path;
     if (io.emit) b.shadow[sslot] = io.rec;
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {

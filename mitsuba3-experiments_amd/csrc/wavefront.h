@@ -86,7 +86,7 @@ struct WaveBuffers {
   float4 *hit;
   uint32_t *queue[2];
   ShadowRec *shadow;
-  uint32_t *counters;   // per bounce b: [4b+0] rays, [4b+1] shadow rays, [4b+2], [4b+3] unused
+  uint32_t *counters;   // per bounce b: [4b+0] rays of bounce b, [4b+1] shadow rays of bounce b-1 (one 8-B pair with the queue shade b-1 fills), [4b+2], [4b+3] unused
   uint32_t *xheads;     // per bounce b: slot 2b closest-hit, 2b+1 shadow claim cursors (kXSlotWords each)
   unsigned long long *stats;  // nodes_c, tris_c, nodes_s, tris_s, rays_c, rays_s
   uint32_t capacity;
