@@ -2,22 +2,39 @@
 configs[1]) on the bedroom proxy at 1280x720 spp=256 (the metric's
 resolution and spp), one process per GPU.
 
-A step renders the full 1280x720 film at `--spp` samples per pixel on every
-rank; rank r traces the global sample range [r*spp, (r+1)*spp) of every pixel
-(weak scaling: per-GPU work is fixed, the job's spp grows with N), and the
-per-rank films are gathered to rank 0 over RCCL and summed in rank order.
-Inputs (scene, BVH) are resident in HBM before the timed region; the film
-stays in HBM and only the gather crosses GPUs.
+A step renders ONE 1280x720 film at a fixed global spp=256 (strong scaling:
+the job's work is the same at every N). Rank r of N traces the global sample
+range [r*256/N, (r+1)*256/N) of every pixel with global-lane seeding
+(path.py:156-161: lane = pixel*spp + sample), so the N=1 and N>1 films hold
+the same paths; the per-rank films are gathered to rank 0 over RCCL and
+summed in rank order (deterministic). Inputs (scene, BVH) are resident in HBM
+before the timed region; the film stays in HBM and only the gather crosses
+GPUs. The timed region includes the gather.
+
+`python bench.py --gpus N` without a torchrun environment starts the N rank
+processes itself (torch.distributed.run, before this process touches the
+GPU) and exits with their status; under torchrun WORLD_SIZE must equal N.
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
-`roofline` for the closest-hit traversal kernel (HIP-event time per launch
-over the timed region; algorithmic bytes from the in-kernel visit counters of
-one extra, untimed step with the same seed as the first timed step) and
-`cpu_baseline` (the oracle/ CPU restatement on a bounded sample).
+`roofline` for the closest-hit traversal kernel and `cpu_baseline` (the
+oracle/ CPU restatement on a bounded sample, N=1 only). The roofline is
+stated against the memory level that serves the traversal's bytes: the
+algorithmic bytes (32 + 16 + 64 N_node + 48 N_tri per ray, exact
+visit counts from the in-kernel counters of one extra, untimed step) divided
+by the HIP-event time of the launches, against the L2-resident random-gather
+rate of MI355X_MICROARCH.md ("Indexed rows: gather into LDS", 16.8-18.8 TB/s).
+Its `hbm` sub-object is the DRAM/fabric side: the committed rocprofv3 PMC
+traffic of the same kernel (FETCH_SIZE x2 + WRITE_SIZE per launch,
+profiles/*_pmc_traffic.json) over the same launch time, against the 8 TB/s
+HBM peak; the PMC file is used only when its recorded source hash and bench
+arguments match this build and this run (otherwise `traffic` is null).
 """
 import argparse
+import hashlib
+import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -26,7 +43,13 @@ sys.path.insert(0, os.path.join(ROOT, "mitsuba3-experiments_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
-NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES = 64, 48, 32, 16
+# MI355X_MICROARCH.md "Indexed rows: gather into LDS": rows shared by every
+# workgroup, served from the XCD's L2: 16.8-18.8 TB/s chip-wide (upper end).
+L2_GATHER_PEAK_GBS = 18800.0
+L2_STREAM_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate
+NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES, OCC_BYTES = 64, 48, 32, 16, 4
+# SURVEY §8d wavefront path state per lane per bounce, read + written
+SHADE_BYTES_PER_PATH_BOUNCE = 2 * 108 + 32
 
 
 def parse():
@@ -34,7 +57,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--spp", type=int, default=256, help="global samples per pixel (split over the ranks)")
     p.add_argument("--width", type=int, default=1280)
     p.add_argument("--height", type=int, default=720)
     p.add_argument("--max-depth", type=int, default=8)
@@ -50,21 +73,93 @@ def parse():
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="N>1 ranks: nccl (RCCL, the measurement) or gloo (host-staged device tensors; lets "
                         "several ranks share one GPU in a rehearsal of the N>1 code path)")
+    p.add_argument("--master-port", type=int, default=29517, help="rendezvous port when bench.py starts the ranks")
+    p.add_argument("--dump-film", default="", help="save rank 0's combined film of the seed-0 step (.npy; tests)")
     return p.parse_args()
+
+
+def spawn_ranks(args) -> int:
+    """Start the N rank processes (one per GPU) under torch.distributed.run.
+    Runs before this process makes any GPU call; the ranks are children, not
+    an exec of this process."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={args.master_port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
+def src_sha() -> str:
+    """Hash of the sources that make libmtx.so (kernels, host runtime, shared
+    headers, build flags): a PMC profile is valid for the build it measured."""
+    h = hashlib.sha256()
+    pats = ["mitsuba3-experiments_amd/csrc/*.hip", "mitsuba3-experiments_amd/csrc/*.h",
+            "mitsuba3-experiments_amd/csrc/*.cpp", "mitsuba3-experiments_amd/csrc/Makefile",
+            "include/*.h", "include/mtx_core/*.h"]
+    for f in sorted(x for p in pats for x in glob.glob(os.path.join(ROOT, p))):
+        h.update(os.path.relpath(f, ROOT).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def traffic_key(args) -> str:
+    """The bench arguments a PMC profile depends on (per-launch traffic)."""
+    return f"path_mis {args.width}x{args.height} spp={args.spp} md={args.max_depth} rr={args.rr_depth} chunk={args.chunk}"
+
+
+def measured_traffic(kernels, key):
+    """HBM-side bytes per launch of each kernel in `kernels` from the newest
+    committed rocprofv3 PMC summary (profiles/*_pmc_traffic.json, FETCH_SIZE x2
+    + WRITE_SIZE, tools/pmc_summary.py) whose src_sha and bench key match this
+    build and run. Returns ({kernel: bytes}, source or reason)."""
+    sha = src_sha()
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=os.path.getmtime)
+    reason = "no profiles/*_pmc_traffic.json"
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("src_sha") != sha:
+            reason = f"stale: {os.path.basename(f)} src_sha {d.get('src_sha')} != {sha}"
+            continue
+        if d.get("bench_key") != key:
+            reason = f"{os.path.basename(f)}: bench args differ"
+            continue
+        ks = d.get("kernels", {})
+        return {k: (int(ks[k]["hbm_bytes_per_launch"]) if k in ks else None) for k in kernels}, \
+            os.path.relpath(f, ROOT)
+    return {k: None for k in kernels}, reason
+
+
+def _kernel_entry(ms_per_step, launches, traffic, alg_bytes_per_step=None, alg_peak=None, alg_bound=None):
+    e = {"ms_per_step": round(ms_per_step, 3), "launches_per_step": int(launches)}
+    launch_s = ms_per_step / 1e3 / max(1, launches)
+    if alg_bytes_per_step is not None and ms_per_step > 0:
+        ach = alg_bytes_per_step / (ms_per_step / 1e3) / 1e9
+        e.update({"alg_bytes_per_launch": int(alg_bytes_per_step / max(1, launches)),
+                  "alg_GBps": round(ach, 1), "alg_bound": alg_bound, "alg_peak_GBps": alg_peak,
+                  "alg_frac": round(ach / alg_peak, 4)})
+    if traffic is not None and launch_s > 0:
+        hb = traffic / launch_s / 1e9
+        e.update({"hbm_bytes_per_launch": int(traffic), "hbm_GBps": round(hb, 1),
+                  "hbm_frac": round(hb / HBM_PEAK_GBS, 4)})
+    return e
 
 
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     if args.workload != "path_mis":
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_workloads
 
         return bench_workloads.run(args)
-    import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU (--backend gloo)
@@ -75,19 +170,21 @@ def main():
         else:
             dist.init_process_group("gloo")
 
-    from mtx import PathIntegrator, scene
+    from mtx import PathIntegrator, distributed, scene
 
     sc = scene.bedroom(width=args.width, height=args.height)
     integ = PathIntegrator({"max_depth": args.max_depth, "rr_depth": args.rr_depth})
     W, H, spp = sc.width, sc.height, args.spp
+    s0, s1 = distributed.sample_range(spp, world, rank)
     film = torch.empty((H + 2, W + 2, 4), dtype=torch.float32, device=f"cuda:{local}")
-    from mtx import distributed
+
+    combined = [film]
 
     def step(i, stats=False, counters=False):
-        r = integ.render_film(sc, seed=i, spp=spp, spp_total=spp * world, sample_offset=spp * rank, out=film,
+        r = integ.render_film(sc, seed=i, spp=s1 - s0, spp_total=spp, sample_offset=s0, out=film,
                               stats=stats, chunk_paths=args.chunk, counters=counters)
         if world > 1:
-            distributed.gather_sum(film)  # RCCL all_gather, rank-order sum on rank 0
+            combined[0] = distributed.gather_sum(film)  # RCCL gather to rank 0, rank-order sum
         return r[1] if stats else None
 
     for i in range(args.warmup):
@@ -100,11 +197,7 @@ def main():
     agg = None
     for i in range(args.steps):
         st = step(i, stats=True)
-        if agg is None:
-            agg = dict(st)
-        else:
-            for k, v in st.items():
-                agg[k] += v
+        agg = dict(st) if agg is None else {k: agg[k] + v for k, v in st.items()}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -116,87 +209,95 @@ def main():
         elapsed = float(t.item())
     # visit counters (deterministic): one untimed step, same seed as step 0
     cnt = step(0, stats=True, counters=True)
+    if args.dump_film and rank == 0:
+        import numpy as np
 
-    paths_per_rank = W * H * spp
-    value = world * paths_per_rank * args.steps / elapsed / 1e6
-    # roofline of the dominant kernel: closest-hit traversal
-    alg_bytes = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
-                 + cnt["tris_closest"] * TRI_BYTES)  # per step
-    launches = max(1, cnt["trace_launches"])  # per step
-    trace_s = agg["trace_ms"] / 1e3 / args.steps  # per step, counters off
-    achieved = alg_bytes / trace_s / 1e9 if trace_s > 0 else 0.0
+        np.save(args.dump_film, combined[0].cpu().numpy())
 
-    traffic, traffic_src = measured_traffic("mtxd::k_trace_closest<false>")
+    value = W * H * spp * args.steps / elapsed / 1e6
+    K = args.steps
+    # rank-local per-step figures (this rank's launches)
+    alg_closest = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
+                   + cnt["tris_closest"] * TRI_BYTES)
+    alg_shadow = (cnt["rays_shadow"] * (RAY_BYTES + OCC_BYTES) + cnt["nodes_shadow"] * NODE_BYTES
+                  + cnt["tris_shadow"] * TRI_BYTES)
+    launches = max(1, cnt["trace_launches"])
+    trace_ms = agg["trace_ms"] / K  # counters off
+    trace_s = trace_ms / 1e3
+    achieved = alg_closest / trace_s / 1e9 if trace_s > 0 else 0.0
+    names = {"closest": "mtxd::k_trace_closest<false>", "shadow": "mtxd::k_trace_shadow<false>",
+             "shade": "mtxd::k_shade<2>"}
+    traffic, traffic_src = (measured_traffic(list(names.values()), traffic_key(args)) if world == 1
+                            else ({k: None for k in names.values()}, "N>1: PMC profiles are N=1"))
+    tc = traffic[names["closest"]]
+    launch_s = trace_s / launches
+    hbm_ach = tc / launch_s / 1e9 if (tc is not None and launch_s > 0) else None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(sc, integ, args)
         out = {
             "metric": "Mpaths/sec on bedroom@1280×720 spp=256, 1/2/4/8 GPUs; HBM GB/s vs peak",
             "value": round(value, 3),
             "unit": "Mpaths/s",
-            "n_gpus": world,
-            "steps": args.steps,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
+            "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(elapsed / K * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: deterministic bedroom proxy (scene.xml camera/BSDFs/emitters, "
                     f"{sc.n_tris} procedural triangles)",
             "config": {
-                "workload": f"path-mis.py NEE+MIS (BASELINE configs[1]) on bedroom-proxy {W}x{H}, spp={spp} per GPU "
-                            f"(global sample range per rank), max_depth={args.max_depth}, rr_depth={args.rr_depth}",
-                "global_spp": spp * world,
-                "paths_per_step": paths_per_rank * world,
-                "parallelism": f"sample-range shards x{world}, RCCL all_gather of films",
+                "workload": f"path-mis.py NEE+MIS (BASELINE configs[1]) on bedroom-proxy {W}x{H}, global spp={spp} "
+                            f"split over {world} rank(s) by sample range, max_depth={args.max_depth}, "
+                            f"rr_depth={args.rr_depth}",
+                "global_spp": spp,
+                "spp_per_rank": s1 - s0,
+                "paths_per_step": W * H * spp,
+                "parallelism": f"sample-range shards x{world}" + (", RCCL gather of films to rank 0" if world > 1 else ""),
             },
             "roofline": {
-                "bound": "hbm",
+                "bound": "l2",
                 "kernel": "k_trace_closest (4-wide quantised BVH, closest hit)",
                 "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
+                "peak": L2_GATHER_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "frac": round(achieved / L2_GATHER_PEAK_GBS, 4),
+                "traffic": tc,
                 "traffic_source": traffic_src,
-                "avg_launch_ms": round(trace_s * 1e3 / launches, 4),
+                "peak_source": "MI355X_MICROARCH.md 'Indexed rows: gather into LDS': L2-served random row "
+                               "gathers 16.8-18.8 TB/s chip-wide (node array + triangles stay in L2 / Infinity "
+                               "Cache: PMC fabric traffic << algorithmic bytes)",
+                "frac_vs_l2_stream_peak": round(achieved / L2_STREAM_PEAK_GBS, 4),
+                "hbm": None if hbm_ach is None else {
+                    "achieved": round(hbm_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(hbm_ach / HBM_PEAK_GBS, 4),
+                    "bytes_per_launch": tc, "definition": "PMC FETCH_SIZE x2 + WRITE_SIZE per launch / avg launch time"},
+                "avg_launch_ms": round(trace_ms / launches, 4),
                 "launches_per_step": int(launches),
-                "alg_bytes_per_launch": int(alg_bytes / launches),
+                "alg_bytes_per_launch": int(alg_closest / launches),
                 "rays_per_step": int(cnt["rays_closest"]),
                 "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
                 "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2),
-                "simd_util_node_phase": round(cnt["nodes_closest"] / max(1, 64 * cnt["wave_node_iters"]), 3),
-                "simd_util_leaf_phase": round(cnt["tris_closest"] / max(1, 64 * cnt["wave_leaf_iters"]), 3),
+                "active_lane_frac_node_phase": round(cnt["nodes_closest"] / max(1, 64 * cnt["wave_node_iters"]), 3),
+                "tris_per_lane_leaf_step": round(cnt["tris_closest"] / max(1, 64 * cnt["wave_leaf_iters"]), 3),
             },
-            "kernels_ms_per_step": {
-                "trace_closest": round(agg["trace_ms"] / args.steps, 3),
-                "trace_shadow": round(agg["shadow_ms"] / args.steps, 3),
-                "shade": round(agg["shade_ms"] / args.steps, 3),
-                "other": round(agg["other_ms"] / args.steps, 3),
+            "kernels": {
+                "trace_closest": _kernel_entry(trace_ms, launches, tc, alg_closest, L2_GATHER_PEAK_GBS, "l2"),
+                "trace_shadow": _kernel_entry(agg["shadow_ms"] / K, cnt["shadow_launches"], traffic[names["shadow"]],
+                                              alg_shadow, L2_GATHER_PEAK_GBS, "l2"),
+                "shade": _kernel_entry(agg["shade_ms"] / K, cnt["trace_launches"], traffic[names["shade"]],
+                                       cnt["rays_closest"] * SHADE_BYTES_PER_PATH_BOUNCE, HBM_PEAK_GBS, "hbm"),
+                "other_ms_per_step": round(agg["other_ms"] / K, 3),
             },
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def measured_traffic(kernel):
-    """HBM-side bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/*_pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE, made by
-    tools/profile_session.sh + tools/pmc_summary.py on this bench command)."""
-    import glob
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
-        return None, None
-    return int(k["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(sc, integ, args):

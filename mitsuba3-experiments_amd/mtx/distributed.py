@@ -2,13 +2,14 @@
 
 The reference has no distributed code; the path shards
 naturally (§8e):
-  * sample shards (weak scaling, bench.py): every rank traces the global
-    sample range [r*spp, (r+1)*spp) of every pixel; films are gathered to
-    rank 0 and summed in rank order (deterministic).
+  * sample shards (strong scaling, bench.py): rank r traces the global
+    sample range [r*spp/N, (r+1)*spp/N) of every pixel of one fixed-spp
+    render; films are gathered to rank 0 and summed in rank order
+    (deterministic).
   * row bands (strong scaling): rank r traces film rows [y0_r, y1_r); each
     band carries its 1-row tent halo above and below, stitched on rank 0 by
     adding the overlapping halo rows in rank order.
-One collective per render (an all_gather of ~15 MB films for 1280x720);
+One collective per render (a gather of ~15 MB films to rank 0 for 1280x720);
 no data-path exchange during tracing.
 
 prefix_sum (prefix_sum.py:9-36) on a u32 array split into contiguous
@@ -35,6 +36,13 @@ def row_bands(height: int, world: int):
     return [(edges[r], edges[r + 1]) for r in range(world)]
 
 
+def sample_range(spp: int, world: int, rank: int):
+    """Strong-scaling sample shard: rank r traces the global samples
+    [r*spp//N, (r+1)*spp//N) of every pixel (global-lane seeding keeps each
+    path identical to the single-GPU render, path.py:156-161)."""
+    return rank * spp // world, (rank + 1) * spp // world
+
+
 def _to_tensor(film, like_device=None):
     import torch
 
@@ -59,16 +67,19 @@ def _comm(t, group=None):
 
 def gather_sum(film, group=None):
     """Sum of every rank's film in rank order, returned on rank 0 (None elsewhere).
-    `film` is a torch tensor (device for nccl, cpu for gloo) or numpy array."""
+    `film` is a torch tensor (device for nccl, cpu for gloo) or numpy array.
+    One gather to rank 0 (point-to-point receives over xGMI with RCCL), then
+    a fixed rank-order sum: deterministic."""
     import torch
     import torch.distributed as dist
 
     t = _to_tensor(film)
     c = _comm(t, group)
     world = dist.get_world_size(group)
-    parts = [torch.empty_like(c) for _ in range(world)]
-    dist.all_gather(parts, c, group=group)
-    if dist.get_rank(group) != 0:
+    rank = dist.get_rank(group)
+    parts = [torch.empty_like(c) for _ in range(world)] if rank == 0 else None
+    dist.gather(c, parts, dst=0, group=group)
+    if rank != 0:
         return None
     total = torch.zeros_like(c)
     for p in parts:
@@ -105,12 +116,14 @@ def gather_bands(band, y0: int, y1: int, height: int, group=None):
 
 def render_sharded(render, height: int, spp: int, mode: str = "samples", group=None):
     """Run `render(spp, spp_total, sample_offset, y0, y1)` for this rank's shard
-    and combine on rank 0. `render` returns a film (numpy or tensor)."""
+    of ONE render at `spp` global samples per pixel (strong scaling) and
+    combine on rank 0. `render` returns a film (numpy or tensor)."""
     import torch.distributed as dist
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     if mode == "samples":
-        film = render(spp, spp * world, spp * rank, 0, height)
+        s0, s1 = sample_range(spp, world, rank)
+        film = render(s1 - s0, spp, s0, 0, height)
         return gather_sum(film, group)
     if mode == "rows":
         y0, y1 = row_bands(height, world)[rank]

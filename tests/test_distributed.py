@@ -37,7 +37,7 @@ def _worker(rank, world, port, mode, out_path):
         a = integ.render_args(sc, 4, spp, y0, y1, spp_total, off)
         return oracle.render(sc, a)
 
-    full = distributed.render_sharded(render, sc.height, 4, mode)
+    full = distributed.render_sharded(render, sc.height, 8 if mode == "samples" else 4, mode)
     if rank == 0:
         np.save(out_path, full.numpy())
     dist.barrier()

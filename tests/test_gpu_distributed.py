@@ -53,7 +53,7 @@ def _worker(rank, world, port, kind, out_dir):
             return integ.render_film(sc, seed=3, spp=spp, y0=y0, y1=y1, spp_total=spp_total, sample_offset=off,
                                      out=out)
 
-        films.append(distributed.render_sharded(render, sc.height, 4, kind))
+        films.append(distributed.render_sharded(render, sc.height, 8 if kind == "samples" else 4, kind))
     elif kind == "pssmlt":
         integ = load_dict({"type": "pssmlt_simple", "iterations": 6})
         y0, y1 = distributed.row_bands(sc.height, world)[rank]
@@ -150,3 +150,35 @@ def test_two_rank_prefix_sum_u32(tmp_path, oracle):
     x = _scan_input()
     for g, inc in zip(got, (True, False)):
         assert np.array_equal(g.astype(np.uint32), oracle.prefix_sum_u32(x, inclusive=inc))
+
+
+def _bench_film(tmp_path, n, backend="gloo"):
+    """Run bench.py itself (the driver's command) at a small film size and
+    return (JSON line, rank 0's combined seed-0 film)."""
+    import json
+    import subprocess
+    import sys
+
+    out = os.path.join(tmp_path, f"film{n}.npy")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--backend", backend,
+           "--width", "64", "--height", "36", "--spp", "8", "--steps", "1", "--warmup", "0",
+           "--no-cpu-baseline", "--dump-film", out, "--master-port", str(_free_port())]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    return line, np.load(out)
+
+
+@pytest.mark.gpu
+def test_bench_gpus2_strong_scaling(tmp_path):
+    """`bench.py --gpus 2` starts two ranks itself (gloo rehearsal on one GPU),
+    splits the FIXED global spp between them and reports n_gpus 2; its film
+    equals the N=1 film of the same command within the stated rtol (the
+    rank-order sum of two sample shards reorders the float accumulation)."""
+    l1, f1 = _bench_film(tmp_path, 1)
+    l2, f2 = _bench_film(tmp_path, 2)
+    assert l1["n_gpus"] == 1 and l2["n_gpus"] == 2
+    assert l1["config"]["global_spp"] == l2["config"]["global_spp"] == 8
+    assert l2["config"]["spp_per_rank"] == 4 and l2["scaling"] == "strong"
+    assert l1["roofline"]["frac"] <= 1.0
+    np.testing.assert_allclose(f2, f1, rtol=2e-6, atol=1e-6)
