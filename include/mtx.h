@@ -155,8 +155,9 @@ enum {
   MTX_INT_RESTIR_GI = 5,     /* restirgi.py:182-588 */
   MTX_INT_PSSMLT_PATH = 6,   /* pssmlt.py:167-228 + pssmltpath.py:17-190 ("pssmlt") */
   MTX_INT_NERAD_RHS = 7,     /* nerad.py:174-233 Integrator.sample_rhs (internal: mtx_nerad_*) */
-  MTX_INT_NERAD = 8          /* nerad.py:235-254 Integrator.sample: next_smooth_si + the uploaded field
+  MTX_INT_NERAD = 8,         /* nerad.py:235-254 Integrator.sample: next_smooth_si + the uploaded field
                                 (max_depth = 11: first hit + up to 10 delta bounces) */
+  MTX_INT_SIMPLE = 9         /* simple.py:14-116 ("integrator"): BSDF sampling only, no NEE */
 };
 
 typedef struct mtx_render_args {

@@ -523,7 +523,7 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
   }
   if (a->integrator != MTX_INT_PATH && a->integrator != MTX_INT_PATH_MIS && a->integrator != MTX_INT_NRC &&
       a->integrator != MTX_INT_PSSMLT_SIMPLE && a->integrator != MTX_INT_RESTIR_GI &&
-      a->integrator != MTX_INT_PSSMLT_PATH && a->integrator != MTX_INT_NERAD) {
+      a->integrator != MTX_INT_PSSMLT_PATH && a->integrator != MTX_INT_NERAD && a->integrator != MTX_INT_SIMPLE) {
     mtx_set_error("integrator %u is not supported by this entry point", a->integrator);
     return MTX_E_UNSUPPORTED;
   }
@@ -618,8 +618,8 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     e = tm.begin(2);
     mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), c->stream);
     tm.end(2, e);
-    if (p.integrator != MTX_INT_PSSMLT_SIMPLE && !nerad_render &&
-        !(nerad && bounce > 0)) {  // PSSMLT and the nerad render trace no NEE rays
+    if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
+        !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays
       e = tm.begin(1);
       mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
       tm.end(1, e);

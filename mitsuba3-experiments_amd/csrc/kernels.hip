@@ -133,6 +133,8 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   if (p.integrator == MTX_INT_PATH_MIS) {
     depth = 0;
     flags = PF_PREV_DELTA;  // prev_bsdf_delta = True (path-mis.py:46)
+  } else if (p.integrator == MTX_INT_SIMPLE) {
+    depth = 0;  // simple.py:27
   } else {
     depth = 1;  // path.py:230, nrc.py:39
   }
@@ -490,6 +492,58 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   return active;
 }
 
+// simple.py:55-113 — one bounce of the BSDF-only path tracer: emission at
+// the hit without MIS (:69-70, masked by prev_bsdf_pdf > 0), BSDF sample
+// masked by active_next (:79), spawn (:84), depth on a valid hit (:102), RR
+// (:104-111). 4 draws per executed bounce. The same loop as
+// pssmltsimple.py:60-131 without the mutation; bounce 0 starts from the
+// constant initial state (f = 1, eta = 1, L = 0, prev_bsdf_pdf = 1).
+__device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
+                                             const ChunkParams &p, uint32_t bounce, uint32_t path) {
+  const float4 rd = b.ray_d[path];
+  const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
+  const uint4 mi = b.misc[path];
+  const float4 h = b.hit[path];
+  Pcg32 rng;
+  rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
+  rng.seq = mi.z;
+  uint32_t depth = mi.w & 0xffffu;
+  const uint32_t flags = mi.w >> 16;
+  V3 T = V3{th.x, th.y, th.z};
+  float eta = th.w;
+  V3 L = V3{Lr.x, Lr.y, Lr.z};
+  const float prev_pdf = Lr.w;
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{rd.x, rd.y, rd.z});
+  const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
+  L = fma3v(T, le, L);
+  const bool active_next = (depth + 1 < p.max_depth) && si.valid;
+  const float s1 = rng.next_1d();
+  const V2 s2 = rng.next_2d();
+  BSDFSample bs;
+  bs.wo = v3s(0.f);
+  bs.pdf = 0.f;
+  bs.eta = 0.f;
+  bs.type = 0;
+  V3 w = v3s(0.f);
+  if (active_next) w = bsdf_sample(sv.bsdf, sv.materials[si.material], si.uv, si.wi, s1, s2, &bs);
+  const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
+  T = T * w;
+  eta *= bs.eta;
+  if (si.valid) depth += 1;
+  const float fmax_ = hmax(T);
+  const float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);
+  const bool rr_active = depth >= p.rr_depth;
+  const bool rr_continue = rng.next_1d() < rr_prob;
+  if (rr_active) T = T * rcp(rr_prob);
+  const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
+  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
+  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  return active;
+}
+
 // pssmltpath.py:17-168 — one bounce of a PSSMLT proposal with NEE + MIS:
 // emission at the hit weighted against the previous BSDF sample (:71-82),
 // unmasked BSDF sample (:99-101), mutation of the local direction AND of the
@@ -741,6 +795,8 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
     if (valid) {
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
         cont = shade_pssmlt(s, sv, b, p, path);
+      else if constexpr (INT == MTX_INT_SIMPLE)
+        cont = shade_simple(s, sv, b, p, bounce, path);
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
         cont = shade_pssmlt_path(s, sv, b, p, path, io);
       else if constexpr (INT == MTX_INT_NERAD_RHS)
@@ -926,6 +982,7 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
   uint8_t v = 1;
   if (p.integrator == MTX_INT_PATH_MIS) v = (flags & PF_VALID_RAY) ? 1 : 0;
   if (p.integrator == MTX_INT_NRC) v = (flags & PF_PRIMARY_VALID) ? 1 : 0;
+  if (p.integrator == MTX_INT_SIMPLE) v = (b.misc[i].w & 0xffffu) != 0 ? 1 : 0;  // simple.py:118
   valid_out[i] = v;
 }
 
@@ -1120,6 +1177,9 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
       break;
     case MTX_INT_PSSMLT_SIMPLE:
       hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_SIMPLE>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+      break;
+    case MTX_INT_SIMPLE:
+      hipLaunchKernelGGL(k_shade<MTX_INT_SIMPLE>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
     case MTX_INT_PSSMLT_PATH:
       hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);

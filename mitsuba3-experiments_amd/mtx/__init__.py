@@ -16,6 +16,7 @@ from .integrators import (  # noqa: F401
     PssmltPath,
     PssmltSimple,
     RestirIntegrator,
+    Simple,
     develop,
     load_dict,
     register_integrator,

@@ -25,6 +25,7 @@ MTX_INT_RESTIR_GI = 5
 MTX_INT_PSSMLT_PATH = 6
 MTX_INT_NERAD_RHS = 7
 MTX_INT_NERAD = 8
+MTX_INT_SIMPLE = 9
 
 MTX_RESTIR_BIAS_CORRECTION = 1
 MTX_RESTIR_JACOBIAN = 2

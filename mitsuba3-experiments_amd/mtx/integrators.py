@@ -167,6 +167,21 @@ class PathIntegrator(SamplingIntegrator):
         self.rr_depth = self.props.get("rr_depth", 2)  # path-mis.py:22
 
 
+class Simple(SamplingIntegrator):
+    """simple.py:8-116 ("integrator"): BSDF sampling only (no emitter
+    sampling, no MIS), Russian roulette. The estimator without NEE that the
+    NEE + MIS integrators must agree with in expectation (the reference's
+    parity-vs-other-integrator pattern, path.py:332-359, testpssmlt.py)."""
+
+    integrator_id = _abi.MTX_INT_SIMPLE
+    name = "integrator"
+
+    def __init__(self, props=None):
+        super().__init__(props)
+        self.max_depth = self.props.get("max_depth", 8)  # simple.py:11
+        self.rr_depth = self.props.get("rr_depth", 2)  # simple.py:12
+
+
 class NRCIntegrator(SamplingIntegrator):
     """nrc.py:17-125: NEE + MIS path segments truncated by the NRC spread
     heuristic (a < c * a0, c = 0.01); no primary emission (nrc.py:118)."""
@@ -372,6 +387,7 @@ register_integrator("pssmlt_simple", lambda props: PssmltSimple(props))
 register_integrator("pssmlt", lambda props: PssmltPath(props))  # pssmltpath.py:193
 register_integrator("path_test", lambda props: PathIntegrator(props))
 register_integrator("nrc", lambda props: NRCIntegrator(props))
+register_integrator("integrator", lambda props: Simple(props))  # simple.py:119
 register_integrator("nerad", lambda props: NeradIntegrator(props))
 
 

@@ -291,3 +291,20 @@ def nerad_render_samples(scene, args):
     d = scene.desc()
     lib().orc_nerad_render_samples(C.byref(d), C.byref(args), lanes.ctypes.data, pos.ctypes.data)
     return lanes, pos
+
+
+def probe(scene, op, inputs):
+    """orc_probe: the shared sensor / spawn / emitter primitives item by item
+    (op 0 camera_ray, 1 spawn_ray, 2 spawn_ray_to, 3 sample_emitter_direction,
+    4 pdf_emitter_direction + emitter_eval); 16 floats in and out per item."""
+    ops = {"camera_ray": 0, "spawn_ray": 1, "spawn_ray_to": 2, "sample_emitter": 3, "pdf_emitter": 4}
+    x = np.zeros((len(inputs), 16), np.float32)
+    a = np.asarray(inputs, np.float32)
+    x[:, : a.shape[1]] = a
+    out = np.zeros_like(x)
+    d = scene.desc()
+    L = lib()
+    L.orc_probe.argtypes = [C.POINTER(_abi.SceneDesc), C.c_int, C.c_uint64, C.c_void_p, C.c_void_p]
+    rc = L.orc_probe(C.byref(d), ops[op], len(x), x.ctypes.data, out.ctypes.data)
+    assert rc == 0
+    return out

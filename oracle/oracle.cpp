@@ -261,6 +261,43 @@ V3 orc_path_mis(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uin
   return valid_ray ? result : v3s(0.f);  // :155
 }
 
+// ---------------------------- simple.py:14-116 -----------------------------
+// BSDF-sampling-only path tracer ("integrator"); the test estimator without
+// NEE that the NEE + MIS integrators must agree with in expectation.
+V3 orc_simple(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_t rr_depth, bool *valid_out) {
+  V3 f = v3s(1.f), L = v3s(0.f);
+  float eta = 1.f;
+  uint32_t depth = 0;
+  float prev_bsdf_pdf = 1.f;
+  bool active = true;
+  while (active) {  // :55
+    SurfaceInteraction si = intersect(s, ray);  // :57-59
+    V3 le = (prev_bsdf_pdf > 0.f) ? emitter_eval(s, si.emitter, si.wi) : v3s(0.f);
+    L = fma3v(f, le, L);  // :69-70
+    bool active_next = (depth + 1 < max_depth) && si.valid;  // :72
+    float s1 = rng.next_1d();  // :77-78
+    V2 s2 = rng.next_2d();
+    BSDFSample bs{};
+    bs.wo = v3s(0.f);
+    V3 bsdf_weight = v3s(0.f);
+    if (active_next)  // bsdf.sample(..., active_next) (:80)
+      bsdf_weight = bsdf_sample(s.bsdf, s.materials[si.material], si.uv, si.wi, s1, s2, &bs);
+    ray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));  // :86
+    f = f * bsdf_weight;  // :98
+    eta *= bs.eta;
+    prev_bsdf_pdf = bs.pdf;
+    if (si.valid) depth += 1;  // :106
+    float fmax_ = hmax(f);
+    float rr_prob = fminf(fmax_ * sqr(eta), 0.95f);  // :110
+    bool rr_active = depth >= rr_depth;
+    bool rr_continue = rng.next_1d() < rr_prob;
+    if (rr_active) f = f * rcp(rr_prob);  // :114
+    active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);  // :116
+  }
+  *valid_out = depth != 0;  // :118
+  return L;
+}
+
 // ---------------------------- path.py:194-302 ------------------------------
 V3 orc_path(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uint32_t rr_depth, bool *valid_out) {
   V3 L = v3s(0.f), f = v3s(1.f);
@@ -514,6 +551,7 @@ V3 run_integrator(const SceneView &s, const mtx_render_args &a, Pcg32 &rng, cons
   switch (a.integrator) {
     case MTX_INT_PATH: return orc_path(s, rng, ray, a.max_depth, a.rr_depth, valid);
     case MTX_INT_NRC: return orc_nrc(s, rng, ray, a.max_depth, a.nrc_c, valid, (a.flags & 4u) ? query : nullptr);
+    case MTX_INT_SIMPLE: return orc_simple(s, rng, ray, a.max_depth, a.rr_depth, valid);
     default: return orc_path_mis(s, rng, ray, a.max_depth, a.rr_depth, valid);
   }
 }
@@ -1170,6 +1208,54 @@ int orc_bsdf_probe(const mtx_scene_desc *d, uint32_t mat, uint64_t n, const floa
     o[10] = w.x; o[11] = w.y; o[12] = w.z;
     o[13] = val2.x; o[14] = val2.y; o[15] = val2.z;
     out2[i] = pdf2;
+  }
+  return 0;
+}
+
+// Probes of the shared sensor / ray-spawn / emitter primitives (mtx_core/
+// interaction.h) for the independent numpy pins of tests/test_core_pins.py.
+// 16 floats in, 16 floats out per item:
+//   op 0 camera_ray(in[0..1])                    -> o[0..2], d[3..5], maxt[6]
+//   op 1 spawn_ray(p=in[0..2], n=in[3..5], d=in[6..8])    -> o, d, maxt
+//   op 2 spawn_ray_to(p=in[0..2], n=in[3..5], t=in[6..8]) -> o, d, maxt
+//   op 3 sample_emitter_direction(ref=in[0..2], u=in[3..4])
+//        -> weight[0..2], p[3..5], n[6..8], d[9..11], dist[12], pdf[13], emitter[14]
+//   op 4 pdf_emitter_direction(emitter=in[0], d=in[1..3], dist=in[4], n=in[5..7]) -> pdf[0];
+//        emitter_eval(emitter, wi_local=in[8..10]) -> [1..3]
+int orc_probe(const mtx_scene_desc *d, int op, uint64_t n, const float *in, float *out) {
+  SceneView s = make_view(d);
+  for (uint64_t i = 0; i < n; ++i) {
+    const float *a = in + 16 * i;
+    float *o = out + 16 * i;
+    for (int k = 0; k < 16; ++k) o[k] = 0.f;
+    V3 x{a[0], a[1], a[2]}, y{a[3], a[4], a[5]}, z{a[6], a[7], a[8]};
+    Ray r{};
+    switch (op) {
+      case 0: r = camera_ray(s.camera, V2{a[0], a[1]}); break;
+      case 1: r = spawn_ray(x, y, z); break;
+      case 2: r = spawn_ray_to(x, y, z); break;
+      case 3: {
+        DirectionSample ds{};
+        V3 w = sample_emitter_direction(s, x, V2{a[3], a[4]}, &ds);
+        o[0] = w.x; o[1] = w.y; o[2] = w.z;
+        o[3] = ds.p.x; o[4] = ds.p.y; o[5] = ds.p.z;
+        o[6] = ds.n.x; o[7] = ds.n.y; o[8] = ds.n.z;
+        o[9] = ds.d.x; o[10] = ds.d.y; o[11] = ds.d.z;
+        o[12] = ds.dist; o[13] = ds.pdf; o[14] = (float)ds.emitter;
+        continue;
+      }
+      case 4: {
+        const int32_t e = (int32_t)a[0];
+        o[0] = pdf_emitter_direction(s, e, V3{a[1], a[2], a[3]}, a[4], V3{a[5], a[6], a[7]});
+        V3 le = emitter_eval(s, e, V3{a[8], a[9], a[10]});
+        o[1] = le.x; o[2] = le.y; o[3] = le.z;
+        continue;
+      }
+      default: return -1;
+    }
+    o[0] = r.o.x; o[1] = r.o.y; o[2] = r.o.z;
+    o[3] = r.d.x; o[4] = r.d.y; o[5] = r.d.z;
+    o[6] = r.maxt;
   }
   return 0;
 }

@@ -6,7 +6,7 @@ against drift; their contents are data (inputs and outputs), nothing from
 the reference's sources. Vectors:
   rng_seed0 / rng_seed7   first 64 draws of sampler lanes 0..1023
   trace_rays / trace_hits 4096 rays on the 2 %-budget bedroom proxy
-  film_<integrator>       64x36, spp 16, seed 0 films (path_test, mypath, nrc)
+  film_<integrator>       64x36, spp 16, seed 0 films (path_test, mypath, nrc, integrator = simple.py)
   film_pssmlt_simple      32x18, spp 2, seed 2, 60 Metropolis iterations
   film_pssmlt             the same for pssmltpath.py (NEE + MIS proposals)
   film_restirgi_f<k>      64x36 ReSTIR GI frames 0..2 (test-restir-spatial.py
@@ -29,7 +29,7 @@ sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd"), os.path.join(ROO
 import binding as oracle  # noqa: E402
 from mtx import load_dict, scene  # noqa: E402
 
-INTEGRATORS = ("path_test", "mypath", "nrc")
+INTEGRATORS = ("path_test", "mypath", "nrc", "integrator")
 RESTIR_PROPS = {"jacobian": False, "bias_correction": True, "max_M_spatial": 500, "max_M_temporal": 30}
 
 

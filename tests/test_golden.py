@@ -32,7 +32,7 @@ def test_golden_trace(golden, oracle, small_scene):
     assert np.array_equal(oracle.trace(small_scene, golden["trace_rays"])[0], golden["trace_hits"])
 
 
-@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc"])
+@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc", "integrator"])
 def test_golden_films_oracle(golden, oracle, small_scene, name):
     from mtx import load_dict
 
@@ -54,7 +54,7 @@ def test_golden_independent_of_bvh_collapse(golden, oracle, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc"])
+@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc", "integrator"])
 def test_golden_films_gpu(golden, small_scene, name):
     from mtx import load_dict
 

@@ -16,7 +16,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-INTEGRATORS = ["path_test", "mypath", "nrc"]
+INTEGRATORS = ["path_test", "mypath", "nrc", "integrator"]
 
 
 def _ctx():
