@@ -137,6 +137,7 @@ struct mtx_ctx {
   uint32_t lds_stack = mtxd::kLdsStack;
   uint32_t trace_batch = 256;
   uint32_t refill_lanes = 16;
+  uint32_t urefill = 16;
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
@@ -188,6 +189,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
+  if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
@@ -376,6 +378,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
   s.trace_batch = c->trace_batch;
   s.refill_lanes = c->refill_lanes;
+  s.urefill = c->urefill;
   s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
   s.shade_sort = c->shade_sort;

@@ -335,9 +335,9 @@ __device__ __forceinline__ uint32_t xseg_bound(uint32_t count, uint32_t k) {
 // queue and share BVH nodes in that XCD's L2; exhausted segments send the
 // wave on to the next XCD's segment.
 template <bool ANY, bool STATS = false, class Src>
-__device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
-                                           int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
-                                           uint32_t *wave_iters = nullptr) {
+__device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
+                                              int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
+                                              uint32_t *wave_iters = nullptr) {
   const uint32_t lane = lane_id();
   int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
   const int lds_n = (int)s.lds_entries;
@@ -537,6 +537,212 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
       if (idle == ~0ull || (!exhausted && (uint32_t)__popcll(idle) >= s.refill_lanes)) break;
     }
   }
+}
+
+
+// ---------------------------------------------------------------------------
+// Unified single-step traversal (A/B against while-while: MTX_TRAV_UNIFIED).
+//
+// Every iteration each lane with a ray performs one unit of work: one inner
+// node visit, then (same iteration) one triangle test if its current leaf
+// has triangles left. A lane reaching a leaf starts on its triangles in the
+// same iteration; a lane that finishes its ray is refilled once enough lanes
+// of the wave are idle. Nothing waits for the slowest lane of the wave to
+// reach a leaf (the while-while phase barrier), so more lanes do work per
+// wave-instruction; the price is that both code paths run in an iteration
+// whenever the wave holds lanes of both kinds. Each ray's visit sequence is
+// the plain front-to-back order of `traverse` (the oracle's), with or
+// without STATS.
+// ---------------------------------------------------------------------------
+template <bool ANY, bool STATS = false, class Src>
+__device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
+                                             int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
+                                             uint32_t *wave_iters = nullptr) {
+  const uint32_t lane = lane_id();
+  int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
+  const int lds_n = (int)s.lds_entries;
+  bool has = false, exhausted = false, hit = false, drained = false;
+  uint32_t res_lo = 0, res_hi = 0;
+  uint32_t payload = 0, prim = 0xffffffffu;
+  TraceRay r;
+  float tbest = 0.f, bu = 0.f, bv = 0.f;
+  int32_t node = -1;          // >= 0: inner node to visit next
+  uint32_t tri = 0, tri_end = 0;  // triangles [tri, tri_end) of the current leaf
+  int sp = 0;
+  const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
+  const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
+  if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + batch - 1) / batch) return;
+  uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
+  // next work item of a lane from its stack: an inner node, a leaf's
+  // triangle range, or nothing (the ray is finished)
+  auto pop_next = [&]() {
+    node = -1;
+    while (sp > 0) {
+      --sp;
+      const int32_t e = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];
+      if (e >= 0) {
+        node = e;
+        return;
+      }
+      uint32_t first, cnt;
+      leaf_decode(e, &first, &cnt);
+      tri = first;
+      tri_end = first + cnt;
+      return;
+    }
+  };
+  while (true) {
+    if (!exhausted) {
+      const uint64_t idle = __ballot(!has);
+      const uint32_t n = (uint32_t)__popcll(idle);
+      if (n >= s.urefill || idle == ~0ull) {
+        const uint32_t left = res_hi - res_lo;
+        uint32_t base2 = 0, got2 = 0;
+        if (left < n && !drained) {
+          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
+          while (true) {  // wave-uniform
+            const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
+            const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
+            uint32_t b = 0xffffffffu;
+            if (hi > lo) {
+              if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
+              b = __builtin_amdgcn_readlane(b, leader);
+            }
+            if (hi > lo && b < hi - lo) {
+              base2 = lo + b;
+              got2 = min(batch, hi - lo - b);
+              break;
+            }
+            if (++tries >= kXcds) {
+              drained = true;
+              break;
+            }
+            seg = (seg + 1) & (kXcds - 1u);
+          }
+        }
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        uint32_t k = 0;
+        bool ok = false;
+        if (rk < left) {
+          k = res_lo + rk;
+          ok = true;
+        } else if (rk - left < got2) {
+          k = base2 + (rk - left);
+          ok = true;
+        }
+        if (n <= left) {
+          res_lo += n;
+        } else {
+          const uint32_t used2 = min(n - left, got2);
+          res_lo = base2 + used2;
+          res_hi = base2 + got2;
+        }
+        if (!has && ok) {
+          src.load(k, r, tbest, payload);
+          prim = 0xffffffffu;
+          bu = bv = 0.f;
+          hit = false;
+          node = 0;
+          tri = tri_end = 0;
+          sp = 0;
+          has = true;
+        }
+        exhausted = drained && res_lo >= res_hi;
+      }
+    }
+    if (__ballot(has) == 0) break;
+    // ---- one inner-node visit
+    if (has && node >= 0) {
+      if (STATS) {
+        const uint64_t m = __ballot(true);
+        if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[0];
+      }
+      int4 rf;
+      uint32_t key[4];
+      ++nv;
+      const int n = wide_visit(s, r, node, tbest, rf, key);
+      if (n > 0) {
+        const int32_t c1 = wide_ref(key[1], rf.x, rf.y, rf.z, rf.w);
+        const int32_t c2 = wide_ref(key[2], rf.x, rf.y, rf.z, rf.w);
+        const int32_t c3 = wide_ref(key[3], rf.x, rf.y, rf.z, rf.w);
+        const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
+        if (sp + 3 <= lds_n) {
+          stk[sp * kTraceBlock] = e0;
+          stk[(sp + 1) * kTraceBlock] = e1;
+          stk[(sp + 2) * kTraceBlock] = c1;
+        } else {
+          const int32_t e[3] = {e0, e1, c1};
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            if (j < n - 1) {
+              const int q = sp + j;
+              if (q < lds_n)
+                stk[q * kTraceBlock] = e[j];
+              else
+                ovf[(size_t)(q - lds_n) * s.ovf_threads] = e[j];
+            }
+        }
+        sp += n - 1;
+        const int32_t c0 = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
+        if (c0 >= 0) {
+          node = c0;
+        } else {
+          uint32_t first, cnt;
+          leaf_decode(c0, &first, &cnt);
+          tri = first;
+          tri_end = first + cnt;
+          node = -1;
+        }
+      } else {
+        pop_next();
+      }
+    }
+    // ---- one triangle test
+    if (has && tri < tri_end) {
+      if (STATS) {
+        const uint64_t m = __ballot(true);
+        if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
+      }
+      const uint32_t pr = tri;
+      const float4 g0 = s.tri[3 * pr + 0], g1 = s.tri[3 * pr + 1], g2 = s.tri[3 * pr + 2];
+      float t, u, v;
+      ++tv;
+      ++tri;
+      if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+        if (ANY) {
+          hit = true;
+          tri = tri_end;
+          sp = 0;
+        } else if (t < tbest || (t == tbest && pr < prim)) {
+          tbest = t;
+          prim = pr;
+          bu = u;
+          bv = v;
+        }
+      }
+      if (tri >= tri_end) pop_next();
+    }
+    if (has && node < 0 && tri >= tri_end) {
+      src.finish(payload, hit, tbest, prim, bu, bv);
+      has = false;
+      ++nr;
+    }
+  }
+}
+
+// bit 0: closest-hit kernels, bit 1: any-hit kernels use trace_loop_u
+#ifndef MTX_TRAV_UNIFIED
+#define MTX_TRAV_UNIFIED 1
+#endif
+template <bool ANY, bool STATS = false, class Src>
+__device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
+                                           int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
+                                           uint32_t *wave_iters = nullptr) {
+  if ((MTX_TRAV_UNIFIED >> (ANY ? 1 : 0)) & 1)
+    trace_loop_u<ANY, STATS>(s, src, count, heads, stk, nv, tv, nr, wave_iters);
+  else
+    trace_loop_ww<ANY, STATS>(s, src, count, heads, stk, nv, tv, nr, wave_iters);
 }
 
 }  // namespace mtxd
