@@ -287,8 +287,11 @@ def main():
             },
             "kernels": {
                 "trace_closest": _kernel_entry(trace_ms, launches, tc, alg_closest, L2_GATHER_PEAK_GBS, "l2"),
-                "trace_shadow": _kernel_entry(agg["shadow_ms"] / K, cnt["shadow_launches"], traffic[names["shadow"]],
-                                              alg_shadow, L2_GATHER_PEAK_GBS, "l2"),
+                "trace_shadow": dict(_kernel_entry(agg["shadow_ms"] / K, cnt["shadow_launches"], traffic[names["shadow"]],
+                                                   alg_shadow, L2_GATHER_PEAK_GBS, "l2"),
+                                     rays_per_step=int(cnt["rays_shadow"]),
+                                     node_visits_per_ray=round(cnt["nodes_shadow"] / max(1, cnt["rays_shadow"]), 2),
+                                     tri_visits_per_ray=round(cnt["tris_shadow"] / max(1, cnt["rays_shadow"]), 2)),
                 "shade": _kernel_entry(agg["shade_ms"] / K, cnt["trace_launches"], traffic[names["shade"]],
                                        cnt["rays_closest"] * SHADE_BYTES_PER_PATH_BOUNCE, HBM_PEAK_GBS, "hbm"),
                 "other_ms_per_step": round(agg["other_ms"] / K, 3),
