@@ -244,3 +244,31 @@ def test_pssmlt_film_bit_exact(small_scene, oracle, iterations, name):
     np.testing.assert_array_equal(film, ref)
     if iterations > 41:
         assert film[..., 3].sum() > 0
+
+
+def test_prims_bucket_path_at_benchmark_scale(oracle):
+    """The hand-written partition + per-bucket kernels (prims.hip) at the
+    SURVEY §8d primitive sizes: hashgrid 2^22 points (res 100, n_cells = n;
+    and 2^24 cells: the 13-bit buckets), clustered points (every point in a
+    few hundred cells: long election rounds), scatter_reduce 2^22 values into
+    2^20 targets for add / min / max -- all bit-exact against the oracle
+    (ascending original index within a cell / per target)."""
+    from mtx import primitives
+
+    rng = np.random.default_rng(21)
+    n = 1 << 22
+    p = rng.random((3, n), dtype=np.float32)
+    for nc in (n, 1 << 24):
+        g = primitives.HashGrid(p, 100, nc)
+        for a, b in zip((g.cell, g.cell_size, g.cell_offset, g.sample_idx), oracle.hashgrid(p, 100, nc)):
+            assert np.array_equal(a, b), nc
+    q = (rng.integers(0, 8, (3, 1 << 18)) / 8.0).astype(np.float32)  # 512 distinct points
+    g = primitives.HashGrid(q, 100, 1 << 16)
+    for a, b in zip((g.cell, g.cell_size, g.cell_offset, g.sample_idx), oracle.hashgrid(q, 100, 1 << 16)):
+        assert np.array_equal(a, b)
+    nt, nv = 1 << 20, 1 << 22
+    idx = rng.integers(0, nt, nv, dtype=np.uint32)
+    val = (rng.random(nv, dtype=np.float32) - 0.5).astype(np.float32)
+    for op in (0, 1, 2):
+        tgt = rng.random(nt, dtype=np.float32)
+        assert np.array_equal(primitives.scatter_reduce_with(op, tgt, val, idx), oracle.scatter_reduce(op, tgt, val, idx))
