@@ -308,3 +308,42 @@ def probe(scene, op, inputs):
     rc = L.orc_probe(C.byref(d), ops[op], len(x), x.ctypes.data, out.ctypes.data)
     assert rc == 0
     return out
+
+
+# ---- multi-core CPU baselines (bench.py cpu_baseline legs; equal results) --
+def prefix_sum_u32_mt(x, inclusive=True):
+    x = np.ascontiguousarray(x, np.uint32)
+    out = np.zeros_like(x)
+    L = lib()
+    L.orc_prefix_sum_u32_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_int]
+    L.orc_prefix_sum_u32_mt(x.ctypes.data, out.ctypes.data, len(x), int(inclusive))
+    return out
+
+
+def prefix_sum_f32_hs_mt(x):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros_like(x)
+    L = lib()
+    L.orc_prefix_sum_f32_hs_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+    L.orc_prefix_sum_f32_hs_mt(x.ctypes.data, out.ctypes.data, len(x))
+    return out
+
+
+def hashgrid_mt(p, resolution, n_cells):
+    p = np.ascontiguousarray(p, np.float32).reshape(3, -1)
+    n = p.shape[1]
+    out = [np.zeros(n, np.uint32), np.zeros(n_cells, np.uint32), np.zeros(n_cells, np.uint32), np.zeros(n, np.uint32)]
+    L = lib()
+    L.orc_hashgrid_mt.argtypes = [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32] + [C.c_void_p] * 4
+    L.orc_hashgrid_mt(p.ctypes.data, n, resolution, n_cells, *[a.ctypes.data for a in out])
+    return tuple(out)
+
+
+def scatter_reduce_mt(op, target, value, index):
+    t = np.array(target, np.float32)
+    v = np.ascontiguousarray(value, np.float32)
+    i = np.ascontiguousarray(index, np.uint32)
+    L = lib()
+    L.orc_scatter_reduce_f32_mt.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint64]
+    L.orc_scatter_reduce_f32_mt(op, t.ctypes.data, len(t), v.ctypes.data, i.ctypes.data, len(v))
+    return t

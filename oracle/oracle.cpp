@@ -33,7 +33,10 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include <algorithm>
+#include <parallel/algorithm>
 #include <vector>
 
 #include "mtx.h"
@@ -1141,6 +1144,122 @@ int orc_hashgrid(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uin
     acc += cell_size[c];
   }
   for (uint64_t i = 0; i < n; ++i) sample_idx[cell_offset[cell[i]] + rank[i]] = (uint32_t)i;
+  return 0;
+}
+
+// ------------------- multi-core CPU baselines (OpenMP) ----------------------
+// The same results as the sequential restatements above (tested equal),
+// computed with every host thread: bench.py's cpu_baseline leg times these
+// for the primitive lines (all host cores). Not used as checkers.
+
+// u32 scan: per-thread chunk sums, exclusive scan of the chunk sums, local pass.
+int orc_prefix_sum_u32_mt(const uint32_t *in, uint32_t *out, uint64_t n, int inclusive) {
+  const int T = omp_get_max_threads();
+  std::vector<uint32_t> part(T + 1, 0);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+    uint32_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += in[i];
+    part[t + 1] = s;
+#pragma omp barrier
+#pragma omp single
+    for (int k = 0; k < T; ++k) part[k + 1] += part[k];
+    uint32_t acc = part[t];
+    for (uint64_t i = lo; i < hi; ++i) {
+      const uint32_t v = in[i];
+      if (inclusive) {
+        acc += v;
+        out[i] = acc;
+      } else {
+        out[i] = acc;
+        acc += v;
+      }
+    }
+  }
+  return 0;
+}
+
+// Hillis-Steele passes in the reference's order, each pass over all threads.
+int orc_prefix_sum_f32_hs_mt(const float *in, float *out, uint64_t n) {
+  std::vector<float> x(in, in + n), y(n);
+  for (uint64_t st = 1; st < n; st <<= 1) {
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < (int64_t)n; ++j) y[j] = (uint64_t)j >= st ? x[j] + x[j - st] : x[j];
+    x.swap(y);
+  }
+  if (n) memcpy(out, x.data(), n * sizeof(float));
+  return 0;
+}
+
+// Hash grid: bbox (parallel reduction), cells in parallel, then a parallel
+// sort of (cell, index) pairs (libstdc++ parallel mode) = ascending index
+// within a cell, and the run bounds in parallel.
+int orc_hashgrid_mt(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
+                    uint32_t *cell_offset, uint32_t *sample_idx) {
+  const float *px = p, *py = p + n, *pz = p + 2 * n;
+  float bbmin = INFINITY, bbmax = -INFINITY;
+#pragma omp parallel for reduction(min : bbmin) reduction(max : bbmax)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    bbmin = fminf(bbmin, fminf(px[i], fminf(py[i], pz[i])));
+    bbmax = fmaxf(bbmax, fmaxf(px[i], fmaxf(py[i], pz[i])));
+  }
+  const float ext = bbmax - bbmin, fres = (float)res;
+  std::vector<uint64_t> key(n);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i) {
+    const uint32_t x = (uint32_t)((px[i] - bbmin) / ext * fres);
+    const uint32_t y = (uint32_t)((py[i] - bbmin) / ext * fres);
+    const uint32_t z = (uint32_t)((pz[i] - bbmin) / ext * fres);
+    const uint32_t h = ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
+    cell[i] = h;
+    key[i] = ((uint64_t)h << 32) | (uint64_t)i;
+  }
+  __gnu_parallel::sort(key.begin(), key.end());
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < (int64_t)n_cells; ++c) cell_size[c] = 0;
+#pragma omp parallel for schedule(static)
+  for (int64_t k = 0; k < (int64_t)n; ++k) {
+    const uint32_t c = (uint32_t)(key[k] >> 32);
+    sample_idx[k] = (uint32_t)key[k];
+    if (k == 0 || (uint32_t)(key[k - 1] >> 32) != c) cell_offset[c] = (uint32_t)k;  // run start
+  }
+#pragma omp parallel for schedule(static)
+  for (int64_t k = 0; k < (int64_t)n; ++k) {
+    const uint32_t c = (uint32_t)(key[k] >> 32);
+    if (k + 1 == (int64_t)n || (uint32_t)(key[k + 1] >> 32) != c) cell_size[c] = (uint32_t)(k + 1) - cell_offset[c];
+  }
+  // empty cells: offset = start of the next non-empty run (exclusive scan)
+  uint32_t next = (uint32_t)n;
+  for (int64_t c = (int64_t)n_cells - 1; c >= 0; --c) {
+    if (cell_size[c]) next = cell_offset[c];
+    else cell_offset[c] = next;
+  }
+  return 0;
+}
+
+// Scatter-reduce: parallel sort of (target, index) pairs, then every target
+// folds its values in ascending index order (targets in parallel).
+int orc_scatter_reduce_f32_mt(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
+                              uint64_t n_value) {
+  std::vector<uint64_t> key(n_value);
+  for (uint64_t i = 0; i < n_value; ++i)
+    if (index[i] >= n_target) return -1;
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n_value; ++i) key[i] = ((uint64_t)index[i] << 32) | (uint64_t)i;
+  __gnu_parallel::sort(key.begin(), key.end());
+#pragma omp parallel for schedule(static)
+  for (int64_t k = 0; k < (int64_t)n_value; ++k) {
+    const uint32_t t = (uint32_t)(key[k] >> 32);
+    if (k > 0 && (uint32_t)(key[k - 1] >> 32) == t) continue;  // not the run start
+    float a = target[t];
+    for (int64_t j = k; j < (int64_t)n_value && (uint32_t)(key[j] >> 32) == t; ++j) {
+      const float b = value[(uint32_t)key[j]];
+      a = op == 0 ? a + b : (op == 1 ? fminf(a, b) : fmaxf(a, b));
+    }
+    target[t] = a;
+  }
   return 0;
 }
 

@@ -116,3 +116,23 @@ def test_prefix_sum_kat(oracle):
     u = np.arange(1, 100, dtype=np.uint32)
     assert np.array_equal(oracle.prefix_sum_u32(u), np.cumsum(u).astype(np.uint32))
     assert np.array_equal(oracle.prefix_sum_u32(u, False), (np.cumsum(u) - u).astype(np.uint32))
+
+
+def test_multicore_primitive_baselines_equal_sequential(oracle):
+    """The OpenMP CPU baselines bench.py times (all host cores) compute the
+    same arrays as the sequential restatements, bit for bit."""
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 1 << 16, 100003, dtype=np.uint32)
+    for inc in (True, False):
+        assert np.array_equal(oracle.prefix_sum_u32_mt(x, inc), oracle.prefix_sum_u32(x, inc))
+    f = rng.random(70001, dtype=np.float32)
+    assert np.array_equal(oracle.prefix_sum_f32_hs_mt(f), oracle.prefix_sum_f32_hs(f))
+    p = rng.random((3, 50000), dtype=np.float32)
+    for nc in (50000, 97, 1, 1 << 20):
+        for a, b in zip(oracle.hashgrid_mt(p, 100, nc), oracle.hashgrid(p, 100, nc)):
+            assert np.array_equal(a, b), nc
+    idx = rng.integers(0, 1000, 60000, dtype=np.uint32)
+    val = rng.random(60000, dtype=np.float32) - 0.5
+    for op in (0, 1, 2):
+        tgt = rng.random(1000, dtype=np.float32)
+        assert np.array_equal(oracle.scatter_reduce_mt(op, tgt, val, idx), oracle.scatter_reduce(op, tgt, val, idx))

@@ -235,21 +235,21 @@ def restir(args):
     px = sc.width * sc.height
     cpu = None
     if rk.world == 1:
-        # CPU: the oracle's frame loop on a reduced film
+        # CPU: the oracle's frame loop on the same 1920x1080 film (frame 0,
+        # then as many frames as fit the CPU budget, at most 3)
         oracle.build()
-        small = sc.with_film(240, 135)
-        orc = oracle.RestirOracle(small)
+        orc = oracle.RestirOracle(sc)
         ci = RestirIntegrator(RESTIR_C4)
         t1 = time.perf_counter()
         nf = 0
         while nf < 3 and (nf == 0 or time.perf_counter() - t1 < args.cpu_seconds):
             ci.n = nf
-            orc.frame(small, ci.render_args(small, nf, 1))
+            orc.frame(sc, ci.render_args(sc, nf, 1))
             nf += 1
         c = time.perf_counter() - t1
-        cpu = {"value": round(240 * 135 * nf / c / 1e6, 4), "unit": "Mpixel-frames/s", "cores": _threads(),
-               "kind": "port", "sample": f"{nf} frames at 240x135 ({c:.1f} s), same properties; oracle/oracle.cpp "
-                                         "orc_restir_frame (OpenMP)"}
+        cpu = {"value": round(sc.width * sc.height * nf / c / 1e6, 4), "unit": "Mpixel-frames/s", "cores": _threads(),
+               "kind": "port", "sample": f"{nf} frames at {sc.width}x{sc.height} ({c:.1f} s), same properties; "
+                                         "oracle/oracle.cpp orc_restir_frame (OpenMP)"}
     if rk.rank == 0:
         _line(f"ReSTIR GI Mpixel-frames/sec on bedroom@1920x1080 (C4, {rk.world} GPU)", px / dt / 1e6,
               "Mpixel-frames/s", args.frames, W, dt * 1e3,
@@ -352,22 +352,23 @@ def prims(args):
     n = 1 << 28
     x = rng.integers(0, 1 << 16, n, dtype=np.uint32)
     ms = best(lambda: primitives.prefix_sum(x))
-    nc = 1 << 26
-    c = cpu_time(lambda: oracle.prefix_sum_u32(x[:nc]))
+    nc = 1 << 28
+    c = cpu_time(lambda: oracle.prefix_sum_u32_mt(x[:nc]))
     ach = 8 * n / (ms / 1e3) / 1e9
     _line("prefix_sum u32 Gelem/sec (prefix_sum.py:9-36), n=2^28", n / (ms / 1e3) / 1e9, "Gelem/s", 3, 1, ms,
           {"workload": "inclusive scan of 2^28 u32, decoupled look-back", "n": n},
           {"bound": "hbm", "kernel": "scan_u32 (decoupled look-back)", "achieved": round(ach, 1),
            "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
            "alg_bytes_per_launch": 8 * n},
-          {"value": round(nc / c / 1e9, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
-           "sample": f"2^26 elements ({c:.2f} s), oracle orc_prefix_sum_u32"}, dtype="u32")
+          {"value": round(nc / c / 1e9, 4), "unit": "Gelem/s", "cores": _threads(), "kind": "port",
+           "sample": f"same 2^28 elements ({c:.2f} s), oracle orc_prefix_sum_u32_mt (OpenMP, equal to the "
+                     "sequential restatement)"}, dtype="u32")
     del x
     # prefix_sum f32 in Hillis-Steele order, n = 2^24
     n = 1 << 24
     xf = rng.random(n, dtype=np.float32)
     ms = best(lambda: primitives.prefix_sum(xf))
-    c = cpu_time(lambda: oracle.prefix_sum_f32_hs(xf[: 1 << 22]))
+    c = cpu_time(lambda: oracle.prefix_sum_f32_hs_mt(xf))
     passes = int(np.floor(np.log2(n))) + 1
     ach = 8 * n / (ms / 1e3) / 1e9
     hs_bytes = 12 * n * (1 + max(0, passes - 11))
@@ -380,31 +381,30 @@ def prims(args):
            "hs_pass_bytes_per_launch": hs_bytes, "hs_pass_GBs": round(hs_bytes / (ms / 1e3) / 1e9, 1),
            "hs_note": "bytes the reference's Hillis-Steele order needs with 11 passes fused in LDS "
                       "(12 B/element) + one 2-read/1-write pass per remaining level (12 B/element each)"},
-          {"value": round((1 << 22) / c / 1e9, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
-           "sample": f"2^22 elements ({c:.2f} s), oracle orc_prefix_sum_f32_hs"})
+          {"value": round(n / c / 1e9, 4), "unit": "Gelem/s", "cores": _threads(), "kind": "port",
+           "sample": f"same 2^24 elements ({c:.2f} s), oracle orc_prefix_sum_f32_hs_mt (OpenMP passes)"})
     # hash grid, n = 2^24 points, res 100, n_cells = n (hashgrid.py:16-84)
     n = 1 << 24
     p = rng.random((3, n), dtype=np.float32)
     ms = best(lambda: primitives.HashGrid(p, 100, n))
-    nc = 1 << 22
-    pc = np.ascontiguousarray(p[:, :nc])
-    c = cpu_time(lambda: oracle.hashgrid(pc, 100, nc))
+    nc = n
+    c = cpu_time(lambda: oracle.hashgrid_mt(p, 100, nc))
     ach = 32 * n / (ms / 1e3) / 1e9
     _line("hashgrid build Msamples/sec (hashgrid.py:16-84), n=2^24", n / (ms / 1e3) / 1e6, "Msamples/s", 3, 1, ms,
           {"workload": "bbox reduce, hash + rank, scan, fill; res 100, n_cells = n", "n": n},
           {"bound": "hbm", "kernel": "hashgrid_build (4 kernels)", "achieved": round(ach, 1),
            "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
            "alg_bytes_per_launch": 32 * n, "note": "SURVEY §8d: ~32 B/sample"},
-          {"value": round(nc / c / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
-           "sample": f"2^22 points ({c:.2f} s), oracle orc_hashgrid"}, dtype="u32")
-    del p, pc
+          {"value": round(nc / c / 1e6, 4), "unit": "Msamples/s", "cores": _threads(), "kind": "port",
+           "sample": f"same 2^24 points ({c:.2f} s), oracle orc_hashgrid_mt (OpenMP, parallel sort)"}, dtype="u32")
+    del p
     # scatter_reduce add, nv = 2^24, nt = 2^20 (reductions.py:12-54)
     nv, nt = 1 << 24, 1 << 20
     idx = rng.integers(0, nt, nv, dtype=np.uint32)
     val = rng.random(nv, dtype=np.float32)
     tgt = np.zeros(nt, np.float32)
     ms = best(lambda: primitives.scatter_reduce_with("add", tgt, val, idx))
-    c = cpu_time(lambda: oracle.scatter_reduce(0, tgt, val, idx))
+    c = cpu_time(lambda: oracle.scatter_reduce_mt(0, tgt, val, idx))
     ach = 16 * nv / (ms / 1e3) / 1e9
     _line("scatter_reduce add Gvalues/sec (reductions.py:12-54), nv=2^24 nt=2^20", nv / (ms / 1e3) / 1e9,
           "Gvalues/s", 3, 1, ms,
@@ -413,8 +413,8 @@ def prims(args):
           {"bound": "hbm", "kernel": "scatter_reduce rounds", "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_launch": 16 * nv,
            "note": "SURVEY §8d: 16 B/value"},
-          {"value": round(nv / c / 1e9, 4), "unit": "Gvalues/s", "cores": 1, "kind": "port",
-           "sample": f"same {nv} values ({c:.2f} s), oracle orc_scatter_reduce_f32"})
+          {"value": round(nv / c / 1e9, 4), "unit": "Gvalues/s", "cores": _threads(), "kind": "port",
+           "sample": f"same {nv} values ({c:.2f} s), oracle orc_scatter_reduce_f32_mt (OpenMP, parallel sort)"})
 
 
 # ------------------------------------------------- radiance field (MFMA) --
