@@ -302,9 +302,12 @@ int mtx_prefix_sum_f32_hs(mtx_ctx *ctx, const float *in, float *out, uint64_t n)
  * by sample index). p: 3n floats (x[n], y[n], z[n] planes). */
 int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells,
                        uint32_t *cell, uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx);
-/* reductions.py:12-54 scatter_reduce_with for op in {ADD=0, MIN=1, MAX=2}:
- * target[index[i]] = op(target[index[i]], value[i]). ADD sums each target's
- * values in ascending i order (deterministic). target is read-modify-write. */
+/* reductions.py:12-54 scatter_reduce_with for func in {ADD=0, MIN=1, MAX=2,
+ * MUL=3}: target[index[i]] = func(target[index[i]], value[i]), each target's
+ * values applied in ascending i order (deterministic; the reference's order
+ * is race-defined). The reference takes any Python callable (:12, :53); a
+ * device kernel cannot run one, so the op table is fixed.
+ * target is read-modify-write. */
 int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value);
 

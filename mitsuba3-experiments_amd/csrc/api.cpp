@@ -1379,7 +1379,7 @@ int mtx_hashgrid_build(mtx_ctx *c, const float *p, uint64_t n, uint32_t resoluti
 
 int mtx_scatter_reduce_f32(mtx_ctx *c, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value) {
-  if (!c || !target || (n_value && (!value || !index)) || op < 0 || op > 2) {
+  if (!c || !target || (n_value && (!value || !index)) || op < 0 || op > 3) {
     mtx_set_error("mtx_scatter_reduce_f32: bad argument");
     return MTX_E_ARG;
   }

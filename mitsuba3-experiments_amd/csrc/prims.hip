@@ -9,25 +9,21 @@
 //   Hillis-Steele summation order (bit-identical results): the first 11
 //   passes run in LDS on a tile plus its 2047-element halo, the remaining
 //   passes (offsets >= 2048) as coalesced full-array passes.
-// * hashgrid_build: hashgrid.py:16-90 — scalar bbox reduction, cell hash,
-//   then the cell grouping as one stable radix sort of (cell, sample index)
-//   pairs: sample_idx is the sorted index column, so within a cell the
-//   samples come in ascending index order (one valid outcome of the
-//   reference's race-defined winner election, :52-63, and the exact order of
-//   the CPU restatement); cell_offset (:65-76) and cell_size come from the
-//   run boundaries of the sorted cells. Sequential passes replace the
-//   random-address rank atomics and scatter.
+// * hashgrid_build: hashgrid.py:16-90 — bbox reduction, then the cell
+//   grouping as a hand-written stable counting multisplit (see "stable
+//   group-by" below): per-tile histograms of the top cell digit fused with
+//   the hash, a scan, a stable split into buckets, and one workgroup per
+//   bucket that counts its cells in LDS, writes cell_size / cell_offset
+//   (:65-76) and places sample_idx. Within a cell the samples come in
+//   ascending index order (one valid outcome of the reference's
+//   race-defined winner election, :52-63, and the oracle's order).
 // * scatter_reduce_f32: reductions.py:12-54 — the reference serialises each
 //   target with host-synchronised winner-election rounds (race-defined
-//   order). Here: one stable radix sort of (index, value) pairs (rocPRIM,
-//   header-only), segment bounds from the sorted keys, then one thread per
-//   target folds its segment in ascending original position — every target
-//   receives its values in ascending index order (deterministic), with no
-//   host round trips.
+//   order). Here the same stable group-by by target index, then one ordered
+//   fold per target in LDS-bucket order: every target receives its values
+//   in ascending index order (deterministic), with no host round trips and
+//   no global atomics.
 #include <hip/hip_runtime.h>
-
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "mtx.h"
 #include "prims.h"
@@ -262,18 +258,6 @@ __global__ void k_minmax_final(float2 *partial, int m) {
   if (threadIdx.x == 0) partial[m] = make_float2(smin[0], smax[0]);
 }
 
-__global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t res, uint32_t n_cells,
-                             const float2 *bbox, uint32_t *cell) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float2 bb = *bbox;
-  const float bbmin = bb.x, ext = bb.y - bb.x, fres = (float)res;
-  const uint32_t x = (uint32_t)((p[i] - bbmin) / ext * fres);
-  const uint32_t y = (uint32_t)((p[n + i] - bbmin) / ext * fres);
-  const uint32_t z = (uint32_t)((p[2 * n + i] - bbmin) / ext * fres);
-  cell[i] = ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
-}
-
 // cell_offset[c] = number of samples with cell < c and cell_size[c], from
 // the sorted cells. Block b holds keys [i0, i1) (kHashTile of them) in LDS
 // and owns the cells (key[i0-1], key[i1-1]] (the first block from cell 0,
@@ -356,30 +340,664 @@ __global__ void k_hash_offsets_search(const uint32_t *__restrict__ key, uint64_t
   cell_size[c] = (uint32_t)(lower(c + 1) - b);
 }
 
-// --------------------------- scatter reduce -------------------------------
-__global__ void k_sr_bounds(const uint32_t *keys, uint64_t n, uint32_t *seg_start, uint32_t *seg_end) {
+// ------------------ stable group-by (hashgrid, scatter-reduce) -------------
+// hashgrid.py:52-84 and reductions.py:23-54 both group elements by a u32 key
+// (cell / target index) and, for determinism, keep ascending element index
+// inside a key (one of the reference's race-defined outcomes, and the
+// oracle's order). Hand-written counting multisplits, no global atomics:
+// * keys < 2^24 (two levels): k_tile_split sorts every tile stably by the
+//   top digit (key >> s, at most 12 bits) in LDS and writes it back
+//   contiguously with a per-tile digit table; k_bucket_sort gives each
+//   bucket one workgroup that gathers its runs from all tiles into LDS,
+//   counts its 2^s keys, writes their cell_size / cell_offset (or folds
+//   their values) and places every element at its final position. HBM
+//   traffic: the keys/points read once, one 4-8 B record written and
+//   gathered back, the outputs written once.
+// * wider keys: LSD passes of k_ms_place over 12-bit digits, then the run
+//   bounds of the sorted keys.
+// Stability comes from one construction: a wave owns a contiguous run of
+// elements and a private LDS counter row; inside a 64-element round, lanes
+// with equal digits are found with one ballot per digit bit (a match mask)
+// and ranked in lane order; the waves' bases for a digit are prefix sums
+// over the waves in order. A wave's own LDS reads and writes complete in
+// program order, so the read-then-bump of a counter needs no atomic.
+constexpr int kMsWaves = 8;
+constexpr int kMsThreads = 64 * kMsWaves;
+constexpr int kMsRounds = 32;
+constexpr uint32_t kMsSub = 64u * kMsRounds;     // elements per wave
+constexpr uint32_t kMsTile = kMsSub * kMsWaves;  // elements per workgroup
+constexpr int kMsMaxBits = 12;                   // 8 waves x 4096 counters x 4 B = 128 KB of LDS
+
+// Tile of a workgroup: consecutive tiles on one XCD (workgroups are dealt to
+// the 8 XCDs round robin), so the [digit][tile] table's columns share lines
+// inside one L2. A bijection of [0, tiles).
+__device__ __forceinline__ uint32_t ms_tile(uint32_t blk, uint32_t tiles) {
+  const uint32_t x = blk & 7u, j = blk >> 3, q = tiles >> 3, r = tiles & 7u;
+  return x * q + min(x, r) + j;
+}
+
+// Lanes of `active` whose digit equals this lane's (bits ballots).
+__device__ __forceinline__ uint64_t ms_match(uint32_t d, int bits, uint64_t active) {
+  uint64_t m = active;
+  for (int j = 0; j < bits; ++j) {
+    const uint32_t bit = (d >> j) & 1u;
+    const uint64_t bal = __ballot(bit);
+    m &= bit ? bal : ~bal;
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t hg_cell(const float *__restrict__ p, uint64_t n, uint64_t i, float bbmin,
+                                            float ext, float fres, uint32_t n_cells) {
+  // hashgrid.py:86-90 with hash :8-12 (u32 wraparound); the oracle's exact
+  // operation order (orc_hashgrid)
+  const uint32_t x = (uint32_t)((p[i] - bbmin) / ext * fres);
+  const uint32_t y = (uint32_t)((p[n + i] - bbmin) / ext * fres);
+  const uint32_t z = (uint32_t)((p[2 * n + i] - bbmin) / ext * fres);
+  return ((x * 73856093u) ^ (y * 19349663u) ^ (z * 83492791u)) % n_cells;
+}
+
+// Per-tile digit histogram: hist[digit * tiles + tile]. HASH: the keys are
+// the hash-grid cells, computed here from the points and stored to `cell`.
+template <bool HASH>
+__global__ __launch_bounds__(kMsThreads) void k_ms_hist(const uint32_t *__restrict__ keys,
+                                                        const float *__restrict__ p, uint64_t n, uint32_t res,
+                                                        uint32_t n_cells, const float2 *__restrict__ bbox,
+                                                        uint32_t *__restrict__ cell, int shift, int bits,
+                                                        uint32_t *__restrict__ hist, uint32_t tiles) {
+  extern __shared__ uint32_t s_cnt[];
+  const uint32_t B = 1u << bits, t = ms_tile(blockIdx.x, tiles);
+  for (uint32_t b = threadIdx.x; b < B; b += kMsThreads) s_cnt[b] = 0;
+  float bbmin = 0.f, ext = 1.f;
+  if (HASH) {
+    const float2 bb = *bbox;
+    bbmin = bb.x;
+    ext = bb.y - bb.x;
+  }
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)t * kMsTile;
+#pragma unroll 8
+  for (uint32_t r = 0; r < kMsTile / kMsThreads; ++r) {
+    const uint64_t e = t0 + r * kMsThreads + threadIdx.x;
+    if (e < n) {
+      uint32_t k;
+      if (HASH) {
+        k = hg_cell(p, n, e, bbmin, ext, (float)res, n_cells);
+        cell[e] = k;
+      } else {
+        k = keys[e];
+      }
+      atomicAdd(&s_cnt[(k >> shift) & (B - 1u)], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < B; b += kMsThreads) hist[(uint64_t)b * tiles + t] = s_cnt[b];
+}
+
+// Stable multisplit of one tile by digit = (key >> shift) & (2^bits - 1):
+// element e goes to base[digit][tile] + (number of the tile's earlier
+// elements with that digit); base = exclusive scan of k_ms_hist's table.
+// The payload is the element index (INDEX) or pay[e].
+template <bool INDEX>
+__global__ __launch_bounds__(kMsThreads) void k_ms_place(const uint32_t *__restrict__ keys,
+                                                         const uint32_t *__restrict__ pay, uint64_t n, int shift,
+                                                         int bits, const uint32_t *__restrict__ base, uint32_t tiles,
+                                                         uint32_t *__restrict__ keys_out,
+                                                         uint32_t *__restrict__ pay_out) {
+  extern __shared__ uint32_t s_cnt[];  // [kMsWaves][2^bits]
+  const uint32_t B = 1u << bits, t = ms_tile(blockIdx.x, tiles);
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint32_t *cnt = s_cnt + w * B;
+  for (uint32_t b = lane; b < B; b += 64) cnt[b] = 0;
+  const uint64_t s0 = (uint64_t)t * kMsTile + (uint64_t)w * kMsSub;
+  uint32_t k[kMsRounds], v[kMsRounds];
+#pragma unroll
+  for (int r = 0; r < kMsRounds; ++r) {
+    const uint64_t e = s0 + (uint32_t)r * 64u + lane;
+    k[r] = e < n ? keys[e] : 0u;
+    if (!INDEX) v[r] = e < n ? pay[e] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < kMsRounds; ++r)
+    if (s0 + (uint32_t)r * 64u + lane < n) atomicAdd(&cnt[(k[r] >> shift) & (B - 1u)], 1u);
+  // the tile's column of bases: all loads in flight before the LDS work
+  constexpr int kCol = (1 << kMsMaxBits) / kMsThreads;
+  uint32_t col[kCol];
+#pragma unroll
+  for (int i = 0; i < kCol; ++i) {
+    const uint32_t b = threadIdx.x + (uint32_t)i * kMsThreads;
+    col[i] = b < B ? base[(uint64_t)b * tiles + t] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kCol; ++i) {
+    const uint32_t b = threadIdx.x + (uint32_t)i * kMsThreads;
+    if (b < B) {
+      uint32_t run = col[i];
+#pragma unroll
+      for (int q = 0; q < kMsWaves; ++q) {
+        const uint32_t c = s_cnt[q * B + b];
+        s_cnt[q * B + b] = run;
+        run += c;
+      }
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int r = 0; r < kMsRounds; ++r) {
+    const uint64_t e = s0 + (uint32_t)r * 64u + lane;
+    const bool ok = e < n;
+    const uint32_t d = (k[r] >> shift) & (B - 1u);
+    const uint64_t peers = ms_match(d, bits, __ballot(ok));
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    const uint32_t p0 = cnt[d];
+    if (ok && rank == 0) cnt[d] = p0 + (uint32_t)__popcll(peers);
+    if (ok) {
+      keys_out[p0 + rank] = k[r];
+      pay_out[p0 + rank] = INDEX ? (uint32_t)e : v[r];
+    }
+  }
+}
+
+__device__ __forceinline__ float sr_apply(int op, float a, float b) {
+  switch (op) {
+    case 0: return a + b;
+    case 1: return fminf(a, b);
+    case 2: return fmaxf(a, b);
+    default: return a * b;
+  }
+}
+
+// ---- two-level path (keys < 2^24) ----
+// Level 1, k_tile_split: one workgroup per tile of T elements sorts the tile
+// stably by the top digit d = key >> s in LDS and writes it back
+// contiguously (no scattered stores: a 4096-way global split of 4-byte
+// elements wrote 12x its bytes to the fabric as partial lines), with the
+// tile's digit table tab[tile][d] = start | end << 16. Level 2,
+// k_bucket_sort: one workgroup per bucket d gathers the bucket's runs from
+// every tile (tile order = element order) into registers, sorts them stably
+// by the 2^s local keys with the same per-wave-row construction, and writes
+// the bucket's slice of the output contiguously (hashgrid: cell_size,
+// cell_offset, sample_idx) or folds each key's run in order (scatter-reduce).
+// Adjacent buckets run on one XCD, so neighbouring digits' runs share L2
+// lines. Records: hashgrid (local key << 14 | position in tile), T = 16384;
+// scatter-reduce {value bits, local key}, T = 8192.
+template <int MODE>
+struct SplitCfg;
+template <>
+struct SplitCfg<0> {
+  static constexpr uint32_t T = 16384, Tiles = 1024;  // Tiles: tile runs level 2 holds in LDS per pass
+  using Rec = uint32_t;
+};
+template <>
+struct SplitCfg<1> {
+  static constexpr uint32_t T = 8192, Tiles = 2048;
+  using Rec = uint2;
+};
+constexpr int kSplitMaxTop = 12;  // level-1 LDS: 8 waves x 4096 digits x u16 + the staged tile
+constexpr int kBkWaves = 4, kBkThreads = 64 * kBkWaves;
+constexpr uint32_t kBkCap = 5120;                    // records per level-2 chunk (20 per thread)
+constexpr uint32_t kBkRounds = kBkCap / kBkThreads;  // rounds of 64 per wave
+
+// Exclusive scan of one value per thread over a workgroup of NW waves.
+template <int NW>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wsum, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= (uint32_t)off) x += y;
+  }
+  __syncthreads();  // s_wsum free
+  if (lane == 63) s_wsum[w] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t sq = s_wsum[q];
+    pre += (uint32_t)q < w ? sq : 0u;
+    tot += sq;
+  }
+  *total = tot;
+  return pre + x - v;
+}
+
+__global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t res, uint32_t n_cells,
+                             const float2 *__restrict__ bbox, uint32_t *__restrict__ cell) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float2 bb = *bbox;
+  cell[i] = hg_cell(p, n, i, bb.x, bb.y - bb.x, (float)res, n_cells);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__ keys, const float *__restrict__ value,
+                                                    uint64_t n, int s, int top, uint32_t *__restrict__ tab,
+                                                    typename SplitCfg<MODE>::Rec *__restrict__ out1) {
+  using Rec = typename SplitCfg<MODE>::Rec;
+  constexpr uint32_t T = SplitCfg<MODE>::T, R = T / 512;  // rounds of 64 per wave
+  extern __shared__ uint32_t lds[];
+  __shared__ uint32_t s_wsum[8];
+  const uint32_t B = 1u << top, L1 = (1u << s) - 1u;
+  uint32_t *rows = lds;  // [8][B] u16 counters, two per word
+  Rec *stage = (Rec *)(lds + 4 * B);
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t t0 = (uint64_t)blockIdx.x * T;
+  const uint32_t tsize = (uint32_t)min((uint64_t)T, n - t0);
+  uint32_t *row = rows + w * (B / 2);
+  uint16_t *row16 = (uint16_t *)row;
+  for (uint32_t i = lane; i < B / 2; i += 64) row[i] = 0;
+  uint32_t key[R], val[R];
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t j = w * (T / 8) + r * 64 + lane;
+    const bool ok = j < tsize;
+    key[r] = ok ? keys[t0 + j] : 0u;
+    if (MODE == 1) val[r] = ok ? __float_as_uint(value[t0 + j]) : 0u;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t d = key[r] >> s;
+    if (w * (T / 8) + r * 64 + lane < tsize) atomicAdd(&row[d >> 1], 1u << ((d & 1u) << 4));
+  }
+  __syncthreads();
+  // digits [8 tid, 8 tid + 8): totals over the waves, tile-level exclusive
+  // scan, the table row, then each wave's base per digit (u16)
+  const uint32_t d0 = threadIdx.x * 8;
+  const bool mine = d0 < B;
+  uint32_t tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (mine) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint4 c = *(const uint4 *)&rows[q * (B / 2) + d0 / 2];
+      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        tot[2 * i] += cw[i] & 0xFFFFu;
+        tot[2 * i + 1] += cw[i] >> 16;
+      }
+    }
+  }
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sum += tot[i];
+  uint32_t all;
+  uint32_t run = block_excl_scan<8>(sum, s_wsum, &all);
+  if (mine) {
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      st[i] = run;
+      run += tot[i];
+    }
+    uint4 *trow = (uint4 *)&tab[(uint64_t)blockIdx.x * B + d0];
+    trow[0] = make_uint4(st[0] | (st[1] << 16), st[1] | (st[2] << 16), st[2] | (st[3] << 16), st[3] | (st[4] << 16));
+    trow[1] = make_uint4(st[4] | (st[5] << 16), st[5] | (st[6] << 16), st[6] | (st[7] << 16), st[7] | (run << 16));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint4 *cp = (uint4 *)&rows[q * (B / 2) + d0 / 2];
+      const uint4 c = *cp;
+      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+      uint32_t nw[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        nw[i] = st[2 * i] | (st[2 * i + 1] << 16);
+        st[2 * i] += cw[i] & 0xFFFFu;
+        st[2 * i + 1] += cw[i] >> 16;
+      }
+      *cp = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t j = w * (T / 8) + r * 64 + lane;
+    const bool ok = j < tsize;
+    const uint32_t d = key[r] >> s;
+    const uint64_t peers = ms_match(d, top, __ballot(ok));
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    const uint32_t p0 = row16[d];
+    if (ok && rank == 0) row16[d] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+    if (ok) {
+      if constexpr (MODE == 0)
+        stage[p0 + rank] = ((key[r] & L1) << 14) | j;
+      else
+        stage[p0 + rank] = make_uint2(val[r], key[r] & L1);
+    }
+  }
+  __syncthreads();
+  // the sorted tile leaves as 16-B stores
+  constexpr uint32_t per = 16 / sizeof(Rec);
+  for (uint32_t j = threadIdx.x * per; j < tsize; j += 512 * per) {
+    if (j + per <= tsize) {
+      *(uint4 *)&out1[t0 + j] = *(const uint4 *)&stage[j];
+    } else {
+      for (uint32_t i = j; i < tsize; ++i) out1[t0 + i] = stage[i];
+    }
+  }
+}
+
+// Per-key pass of level 2 over the 2^s local keys, KPT consecutive keys per
+// thread (conflict-free vector LDS reads): the per-wave u16 counts in rows
+// become per-wave bases. ABS: base = chunk start of the key + the counts of
+// the earlier waves (the chunk's stable order: staging positions); else only
+// the earlier waves' counts (ranks relative to the key's running position).
+// Returns the chunk totals of the thread's keys through tot[] and their
+// chunk starts through cst[].
+template <int KPT>
+__device__ __forceinline__ void bk_keys(uint16_t *rows16, uint32_t L, uint32_t Lr, bool abs, uint32_t *s_wsum,
+                                        uint32_t *tot, uint32_t *cst) {
+  const uint32_t k0 = threadIdx.x * KPT;
+  const bool mine = k0 < L;
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) tot[i] = 0;
+  uint16_t c[kBkWaves][KPT];
+#pragma unroll
+  for (int q = 0; q < kBkWaves; ++q)
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      c[q][i] = mine ? rows16[q * Lr + k0 + i] : (uint16_t)0;
+      tot[i] += c[q][i];
+    }
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) sum += tot[i];
+  uint32_t all;
+  uint32_t run = block_excl_scan<kBkWaves>(sum, s_wsum, &all);
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    cst[i] = run;
+    run += tot[i];
+  }
+  if (mine) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      uint32_t b = abs ? cst[i] : 0u;
+#pragma unroll
+      for (int q = 0; q < kBkWaves; ++q) {
+        rows16[q * Lr + k0 + i] = (uint16_t)b;
+        b += c[q][i];
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBkThreads) void k_bucket_sort(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+                                                            const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
+                                                            int top, uint32_t n_keys, uint32_t nb,
+                                                            uint32_t *__restrict__ cell_size,
+                                                            uint32_t *__restrict__ cell_offset,
+                                                            uint32_t *__restrict__ sample_idx,
+                                                            float *__restrict__ target, int op) {
+  using Rec = typename SplitCfg<MODE>::Rec;
+  constexpr uint32_t T = SplitCfg<MODE>::T, kTiles = SplitCfg<MODE>::Tiles, TPT = kTiles / kBkThreads;
+  extern __shared__ uint32_t lds[];
+  __shared__ uint32_t s_wsum[kBkWaves];
+  __shared__ uint32_t s_pre[kTiles + 1], s_src[kTiles];
+  __shared__ uint32_t s_info[4];  // bucket start, bucket length
+  const uint32_t L = 1u << s, B = 1u << top, Lr = L < 2u ? 2u : L;  // row stride: u16 pairs share a word
+  const uint32_t b = ms_tile(blockIdx.x, nb);
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint16_t *rows16 = (uint16_t *)lds;         // [kBkWaves][Lr]
+  uint32_t *cnt = lds + (kBkWaves / 2) * Lr;  // [L]: running positions (MODE 0) / accumulators (MODE 1)
+  uint32_t *stage = cnt + L;                  // [kBkCap]
+  const uint32_t ngroups = (n_tiles + kTiles - 1) / kTiles;
+  const uint64_t lt = (1ull << lane) - 1ull;
+
+  // the runs of tile group g: s_pre (bucket-sequence prefix), s_src (record
+  // address of the run); returns the group's element count
+  auto load_runs = [&](uint32_t g, uint32_t base) -> uint32_t {
+    uint32_t rs[TPT], rl[TPT], sum = 0, ssum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < TPT; ++i) {
+      const uint32_t t = g * kTiles + threadIdx.x * TPT + i;
+      const uint32_t e = t < n_tiles ? tab[(uint64_t)t * B + b] : 0u;
+      rs[i] = e & 0xFFFFu;
+      rl[i] = (e >> 16) - rs[i];
+      sum += rl[i];
+      ssum += rs[i];
+    }
+    uint32_t tot, stot;
+    uint32_t ex = base + block_excl_scan<kBkWaves>(sum, s_wsum, &tot);
+#pragma unroll
+    for (uint32_t i = 0; i < TPT; ++i) {
+      const uint32_t t = g * kTiles + threadIdx.x * TPT + i;
+      s_pre[threadIdx.x * TPT + i] = ex;
+      s_src[threadIdx.x * TPT + i] = t * T + rs[i];
+      ex += rl[i];
+    }
+    block_excl_scan<kBkWaves>(ssum, s_wsum, &stot);
+    if (threadIdx.x == 0) {
+      s_pre[kTiles] = base + tot;
+      s_info[2] = stot;  // sum of the run starts: elements of smaller digits
+    }
+    __syncthreads();
+    return tot;
+  };
+  // records [c0, c0 + cl) of the sequence (inside the loaded group) into
+  // registers: wave w holds [w*Q, (w+1)*Q), round r lane l = w*Q + 64r + l.
+  // All rounds search (branch-free, fixed steps) and load together: one
+  // latency for the chunk.
+  auto gather = [&](uint32_t c0, uint32_t cl, uint32_t Q, uint32_t *key, uint32_t *pay) {
+    uint32_t j[kBkRounds], lo[kBkRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) {
+      j[r] = c0 + min(w * Q + r * 64 + lane, cl - 1u);
+      lo[r] = 0;
+    }
+#pragma unroll
+    for (uint32_t step = kTiles / 2; step > 0; step >>= 1)
+#pragma unroll
+      for (uint32_t r = 0; r < kBkRounds; ++r) lo[r] += s_pre[lo[r] + step] <= j[r] ? step : 0u;
+    Rec rc[kBkRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) {
+      const bool ok = r * 64 < Q && w * Q + r * 64 + lane < cl;
+      const uint32_t src = s_src[lo[r]] + (j[r] - s_pre[lo[r]]);
+      if (ok) rc[r] = out1[src];
+      if constexpr (MODE == 0) {
+        key[r] = ok ? rc[r] >> 14 : 0u;
+        pay[r] = ok ? (src / T) * T + (rc[r] & 0x3FFFu) : 0u;
+      } else {
+        key[r] = ok ? rc[r].y : 0u;
+        pay[r] = ok ? rc[r].x : 0u;
+      }
+    }
+  };
+  auto zero_rows = [&]() {
+    for (uint32_t i = threadIdx.x; i < (kBkWaves / 2) * Lr; i += kBkThreads) lds[i] = 0;
+  };
+  auto count_rows = [&](uint32_t cl, uint32_t Q, const uint32_t *key) {
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) {
+      const uint32_t jj = w * Q + r * 64 + lane;
+      if (r * 64 < Q && jj < cl) {
+        const uint32_t k = key[r];
+        atomicAdd((uint32_t *)&rows16[w * Lr + (k & ~1u)], 1u << ((k & 1u) << 4));
+      }
+    }
+  };
+  auto keys_pass = [&](bool abs, uint32_t *tot, uint32_t *cst) {
+    const uint32_t kpt = L > kBkThreads ? L / kBkThreads : 1u;
+    switch (kpt) {
+      case 1: bk_keys<1>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
+      case 2: bk_keys<2>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
+      case 4: bk_keys<4>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
+      case 8: bk_keys<8>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
+      default: bk_keys<16>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
+    }
+  };
+  // stable placement of the gathered records: dst(position, payload)
+  auto place = [&](uint32_t cl, uint32_t Q, const uint32_t *key, const uint32_t *pay, auto &&dst) {
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) {
+      if (r * 64 < Q) {  // wave-uniform
+        const uint32_t jj = w * Q + r * 64 + lane;
+        const bool ok = jj < cl;
+        const uint32_t k = key[r];
+        const uint64_t peers = ms_match(k, s, __ballot(ok));
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        const uint32_t p0 = rows16[w * Lr + k];
+        if (ok && rank == 0) rows16[w * Lr + k] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+        if (ok) dst(k, p0 + rank, pay[r]);
+      }
+    }
+  };
+  constexpr int KMAX = 16;  // keys per thread at L = 4096
+  uint32_t tot[KMAX], cst[KMAX];
+  const uint32_t kpt = L > kBkThreads ? L / kBkThreads : 1u, k0 = threadIdx.x * kpt;
+  uint32_t key[kBkRounds], pay[kBkRounds];
+
+  const uint32_t len0 = load_runs(0, 0);
+  const uint32_t start = s_info[2];  // (group 0 alone when ngroups == 1)
+  if (ngroups == 1 && len0 <= kBkCap) {
+    // common case: the whole bucket in one chunk
+    const uint32_t Q = ((len0 + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
+    gather(0, len0, Q, key, pay);
+    zero_rows();
+    __syncthreads();
+    count_rows(len0, Q, key);
+    __syncthreads();
+    keys_pass(true, tot, cst);
+    if (MODE == 0 && k0 < L)
+      for (uint32_t i = 0; i < kpt; ++i) {
+        const uint32_t kk = b * L + k0 + i;
+        if (kk < n_keys) {
+          cell_size[kk] = tot[i];
+          cell_offset[kk] = start + cst[i];
+        }
+      }
+    __syncthreads();
+    place(len0, Q, key, pay, [&](uint32_t, uint32_t pos, uint32_t v) { stage[pos] = v; });
+    __syncthreads();
+    if (MODE == 0) {
+      for (uint32_t i = threadIdx.x; i < len0; i += kBkThreads) sample_idx[start + i] = stage[i];
+    } else if (k0 < L) {
+      for (uint32_t i = 0; i < kpt; ++i) {
+        const uint32_t kk = b * L + k0 + i;
+        if (kk >= n_keys || tot[i] == 0) continue;
+        float acc = target[kk];
+        for (uint32_t m = cst[i]; m < cst[i] + tot[i]; ++m) acc = sr_apply(op, acc, __uint_as_float(stage[m]));
+        target[kk] = acc;
+      }
+    }
+    return;
+  }
+  // general case (long buckets / many tiles): chunks of kBkCap records in
+  // sequence order, group by group
+  if (MODE == 0) {
+    // pass A: per-key counts of the whole bucket
+    for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) cnt[i] = 0;
+    uint32_t base = 0, startsum = 0;
+    for (uint32_t g = 0; g < ngroups; ++g) {
+      const uint32_t gl = g ? load_runs(g, base) : len0;
+      startsum += s_info[2];
+      for (uint32_t c0 = base; c0 < base + gl; c0 += kBkCap) {
+        const uint32_t cl = min(kBkCap, base + gl - c0);
+        const uint32_t Q = ((cl + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
+        gather(c0, cl, Q, key, pay);
+#pragma unroll
+        for (uint32_t r = 0; r < kBkRounds; ++r)
+          if (r * 64 < Q && w * Q + r * 64 + lane < cl) atomicAdd(&cnt[key[r]], 1u);
+      }
+      base += gl;
+      __syncthreads();
+    }
+    // bucket offsets and the per-key outputs
+    {
+      uint32_t sum = 0;
+      if (k0 < L)
+        for (uint32_t i = 0; i < kpt; ++i) sum += cnt[k0 + i];
+      uint32_t all;
+      uint32_t run = startsum + block_excl_scan<kBkWaves>(sum, s_wsum, &all);
+      if (k0 < L)
+        for (uint32_t i = 0; i < kpt; ++i) {
+          const uint32_t kk = b * L + k0 + i, c = cnt[k0 + i];
+          if (kk < n_keys) {
+            cell_size[kk] = c;
+            cell_offset[kk] = run;
+          }
+          cnt[k0 + i] = run;
+          run += c;
+        }
+      __syncthreads();
+    }
+    // pass B: stable placement straight to the output
+    base = 0;
+    for (uint32_t g = 0; g < ngroups; ++g) {
+      const uint32_t gl = load_runs(g, base);
+      for (uint32_t c0 = base; c0 < base + gl; c0 += kBkCap) {
+        const uint32_t cl = min(kBkCap, base + gl - c0);
+        const uint32_t Q = ((cl + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
+        gather(c0, cl, Q, key, pay);
+        zero_rows();
+        __syncthreads();
+        count_rows(cl, Q, key);
+        __syncthreads();
+        keys_pass(false, tot, cst);
+        __syncthreads();
+        place(cl, Q, key, pay, [&](uint32_t k, uint32_t pos, uint32_t v) { sample_idx[cnt[k] + pos] = v; });
+        __syncthreads();
+        if (k0 < L)
+          for (uint32_t i = 0; i < kpt; ++i) cnt[k0 + i] += tot[i];
+        __syncthreads();
+      }
+      base += gl;
+    }
+    return;
+  }
+  // MODE 1: fold chunk by chunk into per-key accumulators (in order)
+  for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) {
+    const uint32_t kk = b * L + i;
+    cnt[i] = kk < n_keys ? __float_as_uint(target[kk]) : 0u;
+  }
+  uint32_t base = 0;
+  for (uint32_t g = 0; g < ngroups; ++g) {
+    const uint32_t gl = g ? load_runs(g, base) : len0;
+    for (uint32_t c0 = base; c0 < base + gl; c0 += kBkCap) {
+      const uint32_t cl = min(kBkCap, base + gl - c0);
+      const uint32_t Q = ((cl + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
+      gather(c0, cl, Q, key, pay);
+      zero_rows();
+      __syncthreads();
+      count_rows(cl, Q, key);
+      __syncthreads();
+      keys_pass(true, tot, cst);
+      __syncthreads();
+      place(cl, Q, key, pay, [&](uint32_t, uint32_t pos, uint32_t v) { stage[pos] = v; });
+      __syncthreads();
+      if (k0 < L)
+        for (uint32_t i = 0; i < kpt; ++i) {
+          float acc = __uint_as_float(cnt[k0 + i]);
+          for (uint32_t m = cst[i]; m < cst[i] + tot[i]; ++m) acc = sr_apply(op, acc, __uint_as_float(stage[m]));
+          cnt[k0 + i] = __float_as_uint(acc);
+        }
+      __syncthreads();
+    }
+    base += gl;
+  }
+  for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) {
+    const uint32_t kk = b * L + i;
+    if (kk < n_keys) target[kk] = __uint_as_float(cnt[i]);
+  }
+}
+
+// Keys >= 2^24 after the LSD passes (keys sorted): fold every run into its
+// target (reductions.py:53 in ascending element order).
+__global__ void k_sorted_fold(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ sorted, uint64_t n,
+                              float *__restrict__ target, int op) {
   const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
-  const uint32_t key = keys[k];
-  if (k == 0 || keys[k - 1] != key) seg_start[key] = (uint32_t)k;
-  if (k == n - 1 || keys[k + 1] != key) seg_end[key] = (uint32_t)(k + 1);
-}
-
-__global__ void k_sr_fold(int op, float *target, uint64_t nt, const float *vals, const uint32_t *seg_start,
-                          const uint32_t *seg_end) {
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
-  const uint32_t b = seg_start[t], e = seg_end[t];
-  if (b >= e) return;
+  const uint32_t t = keys[k];
+  if (k > 0 && keys[k - 1] == t) return;  // not a run start
   float acc = target[t];
-  for (uint32_t k = b; k < e; ++k) {
-    const float v = vals[k];
-    acc = op == 0 ? acc + v : (op == 1 ? fminf(acc, v) : fmaxf(acc, v));
-  }
+  for (uint64_t m = k; m < n && keys[m] == t; ++m) acc = sr_apply(op, acc, __uint_as_float(sorted[m]));
   target[t] = acc;
 }
-
-
 
 inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
@@ -421,78 +1039,217 @@ int scan_f32_hs(float *a, float *b, uint64_t n, float **result, hipStream_t st) 
   return MTX_OK;
 }
 
-static unsigned key_bits(uint64_t n_target);
+static int bits_for(uint64_t k) {
+  int b = 0;
+  while (b < 32 && (1ull << b) < k) ++b;
+  return b;
+}
 
-static size_t hash_sort_temp_bytes(uint64_t n, uint32_t n_cells) {
-  size_t bytes = 0;
-  rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                            rocprim::counting_iterator<uint32_t>(0u), (uint32_t *)nullptr, (size_t)n, 0u,
-                            key_bits(n_cells));
+// Workspace carving (256-B aligned pieces).
+namespace {
+struct Carve {
+  char *base;
+  size_t off = 0;
+  template <class T>
+  T *take(uint64_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T *r = (T *)(base + off);
+    off += count * sizeof(T);
+    return r;
+  }
+};
+
+struct GbPlan {
+  int bits;      // key bits
+  bool msd;      // two-level path (bits <= 24)
+  int top, s;    // two-level: tile-table digit bits (3..12), bucket-local key bits
+  uint32_t tiles;  // LSD tiles
+};
+
+GbPlan gb_plan(uint64_t n, uint64_t n_keys) {
+  GbPlan g;
+  g.bits = bits_for(n_keys);
+  g.msd = g.bits <= 2 * kSplitMaxTop;
+  g.top = g.bits < 3 ? 3 : (g.bits > kSplitMaxTop ? kSplitMaxTop : g.bits);
+  g.s = g.bits > g.top ? g.bits - g.top : 0;
+  g.tiles = (uint32_t)((n + kMsTile - 1) / kMsTile);
+  return g;
+}
+
+template <int MODE>
+uint32_t split_tiles(uint64_t n) {
+  return (uint32_t)((n + SplitCfg<MODE>::T - 1) / SplitCfg<MODE>::T);
+}
+
+// two-level: digit table, level-1 records, (MODE 1) the placed values;
+// LSD: digit histogram + scan + two key/payload buffer pairs.
+template <int MODE>
+size_t gb_bytes(uint64_t n, const GbPlan &g) {
+  size_t bytes = 8 * 1025 + 256;
+  if (g.msd) {
+    bytes += 4 * ((uint64_t)split_tiles<MODE>(n) << g.top) + 256;
+    bytes += sizeof(typename SplitCfg<MODE>::Rec) * n + 256;
+  } else {
+    const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
+    bytes += 2 * (4 * hn + 256) + scan_workspace_bytes(hn) + 256 + 4 * (4 * n + 256);
+  }
   return bytes;
 }
 
-size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells) {
-  return 8ull * 1025 + 4ull * n + hash_sort_temp_bytes(n, n_cells) + 512;
+template <int MODE>
+uint32_t split_lds(int top) {
+  return (16u << top) + (uint32_t)(SplitCfg<MODE>::T * sizeof(typename SplitCfg<MODE>::Rec));
 }
+uint32_t bucket_lds(int s) {
+  const uint32_t Lr = s ? 1u << s : 2u;
+  return 2u * kBkWaves * Lr + 4u * Lr + 4u * kBkCap;
+}
+
+int gb_attrs() {  // per call: the attribute belongs to the current device
+  const int place = kMsWaves * (4 << kMsMaxBits);
+  if (hipFuncSetAttribute((const void *)k_ms_place<true>, hipFuncAttributeMaxDynamicSharedMemorySize, place) ||
+      hipFuncSetAttribute((const void *)k_ms_place<false>, hipFuncAttributeMaxDynamicSharedMemorySize, place) ||
+      hipFuncSetAttribute((const void *)k_tile_split<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)split_lds<0>(kSplitMaxTop)) ||
+      hipFuncSetAttribute((const void *)k_tile_split<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)split_lds<1>(kSplitMaxTop)) ||
+      hipFuncSetAttribute((const void *)k_bucket_sort<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)bucket_lds(kSplitMaxTop)) ||
+      hipFuncSetAttribute((const void *)k_bucket_sort<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)bucket_lds(kSplitMaxTop))) {
+    mtx_set_error("group-by: LDS attribute rejected");
+    return MTX_E_HIP;
+  }
+  return MTX_OK;
+}
+
+// One stable multisplit pass (LSD path): histogram (of keys, or of the
+// hash-grid cells computed from the points when hp != nullptr), scan, place.
+struct HashIn {
+  const float *p;
+  uint32_t res, n_cells;
+  const float2 *bbox;
+};
+int ms_pass(const uint32_t *keys, const uint32_t *pay, uint64_t n, int shift, int bits, uint32_t tiles,
+            uint32_t *hist, uint32_t *hscan, void *scan_ws, uint32_t *keys_out, uint32_t *pay_out,
+            const HashIn *hp, uint32_t *cell, hipStream_t st) {
+  const uint64_t hn = ((uint64_t)1 << bits) * tiles;
+  if (hp)
+    hipLaunchKernelGGL(k_ms_hist<true>, dim3(tiles), dim3(kMsThreads), 4u << bits, st, nullptr, hp->p, n, hp->res,
+                       hp->n_cells, hp->bbox, cell, shift, bits, hist, tiles);
+  else
+    hipLaunchKernelGGL(k_ms_hist<false>, dim3(tiles), dim3(kMsThreads), 4u << bits, st, keys, nullptr, n, 0u, 1u,
+                       nullptr, nullptr, shift, bits, hist, tiles);
+  int rc = scan_u32(hist, hscan, hn, 0, scan_ws, st);
+  if (rc) return rc;
+  const uint32_t lds = (uint32_t)kMsWaves * (4u << bits);
+  if (hp)
+    hipLaunchKernelGGL(k_ms_place<true>, dim3(tiles), dim3(kMsThreads), lds, st, cell, nullptr, n, shift, bits, hscan,
+                       tiles, keys_out, pay_out);
+  else if (!pay)
+    hipLaunchKernelGGL(k_ms_place<true>, dim3(tiles), dim3(kMsThreads), lds, st, keys, nullptr, n, shift, bits, hscan,
+                       tiles, keys_out, pay_out);
+  else
+    hipLaunchKernelGGL(k_ms_place<false>, dim3(tiles), dim3(kMsThreads), lds, st, keys, pay, n, shift, bits, hscan,
+                       tiles, keys_out, pay_out);
+  return MTX_OK;
+}
+}  // namespace
+
+size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells) { return gb_bytes<0>(n, gb_plan(n, n_cells)); }
 
 int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
                    uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st) {
-  char *w = (char *)ws;
-  float2 *partial = (float2 *)w;
-  uint32_t *keys = (uint32_t *)(w + 8 * 1025);
-  void *temp = (void *)(((uintptr_t)(keys + n) + 255) & ~(uintptr_t)255);
-  size_t temp_bytes = hash_sort_temp_bytes(n, n_cells);
+  if (int e = gb_attrs()) return e;
+  const GbPlan g = gb_plan(n, n_cells);
+  Carve cv{(char *)ws};
+  float2 *partial = cv.take<float2>(1025);
   const int m = 1024;
   hipLaunchKernelGGL(k_minmax, dim3(m), dim3(256), 0, st, p, 3 * n, partial);
   hipLaunchKernelGGL(k_minmax_final, dim3(1), dim3(256), 0, st, partial, m);
-  hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell);
-  if (rocprim::radix_sort_pairs(temp, temp_bytes, cell, keys, rocprim::counting_iterator<uint32_t>(0u), sample_idx,
-                                (size_t)n, 0u, key_bits(n_cells), st) != hipSuccess) {
-    mtx_set_error("hashgrid: radix sort failed");
-    return MTX_E_HIP;
+  if (g.msd) {
+    // cells; level 1: per-tile stable split by the top digit; level 2: buckets
+    const uint32_t tiles = split_tiles<0>(n);
+    uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
+    uint32_t *out1 = cv.take<uint32_t>(n);
+    hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell);
+    hipLaunchKernelGGL(k_tile_split<0>, dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n, g.s, g.top,
+                       tab, out1);
+    const uint32_t nb = (uint32_t)(((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s);
+    hipLaunchKernelGGL(k_bucket_sort<0>, dim3(nb), dim3(kBkThreads), bucket_lds(g.s), st, out1, tab, tiles, g.s, g.top,
+                       n_cells, nb, cell_size, cell_offset, sample_idx, nullptr, 0);
+    return MTX_OK;
+  }
+  // LSD: 12-bit digit passes (the first one hashes), then the run bounds
+  const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
+  uint32_t *hist = cv.take<uint32_t>(hn), *hscan = cv.take<uint32_t>(hn);
+  void *scan_ws = cv.take<char>(scan_workspace_bytes(hn));
+  uint32_t *ka = cv.take<uint32_t>(n), *pa = cv.take<uint32_t>(n), *kb = cv.take<uint32_t>(n),
+           *pb = cv.take<uint32_t>(n);
+  const HashIn hin{p, res, n_cells, partial + m};
+  const uint32_t *kin = nullptr, *pin = nullptr;
+  uint32_t *kbuf[2] = {ka, kb}, *pbuf[2] = {pa, pb};
+  int cur = 0, rc;
+  for (int shift = 0; shift < g.bits; shift += kMsMaxBits) {
+    const int bits = g.bits - shift < kMsMaxBits ? g.bits - shift : kMsMaxBits;
+    const bool last = shift + kMsMaxBits >= g.bits;
+    uint32_t *pout = last ? sample_idx : pbuf[cur];
+    if ((rc = ms_pass(kin, pin, n, shift, bits, g.tiles, hist, hscan, scan_ws, kbuf[cur], pout,
+                      shift == 0 ? &hin : nullptr, cell, st)))
+      return rc;
+    kin = kbuf[cur];
+    pin = pout;
+    cur ^= 1;
   }
   if ((uint64_t)n_cells > 4 * n)
-    hipLaunchKernelGGL(k_hash_offsets_search, dim3(nblk(n_cells, 256)), dim3(256), 0, st, keys, n, n_cells,
+    hipLaunchKernelGGL(k_hash_offsets_search, dim3(nblk(n_cells, 256)), dim3(256), 0, st, kin, n, n_cells,
                        cell_offset, cell_size);
   else
-    hipLaunchKernelGGL(k_hash_ranges, dim3(nblk(n, kHashTile)), dim3(256), 0, st, keys, n, n_cells, cell_offset,
+    hipLaunchKernelGGL(k_hash_ranges, dim3(nblk(n, kHashTile)), dim3(256), 0, st, kin, n, n_cells, cell_offset,
                        cell_size);
   return MTX_OK;
 }
 
-static unsigned key_bits(uint64_t n_target) {
-  unsigned b = 1;
-  while (b < 32 && (1ull << b) < n_target) ++b;
-  return b;
-}
-
-static size_t sort_temp_bytes(uint64_t n_value, uint64_t n_target) {
-  size_t bytes = 0;
-  rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr, (const float *)nullptr,
-                            (float *)nullptr, (size_t)n_value, 0u, key_bits(n_target));
-  return bytes;
-}
-
 size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value) {
-  return 8ull * n_value + 8ull * n_target + sort_temp_bytes(n_value, n_target) + 256;
+  return gb_bytes<1>(n_value, gb_plan(n_value, n_target));
 }
 
 int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
                        uint64_t n_value, void *ws, hipStream_t st) {
-  uint32_t *keys = (uint32_t *)ws;
-  float *vals = (float *)(keys + n_value);
-  uint32_t *seg_start = (uint32_t *)(vals + n_value), *seg_end = seg_start + n_target;
-  void *temp = (void *)(((uintptr_t)(seg_end + n_target) + 255) & ~(uintptr_t)255);
-  size_t temp_bytes = sort_temp_bytes(n_value, n_target);
-  if (rocprim::radix_sort_pairs(temp, temp_bytes, index, keys, value, vals, (size_t)n_value, 0u,
-                                key_bits(n_target), st) != hipSuccess) {
-    mtx_set_error("scatter_reduce: radix sort failed");
-    return MTX_E_HIP;
+  if (int e = gb_attrs()) return e;
+  const uint64_t n = n_value;
+  const GbPlan g = gb_plan(n, n_target);
+  Carve cv{(char *)ws};
+  cv.take<float2>(1025);
+  if (g.msd) {
+    const uint32_t tiles = split_tiles<1>(n);
+    uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
+    uint2 *out1 = cv.take<uint2>(n);
+    hipLaunchKernelGGL(k_tile_split<1>, dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n, g.s, g.top,
+                       tab, out1);
+    const uint32_t nb = (uint32_t)((n_target + (1ull << g.s) - 1) >> g.s);
+    hipLaunchKernelGGL(k_bucket_sort<1>, dim3(nb), dim3(kBkThreads), bucket_lds(g.s), st, out1, tab, tiles, g.s, g.top,
+                       (uint32_t)n_target, nb, nullptr, nullptr, nullptr, target, op);
+    return MTX_OK;
   }
-  if (hipMemsetAsync(seg_start, 0, 8ull * n_target, st) != hipSuccess) return MTX_E_HIP;
-  hipLaunchKernelGGL(k_sr_bounds, dim3(nblk(n_value, 256)), dim3(256), 0, st, keys, n_value, seg_start, seg_end);
-  hipLaunchKernelGGL(k_sr_fold, dim3(nblk(n_target, 256)), dim3(256), 0, st, op, target, n_target, vals, seg_start,
-                     seg_end);
+  const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
+  uint32_t *hist = cv.take<uint32_t>(hn), *hscan = cv.take<uint32_t>(hn);
+  void *scan_ws = cv.take<char>(scan_workspace_bytes(hn));
+  uint32_t *ka = cv.take<uint32_t>(n), *pa = cv.take<uint32_t>(n), *kb = cv.take<uint32_t>(n),
+           *pb = cv.take<uint32_t>(n);
+  const uint32_t *kin = index, *pin = (const uint32_t *)value;
+  uint32_t *kbuf[2] = {ka, kb}, *pbuf[2] = {pa, pb};
+  int cur = 0, rc;
+  for (int shift = 0; shift < g.bits; shift += kMsMaxBits) {
+    const int bits = g.bits - shift < kMsMaxBits ? g.bits - shift : kMsMaxBits;
+    if ((rc = ms_pass(kin, pin, n, shift, bits, g.tiles, hist, hscan, scan_ws, kbuf[cur], pbuf[cur], nullptr, nullptr,
+                      st)))
+      return rc;
+    kin = kbuf[cur];
+    pin = pbuf[cur];
+    cur ^= 1;
+  }
+  hipLaunchKernelGGL(k_sorted_fold, dim3(nblk(n, 256)), dim3(256), 0, st, kin, pin, n, target, op);
   return MTX_OK;
 }
 

@@ -6,7 +6,8 @@ import numpy as np
 
 from ._lib import check, context, lib
 
-ADD, MIN, MAX = 0, 1, 2
+ADD, MIN, MAX, MUL = 0, 1, 2, 3
+_OPS = {"add": ADD, "min": MIN, "max": MAX, "mul": MUL}
 
 
 def prefix_sum(x, inclusive: bool = True, device: int | None = None):
@@ -63,11 +64,18 @@ class HashGrid:
 
 
 def scatter_reduce_with(op, target, value, index, device: int | None = None):
-    """reductions.py:12-54 for op in {ADD, MIN, MAX} (or 'add'/'min'/'max').
-    Returns the updated target; each target receives its values in ascending
-    index order."""
+    """reductions.py:12-54 for func in {ADD, MIN, MAX, MUL} (or 'add' / 'min' /
+    'max' / 'mul'). Returns the updated target; each target receives its
+    values in ascending index order. The reference accepts any callable
+    (`func(a, b)`, reductions.py:53); a device kernel cannot call Python, so
+    other callables raise TypeError (decided limitation)."""
     if isinstance(op, str):
-        op = {"add": ADD, "min": MIN, "max": MAX}[op]
+        if op not in _OPS:
+            raise TypeError(f"scatter_reduce_with: unsupported func {op!r} (device ops: add, min, max, mul)")
+        op = _OPS[op]
+    elif callable(op):
+        raise TypeError("scatter_reduce_with: arbitrary Python callables cannot run on the device; "
+                        "use one of 'add', 'min', 'max', 'mul'")
     t = np.array(target, np.float32)
     v = np.ascontiguousarray(value, np.float32)
     i = np.ascontiguousarray(index, np.uint32)

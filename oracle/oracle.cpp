@@ -1256,7 +1256,7 @@ int orc_scatter_reduce_f32_mt(int op, float *target, uint64_t n_target, const fl
     float a = target[t];
     for (int64_t j = k; j < (int64_t)n_value && (uint32_t)(key[j] >> 32) == t; ++j) {
       const float b = value[(uint32_t)key[j]];
-      a = op == 0 ? a + b : (op == 1 ? fminf(a, b) : fmaxf(a, b));
+      a = op == 0 ? a + b : (op == 1 ? fminf(a, b) : (op == 2 ? fmaxf(a, b) : a * b));
     }
     target[t] = a;
   }
@@ -1265,14 +1265,14 @@ int orc_scatter_reduce_f32_mt(int op, float *target, uint64_t n_target, const fl
 
 // ----------------------------- reductions.py -------------------------------
 // Every target index receives func(target, value) for each of its values,
-// applied in ascending value-index order.
+// applied in ascending value-index order. func: 0 add, 1 min, 2 max, 3 mul.
 int orc_scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
                            uint64_t n_value) {
   for (uint64_t i = 0; i < n_value; ++i) {
     uint32_t t = index[i];
     if (t >= n_target) return -1;
     float a = target[t], b = value[i];
-    target[t] = op == 0 ? a + b : (op == 1 ? fminf(a, b) : fmaxf(a, b));
+    target[t] = op == 0 ? a + b : (op == 1 ? fminf(a, b) : (op == 2 ? fmaxf(a, b) : a * b));
   }
   return 0;
 }

@@ -136,3 +136,23 @@ def test_multicore_primitive_baselines_equal_sequential(oracle):
     for op in (0, 1, 2):
         tgt = rng.random(1000, dtype=np.float32)
         assert np.array_equal(oracle.scatter_reduce_mt(op, tgt, val, idx), oracle.scatter_reduce(op, tgt, val, idx))
+
+
+def test_scatter_reduce_mul_and_callable_rejected(oracle):
+    """reductions.py:12 takes any func; the device op table adds mul
+    (sequential product per target) and rejects Python callables."""
+    from mtx import primitives
+
+    rng = np.random.default_rng(3)
+    idx = rng.integers(0, 7, 200).astype(np.uint32)
+    val = (0.9 + 0.2 * rng.random(200)).astype(np.float32)
+    tgt = np.ones(7, np.float32)
+    ref = tgt.copy()
+    for i, v in zip(idx, val):
+        ref[i] = np.float32(ref[i] * v)
+    assert np.array_equal(oracle.scatter_reduce(3, tgt, val, idx), ref)
+    assert np.array_equal(oracle.scatter_reduce_mt(3, tgt, val, idx), ref)
+    with pytest.raises(TypeError):
+        primitives.scatter_reduce_with(lambda a, b: a + b, tgt, val, idx)
+    with pytest.raises(TypeError):
+        primitives.scatter_reduce_with("xor", tgt, val, idx)

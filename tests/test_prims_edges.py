@@ -101,3 +101,44 @@ def test_scatter_reduce_empty_and_invalid():
                                                          np.zeros(0, np.uint32)), t)
     with pytest.raises(MtxError):
         primitives.scatter_reduce_with("add", t, np.ones(3, np.float32), np.array([0, 5, 1], np.uint32))
+
+
+def test_hashgrid_wide_keys_lsd_path(oracle):
+    """n_cells >= 2^25: the LSD passes of the multisplit (12-bit digits) and
+    the run-bounds kernels (dense: k_hash_ranges; sparse: lower bounds)."""
+    rng = np.random.default_rng(13)
+    p = rng.random((3, 1 << 23), dtype=np.float32)
+    _grid_vs_oracle(oracle, p, 400, (1 << 25) + 3)  # n_cells <= 4 n: run bounds
+    _grid_vs_oracle(oracle, np.ascontiguousarray(p[:, :1 << 16]), 100, (1 << 25) + 3)  # sparse
+
+
+@pytest.mark.parametrize("n_cells", [1 << 12, (1 << 12) + 1, 5000, 1 << 20])
+def test_hashgrid_digit_splits_clustered(oracle, n_cells):
+    """Every top/local digit split of the two-level path (local bits 0, 1, 1,
+    8) with clustered points: a few cells hold most samples, so single
+    buckets span many tiles and one workgroup's waves split a long run."""
+    rng = np.random.default_rng(14)
+    n = (1 << 20) + 77
+    q = (rng.integers(0, 6, (3, n)) / 6.0).astype(np.float32)
+    q[:, : n // 3] = rng.random((3, n // 3), dtype=np.float32)
+    _grid_vs_oracle(oracle, q, 64, n_cells)
+
+
+@pytest.mark.parametrize("nt", [1, 3000, 1 << 16, (1 << 25) + 1])
+def test_scatter_reduce_paths_and_mul(oracle, nt):
+    """Targets below 2^12 (one key per bucket), the two-level path and the
+    LSD path (2^25 + 1 targets); add / min / max / mul folded in ascending
+    index order, bit-exact vs the oracle."""
+    from mtx import primitives
+
+    rng = np.random.default_rng(15)
+    nv = (1 << 20) + 5
+    idx = (rng.integers(0, nt, nv) if nt > 1 else np.zeros(nv)).astype(np.uint32)
+    idx[: nv // 4] = idx[0]  # one hot target
+    for op in ("add", "min", "max", "mul"):
+        val = (rng.random(nv, dtype=np.float32) * (0.02 if op == "mul" else 1.0)
+               + (0.99 if op == "mul" else -0.5)).astype(np.float32)
+        tgt = rng.random(nt, dtype=np.float32)
+        o = {"add": 0, "min": 1, "max": 2, "mul": 3}[op]
+        assert np.array_equal(primitives.scatter_reduce_with(op, tgt, val, idx),
+                              oracle.scatter_reduce(o, tgt, val, idx)), op
