@@ -347,7 +347,7 @@ __global__ void k_hash_offsets_search(const uint32_t *__restrict__ key, uint64_t
 // oracle's order). Hand-written counting multisplits, no global atomics:
 // * keys < 2^24 (two levels): k_tile_split sorts every tile stably by the
 //   top digit (key >> s, at most 12 bits) in LDS and writes it back
-//   contiguously with a per-tile digit table; k_bucket_sort gives each
+//   contiguously with a per-tile digit table; k_bucket_fast gives each
 //   bucket one workgroup that gathers its runs from all tiles into LDS,
 //   counts its 2^s keys, writes their cell_size / cell_offset (or folds
 //   their values) and places every element at its final position. HBM
@@ -515,7 +515,7 @@ __device__ __forceinline__ float sr_apply(int op, float a, float b) {
 // contiguously (no scattered stores: a 4096-way global split of 4-byte
 // elements wrote 12x its bytes to the fabric as partial lines), with the
 // tile's digit table tab[tile][d] = start | end << 16. Level 2,
-// k_bucket_sort: one workgroup per bucket d gathers the bucket's runs from
+// k_bucket_fast: one workgroup per bucket d gathers the bucket's runs from
 // every tile (tile order = element order) into registers, sorts them stably
 // by the 2^s local keys with the same per-wave-row construction, and writes
 // the bucket's slice of the output contiguously (hashgrid: cell_size,
@@ -680,242 +680,379 @@ __global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__
   }
 }
 
-// Per-key pass of level 2 over the 2^s local keys, KPT consecutive keys per
-// thread (conflict-free vector LDS reads): the per-wave u16 counts in rows
-// become per-wave bases. ABS: base = chunk start of the key + the counts of
-// the earlier waves (the chunk's stable order: staging positions); else only
-// the earlier waves' counts (ranks relative to the key's running position).
-// Returns the chunk totals of the thread's keys through tot[] and their
-// chunk starts through cst[].
+// Exclusive scan of two values per thread at once (one barrier pair).
+template <int NW>
+__device__ __forceinline__ uint2 block_excl_scan2(uint2 v, uint32_t (*s_wsum)[NW], uint2 *total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint2 x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t ya = __shfl_up(x.x, off), yb = __shfl_up(x.y, off);
+    if (lane >= (uint32_t)off) {
+      x.x += ya;
+      x.y += yb;
+    }
+  }
+  __syncthreads();
+  if (lane == 63) {
+    s_wsum[0][w] = x.x;
+    s_wsum[1][w] = x.y;
+  }
+  __syncthreads();
+  uint2 pre = make_uint2(0, 0), tot = make_uint2(0, 0);
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const uint32_t a = s_wsum[0][q], c = s_wsum[1][q];
+    if ((uint32_t)q < w) {
+      pre.x += a;
+      pre.y += c;
+    }
+    tot.x += a;
+    tot.y += c;
+  }
+  *total = tot;
+  return make_uint2(pre.x + x.x - v.x, pre.y + x.y - v.y);
+}
+
+// KPT u16 counters of row q for keys [k0, k0 + KPT) (vector LDS access).
 template <int KPT>
-__device__ __forceinline__ void bk_keys(uint16_t *rows16, uint32_t L, uint32_t Lr, bool abs, uint32_t *s_wsum,
-                                        uint32_t *tot, uint32_t *cst) {
+__device__ __forceinline__ void rows_read(const uint16_t *p, uint32_t *c) {
+  if constexpr (KPT >= 8) {
+#pragma unroll
+    for (int v = 0; v < KPT / 8; ++v) {
+      const uint4 x = ((const uint4 *)p)[v];
+      const uint32_t wv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        c[8 * v + 2 * i] = wv[i] & 0xFFFFu;
+        c[8 * v + 2 * i + 1] = wv[i] >> 16;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) c[i] = p[i];
+  }
+}
+template <int KPT>
+__device__ __forceinline__ void rows_write(uint16_t *p, const uint32_t *c) {
+  if constexpr (KPT >= 8) {
+#pragma unroll
+    for (int v = 0; v < KPT / 8; ++v)
+      ((uint4 *)p)[v] = make_uint4(c[8 * v] | (c[8 * v + 1] << 16), c[8 * v + 2] | (c[8 * v + 3] << 16),
+                                   c[8 * v + 4] | (c[8 * v + 5] << 16), c[8 * v + 6] | (c[8 * v + 7] << 16));
+  } else {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) p[i] = (uint16_t)c[i];
+  }
+}
+
+// Per-key pass over the bucket's 2^s local keys, KPT consecutive keys per
+// thread: the per-wave u16 counts in rows become per-wave bases. ABS: base =
+// chunk start of the key + the earlier waves' counts (staging positions of
+// the chunk's stable order); else the earlier waves' counts only (ranks
+// relative to the key's running position). Returns the chunk totals of the
+// thread's keys (tot) and their chunk starts (cst).
+template <int KPT>
+__device__ __forceinline__ void bk_keys(uint16_t *rows16, uint32_t L, uint32_t Lr, bool abs,
+                                        uint32_t (*s_wsum)[kBkWaves], uint32_t *tot, uint32_t *cst) {
   const uint32_t k0 = threadIdx.x * KPT;
   const bool mine = k0 < L;
+  const uint32_t kr = mine ? k0 : 0u;
+  uint32_t c[kBkWaves][KPT];
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) tot[i] = 0;
-  uint16_t c[kBkWaves][KPT];
-#pragma unroll
-  for (int q = 0; q < kBkWaves; ++q)
-#pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-      c[q][i] = mine ? rows16[q * Lr + k0 + i] : (uint16_t)0;
-      tot[i] += c[q][i];
-    }
+  for (int q = 0; q < kBkWaves; ++q) rows_read<KPT>(rows16 + q * Lr + kr, c[q]);
   uint32_t sum = 0;
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) sum += tot[i];
-  uint32_t all;
-  uint32_t run = block_excl_scan<kBkWaves>(sum, s_wsum, &all);
+  for (int i = 0; i < KPT; ++i) {
+    tot[i] = 0;
+#pragma unroll
+    for (int q = 0; q < kBkWaves; ++q) tot[i] += mine ? c[q][i] : 0u;
+    sum += tot[i];
+  }
+  uint2 all;
+  uint32_t run = block_excl_scan2<kBkWaves>(make_uint2(sum, 0), s_wsum, &all).x;
 #pragma unroll
   for (int i = 0; i < KPT; ++i) {
     cst[i] = run;
     run += tot[i];
   }
   if (mine) {
+    uint32_t bse[KPT];
 #pragma unroll
-    for (int i = 0; i < KPT; ++i) {
-      uint32_t b = abs ? cst[i] : 0u;
+    for (int i = 0; i < KPT; ++i) bse[i] = abs ? cst[i] : 0u;
 #pragma unroll
-      for (int q = 0; q < kBkWaves; ++q) {
-        rows16[q * Lr + k0 + i] = (uint16_t)b;
-        b += c[q][i];
-      }
+    for (int q = 0; q < kBkWaves; ++q) {
+      rows_write<KPT>(rows16 + q * Lr + k0, bse);
+#pragma unroll
+      for (int i = 0; i < KPT; ++i) bse[i] += c[q][i];
     }
   }
 }
 
+// Lanes of `active` whose local key equals this lane's (s <= 12 bits).
+__device__ __forceinline__ uint64_t bk_match(uint32_t k, int s, uint64_t active) {
+  uint64_t m = active;
+#pragma unroll
+  for (int j = 0; j < kSplitMaxTop; ++j)
+    if (j < s) {  // uniform
+      const uint32_t bit = (k >> j) & 1u;
+      const uint64_t bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
+    }
+  return m;
+}
+
+// Level-2 runs of tile group g of bucket b into LDS: s_pre (prefix in the
+// bucket's element sequence, from `base`), s_src (record address of the
+// run). Returns {group element count, sum of the run starts}.
 template <int MODE>
-__global__ __launch_bounds__(kBkThreads) void k_bucket_sort(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+__device__ __forceinline__ uint2 bk_load_runs(const uint32_t *__restrict__ tab, uint32_t n_tiles, uint32_t B,
+                                              uint32_t b, uint32_t g, uint32_t base, uint32_t *s_pre,
+                                              uint32_t *s_src, uint32_t (*s_wsum)[kBkWaves]) {
+  constexpr uint32_t T = SplitCfg<MODE>::T, kTiles = SplitCfg<MODE>::Tiles, TPT = kTiles / kBkThreads;
+  uint32_t rs[TPT], rl[TPT], sum = 0, ssum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < TPT; ++i) {
+    const uint32_t t = g * kTiles + threadIdx.x * TPT + i;
+    const uint32_t e = t < n_tiles ? tab[(uint64_t)t * B + b] : 0u;
+    rs[i] = e & 0xFFFFu;
+    rl[i] = (e >> 16) - rs[i];
+    sum += rl[i];
+    ssum += rs[i];
+  }
+  uint2 tot;
+  const uint2 ex = block_excl_scan2<kBkWaves>(make_uint2(sum, ssum), s_wsum, &tot);
+  uint32_t run = base + ex.x;
+#pragma unroll
+  for (uint32_t i = 0; i < TPT; ++i) {
+    const uint32_t t = g * kTiles + threadIdx.x * TPT + i;
+    s_pre[threadIdx.x * TPT + i] = run;
+    s_src[threadIdx.x * TPT + i] = t * T + rs[i];
+    run += rl[i];
+  }
+  if (threadIdx.x == 0) s_pre[kTiles] = base + tot.x;
+  return tot;
+}
+
+// Records [c0, c0 + cl) of the bucket sequence (inside the loaded group) into
+// registers: wave w holds [w*Q, (w+1)*Q), round r lane l = w*Q + 64r + l.
+// All rounds search (branch-free, fixed steps) and load together.
+template <int MODE>
+__device__ __forceinline__ void bk_gather(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+                                          const uint32_t *s_pre, const uint32_t *s_src, uint32_t c0, uint32_t cl,
+                                          uint32_t Q, uint32_t *key, uint32_t *pay) {
+  using Rec = typename SplitCfg<MODE>::Rec;
+  constexpr uint32_t T = SplitCfg<MODE>::T, kTiles = SplitCfg<MODE>::Tiles;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint32_t j[kBkRounds], lo[kBkRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kBkRounds; ++r) {
+    j[r] = c0 + min(w * Q + r * 64 + lane, cl - 1u);
+    lo[r] = 0;
+  }
+#pragma unroll
+  for (uint32_t step = kTiles / 2; step > 0; step >>= 1)
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) lo[r] += s_pre[lo[r] + step] <= j[r] ? step : 0u;
+  Rec rc[kBkRounds];
+  uint32_t src[kBkRounds];
+#pragma unroll
+  for (uint32_t r = 0; r < kBkRounds; ++r) {
+    src[r] = s_src[lo[r]] + (j[r] - s_pre[lo[r]]);
+    rc[r] = out1[src[r]];  // clamped index: always a valid record of the chunk
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kBkRounds; ++r) {
+    if constexpr (MODE == 0) {
+      key[r] = rc[r] >> 14;
+      pay[r] = (src[r] / T) * T + (rc[r] & 0x3FFFu);
+    } else {
+      key[r] = rc[r].y;
+      pay[r] = rc[r].x;
+    }
+  }
+}
+
+// Level 2, common case: one workgroup per bucket whose elements fit one
+// chunk (kBkCap) and whose tiles fit one group; others are listed in
+// `slow` for k_bucket_slow. 2^s = KPT * 256 local keys (KPT = 1: up to 256).
+template <int MODE, int KPT>
+__global__ __launch_bounds__(kBkThreads) void k_bucket_fast(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
                                                             const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
                                                             int top, uint32_t n_keys, uint32_t nb,
                                                             uint32_t *__restrict__ cell_size,
                                                             uint32_t *__restrict__ cell_offset,
                                                             uint32_t *__restrict__ sample_idx,
-                                                            float *__restrict__ target, int op) {
-  using Rec = typename SplitCfg<MODE>::Rec;
-  constexpr uint32_t T = SplitCfg<MODE>::T, kTiles = SplitCfg<MODE>::Tiles, TPT = kTiles / kBkThreads;
+                                                            float *__restrict__ target, int op,
+                                                            uint32_t *__restrict__ slow) {
+  constexpr uint32_t kTiles = SplitCfg<MODE>::Tiles;
   extern __shared__ uint32_t lds[];
-  __shared__ uint32_t s_wsum[kBkWaves];
+  __shared__ uint32_t s_wsum[2][kBkWaves];
   __shared__ uint32_t s_pre[kTiles + 1], s_src[kTiles];
-  __shared__ uint32_t s_info[4];  // bucket start, bucket length
   const uint32_t L = 1u << s, B = 1u << top, Lr = L < 2u ? 2u : L;  // row stride: u16 pairs share a word
   const uint32_t b = ms_tile(blockIdx.x, nb);
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  uint16_t *rows16 = (uint16_t *)lds;         // [kBkWaves][Lr]
-  uint32_t *cnt = lds + (kBkWaves / 2) * Lr;  // [L]: running positions (MODE 0) / accumulators (MODE 1)
-  uint32_t *stage = cnt + L;                  // [kBkCap]
+  uint16_t *rows16 = (uint16_t *)lds;           // [kBkWaves][Lr]
+  uint32_t *stage = lds + (kBkWaves / 2) * Lr;  // [kBkCap]
+  const uint2 rt = bk_load_runs<MODE>(tab, n_tiles, B, b, 0, 0, s_pre, s_src, s_wsum);
+  const uint32_t len = rt.x, start = rt.y;
+  if (len > kBkCap) {  // uniform
+    if (threadIdx.x == 0) slow[1 + atomicAdd(&slow[0], 1u)] = b;
+    return;
+  }
+  for (uint32_t i = threadIdx.x; i < (kBkWaves / 2) * Lr; i += kBkThreads) lds[i] = 0;
+  __syncthreads();
+  const uint32_t Q = ((len + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
+  uint32_t key[kBkRounds], pay[kBkRounds];
+  if (len) bk_gather<MODE>(out1, s_pre, s_src, 0, len, Q, key, pay);
+#pragma unroll
+  for (uint32_t r = 0; r < kBkRounds; ++r)
+    if (w * Q + r * 64 + lane < len && r * 64 < Q)
+      atomicAdd((uint32_t *)&rows16[w * Lr + (key[r] & ~1u)], 1u << ((key[r] & 1u) << 4));
+  __syncthreads();
+  uint32_t tot[KPT], cst[KPT];
+  bk_keys<KPT>(rows16, L, Lr, true, s_wsum, tot, cst);
+  const uint32_t k0 = threadIdx.x * KPT;
+  if (MODE == 0 && k0 < L) {
+    const uint32_t kk = b * L + k0;
+    if constexpr (KPT >= 4) {
+      if (kk + KPT <= n_keys) {
+#pragma unroll
+        for (int v = 0; v < KPT / 4; ++v) {
+          ((uint4 *)&cell_size[kk])[v] = make_uint4(tot[4 * v], tot[4 * v + 1], tot[4 * v + 2], tot[4 * v + 3]);
+          ((uint4 *)&cell_offset[kk])[v] = make_uint4(start + cst[4 * v], start + cst[4 * v + 1],
+                                                      start + cst[4 * v + 2], start + cst[4 * v + 3]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < KPT; ++i)
+          if (kk + i < n_keys) {
+            cell_size[kk + i] = tot[i];
+            cell_offset[kk + i] = start + cst[i];
+          }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < KPT; ++i)
+        if (kk + i < n_keys) {
+          cell_size[kk + i] = tot[i];
+          cell_offset[kk + i] = start + cst[i];
+        }
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (uint32_t r = 0; r < kBkRounds; ++r) {
+    if (r * 64 < Q) {  // uniform
+      const bool ok = w * Q + r * 64 + lane < len;
+      const uint32_t k = key[r];
+      const uint64_t peers = bk_match(k, s, __ballot(ok));
+      const uint32_t rank = (uint32_t)__popcll(peers & lt);
+      const uint32_t p0 = rows16[w * Lr + k];
+      if (ok && rank == 0) rows16[w * Lr + k] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+      if (ok) stage[p0 + rank] = pay[r];
+    }
+  }
+  __syncthreads();
+  if (MODE == 0) {
+    for (uint32_t i = threadIdx.x; i < len; i += kBkThreads) sample_idx[start + i] = stage[i];
+  } else if (k0 < L) {
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const uint32_t kk = b * L + k0 + i;
+      if (kk >= n_keys || tot[i] == 0) continue;
+      float acc = target[kk];
+      for (uint32_t m = cst[i]; m < cst[i] + tot[i]; ++m) acc = sr_apply(op, acc, __uint_as_float(stage[m]));
+      target[kk] = acc;
+    }
+  }
+}
+
+// Level 2, general case: the buckets k_bucket_fast listed (or every bucket
+// when the tiles exceed one group: list == nullptr), in chunks of kBkCap
+// records in sequence order, group by group. MODE 0: a counting pass for the
+// bucket offsets, then stable placement straight to the output; MODE 1:
+// chunk-wise stable order in LDS, folded into per-key accumulators in order.
+template <int MODE, int KPT>
+__global__ __launch_bounds__(kBkThreads) void k_bucket_slow(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+                                                            const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
+                                                            int top, uint32_t n_keys, uint32_t nb,
+                                                            uint32_t *__restrict__ cell_size,
+                                                            uint32_t *__restrict__ cell_offset,
+                                                            uint32_t *__restrict__ sample_idx,
+                                                            float *__restrict__ target, int op,
+                                                            const uint32_t *__restrict__ list) {
+  constexpr uint32_t kTiles = SplitCfg<MODE>::Tiles;
+  extern __shared__ uint32_t lds[];
+  __shared__ uint32_t s_wsum[2][kBkWaves];
+  __shared__ uint32_t s_pre[kTiles + 1], s_src[kTiles];
+  if (list && blockIdx.x >= list[0]) return;
+  const uint32_t L = 1u << s, B = 1u << top, Lr = L < 2u ? 2u : L;
+  const uint32_t b = list ? list[1 + blockIdx.x] : blockIdx.x;
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  uint16_t *rows16 = (uint16_t *)lds;           // [kBkWaves][Lr]
+  uint32_t *stage = lds + (kBkWaves / 2) * Lr;  // [kBkCap]
+  uint32_t *cnt = stage + kBkCap;               // [L]: positions (MODE 0) / accumulators (MODE 1)
   const uint32_t ngroups = (n_tiles + kTiles - 1) / kTiles;
   const uint64_t lt = (1ull << lane) - 1ull;
-
-  // the runs of tile group g: s_pre (bucket-sequence prefix), s_src (record
-  // address of the run); returns the group's element count
-  auto load_runs = [&](uint32_t g, uint32_t base) -> uint32_t {
-    uint32_t rs[TPT], rl[TPT], sum = 0, ssum = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < TPT; ++i) {
-      const uint32_t t = g * kTiles + threadIdx.x * TPT + i;
-      const uint32_t e = t < n_tiles ? tab[(uint64_t)t * B + b] : 0u;
-      rs[i] = e & 0xFFFFu;
-      rl[i] = (e >> 16) - rs[i];
-      sum += rl[i];
-      ssum += rs[i];
-    }
-    uint32_t tot, stot;
-    uint32_t ex = base + block_excl_scan<kBkWaves>(sum, s_wsum, &tot);
-#pragma unroll
-    for (uint32_t i = 0; i < TPT; ++i) {
-      const uint32_t t = g * kTiles + threadIdx.x * TPT + i;
-      s_pre[threadIdx.x * TPT + i] = ex;
-      s_src[threadIdx.x * TPT + i] = t * T + rs[i];
-      ex += rl[i];
-    }
-    block_excl_scan<kBkWaves>(ssum, s_wsum, &stot);
-    if (threadIdx.x == 0) {
-      s_pre[kTiles] = base + tot;
-      s_info[2] = stot;  // sum of the run starts: elements of smaller digits
-    }
-    __syncthreads();
-    return tot;
-  };
-  // records [c0, c0 + cl) of the sequence (inside the loaded group) into
-  // registers: wave w holds [w*Q, (w+1)*Q), round r lane l = w*Q + 64r + l.
-  // All rounds search (branch-free, fixed steps) and load together: one
-  // latency for the chunk.
-  auto gather = [&](uint32_t c0, uint32_t cl, uint32_t Q, uint32_t *key, uint32_t *pay) {
-    uint32_t j[kBkRounds], lo[kBkRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < kBkRounds; ++r) {
-      j[r] = c0 + min(w * Q + r * 64 + lane, cl - 1u);
-      lo[r] = 0;
-    }
-#pragma unroll
-    for (uint32_t step = kTiles / 2; step > 0; step >>= 1)
-#pragma unroll
-      for (uint32_t r = 0; r < kBkRounds; ++r) lo[r] += s_pre[lo[r] + step] <= j[r] ? step : 0u;
-    Rec rc[kBkRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < kBkRounds; ++r) {
-      const bool ok = r * 64 < Q && w * Q + r * 64 + lane < cl;
-      const uint32_t src = s_src[lo[r]] + (j[r] - s_pre[lo[r]]);
-      if (ok) rc[r] = out1[src];
-      if constexpr (MODE == 0) {
-        key[r] = ok ? rc[r] >> 14 : 0u;
-        pay[r] = ok ? (src / T) * T + (rc[r] & 0x3FFFu) : 0u;
-      } else {
-        key[r] = ok ? rc[r].y : 0u;
-        pay[r] = ok ? rc[r].x : 0u;
-      }
-    }
-  };
-  auto zero_rows = [&]() {
+  const uint32_t k0 = threadIdx.x * KPT;
+  uint32_t key[kBkRounds], pay[kBkRounds], tot[KPT], cst[KPT];
+  auto chunk_rows = [&](uint32_t c0, uint32_t cl, uint32_t Q, bool abs) {
+    bk_gather<MODE>(out1, s_pre, s_src, c0, cl, Q, key, pay);
     for (uint32_t i = threadIdx.x; i < (kBkWaves / 2) * Lr; i += kBkThreads) lds[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r)
+      if (w * Q + r * 64 + lane < cl && r * 64 < Q)
+        atomicAdd((uint32_t *)&rows16[w * Lr + (key[r] & ~1u)], 1u << ((key[r] & 1u) << 4));
+    __syncthreads();
+    bk_keys<KPT>(rows16, L, Lr, abs, s_wsum, tot, cst);
+    __syncthreads();
   };
-  auto count_rows = [&](uint32_t cl, uint32_t Q, const uint32_t *key) {
+  auto place = [&](uint32_t cl, uint32_t Q, auto &&dst) {
 #pragma unroll
     for (uint32_t r = 0; r < kBkRounds; ++r) {
-      const uint32_t jj = w * Q + r * 64 + lane;
-      if (r * 64 < Q && jj < cl) {
+      if (r * 64 < Q) {
+        const bool ok = w * Q + r * 64 + lane < cl;
         const uint32_t k = key[r];
-        atomicAdd((uint32_t *)&rows16[w * Lr + (k & ~1u)], 1u << ((k & 1u) << 4));
-      }
-    }
-  };
-  auto keys_pass = [&](bool abs, uint32_t *tot, uint32_t *cst) {
-    const uint32_t kpt = L > kBkThreads ? L / kBkThreads : 1u;
-    switch (kpt) {
-      case 1: bk_keys<1>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
-      case 2: bk_keys<2>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
-      case 4: bk_keys<4>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
-      case 8: bk_keys<8>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
-      default: bk_keys<16>(rows16, L, Lr, abs, s_wsum, tot, cst); break;
-    }
-  };
-  // stable placement of the gathered records: dst(position, payload)
-  auto place = [&](uint32_t cl, uint32_t Q, const uint32_t *key, const uint32_t *pay, auto &&dst) {
-#pragma unroll
-    for (uint32_t r = 0; r < kBkRounds; ++r) {
-      if (r * 64 < Q) {  // wave-uniform
-        const uint32_t jj = w * Q + r * 64 + lane;
-        const bool ok = jj < cl;
-        const uint32_t k = key[r];
-        const uint64_t peers = ms_match(k, s, __ballot(ok));
+        const uint64_t peers = bk_match(k, s, __ballot(ok));
         const uint32_t rank = (uint32_t)__popcll(peers & lt);
         const uint32_t p0 = rows16[w * Lr + k];
         if (ok && rank == 0) rows16[w * Lr + k] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
         if (ok) dst(k, p0 + rank, pay[r]);
       }
     }
+    __syncthreads();
   };
-  constexpr int KMAX = 16;  // keys per thread at L = 4096
-  uint32_t tot[KMAX], cst[KMAX];
-  const uint32_t kpt = L > kBkThreads ? L / kBkThreads : 1u, k0 = threadIdx.x * kpt;
-  uint32_t key[kBkRounds], pay[kBkRounds];
-
-  const uint32_t len0 = load_runs(0, 0);
-  const uint32_t start = s_info[2];  // (group 0 alone when ngroups == 1)
-  if (ngroups == 1 && len0 <= kBkCap) {
-    // common case: the whole bucket in one chunk
-    const uint32_t Q = ((len0 + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
-    gather(0, len0, Q, key, pay);
-    zero_rows();
-    __syncthreads();
-    count_rows(len0, Q, key);
-    __syncthreads();
-    keys_pass(true, tot, cst);
-    if (MODE == 0 && k0 < L)
-      for (uint32_t i = 0; i < kpt; ++i) {
-        const uint32_t kk = b * L + k0 + i;
-        if (kk < n_keys) {
-          cell_size[kk] = tot[i];
-          cell_offset[kk] = start + cst[i];
-        }
-      }
-    __syncthreads();
-    place(len0, Q, key, pay, [&](uint32_t, uint32_t pos, uint32_t v) { stage[pos] = v; });
-    __syncthreads();
-    if (MODE == 0) {
-      for (uint32_t i = threadIdx.x; i < len0; i += kBkThreads) sample_idx[start + i] = stage[i];
-    } else if (k0 < L) {
-      for (uint32_t i = 0; i < kpt; ++i) {
-        const uint32_t kk = b * L + k0 + i;
-        if (kk >= n_keys || tot[i] == 0) continue;
-        float acc = target[kk];
-        for (uint32_t m = cst[i]; m < cst[i] + tot[i]; ++m) acc = sr_apply(op, acc, __uint_as_float(stage[m]));
-        target[kk] = acc;
-      }
-    }
-    return;
-  }
-  // general case (long buckets / many tiles): chunks of kBkCap records in
-  // sequence order, group by group
   if (MODE == 0) {
-    // pass A: per-key counts of the whole bucket
     for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) cnt[i] = 0;
     uint32_t base = 0, startsum = 0;
-    for (uint32_t g = 0; g < ngroups; ++g) {
-      const uint32_t gl = g ? load_runs(g, base) : len0;
-      startsum += s_info[2];
-      for (uint32_t c0 = base; c0 < base + gl; c0 += kBkCap) {
-        const uint32_t cl = min(kBkCap, base + gl - c0);
+    for (uint32_t g = 0; g < ngroups; ++g) {  // pass A: per-key counts
+      const uint2 rt = bk_load_runs<MODE>(tab, n_tiles, B, b, g, base, s_pre, s_src, s_wsum);
+      __syncthreads();
+      startsum += rt.y;
+      for (uint32_t c0 = base; c0 < base + rt.x; c0 += kBkCap) {
+        const uint32_t cl = min(kBkCap, base + rt.x - c0);
         const uint32_t Q = ((cl + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
-        gather(c0, cl, Q, key, pay);
+        bk_gather<MODE>(out1, s_pre, s_src, c0, cl, Q, key, pay);
 #pragma unroll
         for (uint32_t r = 0; r < kBkRounds; ++r)
           if (r * 64 < Q && w * Q + r * 64 + lane < cl) atomicAdd(&cnt[key[r]], 1u);
       }
-      base += gl;
+      base += rt.x;
       __syncthreads();
     }
-    // bucket offsets and the per-key outputs
-    {
+    {  // bucket offsets and the per-key outputs
       uint32_t sum = 0;
       if (k0 < L)
-        for (uint32_t i = 0; i < kpt; ++i) sum += cnt[k0 + i];
-      uint32_t all;
-      uint32_t run = startsum + block_excl_scan<kBkWaves>(sum, s_wsum, &all);
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) sum += cnt[k0 + i];
+      uint2 all;
+      uint32_t run = startsum + block_excl_scan2<kBkWaves>(make_uint2(sum, 0), s_wsum, &all).x;
       if (k0 < L)
-        for (uint32_t i = 0; i < kpt; ++i) {
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
           const uint32_t kk = b * L + k0 + i, c = cnt[k0 + i];
           if (kk < n_keys) {
             cell_size[kk] = c;
@@ -926,59 +1063,47 @@ __global__ __launch_bounds__(kBkThreads) void k_bucket_sort(const typename Split
         }
       __syncthreads();
     }
-    // pass B: stable placement straight to the output
     base = 0;
-    for (uint32_t g = 0; g < ngroups; ++g) {
-      const uint32_t gl = load_runs(g, base);
-      for (uint32_t c0 = base; c0 < base + gl; c0 += kBkCap) {
-        const uint32_t cl = min(kBkCap, base + gl - c0);
+    for (uint32_t g = 0; g < ngroups; ++g) {  // pass B: placement
+      const uint2 rt = bk_load_runs<MODE>(tab, n_tiles, B, b, g, base, s_pre, s_src, s_wsum);
+      __syncthreads();
+      for (uint32_t c0 = base; c0 < base + rt.x; c0 += kBkCap) {
+        const uint32_t cl = min(kBkCap, base + rt.x - c0);
         const uint32_t Q = ((cl + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
-        gather(c0, cl, Q, key, pay);
-        zero_rows();
-        __syncthreads();
-        count_rows(cl, Q, key);
-        __syncthreads();
-        keys_pass(false, tot, cst);
-        __syncthreads();
-        place(cl, Q, key, pay, [&](uint32_t k, uint32_t pos, uint32_t v) { sample_idx[cnt[k] + pos] = v; });
-        __syncthreads();
+        chunk_rows(c0, cl, Q, false);
+        place(cl, Q, [&](uint32_t k, uint32_t pos, uint32_t v) { sample_idx[cnt[k] + pos] = v; });
         if (k0 < L)
-          for (uint32_t i = 0; i < kpt; ++i) cnt[k0 + i] += tot[i];
+#pragma unroll
+          for (int i = 0; i < KPT; ++i) cnt[k0 + i] += tot[i];
         __syncthreads();
       }
-      base += gl;
+      base += rt.x;
     }
     return;
   }
-  // MODE 1: fold chunk by chunk into per-key accumulators (in order)
   for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) {
     const uint32_t kk = b * L + i;
     cnt[i] = kk < n_keys ? __float_as_uint(target[kk]) : 0u;
   }
   uint32_t base = 0;
   for (uint32_t g = 0; g < ngroups; ++g) {
-    const uint32_t gl = g ? load_runs(g, base) : len0;
-    for (uint32_t c0 = base; c0 < base + gl; c0 += kBkCap) {
-      const uint32_t cl = min(kBkCap, base + gl - c0);
+    const uint2 rt = bk_load_runs<MODE>(tab, n_tiles, B, b, g, base, s_pre, s_src, s_wsum);
+    __syncthreads();
+    for (uint32_t c0 = base; c0 < base + rt.x; c0 += kBkCap) {
+      const uint32_t cl = min(kBkCap, base + rt.x - c0);
       const uint32_t Q = ((cl + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
-      gather(c0, cl, Q, key, pay);
-      zero_rows();
-      __syncthreads();
-      count_rows(cl, Q, key);
-      __syncthreads();
-      keys_pass(true, tot, cst);
-      __syncthreads();
-      place(cl, Q, key, pay, [&](uint32_t, uint32_t pos, uint32_t v) { stage[pos] = v; });
-      __syncthreads();
+      chunk_rows(c0, cl, Q, true);
+      place(cl, Q, [&](uint32_t, uint32_t pos, uint32_t v) { stage[pos] = v; });
       if (k0 < L)
-        for (uint32_t i = 0; i < kpt; ++i) {
+#pragma unroll
+        for (int i = 0; i < KPT; ++i) {
           float acc = __uint_as_float(cnt[k0 + i]);
           for (uint32_t m = cst[i]; m < cst[i] + tot[i]; ++m) acc = sr_apply(op, acc, __uint_as_float(stage[m]));
           cnt[k0 + i] = __float_as_uint(acc);
         }
       __syncthreads();
     }
-    base += gl;
+    base += rt.x;
   }
   for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) {
     const uint32_t kk = b * L + i;
@@ -1084,11 +1209,12 @@ uint32_t split_tiles(uint64_t n) {
 // two-level: digit table, level-1 records, (MODE 1) the placed values;
 // LSD: digit histogram + scan + two key/payload buffer pairs.
 template <int MODE>
-size_t gb_bytes(uint64_t n, const GbPlan &g) {
+size_t gb_bytes(uint64_t n, uint64_t n_keys, const GbPlan &g) {
   size_t bytes = 8 * 1025 + 256;
   if (g.msd) {
     bytes += 4 * ((uint64_t)split_tiles<MODE>(n) << g.top) + 256;
     bytes += sizeof(typename SplitCfg<MODE>::Rec) * n + 256;
+    bytes += 4 * ((n_keys >> g.s) + 2) + 256;  // level-2 slow-bucket list
   } else {
     const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
     bytes += 2 * (4 * hn + 256) + scan_workspace_bytes(hn) + 256 + 4 * (4 * n + 256);
@@ -1100,9 +1226,9 @@ template <int MODE>
 uint32_t split_lds(int top) {
   return (16u << top) + (uint32_t)(SplitCfg<MODE>::T * sizeof(typename SplitCfg<MODE>::Rec));
 }
-uint32_t bucket_lds(int s) {
+uint32_t bucket_lds(int s, bool slow) {
   const uint32_t Lr = s ? 1u << s : 2u;
-  return 2u * kBkWaves * Lr + 4u * Lr + 4u * kBkCap;
+  return 2u * kBkWaves * Lr + 4u * kBkCap + (slow ? 4u << s : 0u);
 }
 
 int gb_attrs() {  // per call: the attribute belongs to the current device
@@ -1112,15 +1238,51 @@ int gb_attrs() {  // per call: the attribute belongs to the current device
       hipFuncSetAttribute((const void *)k_tile_split<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)split_lds<0>(kSplitMaxTop)) ||
       hipFuncSetAttribute((const void *)k_tile_split<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)split_lds<1>(kSplitMaxTop)) ||
-      hipFuncSetAttribute((const void *)k_bucket_sort<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)bucket_lds(kSplitMaxTop)) ||
-      hipFuncSetAttribute((const void *)k_bucket_sort<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)bucket_lds(kSplitMaxTop))) {
+                          (int)split_lds<1>(kSplitMaxTop))) {
     mtx_set_error("group-by: LDS attribute rejected");
     return MTX_E_HIP;
   }
   return MTX_OK;
+}
+
+// Level 2 for 2^s local keys: k_bucket_fast over every bucket, then
+// k_bucket_slow over the buckets it listed (long buckets); with more tiles
+// than one level-2 group, k_bucket_slow over every bucket.
+template <int MODE, int KPT>
+int bk_launch_k(const typename SplitCfg<MODE>::Rec *out1, const uint32_t *tab, uint32_t tiles, int s, int top,
+                uint32_t n_keys, uint32_t *cs, uint32_t *co, uint32_t *si, float *tgt, int op, uint32_t *slow,
+                hipStream_t st) {
+  const uint32_t nb = (uint32_t)(((uint64_t)n_keys + (1ull << s) - 1) >> s);
+  const int lf = (int)bucket_lds(s, false), ls = (int)bucket_lds(s, true);
+  if (hipFuncSetAttribute((const void *)k_bucket_fast<MODE, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, lf) ||
+      hipFuncSetAttribute((const void *)k_bucket_slow<MODE, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, ls)) {
+    mtx_set_error("group-by: LDS attribute rejected");
+    return MTX_E_HIP;
+  }
+  if (tiles <= SplitCfg<MODE>::Tiles) {
+    if (hipMemsetAsync(slow, 0, 4, st) != hipSuccess) return MTX_E_HIP;
+    hipLaunchKernelGGL((k_bucket_fast<MODE, KPT>), dim3(nb), dim3(kBkThreads), lf, st, out1, tab, tiles, s, top,
+                       n_keys, nb, cs, co, si, tgt, op, slow);
+    hipLaunchKernelGGL((k_bucket_slow<MODE, KPT>), dim3(nb), dim3(kBkThreads), ls, st, out1, tab, tiles, s, top,
+                       n_keys, nb, cs, co, si, tgt, op, (const uint32_t *)slow);
+  } else {
+    hipLaunchKernelGGL((k_bucket_slow<MODE, KPT>), dim3(nb), dim3(kBkThreads), ls, st, out1, tab, tiles, s, top,
+                       n_keys, nb, cs, co, si, tgt, op, (const uint32_t *)nullptr);
+  }
+  return MTX_OK;
+}
+template <int MODE>
+int bk_launch(const typename SplitCfg<MODE>::Rec *out1, const uint32_t *tab, uint32_t tiles, int s, int top,
+              uint32_t n_keys, uint32_t *cs, uint32_t *co, uint32_t *si, float *tgt, int op, uint32_t *slow,
+              hipStream_t st) {
+  const uint32_t L = 1u << s, kpt = L > (uint32_t)kBkThreads ? L / kBkThreads : 1u;
+  switch (kpt) {
+    case 1: return bk_launch_k<MODE, 1>(out1, tab, tiles, s, top, n_keys, cs, co, si, tgt, op, slow, st);
+    case 2: return bk_launch_k<MODE, 2>(out1, tab, tiles, s, top, n_keys, cs, co, si, tgt, op, slow, st);
+    case 4: return bk_launch_k<MODE, 4>(out1, tab, tiles, s, top, n_keys, cs, co, si, tgt, op, slow, st);
+    case 8: return bk_launch_k<MODE, 8>(out1, tab, tiles, s, top, n_keys, cs, co, si, tgt, op, slow, st);
+    default: return bk_launch_k<MODE, 16>(out1, tab, tiles, s, top, n_keys, cs, co, si, tgt, op, slow, st);
+  }
 }
 
 // One stable multisplit pass (LSD path): histogram (of keys, or of the
@@ -1156,7 +1318,8 @@ int ms_pass(const uint32_t *keys, const uint32_t *pay, uint64_t n, int shift, in
 }
 }  // namespace
 
-size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells) { return gb_bytes<0>(n, gb_plan(n, n_cells)); }
+size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells) { return gb_bytes<0>(n, n_cells, gb_plan(n, n_cells)); }
+
 
 int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
                    uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st) {
@@ -1175,10 +1338,9 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
     hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell);
     hipLaunchKernelGGL(k_tile_split<0>, dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n, g.s, g.top,
                        tab, out1);
-    const uint32_t nb = (uint32_t)(((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s);
-    hipLaunchKernelGGL(k_bucket_sort<0>, dim3(nb), dim3(kBkThreads), bucket_lds(g.s), st, out1, tab, tiles, g.s, g.top,
-                       n_cells, nb, cell_size, cell_offset, sample_idx, nullptr, 0);
-    return MTX_OK;
+    uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s));
+    return bk_launch<0>(out1, tab, tiles, g.s, g.top, n_cells, cell_size, cell_offset, sample_idx, nullptr, 0, slow,
+                        st);
   }
   // LSD: 12-bit digit passes (the first one hashes), then the run bounds
   const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
@@ -1211,7 +1373,7 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
 }
 
 size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value) {
-  return gb_bytes<1>(n_value, gb_plan(n_value, n_target));
+  return gb_bytes<1>(n_value, n_target, gb_plan(n_value, n_target));
 }
 
 int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
@@ -1227,10 +1389,9 @@ int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *va
     uint2 *out1 = cv.take<uint2>(n);
     hipLaunchKernelGGL(k_tile_split<1>, dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n, g.s, g.top,
                        tab, out1);
-    const uint32_t nb = (uint32_t)((n_target + (1ull << g.s) - 1) >> g.s);
-    hipLaunchKernelGGL(k_bucket_sort<1>, dim3(nb), dim3(kBkThreads), bucket_lds(g.s), st, out1, tab, tiles, g.s, g.top,
-                       (uint32_t)n_target, nb, nullptr, nullptr, nullptr, target, op);
-    return MTX_OK;
+    uint32_t *slow = cv.take<uint32_t>(1 + ((n_target + (1ull << g.s) - 1) >> g.s));
+    return bk_launch<1>(out1, tab, tiles, g.s, g.top, (uint32_t)n_target, nullptr, nullptr, nullptr, target, op, slow,
+                        st);
   }
   const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
   uint32_t *hist = cv.take<uint32_t>(hn), *hscan = cv.take<uint32_t>(hn);
