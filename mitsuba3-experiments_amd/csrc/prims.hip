@@ -24,6 +24,7 @@
 //   in ascending index order (deterministic), with no host round trips and
 //   no global atomics.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "mtx.h"
 #include "prims.h"
@@ -572,7 +573,7 @@ __global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t r
   cell[i] = hg_cell(p, n, i, bb.x, bb.y - bb.x, (float)res, n_cells);
 }
 
-template <int MODE>
+template <int MODE, bool RANK>
 __global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__ keys, const float *__restrict__ value,
                                                     uint64_t n, int s, int top, uint32_t *__restrict__ tab,
                                                     typename SplitCfg<MODE>::Rec *__restrict__ out1) {
@@ -657,15 +658,23 @@ __global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__
     const uint32_t j = w * (T / 8) + r * 64 + lane;
     const bool ok = j < tsize;
     const uint32_t d = key[r] >> s;
-    const uint64_t peers = ms_match(d, top, __ballot(ok));
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    const uint32_t p0 = row16[d];
-    if (ok && rank == 0) row16[d] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+    uint32_t pos;
+    if constexpr (RANK) {
+      // same-address LDS atomics of one wave return in lane order (checked
+      // once per device, lds_lane_order()): the old value is the position
+      pos = ok ? (atomicAdd(&row[d >> 1], 1u << ((d & 1u) << 4)) >> ((d & 1u) << 4)) & 0xFFFFu : 0u;
+    } else {
+      const uint64_t peers = ms_match(d, top, __ballot(ok));
+      const uint32_t rank = (uint32_t)__popcll(peers & lt);
+      const uint32_t p0 = row16[d];
+      if (ok && rank == 0) row16[d] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+      pos = p0 + rank;
+    }
     if (ok) {
       if constexpr (MODE == 0)
-        stage[p0 + rank] = ((key[r] & L1) << 14) | j;
+        stage[pos] = ((key[r] & L1) << 14) | j;
       else
-        stage[p0 + rank] = make_uint2(val[r], key[r] & L1);
+        stage[pos] = make_uint2(val[r], key[r] & L1);
     }
   }
   __syncthreads();
@@ -876,7 +885,7 @@ __device__ __forceinline__ void bk_gather(const typename SplitCfg<MODE>::Rec *__
 // Level 2, common case: one workgroup per bucket whose elements fit one
 // chunk (kBkCap) and whose tiles fit one group; others are listed in
 // `slow` for k_bucket_slow. 2^s = KPT * 256 local keys (KPT = 1: up to 256).
-template <int MODE, int KPT>
+template <int MODE, int KPT, bool RANK>
 __global__ __launch_bounds__(kBkThreads) void k_bucket_fast(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
                                                             const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
                                                             int top, uint32_t n_keys, uint32_t nb,
@@ -947,11 +956,19 @@ __global__ __launch_bounds__(kBkThreads) void k_bucket_fast(const typename Split
     if (r * 64 < Q) {  // uniform
       const bool ok = w * Q + r * 64 + lane < len;
       const uint32_t k = key[r];
-      const uint64_t peers = bk_match(k, s, __ballot(ok));
-      const uint32_t rank = (uint32_t)__popcll(peers & lt);
-      const uint32_t p0 = rows16[w * Lr + k];
-      if (ok && rank == 0) rows16[w * Lr + k] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
-      if (ok) stage[p0 + rank] = pay[r];
+      if constexpr (RANK) {  // lane-ordered LDS atomics (see k_tile_split)
+        if (ok) {
+          const uint32_t sh = (k & 1u) << 4;
+          const uint32_t pos = (atomicAdd((uint32_t *)&rows16[w * Lr + (k & ~1u)], 1u << sh) >> sh) & 0xFFFFu;
+          stage[pos] = pay[r];
+        }
+      } else {
+        const uint64_t peers = bk_match(k, s, __ballot(ok));
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        const uint32_t p0 = rows16[w * Lr + k];
+        if (ok && rank == 0) rows16[w * Lr + k] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+        if (ok) stage[p0 + rank] = pay[r];
+      }
     }
   }
   __syncthreads();
@@ -1124,6 +1141,26 @@ __global__ void k_sorted_fold(const uint32_t *__restrict__ keys, const uint32_t 
   target[t] = acc;
 }
 
+// Self-check of the lane-ordered LDS atomic property the RANK kernels use:
+// random keys with many collisions per wave instruction; counts returns
+// that differ from (base + number of lower lanes with the same key).
+__global__ __launch_bounds__(512) void k_lds_order_probe(uint32_t seed, uint32_t *bad) {
+  __shared__ uint32_t cnt[8][64];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  cnt[w][lane] = 0;
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t x = seed ^ (blockIdx.x * 7919u + threadIdx.x * 104729u);
+  for (int r = 0; r < 64; ++r) {
+    x = x * 1664525u + 1013904223u;
+    const uint32_t k = (x >> 20) % (1u + (uint32_t)r % 16u);  // 1..16 distinct keys per round
+    const uint32_t old = atomicAdd(&cnt[w][k], 1u);
+    const uint64_t m = ms_match(k, 4, ~0ull);
+    const uint32_t base = __shfl(old, __ffsll((unsigned long long)m) - 1);
+    if (old != base + (uint32_t)__popcll(m & lt)) atomicAdd(bad, 1u);
+  }
+}
+
 inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
@@ -1231,13 +1268,44 @@ uint32_t bucket_lds(int s, bool slow) {
   return 2u * kBkWaves * Lr + 4u * kBkCap + (slow ? 4u << s : 0u);
 }
 
+// One-time check per device that same-address LDS atomics of a wave return
+// in ascending lane order (observed on gfx950; not a documented guarantee):
+// the RANK kernels rely on it, the ballot-match kernels do not.
+bool lds_lane_order(hipStream_t st) {
+  static int state[64];  // 0 unknown, 1 holds, 2 fails
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+  if (state[dev]) return state[dev] == 1;
+  const char *env = getenv("MTX_LDS_RANK");  // "0": always the ballot-match kernels
+  if (env && env[0] == '0') {
+    state[dev] = 2;
+    return false;
+  }
+  uint32_t *d_bad = nullptr, bad = 1;
+  if (hipMalloc(&d_bad, 4) == hipSuccess) {
+    if (hipMemsetAsync(d_bad, 0, 4, st) == hipSuccess) {
+      hipLaunchKernelGGL(k_lds_order_probe, dim3(256), dim3(512), 0, st, 12345u, d_bad);
+      if (hipMemcpyAsync(&bad, d_bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+          hipStreamSynchronize(st) != hipSuccess)
+        bad = 1;
+    }
+    hipFree(d_bad);
+  }
+  state[dev] = bad == 0 ? 1 : 2;
+  return bad == 0;
+}
+
 int gb_attrs() {  // per call: the attribute belongs to the current device
   const int place = kMsWaves * (4 << kMsMaxBits);
   if (hipFuncSetAttribute((const void *)k_ms_place<true>, hipFuncAttributeMaxDynamicSharedMemorySize, place) ||
       hipFuncSetAttribute((const void *)k_ms_place<false>, hipFuncAttributeMaxDynamicSharedMemorySize, place) ||
-      hipFuncSetAttribute((const void *)k_tile_split<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void *)k_tile_split<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)split_lds<0>(kSplitMaxTop)) ||
-      hipFuncSetAttribute((const void *)k_tile_split<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void *)k_tile_split<1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)split_lds<1>(kSplitMaxTop)) ||
+      hipFuncSetAttribute((const void *)k_tile_split<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)split_lds<0>(kSplitMaxTop)) ||
+      hipFuncSetAttribute((const void *)k_tile_split<1, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)split_lds<1>(kSplitMaxTop))) {
     mtx_set_error("group-by: LDS attribute rejected");
     return MTX_E_HIP;
@@ -1252,17 +1320,25 @@ template <int MODE, int KPT>
 int bk_launch_k(const typename SplitCfg<MODE>::Rec *out1, const uint32_t *tab, uint32_t tiles, int s, int top,
                 uint32_t n_keys, uint32_t *cs, uint32_t *co, uint32_t *si, float *tgt, int op, uint32_t *slow,
                 hipStream_t st) {
+  const bool rank = lds_lane_order(st);
   const uint32_t nb = (uint32_t)(((uint64_t)n_keys + (1ull << s) - 1) >> s);
   const int lf = (int)bucket_lds(s, false), ls = (int)bucket_lds(s, true);
-  if (hipFuncSetAttribute((const void *)k_bucket_fast<MODE, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, lf) ||
+  if (hipFuncSetAttribute((const void *)k_bucket_fast<MODE, KPT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          lf) ||
+      hipFuncSetAttribute((const void *)k_bucket_fast<MODE, KPT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          lf) ||
       hipFuncSetAttribute((const void *)k_bucket_slow<MODE, KPT>, hipFuncAttributeMaxDynamicSharedMemorySize, ls)) {
     mtx_set_error("group-by: LDS attribute rejected");
     return MTX_E_HIP;
   }
   if (tiles <= SplitCfg<MODE>::Tiles) {
     if (hipMemsetAsync(slow, 0, 4, st) != hipSuccess) return MTX_E_HIP;
-    hipLaunchKernelGGL((k_bucket_fast<MODE, KPT>), dim3(nb), dim3(kBkThreads), lf, st, out1, tab, tiles, s, top,
-                       n_keys, nb, cs, co, si, tgt, op, slow);
+    if (rank)
+      hipLaunchKernelGGL((k_bucket_fast<MODE, KPT, true>), dim3(nb), dim3(kBkThreads), lf, st, out1, tab, tiles, s,
+                         top, n_keys, nb, cs, co, si, tgt, op, slow);
+    else
+      hipLaunchKernelGGL((k_bucket_fast<MODE, KPT, false>), dim3(nb), dim3(kBkThreads), lf, st, out1, tab, tiles, s,
+                         top, n_keys, nb, cs, co, si, tgt, op, slow);
     hipLaunchKernelGGL((k_bucket_slow<MODE, KPT>), dim3(nb), dim3(kBkThreads), ls, st, out1, tab, tiles, s, top,
                        n_keys, nb, cs, co, si, tgt, op, (const uint32_t *)slow);
   } else {
@@ -1336,8 +1412,12 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
     uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
     uint32_t *out1 = cv.take<uint32_t>(n);
     hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell);
-    hipLaunchKernelGGL(k_tile_split<0>, dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n, g.s, g.top,
-                       tab, out1);
+    if (lds_lane_order(st))
+      hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n,
+                         g.s, g.top, tab, out1);
+    else
+      hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n,
+                         g.s, g.top, tab, out1);
     uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s));
     return bk_launch<0>(out1, tab, tiles, g.s, g.top, n_cells, cell_size, cell_offset, sample_idx, nullptr, 0, slow,
                         st);
@@ -1387,8 +1467,12 @@ int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *va
     const uint32_t tiles = split_tiles<1>(n);
     uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
     uint2 *out1 = cv.take<uint2>(n);
-    hipLaunchKernelGGL(k_tile_split<1>, dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n, g.s, g.top,
-                       tab, out1);
+    if (lds_lane_order(st))
+      hipLaunchKernelGGL((k_tile_split<1, true>), dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n,
+                         g.s, g.top, tab, out1);
+    else
+      hipLaunchKernelGGL((k_tile_split<1, false>), dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n,
+                         g.s, g.top, tab, out1);
     uint32_t *slow = cv.take<uint32_t>(1 + ((n_target + (1ull << g.s) - 1) >> g.s));
     return bk_launch<1>(out1, tab, tiles, g.s, g.top, (uint32_t)n_target, nullptr, nullptr, nullptr, target, op, slow,
                         st);

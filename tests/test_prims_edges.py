@@ -142,3 +142,35 @@ def test_scatter_reduce_paths_and_mul(oracle, nt):
         o = {"add": 0, "min": 1, "max": 2, "mul": 3}[op]
         assert np.array_equal(primitives.scatter_reduce_with(op, tgt, val, idx),
                               oracle.scatter_reduce(o, tgt, val, idx)), op
+
+
+def test_groupby_ballot_fallback_matches(tmp_path):
+    """The ballot-match kernels (MTX_LDS_RANK=0: used when the one-time check
+    of lane-ordered LDS atomic returns fails) give the same bits as the
+    default kernels; run in a fresh process so the per-device choice is new."""
+    import subprocess
+    import sys
+
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from mtx import primitives
+rng = np.random.default_rng(31)
+p = rng.random((3, (1 << 20) + 3), dtype=np.float32)
+g = primitives.HashGrid(p, 100, 1 << 20)
+idx = rng.integers(0, 1 << 12, 1 << 20).astype(np.uint32)
+val = rng.random(1 << 20, dtype=np.float32)
+t = primitives.scatter_reduce_with("add", np.zeros(1 << 12, np.float32), val, idx)
+np.savez(sys.argv[2], cell=g.cell, size=g.cell_size, off=g.cell_offset, idx=g.sample_idx, t=t)
+'''
+    import os
+
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mitsuba3-experiments_amd")
+    outs = []
+    for flag in ("1", "0"):
+        f = tmp_path / f"r{flag}.npz"
+        env = dict(os.environ, MTX_LDS_RANK=flag)
+        subprocess.run([sys.executable, "-c", code, pkg, str(f)], check=True, env=env, timeout=300)
+        outs.append(np.load(f))
+    for k in ("cell", "size", "off", "idx", "t"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
