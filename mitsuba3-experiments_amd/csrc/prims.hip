@@ -886,7 +886,7 @@ __device__ __forceinline__ void bk_gather(const typename SplitCfg<MODE>::Rec *__
 // chunk (kBkCap) and whose tiles fit one group; others are listed in
 // `slow` for k_bucket_slow. 2^s = KPT * 256 local keys (KPT = 1: up to 256).
 template <int MODE, int KPT, bool RANK>
-__global__ __launch_bounds__(kBkThreads) void k_bucket_fast(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+__global__ __launch_bounds__(kBkThreads, 3) void k_bucket_fast(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
                                                             const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
                                                             int top, uint32_t n_keys, uint32_t nb,
                                                             uint32_t *__restrict__ cell_size,
@@ -894,26 +894,71 @@ __global__ __launch_bounds__(kBkThreads) void k_bucket_fast(const typename Split
                                                             uint32_t *__restrict__ sample_idx,
                                                             float *__restrict__ target, int op,
                                                             uint32_t *__restrict__ slow) {
-  constexpr uint32_t kTiles = SplitCfg<MODE>::Tiles;
+  using Rec = typename SplitCfg<MODE>::Rec;
+  constexpr uint32_t T = SplitCfg<MODE>::T, kTiles = SplitCfg<MODE>::Tiles, TPT = kTiles / kBkThreads;
   extern __shared__ uint32_t lds[];
   __shared__ uint32_t s_wsum[2][kBkWaves];
-  __shared__ uint32_t s_pre[kTiles + 1], s_src[kTiles];
   const uint32_t L = 1u << s, B = 1u << top, Lr = L < 2u ? 2u : L;  // row stride: u16 pairs share a word
   const uint32_t b = ms_tile(blockIdx.x, nb);
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint16_t *rows16 = (uint16_t *)lds;           // [kBkWaves][Lr]
   uint32_t *stage = lds + (kBkWaves / 2) * Lr;  // [kBkCap]
-  const uint2 rt = bk_load_runs<MODE>(tab, n_tiles, B, b, 0, 0, s_pre, s_src, s_wsum);
-  const uint32_t len = rt.x, start = rt.y;
+  // the bucket's runs (TPT consecutive tiles per thread) and their prefix
+  uint32_t rs[TPT], rl[TPT], sum = 0, ssum = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < TPT; ++i) {
+    const uint32_t t = threadIdx.x * TPT + i;
+    const uint32_t e = t < n_tiles ? tab[(uint64_t)t * B + b] : 0u;
+    rs[i] = e & 0xFFFFu;
+    rl[i] = (e >> 16) - rs[i];
+    sum += rl[i];
+    ssum += rs[i];
+  }
+  uint2 rt;
+  const uint32_t ex = block_excl_scan2<kBkWaves>(make_uint2(sum, ssum), s_wsum, &rt).x;
+  const uint32_t len = rt.x, start = rt.y;  // start: elements of smaller digits in every tile
   if (len > kBkCap) {  // uniform
     if (threadIdx.x == 0) slow[1 + atomicAdd(&slow[0], 1u)] = b;
     return;
+  }
+  // record address of every element of the bucket sequence, written by the
+  // thread owning its tile (runs are short: 2-4 records on average)
+  {
+    uint32_t q = ex;
+#pragma unroll
+    for (uint32_t i = 0; i < TPT; ++i) {
+      const uint32_t a = (threadIdx.x * TPT + i) * T + rs[i];
+      for (uint32_t m = 0; m < rl[i]; ++m) stage[q + m] = a + m;
+      q += rl[i];
+    }
   }
   for (uint32_t i = threadIdx.x; i < (kBkWaves / 2) * Lr; i += kBkThreads) lds[i] = 0;
   __syncthreads();
   const uint32_t Q = ((len + kBkWaves * 64 - 1) / (kBkWaves * 64)) * 64;
   uint32_t key[kBkRounds], pay[kBkRounds];
-  if (len) bk_gather<MODE>(out1, s_pre, s_src, 0, len, Q, key, pay);
+  {
+    uint32_t src[kBkRounds];
+    Rec rc[kBkRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) {
+      const uint32_t jj = w * Q + r * 64 + lane;
+      src[r] = stage[jj < len ? jj : 0u];
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r)
+      if (r * 64 < Q && w * Q + r * 64 + lane < len) rc[r] = out1[src[r]];
+#pragma unroll
+    for (uint32_t r = 0; r < kBkRounds; ++r) {
+      if constexpr (MODE == 0) {
+        key[r] = rc[r] >> 14;
+        pay[r] = (src[r] / T) * T + (rc[r] & 0x3FFFu);
+      } else {
+        key[r] = rc[r].y;
+        pay[r] = rc[r].x;
+      }
+    }
+  }
+  __syncthreads();  // stage is reused for the placement
 #pragma unroll
   for (uint32_t r = 0; r < kBkRounds; ++r)
     if (w * Q + r * 64 + lane < len && r * 64 < Q)
