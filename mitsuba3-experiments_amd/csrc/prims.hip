@@ -576,7 +576,9 @@ __global__ void k_hash_cells(const float *__restrict__ p, uint64_t n, uint32_t r
 template <int MODE, bool RANK>
 __global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__ keys, const float *__restrict__ value,
                                                     uint64_t n, int s, int top, uint32_t *__restrict__ tab,
-                                                    typename SplitCfg<MODE>::Rec *__restrict__ out1) {
+                                                    typename SplitCfg<MODE>::Rec *__restrict__ out1,
+                                                    uint32_t *__restrict__ slow) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) slow[0] = 0;  // level 2's slow-bucket count
   using Rec = typename SplitCfg<MODE>::Rec;
   constexpr uint32_t T = SplitCfg<MODE>::T, R = T / 512;  // rounds of 64 per wave
   extern __shared__ uint32_t lds[];
@@ -1036,22 +1038,16 @@ __global__ __launch_bounds__(kBkThreads, 3) void k_bucket_fast(const typename Sp
 // records in sequence order, group by group. MODE 0: a counting pass for the
 // bucket offsets, then stable placement straight to the output; MODE 1:
 // chunk-wise stable order in LDS, folded into per-key accumulators in order.
+// one bucket of k_bucket_slow
 template <int MODE, int KPT>
-__global__ __launch_bounds__(kBkThreads) void k_bucket_slow(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
-                                                            const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
-                                                            int top, uint32_t n_keys, uint32_t nb,
-                                                            uint32_t *__restrict__ cell_size,
-                                                            uint32_t *__restrict__ cell_offset,
-                                                            uint32_t *__restrict__ sample_idx,
-                                                            float *__restrict__ target, int op,
-                                                            const uint32_t *__restrict__ list) {
+__device__ __forceinline__ void bk_slow_one(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+                                            const uint32_t *__restrict__ tab, uint32_t n_tiles, int s, int top,
+                                            uint32_t n_keys, uint32_t b, uint32_t *__restrict__ cell_size,
+                                            uint32_t *__restrict__ cell_offset, uint32_t *__restrict__ sample_idx,
+                                            float *__restrict__ target, int op, uint32_t *lds,
+                                            uint32_t (*s_wsum)[kBkWaves], uint32_t *s_pre, uint32_t *s_src) {
   constexpr uint32_t kTiles = SplitCfg<MODE>::Tiles;
-  extern __shared__ uint32_t lds[];
-  __shared__ uint32_t s_wsum[2][kBkWaves];
-  __shared__ uint32_t s_pre[kTiles + 1], s_src[kTiles];
-  if (list && blockIdx.x >= list[0]) return;
   const uint32_t L = 1u << s, B = 1u << top, Lr = L < 2u ? 2u : L;
-  const uint32_t b = list ? list[1 + blockIdx.x] : blockIdx.x;
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   uint16_t *rows16 = (uint16_t *)lds;           // [kBkWaves][Lr]
   uint32_t *stage = lds + (kBkWaves / 2) * Lr;  // [kBkCap]
@@ -1170,6 +1166,27 @@ __global__ __launch_bounds__(kBkThreads) void k_bucket_slow(const typename Split
   for (uint32_t i = threadIdx.x; i < L; i += kBkThreads) {
     const uint32_t kk = b * L + i;
     if (kk < n_keys) target[kk] = __uint_as_float(cnt[i]);
+  }
+}
+
+template <int MODE, int KPT>
+__global__ __launch_bounds__(kBkThreads) void k_bucket_slow(const typename SplitCfg<MODE>::Rec *__restrict__ out1,
+                                                            const uint32_t *__restrict__ tab, uint32_t n_tiles, int s,
+                                                            int top, uint32_t n_keys, uint32_t nb,
+                                                            uint32_t *__restrict__ cell_size,
+                                                            uint32_t *__restrict__ cell_offset,
+                                                            uint32_t *__restrict__ sample_idx,
+                                                            float *__restrict__ target, int op,
+                                                            const uint32_t *__restrict__ list) {
+  constexpr uint32_t kTiles = SplitCfg<MODE>::Tiles;
+  extern __shared__ uint32_t lds[];
+  __shared__ uint32_t s_wsum[2][kBkWaves];
+  __shared__ uint32_t s_pre[kTiles + 1], s_src[kTiles];
+  const uint32_t n_work = list ? list[0] : nb;
+  for (uint32_t item = blockIdx.x; item < n_work; item += gridDim.x) {
+    bk_slow_one<MODE, KPT>(out1, tab, n_tiles, s, top, n_keys, list ? list[1 + item] : item, cell_size, cell_offset,
+                           sample_idx, target, op, lds, s_wsum, s_pre, s_src);
+    __syncthreads();
   }
 }
 
@@ -1377,15 +1394,14 @@ int bk_launch_k(const typename SplitCfg<MODE>::Rec *out1, const uint32_t *tab, u
     return MTX_E_HIP;
   }
   if (tiles <= SplitCfg<MODE>::Tiles) {
-    if (hipMemsetAsync(slow, 0, 4, st) != hipSuccess) return MTX_E_HIP;
     if (rank)
       hipLaunchKernelGGL((k_bucket_fast<MODE, KPT, true>), dim3(nb), dim3(kBkThreads), lf, st, out1, tab, tiles, s,
                          top, n_keys, nb, cs, co, si, tgt, op, slow);
     else
       hipLaunchKernelGGL((k_bucket_fast<MODE, KPT, false>), dim3(nb), dim3(kBkThreads), lf, st, out1, tab, tiles, s,
                          top, n_keys, nb, cs, co, si, tgt, op, slow);
-    hipLaunchKernelGGL((k_bucket_slow<MODE, KPT>), dim3(nb), dim3(kBkThreads), ls, st, out1, tab, tiles, s, top,
-                       n_keys, nb, cs, co, si, tgt, op, (const uint32_t *)slow);
+    hipLaunchKernelGGL((k_bucket_slow<MODE, KPT>), dim3(nb < 256u ? nb : 256u), dim3(kBkThreads), ls, st, out1, tab,
+                       tiles, s, top, n_keys, nb, cs, co, si, tgt, op, (const uint32_t *)slow);
   } else {
     hipLaunchKernelGGL((k_bucket_slow<MODE, KPT>), dim3(nb), dim3(kBkThreads), ls, st, out1, tab, tiles, s, top,
                        n_keys, nb, cs, co, si, tgt, op, (const uint32_t *)nullptr);
@@ -1456,14 +1472,14 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
     const uint32_t tiles = split_tiles<0>(n);
     uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
     uint32_t *out1 = cv.take<uint32_t>(n);
+    uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s));
     hipLaunchKernelGGL(k_hash_cells, dim3(nblk(n, 256)), dim3(256), 0, st, p, n, res, n_cells, partial + m, cell);
     if (lds_lane_order(st))
       hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n,
-                         g.s, g.top, tab, out1);
+                         g.s, g.top, tab, out1, slow);
     else
       hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n,
-                         g.s, g.top, tab, out1);
-    uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s));
+                         g.s, g.top, tab, out1, slow);
     return bk_launch<0>(out1, tab, tiles, g.s, g.top, n_cells, cell_size, cell_offset, sample_idx, nullptr, 0, slow,
                         st);
   }
@@ -1512,13 +1528,13 @@ int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *va
     const uint32_t tiles = split_tiles<1>(n);
     uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
     uint2 *out1 = cv.take<uint2>(n);
+    uint32_t *slow = cv.take<uint32_t>(1 + ((n_target + (1ull << g.s) - 1) >> g.s));
     if (lds_lane_order(st))
       hipLaunchKernelGGL((k_tile_split<1, true>), dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n,
-                         g.s, g.top, tab, out1);
+                         g.s, g.top, tab, out1, slow);
     else
       hipLaunchKernelGGL((k_tile_split<1, false>), dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n,
-                         g.s, g.top, tab, out1);
-    uint32_t *slow = cv.take<uint32_t>(1 + ((n_target + (1ull << g.s) - 1) >> g.s));
+                         g.s, g.top, tab, out1, slow);
     return bk_launch<1>(out1, tab, tiles, g.s, g.top, (uint32_t)n_target, nullptr, nullptr, nullptr, target, op, slow,
                         st);
   }
