@@ -391,8 +391,9 @@ def prims(args):
     c = cpu_time(lambda: oracle.hashgrid_mt(p, 100, nc))
     ach = 32 * n / (ms / 1e3) / 1e9
     _line("hashgrid build Msamples/sec (hashgrid.py:16-84), n=2^24", n / (ms / 1e3) / 1e6, "Msamples/s", 3, 1, ms,
-          {"workload": "bbox reduce, hash + rank, scan, fill; res 100, n_cells = n", "n": n},
-          {"bound": "hbm", "kernel": "hashgrid_build (4 kernels)", "achieved": round(ach, 1),
+          {"workload": "bbox reduce, cell hash, per-tile LDS split by the top 12 cell bits, per-bucket LDS sort "
+                       "of the low 12 bits (cell_size / cell_offset / sample_idx); res 100, n_cells = n", "n": n},
+          {"bound": "hbm", "kernel": "hashgrid_build (k_minmax, k_hash_cells, k_tile_split, k_bucket_fast)", "achieved": round(ach, 1),
            "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
            "alg_bytes_per_launch": 32 * n, "note": "SURVEY §8d: ~32 B/sample"},
           {"value": round(nc / c / 1e6, 4), "unit": "Msamples/s", "cores": _threads(), "kind": "port",
@@ -408,9 +409,10 @@ def prims(args):
     ach = 16 * nv / (ms / 1e3) / 1e9
     _line("scatter_reduce add Gvalues/sec (reductions.py:12-54), nv=2^24 nt=2^20", nv / (ms / 1e3) / 1e9,
           "Gvalues/s", 3, 1, ms,
-          {"workload": "deterministic winner-election rounds (ascending index per target)", "n_value": nv,
+          {"workload": "stable group-by target (per-tile LDS split by the top 12 target bits, per-bucket LDS sort "
+                       "of the low 8 bits), ordered fold per target (ascending index)", "n_value": nv,
            "n_target": nt},
-          {"bound": "hbm", "kernel": "scatter_reduce rounds", "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS,
+          {"bound": "hbm", "kernel": "scatter_reduce (k_tile_split, k_bucket_fast)", "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS,
            "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_launch": 16 * nv,
            "note": "SURVEY §8d: 16 B/value"},
           {"value": round(nv / c / 1e9, 4), "unit": "Gvalues/s", "cores": _threads(), "kind": "port",
