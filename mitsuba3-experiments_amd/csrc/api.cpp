@@ -141,6 +141,8 @@ struct mtx_ctx {
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
+  uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
+  DevBuf cq_keys, cq_perm, cq_ws;
   uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -193,6 +195,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
+  if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
   *out = c;
   return MTX_OK;
 }
@@ -210,6 +213,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_nbr, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5,
+                    &c->cq_keys, &c->cq_perm, &c->cq_ws,
                     &c->field_w16, &c->tr_p, &c->tr_m, &c->tr_v, &c->tr_g, &c->tr_wpart, &c->tr_loss, &c->tr_out,
                     &c->tr_dfeat, &c->tr_feat, &c->tr_flag, &c->tr_target, &c->nr_shape_pmf, &c->nr_shape_cdf,
                     &c->nr_tri_off, &c->nr_tri_pmf, &c->nr_tri_cdf, &c->nr_tri_prim, &c->nr_dists, &c->nr_lhs,
@@ -577,8 +581,25 @@ struct Timer {
 
 // Encode + MLP + L += T * out for the chunk's compacted cache queries.
 void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false) {
+  const uint32_t *perm = nullptr;
   hipEvent_t e = tm.begin(4);
-  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream);
+  if (c->cache_sort && !nerad_render) {
+    // encode the queries in Morton order (a stable sort of 24-bit cell codes
+    // with the hash-grid group-by): the hash-grid corner gathers of
+    // neighbouring rows then share table lines. The MLP row order follows;
+    // k_cache_apply maps row q back to query perm[q]. Results are unchanged
+    // (every query's features and MLP column are its own).
+    uint32_t nq = 0;
+    if (hipMemcpyAsync(&nq, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+        hipStreamSynchronize(c->stream) == hipSuccess && nq > 0 && !dalloc(c->cq_keys, 4ull * nq) &&
+        !dalloc(c->cq_perm, 4ull * nq) && !dalloc(c->cq_ws, mtxd::sort24_workspace_bytes(nq))) {
+      mtxd::field_morton_keys(c->field, b.cq_p, nq, (uint32_t *)c->cq_keys.p, c->stream);
+      if (mtxd::sort24((const uint32_t *)c->cq_keys.p, nq, (uint32_t *)c->cq_perm.p, c->cq_ws.p, c->stream) ==
+          MTX_OK)
+        perm = (const uint32_t *)c->cq_perm.p;
+    }
+  }
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream, perm);
   tm.end(4, e);
   e = tm.begin(5);
   mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
@@ -587,7 +608,7 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
   if (nerad_render)
     mtxd::launch_nerad_apply(b, (const float *)c->f_out.p, cap, 1, c->stream);
   else
-    mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream);
+    mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream, perm);
   if (tm.on) {
     uint32_t nq = 0;
     if (hipMemcpyAsync(&nq, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&

@@ -47,7 +47,7 @@ constexpr uint32_t kEncodeBlock = 256;
 
 __global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, const float4 *qp, const float4 *qd,
                                                                const uint32_t *count, uint32_t n_max,
-                                                               uint16_t *feat) {
+                                                               uint16_t *feat, const uint32_t *perm) {
   extern __shared__ uint4 rows[];  // 256 / n_levels rows of 128 B
   const uint32_t n = count ? min(*count, n_max) : n_max;
   const uint32_t L = e.n_levels, qpb = kEncodeBlock / L;
@@ -56,12 +56,13 @@ __global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, 
   for (uint32_t q0 = blockIdx.x * qpb; q0 < n; q0 += gridDim.x * qpb) {
     const uint32_t q = q0 + ql;
     if (ql < qpb && q < n) {
-      const float4 p = qp[q];
+      const uint32_t qs = perm ? perm[q] : q;  // Morton-ordered rows: neighbouring threads share table lines
+      const float4 p = qp[qs];
       const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
       uint16_t *row = row_h + (size_t)kFieldPad * ql;
       field_hashgrid_level(e, pn, l, row + 3 + e.n_features * l);
       if (l == 0) {
-        const float4 d = qd[q];
+        const float4 d = qd[qs];
         field_features_direct(e, pn, V3{d.x, d.y, d.z}, row, kFieldPad);
       }
     }
@@ -227,8 +228,29 @@ void field_prepack(const uint16_t *weights, uint32_t n_in, uint32_t n_hidden, ui
   }
 }
 
+// 8-bit-per-axis Morton code of the query position in the field's box (the
+// encoder's locality order: queries close in space share hash-grid lines).
+__device__ __forceinline__ uint32_t morton_spread8(uint32_t x) {
+  x = (x | (x << 8)) & 0x0300F00Fu;
+  x = (x | (x << 4)) & 0x030C30C3u;
+  x = (x | (x << 2)) & 0x09249249u;
+  return x;
+}
+__global__ void k_morton_keys(FieldEncoding e, const float4 *qp, uint32_t n, uint32_t *keys) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const float4 p = qp[q];
+  const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
+  auto cell = [](float v) { return (uint32_t)fminf(fmaxf(v * 256.f, 0.f), 255.f); };
+  keys[q] = morton_spread8(cell(pn.x)) | (morton_spread8(cell(pn.y)) << 1) | (morton_spread8(cell(pn.z)) << 2);
+}
+
+void field_morton_keys(const FieldEncoding &e, const float4 *qp, uint32_t n, uint32_t *keys, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_morton_keys, dim3((n + 255) / 256), dim3(256), 0, st, e, qp, n, keys);
+}
+
 int field_encode(const FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count, uint32_t n_max,
-                 uint16_t *feat, hipStream_t st) {
+                 uint16_t *feat, hipStream_t st, const uint32_t *perm) {
   if (n_max == 0) return MTX_OK;
   if (e.n_levels == 0 || e.n_levels > kEncodeBlock) {
     mtx_set_error("field_encode: unsupported n_levels %u", e.n_levels);
@@ -236,7 +258,7 @@ int field_encode(const FieldEncoding &e, const float4 *qp, const float4 *qd, con
   }
   const uint32_t qpb = kEncodeBlock / e.n_levels;
   const unsigned blocks = (unsigned)std::min<uint64_t>((n_max + qpb - 1) / qpb, 256ull * 64);
-  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(kEncodeBlock), (size_t)qpb * kFieldPad * 2, st, e, qp, qd, count, n_max, feat);
+  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(kEncodeBlock), (size_t)qpb * kFieldPad * 2, st, e, qp, qd, count, n_max, feat, perm);
   return MTX_OK;
 }
 

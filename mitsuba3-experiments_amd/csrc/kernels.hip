@@ -825,10 +825,10 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
 
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
 // plain sum: L = L + T * out, as the oracle-side composition in the tests).
-__global__ void k_cache_apply(WaveBuffers b, const float *out) {
+__global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *perm) {
   const uint32_t n = *b.cq_count;
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
-    const float4 t = b.cq_t[q];
+    const float4 t = b.cq_t[perm ? perm[q] : q];  // out row q belongs to query perm[q]
     const uint32_t path = __float_as_uint(t.w);
     float4 L = b.L[path];
     L.x = L.x + t.x * out[3 * (size_t)q];
@@ -1210,9 +1210,10 @@ int shade_blocks_per_cu() {
     nb = 2;
   return nb;
 }
-void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st) {
+void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st,
+                        const uint32_t *perm) {
   const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 16384);
-  hipLaunchKernelGGL(k_cache_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out);
+  hipLaunchKernelGGL(k_cache_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out, perm);
 }
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
   hipLaunchKernelGGL(k_mlt_init, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);

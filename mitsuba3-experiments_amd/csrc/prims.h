@@ -20,6 +20,10 @@ size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells);
 int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
                    uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st);
 
+// Stable sort permutation of n keys < 2^24 (hash-grid machinery).
+size_t sort24_workspace_bytes(uint64_t n);
+int sort24(const uint32_t *keys, uint64_t n, uint32_t *perm, void *ws, hipStream_t st);
+
 size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value);
 int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *value, const uint32_t *index,
                        uint64_t n_value, void *ws, hipStream_t st);
@@ -27,8 +31,11 @@ int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *va
 // Radiance field (field.hip)
 uint32_t field_frag_count(uint32_t n_hidden);
 void field_prepack(const uint16_t *weights, uint32_t n_in, uint32_t n_hidden, uint16_t *frag);
+// perm (optional): row i encodes query perm[i]
 int field_encode(const mtx::FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count,
-                 uint32_t n_max, uint16_t *feat, hipStream_t st);
+                 uint32_t n_max, uint16_t *feat, hipStream_t st, const uint32_t *perm = nullptr);
+// 24-bit Morton codes (8 bits per axis of the field's bounding box) of n queries
+void field_morton_keys(const mtx::FieldEncoding &e, const float4 *qp, uint32_t n, uint32_t *keys, hipStream_t st);
 int field_mlp(const uint16_t *feat, const uint32_t *count, uint32_t n_max, const void *wfrag, uint32_t n_hidden,
               float *out, int n_cu, hipStream_t st);
 

@@ -969,7 +969,7 @@ __global__ __launch_bounds__(kBkThreads, 3) void k_bucket_fast(const typename Sp
   uint32_t tot[KPT], cst[KPT];
   bk_keys<KPT>(rows16, L, Lr, true, s_wsum, tot, cst);
   const uint32_t k0 = threadIdx.x * KPT;
-  if (MODE == 0 && k0 < L) {
+  if (MODE == 0 && cell_size && k0 < L) {
     const uint32_t kk = b * L + k0;
     if constexpr (KPT >= 4) {
       if (kk + KPT <= n_keys) {
@@ -1112,7 +1112,7 @@ __device__ __forceinline__ void bk_slow_one(const typename SplitCfg<MODE>::Rec *
 #pragma unroll
         for (int i = 0; i < KPT; ++i) {
           const uint32_t kk = b * L + k0 + i, c = cnt[k0 + i];
-          if (kk < n_keys) {
+          if (kk < n_keys && cell_size) {
             cell_size[kk] = c;
             cell_offset[kk] = run;
           }
@@ -1511,6 +1511,29 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
     hipLaunchKernelGGL(k_hash_ranges, dim3(nblk(n, kHashTile)), dim3(256), 0, st, kin, n, n_cells, cell_offset,
                        cell_size);
   return MTX_OK;
+}
+
+size_t sort24_workspace_bytes(uint64_t n) { return gb_bytes<0>(n, 1u << 24, gb_plan(n, 1u << 24)); }
+
+// Stable sort permutation of n keys < 2^24 (the hash grid's two levels
+// without the per-key outputs): perm[i] = index of the i-th smallest key.
+int sort24(const uint32_t *keys, uint64_t n, uint32_t *perm, void *ws, hipStream_t st) {
+  if (n == 0) return MTX_OK;
+  if (int e = gb_attrs()) return e;
+  const GbPlan g = gb_plan(n, 1u << 24);
+  Carve cv{(char *)ws};
+  cv.take<float2>(1025);
+  const uint32_t tiles = split_tiles<0>(n);
+  uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
+  uint32_t *out1 = cv.take<uint32_t>(n);
+  uint32_t *slow = cv.take<uint32_t>(1 + ((1ull << 24) >> g.s));
+  if (lds_lane_order(st))
+    hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n, g.s,
+                       g.top, tab, out1, slow);
+  else
+    hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n,
+                       g.s, g.top, tab, out1, slow);
+  return bk_launch<0>(out1, tab, tiles, g.s, g.top, 1u << 24, nullptr, nullptr, perm, nullptr, 0, slow, st);
 }
 
 size_t scatter_workspace_bytes(uint64_t n_target, uint64_t n_value) {

@@ -138,3 +138,32 @@ def test_nrc_cache_film_bit_exact(small_scene, oracle, chunk):
     np.testing.assert_array_equal(film, ref)
     plain = load_dict({"type": "nrc"}).render_film(small_scene, seed=3, spp=spp)
     assert not np.array_equal(plain, film)
+
+
+@pytest.mark.gpu
+def test_nrc_cache_morton_order_unchanged(tmp_path):
+    """MTX_CACHE_SORT=1 encodes the cache queries in Morton order (sorted with
+    the hash-grid group-by; measured slower, so off by default); queue order
+    otherwise. Both films are identical (each query's features and MLP column
+    are its own)."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from mtx import load_dict, scene
+from mtx.field import Field
+sc = scene.bedroom(width=64, height=36, scale=0.02, tex_res=64)
+integ = load_dict({"type": "nrc", "field": Field(sc, seed=5, table_scale=1.0)})
+np.save(sys.argv[2], integ.render_film(sc, seed=7, spp=4))
+'''
+    films = []
+    for flag in ("1", "0"):
+        f = tmp_path / f"f{flag}.npy"
+        subprocess.run([sys.executable, "-c", code, os.path.join(root, "mitsuba3-experiments_amd"), str(f)],
+                       check=True, env=dict(os.environ, MTX_CACHE_SORT=flag), timeout=300)
+        films.append(np.load(f))
+    np.testing.assert_array_equal(films[0], films[1])
