@@ -29,6 +29,9 @@
 using namespace mtx;
 
 // Tuning knob: minimum resident shade blocks per CU (caps VGPRs; 1 = none).
+#ifndef MTX_SHADE_PREFETCH
+#define MTX_SHADE_PREFETCH 1  // A/B: 0 = the next step's queue entry and hit load at the step's end
+#endif
 #ifndef MTX_SHADE_MIN_BLOCKS
 #define MTX_SHADE_MIN_BLOCKS 3
 #endif
@@ -231,14 +234,13 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
 
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                           const ChunkParams &p,
-                                           uint32_t bounce, uint32_t path, ShadeIO &io) {
+                                           const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h,
+                                           ShadeIO &io) {
   const float4 ro = b.ray_o[path], rd = b.ray_d[path];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
   const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
   const float4 pv = bounce == 0 ? kInitPrev : b.prev[path];
   const uint4 mi = b.misc[path];
-  const float4 h = b.hit[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -432,11 +434,9 @@ __device__ __forceinline__ float dr_clamp(float x, float lo, float hi) { return 
 // executed bounce consumes 4 draws: the chain's RNG stream continues across
 // the Metropolis iterations.
 __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                             const ChunkParams &p,
-                                             uint32_t path) {
+                                             const ChunkParams &p, uint32_t path, const float4 h) {
   const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path];
   const uint4 mi = b.misc[path];
-  const float4 h = b.hit[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -499,11 +499,10 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
 // pssmltsimple.py:60-131 without the mutation; bounce 0 starts from the
 // constant initial state (f = 1, eta = 1, L = 0, prev_bsdf_pdf = 1).
 __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                             const ChunkParams &p, uint32_t bounce, uint32_t path) {
+                                             const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h) {
   const float4 rd = b.ray_d[path];
   const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
   const uint4 mi = b.misc[path];
-  const float4 h = b.hit[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -552,10 +551,9 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
 // (:118-134, shadow ray), proposed vertex write (:138), RR (:154-166).
 // Draws per bounce: 1 + 2 (BSDF) + 2 (mutation) + 1 (RR).
 __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                                  const ChunkParams &p, uint32_t path, ShadeIO &io) {
+                                                  const ChunkParams &p, uint32_t path, const float4 h, ShadeIO &io) {
   const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
   const uint4 mi = b.misc[path];
-  const float4 h = b.hit[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -663,14 +661,13 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
 // L = Field(si) * f + Le(si) (applied by k_nerad_apply after the field).
 template <bool RENDER>
 __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                            uint32_t bounce, uint32_t path, ShadeIO &io) {
+                                            uint32_t bounce, uint32_t path, const float4 h, ShadeIO &io) {
   const float4 rd = b.ray_d[path];
   // a rendered lane's bounce-0 state is the camera raygen's (nothing stored)
   const float4 Lr = (RENDER && bounce == 0) ? kInitL : b.L[path];
   const float4 pv = (RENDER && bounce == 0) ? kInitPrev : b.prev[path];
   const float4 th = (RENDER && bounce == 0) ? kInitThr : b.thr[path];
   const uint4 mi = b.misc[path];
-  const float4 h = b.hit[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -772,43 +769,58 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
   uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
   const uint32_t stride = gridDim.x * kShadeBlock;
   uint32_t parity = 0;
+  // software pipeline over the persistent loop: the next step's queue entry
+  // loads during this step, its hit record before this step's appends
+  uint32_t path = 0;
+  float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (blockIdx.x * kShadeBlock + threadIdx.x < count) {
+    path = in_q[blockIdx.x * kShadeBlock + threadIdx.x];
+    h = b.hit[path];
+  }
   for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += stride, parity ^= 1u) {
     const uint32_t i = base + threadIdx.x;
+    const uint32_t inext = i + stride;
+    uint32_t path_n = 0;
+    if (MTX_SHADE_PREFETCH && inext < count) path_n = in_q[inext];
     ShadeIO io;
     io.emit = false;
     io.query = false;
     bool cont = false;
-    uint32_t path = 0;
-    if (i < count) path = in_q[i];
     bool valid = i < count;
     if (s.shade_sort) {
       // the block's paths ordered by the shading class of their hit: waves
       // then run one or two BSDF branches instead of all of them
       uint32_t key = kShadeClasses - 1;  // slots past the queue end sort last
       if (valid) {
-        const uint32_t prim = __float_as_uint(b.hit[path].y);
+        const uint32_t prim = __float_as_uint(h.y);
         key = prim == 0xffffffffu ? 0u : (__float_as_uint(s.shade_rec[8 * (size_t)prim + 2].w) >> 8) & 31u;
       }
       path = block_sort_by_key<kShadeBlock>(key, path);
       valid = threadIdx.x < min(count - base, (uint32_t)kShadeBlock);
+      if (valid) h = b.hit[path];
     }
     if (valid) {
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
-        cont = shade_pssmlt(s, sv, b, p, path);
+        cont = shade_pssmlt(s, sv, b, p, path, h);
       else if constexpr (INT == MTX_INT_SIMPLE)
-        cont = shade_simple(s, sv, b, p, bounce, path);
+        cont = shade_simple(s, sv, b, p, bounce, path, h);
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
-        cont = shade_pssmlt_path(s, sv, b, p, path, io);
+        cont = shade_pssmlt_path(s, sv, b, p, path, h, io);
       else if constexpr (INT == MTX_INT_NERAD_RHS)
-        cont = shade_nerad<false>(s, sv, b, bounce, path, io);
+        cont = shade_nerad<false>(s, sv, b, bounce, path, h, io);
       else if constexpr (INT == MTX_INT_NERAD)
-        cont = shade_nerad<true>(s, sv, b, bounce, path, io);
+        cont = shade_nerad<true>(s, sv, b, bounce, path, h, io);
       else
-        cont = shade_path<INT>(s, sv, b, p, bounce, path, io);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, h, io);
+    }
+    const uint32_t path_c = path;
+    if (MTX_SHADE_PREFETCH) {
+      path = path_n;
+      if (inext < count) h = b.hit[path];
     }
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
-    if (cont) out_q[slot] = path;
+    if (cont) out_q[slot] = path_c;
     if (io.emit) b.shadow[sslot] = io.rec;
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
       if (INT != MTX_INT_NRC || p.nrc_cache) {
@@ -819,6 +831,10 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
           b.cq_t[q] = io.qt;
         }
       }
+    }
+    if (!MTX_SHADE_PREFETCH && inext < count) {
+      path = in_q[inext];
+      h = b.hit[path];
     }
   }
 }
