@@ -29,7 +29,7 @@ constexpr int kShadeBlock = 256;
 __device__ __forceinline__ SceneView make_view(const DevScene &s) {
   SceneView v;
   v.nodes = reinterpret_cast<const int32_t *>(s.nodes);
-  v.tri_geom = reinterpret_cast<const float *>(s.tri);
+  v.tri_geom = nullptr;  // device: DevScene::tri (packed, load_tri)
   v.tri_vidx = s.tri_vidx;
   v.tri_shape = s.tri_shape;
   v.vpos = s.vpos;
@@ -76,6 +76,21 @@ __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, 
   }
   return si_from_vertices(t, prim, u, v, ray_d, V3{a.x, a.y, a.z}, V3{b.x, b.y, b.z}, V3{c.x, c.y, c.z},
                           __float_as_uint(a.w), (int32_t)__float_as_uint(b.w), use_n, n0, n1, n2, use_uv, t0, t1, t2);
+}
+
+// Triangle geometry of leaf-order triangle `prim`: 9 packed floats (36 B:
+// v0, e1 = v1 - v0, e2 = v2 - v0; mtx_scene_upload drops the ABI's pads),
+// three dwordx3 loads.
+struct TriGeom {
+  V3 p0, e1, e2;
+};
+__device__ __forceinline__ TriGeom load_tri(const DevScene &s, uint32_t prim) {
+  const float *g = s.tri + 9 * (size_t)prim;
+  TriGeom t;
+  t.p0 = V3{g[0], g[1], g[2]};
+  t.e1 = V3{g[3], g[4], g[5]};
+  t.e2 = V3{g[6], g[7], g[8]};
+  return t;
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
@@ -267,10 +282,10 @@ __device__ __forceinline__ bool traverse(const DevScene &s, int32_t *stk, const 
       leaf_decode(node, &first, &count);
       for (uint32_t k = 0; k < count; ++k) {
         const uint32_t prim = first + k;
-        const float4 g0 = s.tri[3 * prim + 0], g1 = s.tri[3 * prim + 1], g2 = s.tri[3 * prim + 2];
+        const TriGeom g = load_tri(s, prim);
         float t, u, v;
         ++tv;
-        if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+        if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
           if (ANY) {
             hit_any = true;
             break;
@@ -314,6 +329,19 @@ namespace mtxd {
 #endif
 constexpr int32_t kTravDone = INT32_MIN;           // never a valid leaf reference
 constexpr int32_t kTravLeafTaken = INT32_MIN + 1;  // leaf moved to the leaf phase, pop next
+
+// Stack entry e of a lane: LDS for e < lds_n, the global spill area above.
+// The LDS entry is read unconditionally (clamped) and the global one only on
+// the rare deep entries, so the common pop is a ds_read; a select between the
+// two pointers would compile to a flat load (vector-memory + LDS counters,
+// a texture-path slot per pop).
+__device__ __forceinline__ int32_t stack_read(const int32_t *stk, const int32_t *ovf, int e, int lds_n,
+                                              uint32_t ovf_threads) {
+  int32_t v = stk[min(e, lds_n - 1) * kTraceBlock];
+  asm volatile("" : "+v"(v));  // keeps the LDS read (no pointer select + flat load)
+  if (e >= lds_n) v = ovf[(size_t)(e - lds_n) * ovf_threads];
+  return v;
+}
 
 // Src provides: load(k, TraceRay&, float &tmax, uint32_t &payload) and
 // finish(payload, bool any_hit, float t, uint32_t prim, float u, float v).
@@ -362,7 +390,7 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
   auto pop = [&](int &spr) -> int32_t {
     if (spr == 0) return kTravDone;
     --spr;
-    return spr < lds_n ? stk[spr * kTraceBlock] : ovf[(size_t)(spr - lds_n) * s.ovf_threads];
+    return stack_read(stk, ovf, spr, lds_n, s.ovf_threads);
   };
   while (true) {
     if (!exhausted) {
@@ -506,10 +534,10 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
         leaf_decode(lf, &first, &cnt);
         for (uint32_t k = 0; k < cnt; ++k) {
           const uint32_t pr = first + k;
-          const float4 g0 = s.tri[3 * pr + 0], g1 = s.tri[3 * pr + 1], g2 = s.tri[3 * pr + 2];
+          const TriGeom g = load_tri(s, pr);
           float t, u, v;
           ++tv;
-          if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+          if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
             if (ANY) {
               hit = true;
               break;
@@ -579,7 +607,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
     node = -1;
     while (sp > 0) {
       --sp;
-      const int32_t e = sp < lds_n ? stk[sp * kTraceBlock] : ovf[(size_t)(sp - lds_n) * s.ovf_threads];
+      const int32_t e = stack_read(stk, ovf, sp, lds_n, s.ovf_threads);
       if (e >= 0) {
         node = e;
         return;
@@ -705,11 +733,11 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
       }
       const uint32_t pr = tri;
-      const float4 g0 = s.tri[3 * pr + 0], g1 = s.tri[3 * pr + 1], g2 = s.tri[3 * pr + 2];
+      const TriGeom g = load_tri(s, pr);
       float t, u, v;
       ++tv;
       ++tri;
-      if (tri_intersect(r, V3{g0.x, g0.y, g0.z}, V3{g1.x, g1.y, g1.z}, V3{g2.x, g2.y, g2.z}, tbest, &t, &u, &v)) {
+      if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
         if (ANY) {
           hit = true;
           tri = tri_end;

@@ -193,9 +193,11 @@ __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const fl
 // ---------------------------------------------------------------------------
 // Initial path state (init_path, k_rs_begin): throughput 1 / eta 1, L 0 /
 // prev_bsdf_pdf 1, prev_p 0 / spread 0. Never stored: bounce-0 shades use it.
-__device__ constexpr float4 kInitThr = {1.f, 1.f, 1.f, 1.f};
-__device__ constexpr float4 kInitL = {0.f, 0.f, 0.f, 1.f};
-__device__ constexpr float4 kInitPrev = {0.f, 0.f, 0.f, 0.f};
+// (register constants: a select between a __device__ constant and the state
+// plane compiled to a pointer select + flat load per plane)
+#define kInitThr make_float4(1.f, 1.f, 1.f, 1.f)
+#define kInitL make_float4(0.f, 0.f, 0.f, 1.f)
+#define kInitPrev make_float4(0.f, 0.f, 0.f, 0.f)
 
 struct ShadeIO {
   ShadowRec rec;

@@ -42,7 +42,7 @@ constexpr uint32_t kXSlotWords = kXcds * kXHeadStride;
 
 struct DevScene {
   const int4 *nodes;  // 4 x int4 per node
-  const float4 *tri;  // 3 x float4 per triangle
+  const float *tri;   // 9 floats per triangle (v0, e1, e2; device_common.h load_tri)
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;
   const float *vpos;
