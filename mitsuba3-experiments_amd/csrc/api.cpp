@@ -138,6 +138,7 @@ struct mtx_ctx {
   uint32_t trace_batch = 256;
   uint32_t refill_lanes = 16;
   uint32_t urefill = 16;
+  uint32_t tri_min = 0;  // trace_loop_u: triangle step deferred until this many lanes wait on one
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
@@ -192,6 +193,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
+  if (const char *e = getenv("MTX_TRI_MIN")) c->tri_min = (uint32_t)std::max(0, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
@@ -392,6 +394,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.trace_batch = c->trace_batch;
   s.refill_lanes = c->refill_lanes;
   s.urefill = c->urefill;
+  s.tri_min = c->tri_min;
   s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
   s.shade_sort = c->shade_sort;

@@ -726,8 +726,15 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         pop_next();
       }
     }
-    // ---- one triangle test
-    if (has && tri < tri_end) {
+    // ---- one triangle test. Deferred (s.tri_min > 0) until enough lanes
+    // wait on a triangle or no lane has a node to visit: the step then runs
+    // with more lanes busy; every ray's own visit sequence is unchanged.
+    bool tri_step = true;
+    if (s.tri_min) {
+      const uint32_t nt = (uint32_t)__popcll(__ballot(has && tri < tri_end));
+      tri_step = nt >= s.tri_min || __ballot(has && node >= 0) == 0;
+    }
+    if (tri_step && has && tri < tri_end) {
       if (STATS) {
         const uint64_t m = __ballot(true);
         if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];

@@ -63,6 +63,7 @@ struct DevScene {
   uint32_t ovf_threads;    // threads of the persistent trace grid
   uint32_t refill_lanes;   // persistent kernels: refill a wave once this many lanes are idle
   uint32_t urefill;        // unified single-step traversal (trace_loop_u): the same, its own threshold
+  uint32_t tri_min;        // trace_loop_u: run the triangle step once this many lanes wait on one (or no lane has a node)
   uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   uint32_t shade_sort;     // k_shade: order a block's paths by the hit's shading class

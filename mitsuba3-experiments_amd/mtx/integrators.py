@@ -64,6 +64,14 @@ def develop(film: np.ndarray) -> np.ndarray:
     return np.where(w != 0, inner[..., :3] / np.where(w != 0, w, 1), 0).astype(np.float32)
 
 
+def _rows3(v) -> np.ndarray:
+    """A wavefront of 3-vectors as (N, 3) float32 from (N, 3) or (3, N)."""
+    a = np.asarray(v, np.float32)
+    if a.ndim == 2 and a.shape[0] == 3 and a.shape[1] != 3:
+        a = a.T
+    return a.reshape(-1, 3)
+
+
 class SamplingIntegrator:
     integrator_id = 0
     name = ""
@@ -124,10 +132,13 @@ class SamplingIntegrator:
 
     # --------------------------------------------------------------- sample --
     def sample(self, scene, sampler: IndependentSampler, ray, medium=None, active=True):
-        """sample(scene, sampler, ray) over a wavefront of rays (o, d) -> (L, valid, [])."""
-        o, d = ray
-        rays = np.ascontiguousarray(np.concatenate([np.asarray(o, np.float32).reshape(-1, 3),
-                                                    np.asarray(d, np.float32).reshape(-1, 3)], 1))
+        """sample(scene, sampler, ray) over a wavefront of rays -> (L, valid, []).
+
+        `ray` is an (o, d) pair or a ray object with `.o` / `.d` fields (the
+        RayDifferential3f of path.py:195-202); each field is (N, 3) or (3, N)
+        (Dr.Jit's Array3f layout)."""
+        o, d = (ray.o, ray.d) if hasattr(ray, "o") and hasattr(ray, "d") else ray
+        rays = np.ascontiguousarray(np.concatenate([_rows3(o), _rows3(d)], 1))
         n = len(rays)
         if len(sampler.lanes) != n:
             raise MtxError("sampler lanes and rays differ in length")
@@ -403,13 +414,51 @@ def _bind_scene(ctx, scene) -> None:
     ctx.scene = scene  # keep the host arrays alive while bound
 
 
-def register_with_mitsuba() -> bool:
-    """Register the façade names as mi.SamplingIntegrator plugins when Mitsuba
-    is importable (it is not in this image; returns False then)."""
-    try:
-        import mitsuba as mi  # noqa: F401
-    except Exception:
-        return False
+def register_with_mitsuba(mi=None) -> bool:
+    """With Mitsuba importable (it is not in this image: returns False), register
+    every façade name (path.py:305, path-mis.py:158, pssmltsimple.py:145,
+    restirgi.py:591, ...) as an ``mi.SamplingIntegrator`` subclass.
+
+    What this does and does not provide: the registered plugin reads its
+    properties through ``props.get`` (path.py:22-25) and forwards ``render`` /
+    ``sample`` to the mtx integrator, which runs on an :class:`mtx.scene.Scene`
+    (the bedroom proxy, OBJ/XML ingestion of ``mtx.scene.from_xml``). There is
+    no converter from a loaded ``mi.Scene`` (its meshes, BSDF plugins and
+    emitters) to the mtx scene: handing one to the plugin raises MtxError
+    instead of rendering something else. `mi` may be passed explicitly (tests
+    use a stand-in module)."""
+    if mi is None:
+        try:
+            import mitsuba as mi  # noqa: F401
+        except Exception:
+            return False
     for name, ctor in list(_REGISTRY.items()):
-        mi.register_integrator(name, ctor)
+        mi.register_integrator(name, _mitsuba_plugin(mi, name, ctor))
     return True
+
+
+def _mitsuba_plugin(mi, name: str, ctor):
+    """Constructor of the mi.SamplingIntegrator subclass wrapping `ctor`."""
+
+    def _scene(scene):
+        from .scene import Scene
+
+        if not isinstance(scene, Scene):
+            raise MtxError(f"{name}: mtx renders mtx.scene.Scene objects; no mi.Scene converter exists "
+                           "(build the scene with mtx.scene.from_xml / mtx.scene.bedroom)")
+        return scene
+
+    class Plugin(mi.SamplingIntegrator):
+        def __init__(self, props):
+            super().__init__(props)
+            keys = props.keys() if hasattr(props, "keys") else []
+            self.mtx = ctor({k: props[k] for k in keys})
+
+        def render(self, scene, sensor=None, seed=0, spp=1, develop=True, evaluate=True):
+            return self.mtx.render(_scene(scene), sensor, seed, spp, develop, evaluate)
+
+        def sample(self, scene, sampler, ray, medium=None, active=True):
+            return self.mtx.sample(_scene(scene), sampler, ray, medium, active)
+
+    Plugin.__name__ = Plugin.__qualname__ = f"Mtx_{name}"
+    return lambda props: Plugin(props)

@@ -96,6 +96,16 @@ def test_sample_rays_bit_exact(small_scene, oracle, name):
     assert np.array_equal(valid, vc.astype(bool))
     np.testing.assert_array_equal(L, Lc)
     assert np.isfinite(L).all() and (L > 0).any()
+    if name == "path_test":
+        # the RayDifferential3f form of path-mis.py:24-31 (fields .o / .d in
+        # Dr.Jit's (3, N) layout) gives the same lanes
+        class Ray:
+            pass
+
+        r = Ray()
+        r.o, r.d = o.T.copy(), d.T.copy()
+        L2, valid2, _ = integ.sample(small_scene, IndependentSampler(5, lanes, skip=2), r)
+        assert np.array_equal(L2, L) and np.array_equal(valid2, valid)
 
 
 @pytest.mark.parametrize("name", INTEGRATORS)
