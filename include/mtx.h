@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MTX_ABI_VERSION 3
+#define MTX_ABI_VERSION 4
 
 enum {
   MTX_OK = 0,
@@ -109,9 +109,12 @@ typedef struct mtx_camera {
 } mtx_camera;
 
 /* BVH node (64 B): up to 4 children with 8-bit quantised boxes, collapsed
- * from a binned-SAH BVH2 (bvh_build.cpp). Words:
+ * from a binned-SAH BVH2 (bvh_build.cpp); breadth-first, the inner children
+ * of a node consecutive and first in slot order, then its leaves, whose
+ * triangle ranges are consecutive (the device's 48-B node relies on it).
+ * Words:
  *   f[0..2] = origin.xyz (fp32);  w[3] = bytes [ex, ey, ez, n_children],
- *             e* int8: axis scale 2^e
+ *             e* int8 in [-32, 31]: axis scale 2^e
  *   i[4..7] = child refs: >= 0 inner node index,
  *             < 0 leaf: ~c = (first_tri << 3) | (count - 1)
  *   w[8..13] = q_lo.x, q_hi.x, q_lo.y, q_hi.y, q_lo.z, q_hi.z: one byte per
@@ -233,6 +236,12 @@ void mtx_ctx_destroy(mtx_ctx *ctx);
 int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t *tri_vidx, uint32_t n_tris,
                   int32_t *nodes_out, uint32_t *n_nodes_out, float *tri_geom_out, uint32_t *perm_out,
                   uint32_t *depth_out);
+/* Host-only: the 48-B device form of mtx_bvh_build's 64-B nodes (12 words
+ * per node in out; layout at bvh_build.cpp mtx_bvh_device_nodes), which
+ * mtx_scene_upload builds. Fails with MTX_E_ARG unless the nodes follow the
+ * builder's layout (inner children first and consecutive, leaf triangle
+ * ranges consecutive in slot order, exponents in [-32, 31]). */
+int mtx_bvh_device_nodes(const int32_t *nodes, uint32_t n_nodes, uint32_t n_tris, int32_t *out);
 /* Host-only roughplastic precompute (upstream roughplastic constructor):
  * external transmittance table (64 floats) and internal reflectance. */
 int mtx_roughplastic_tables(uint32_t distribution, float alpha, float eta, float *table_out,

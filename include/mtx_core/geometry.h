@@ -68,17 +68,8 @@ MTX_HD float wide_scale(uint32_t e_byte) {
 }
 MTX_HD float wide_decode(float origin, float scale, uint32_t q) { return origin + (float)q * scale; }
 
-// Slab tests of a node's children in the node's quantised frame: with
-// a = 2^e / d and b = (origin - o) / d per axis, a bound q is at
-// t = fma(q, a, b). Children hit within (0, tfar] get the sort key
-// (t bits with the 2 low bits cleared) | slot, misses 0x7f800000 | slot; the
-// four keys are sorted ascending (5 compare-exchanges), so the visit order is
-// by entry distance, near-ties by slot. Returns the number of hits.
-// qlx.. hold the four children's 8-bit bounds, child k in bits [8k, 8k+8).
-// 2^e * x for the int8 exponent in bits [shift, shift + 8) of eb: exact
-// scaling (= wide_scale(e) * x), one v_bfe_i32 + v_ldexp_f32 on the device.
-MTX_HD float wide_axis_scale(uint32_t eb, int shift, float x) {
-  const int e = (int)(int8_t)(uint8_t)((eb >> shift) & 0xffu);
+// 2^e * x, exact (= wide_scale(e) * x): one v_ldexp_f32 on the device.
+MTX_HD float wide_ldexp(float x, int e) {
 #ifdef MTX_DEVICE_COMPILE
   return __builtin_amdgcn_ldexpf(x, e);
 #else
@@ -86,16 +77,25 @@ MTX_HD float wide_axis_scale(uint32_t eb, int shift, float x) {
 #endif
 }
 
-MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint32_t eb, uint32_t qlx,
-                           uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz, float tfar,
-                           uint32_t key[4]) {
-  const int nch = (int)(eb >> 24);
-  const float ax = wide_axis_scale(eb, 0, r.idir.x), bx = (ox - r.o.x) * r.idir.x;
-  const float ay = wide_axis_scale(eb, 8, r.idir.y), by = (oy - r.o.y) * r.idir.y;
-  const float az = wide_axis_scale(eb, 16, r.idir.z), bz = (oz - r.o.z) * r.idir.z;
+// Slab tests of a node's children in the node's quantised frame: with
+// a = 2^e / d and b = (origin - o) / d per axis, a bound q is at
+// t = fma(q, a, b). Children hit within (0, tfar] get the sort key
+// (t bits with the 2 low bits cleared) | slot, misses 0x7f800000 | slot; the
+// four keys are sorted ascending (5 compare-exchanges), so the visit order is
+// by entry distance, near-ties by slot. Returns the number of hits.
+// qlx.. hold the four children's 8-bit bounds, child k in bits [8k, 8k+8).
+// wide_node_order_e takes the axis exponents and child count decoded (the
+// device's 48-B node keeps them in 6-bit fields, mtx_scene_upload).
+MTX_HD int wide_node_order_e(const TraceRay &r, float ox, float oy, float oz, int ex, int ey, int ez, int nch,
+                             uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
+                             float tfar, uint32_t key[4]) {
+  const float ax = wide_ldexp(r.idir.x, ex), bx = (ox - r.o.x) * r.idir.x;
+  const float ay = wide_ldexp(r.idir.y, ey), by = (oy - r.o.y) * r.idir.y;
+  const float az = wide_ldexp(r.idir.z, ez), bz = (oz - r.o.z) * r.idir.z;
   // near / far bound of each axis from the direction's sign: fma(q, a, b)
   // is monotonic in q, so this equals min / max of the two planes (NaN
   // planes of a zero direction component are ignored either way)
+  int n = 0;  // children hit (hit keys sort below every miss key)
   const bool nx_ = r.idir.x < 0.f, ny_ = r.idir.y < 0.f, nz_ = r.idir.z < 0.f;
   const uint32_t qnx = nx_ ? qhx : qlx, qfx = nx_ ? qlx : qhx;
   const uint32_t qny = ny_ ? qhy : qly, qfy = ny_ ? qly : qhy;
@@ -122,6 +122,7 @@ MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint
     const float tmax = fminf(fminf(fminf(fx, fy), fz), tfar);
     const bool hit = k < nch && tmin <= tmax;
     key[k] = hit ? ((f2u(tmin) & 0x7ffffffcu) | (uint32_t)k) : (0x7f800000u | (uint32_t)k);
+    n += hit ? 1 : 0;
   }
 #define MTX_CAS(i, j)                                   \
   {                                                     \
@@ -132,10 +133,17 @@ MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint
   }
   MTX_CAS(0, 1) MTX_CAS(2, 3) MTX_CAS(0, 2) MTX_CAS(1, 3) MTX_CAS(1, 2)
 #undef MTX_CAS
-  int n = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) n += key[k] < 0x7f800000u ? 1 : 0;
   return n;
+}
+
+// The 64-B node form (mtx.h): int8 exponents in eb's bytes 0..2, the child
+// count in byte 3.
+MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint32_t eb, uint32_t qlx,
+                           uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz, float tfar,
+                           uint32_t key[4]) {
+  return wide_node_order_e(r, ox, oy, oz, (int)(int8_t)(uint8_t)(eb & 0xffu), (int)(int8_t)(uint8_t)((eb >> 8) & 0xffu),
+                           (int)(int8_t)(uint8_t)((eb >> 16) & 0xffu), (int)(eb >> 24), qlx, qhx, qly, qhy, qlz, qhz,
+                           tfar, key);
 }
 
 // Child reference of the slot encoded in a sort key.

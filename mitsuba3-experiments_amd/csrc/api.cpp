@@ -315,7 +315,18 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   HIP_TRY(hipSetDevice(c->device));
   int rc = 0;
   hipStream_t st = c->stream;
-  if ((rc = upload(c->nodes, d->nodes, 16ull * d->n_nodes, st))) return rc;
+#ifndef MTX_NODE48
+#define MTX_NODE48 0
+#endif
+  if (MTX_NODE48) {
+    // the device traverses the 48-B node form (bvh_build.cpp mtx_bvh_device_nodes)
+    std::vector<int32_t> n12(12ull * d->n_nodes);
+    if ((rc = mtx_bvh_device_nodes(d->nodes, d->n_nodes, d->n_tris, n12.data()))) return rc;
+    if ((rc = upload(c->nodes, n12.data(), n12.size(), st))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));  // n12 is freed at scope exit
+  } else if ((rc = upload(c->nodes, d->nodes, 16ull * d->n_nodes, st))) {
+    return rc;
+  }
   {
     // device triangles packed to 36 B (the ABI's 48-B records carry 3 pad
     // words): 3.6 instead of 2.7 triangles per 128-B line, same load count

@@ -428,6 +428,52 @@ struct Builder {
   }
 
   bool quant_ok = true;
+  static constexpr int kEMin = -32, kEMax = 31;
+
+  // Device layout (mtx_bvh_device_nodes): nodes in breadth-first order with
+  // the inner children of a node at consecutive indices, a node's slots
+  // ordered inner children first (each group keeps its order), and the
+  // triangles re-ordered so that a node's leaf children are consecutive
+  // ranges in slot order. A child reference is then a base + a small offset.
+  void relayout() {
+    std::vector<int32_t> out(16, 0);
+    std::vector<uint32_t> queue = {0}, tris;
+    tris.reserve(order.size());
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const int32_t *W = &wnodes[16 * (size_t)queue[qi]];
+      int slot[MTX_BVH_WIDTH], m = 0;
+      for (int k = 0; k < (int)((uint32_t)W[3] >> 24); ++k)
+        if (W[4 + k] >= 0) slot[m++] = k;
+      for (int k = 0; k < (int)((uint32_t)W[3] >> 24); ++k) {
+        bool dup = false;  // a one-triangle mesh's root holds its leaf twice
+        for (int j = 0; j < k; ++j) dup = dup || W[4 + j] == W[4 + k];
+        if (W[4 + k] < 0 && !dup) slot[m++] = k;
+      }
+      const int nch = m;
+      int32_t O[16] = {W[0], W[1], W[2], (int32_t)(((uint32_t)W[3] & 0xffffffu) | ((uint32_t)nch << 24)),
+                       0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int a = 0; a < 6; ++a) {
+        uint32_t q = 0;
+        for (int j = 0; j < nch; ++j) q |= (((uint32_t)W[8 + a] >> (8 * slot[j])) & 255u) << (8 * j);
+        O[8 + a] = (int32_t)q;
+      }
+      for (int j = 0; j < nch; ++j) {
+        const int32_t r = W[4 + slot[j]];
+        if (r >= 0) {
+          O[4 + j] = (int32_t)queue.size();
+          queue.push_back((uint32_t)r);
+        } else {
+          const uint32_t code = ~(uint32_t)r, first = code >> 3, cnt = (code & 7u) + 1u;
+          O[4 + j] = ~(int32_t)(((uint32_t)tris.size() << 3) | (cnt - 1u));
+          for (uint32_t t = 0; t < cnt; ++t) tris.push_back(order[first + t]);
+        }
+      }
+      out.resize(16 * queue.size(), 0);
+      std::memcpy(&out[16 * qi], O, sizeof(O));
+    }
+    wnodes.swap(out);
+    order.swap(tris);
+  }
 
   bool encode(uint32_t w, const std::vector<Child> &ch, const int32_t *refs) {
     Box u;
@@ -439,13 +485,14 @@ struct Builder {
     for (int a = 0; a < 3; ++a) {
       const float org = u.lo[a];
       const double ext = (double)u.hi[a] - (double)org;
-      int e = -126;
+      // exponents stay in [kEMin, kEMax]: the device node keeps them in 6 bits
+      int e = kEMin;
       if (ext > 0.0) {
         int ee;
         std::frexp(ext / 255.0, &ee);
-        e = std::max(-126, std::min(127, ee));
+        e = std::max(kEMin, std::min(kEMax, ee));
       }
-      while (e < 127 && mtx::wide_decode(org, mtx::wide_scale((uint32_t)(e & 255)), 255u) < u.hi[a]) ++e;
+      while (e < kEMax && mtx::wide_decode(org, mtx::wide_scale((uint32_t)(e & 255)), 255u) < u.hi[a]) ++e;
       const float sc = mtx::wide_scale((uint32_t)(e & 255));
       const double dsc = std::ldexp(1.0, e);
       for (size_t k = 0; k < ch.size(); ++k) {
@@ -561,6 +608,11 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     mtx_set_error("mtx_bvh_build: child box quantisation failed (non-finite or huge coordinates?)");
     return MTX_E_ARG;
   }
+  b.relayout();
+  if (b.order.size() != n_tris) {
+    mtx_set_error("mtx_bvh_build: internal error (%zu triangles after the relayout for %u)", b.order.size(), n_tris);
+    return MTX_E_ARG;
+  }
   uint32_t n_nodes = (uint32_t)(b.wnodes.size() / 16);
   std::memcpy(nodes_out, b.wnodes.data(), b.wnodes.size() * sizeof(int32_t));
   *n_nodes_out = n_nodes;
@@ -576,6 +628,64 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     g[8] = p2[0] - p0[0]; g[9] = p2[1] - p0[1]; g[10] = p2[2] - p0[2]; g[11] = 0.f;
   }
   if (depth_out) *depth_out = b.wide_depth;
+  return MTX_OK;
+}
+
+// Device form of the nodes (48 B, three dwordx4 loads per visit instead of
+// four): the 64-B node's four child references become two bases and a 24-bit
+// field of per-slot leaf ends, which the builder's layout (relayout) makes
+// sufficient: inner children first, at node_base + slot; leaf slots' triangle
+// ranges consecutive from tri_base, slot k ending at tri_base + end_k. Words:
+//   0..2 origin | 3: ex, ey, ez (6-bit two's complement), nch - 1 (2 bits),
+//   ends[0..11] | 4: node_base (24 bits), ends[12..19] | 5: tri_base (24 bits),
+//   ends[20..23] | 6..11: the quantised bounds (unchanged).
+extern "C" int mtx_bvh_device_nodes(const int32_t *nodes, uint32_t n_nodes, uint32_t n_tris, int32_t *out) {
+  if (!nodes || !out || n_nodes == 0) {
+    mtx_set_error("mtx_bvh_device_nodes: null argument or no nodes");
+    return MTX_E_ARG;
+  }
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    const int32_t *W = nodes + 16 * (size_t)i;
+    const uint32_t eb = (uint32_t)W[3], nch = eb >> 24;
+    auto fail = [&](const char *why) {
+      mtx_set_error("mtx_bvh_device_nodes: node %u %s (build the BVH with mtx_bvh_build)", i, why);
+      return MTX_E_ARG;
+    };
+    if (nch < 1 || nch > MTX_BVH_WIDTH) return fail("has a bad child count");
+    uint32_t ex[3];
+    for (int a = 0; a < 3; ++a) {
+      const int e = (int)(int8_t)(uint8_t)((eb >> (8 * a)) & 0xffu);
+      if (e < -32 || e > 31) return fail("has an axis exponent outside [-32, 31]");
+      ex[a] = (uint32_t)e & 63u;
+    }
+    uint32_t node_base = 0, tri_base = 0, run = 0, ends[4] = {0, 0, 0, 0};
+    bool leaf_seen = false;
+    for (uint32_t k = 0; k < nch; ++k) {
+      const int32_t r = W[4 + k];
+      if (r >= 0) {
+        if (leaf_seen) return fail("has an inner child after a leaf");
+        if (k == 0) node_base = (uint32_t)r;
+        if ((uint32_t)r != node_base + k || (uint32_t)r >= n_nodes) return fail("has non-consecutive inner children");
+      } else {
+        const uint32_t code = ~(uint32_t)r, first = code >> 3, cnt = (code & 7u) + 1u;
+        if (!leaf_seen) tri_base = first;
+        leaf_seen = true;
+        if (first != tri_base + run || (uint64_t)first + cnt > n_tris) return fail("has non-consecutive leaf triangles");
+        run += cnt;
+        ends[k] = run;
+      }
+    }
+    if (node_base >= (1u << 24) || tri_base >= (1u << 24)) return fail("has a base beyond 2^24");
+    const uint32_t E = ends[0] | ends[1] << 6 | ends[2] << 12 | ends[3] << 18;
+    int32_t *O = out + 12 * (size_t)i;
+    O[0] = W[0];
+    O[1] = W[1];
+    O[2] = W[2];
+    O[3] = (int32_t)(ex[0] | ex[1] << 6 | ex[2] << 12 | (nch - 1u) << 18 | (E & 0xfffu) << 20);
+    O[4] = (int32_t)(node_base | ((E >> 12) & 0xffu) << 24);
+    O[5] = (int32_t)(tri_base | ((E >> 20) & 0xfu) << 24);
+    for (int a = 0; a < 6; ++a) O[6 + a] = W[8 + a];
+  }
   return MTX_OK;
 }
 

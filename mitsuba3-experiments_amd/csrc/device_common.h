@@ -237,18 +237,54 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// One visit of a 4-wide node (mtx.h layout): four loads (the last one 8 B)
-// and mtx_core/geometry.h wide_node_order. Returns the number of children
-// hit; key[0..n) in visit order, rf the child references.
+// Child reference of the slot in a sort key, from the 48-B device node's
+// bases and per-slot leaf ends (bvh_build.cpp mtx_bvh_device_nodes): end 0 =
+// inner child node_base + slot; else the leaf of triangles [tri_base +
+// end_{slot-1}, tri_base + end_slot), as the 64-B node's ~(first << 3 | count - 1).
+__device__ __forceinline__ int32_t wide_dref(uint32_t key, uint32_t ends, uint32_t node_base, uint32_t tri_base) {
+  const uint32_t sh = (key & 3u) * 6u;
+  const uint32_t e1 = __builtin_amdgcn_ubfe(ends, sh, 6), e0 = __builtin_amdgcn_ubfe(ends << 6, sh, 6);
+  const int32_t leaf = ~(int32_t)(((tri_base + e0) << 3) | (e1 - e0 - 1u));
+  return e1 == 0u ? (int32_t)(node_base + (key & 3u)) : leaf;
+}
+
+// One visit of a 4-wide node in its 48-B device form: three 16-B loads and
+// mtx_core/geometry.h wide_node_order_e. Returns the number of children hit;
+// c[0..n) are their references in visit order (the same order and refs as
+// the 64-B node gives the oracle).
+#ifndef MTX_NODE48
+#define MTX_NODE48 0  // A/B: 1 = the 48-B node (three loads, references decoded): slower, DESIGN.md
+#endif
 __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
-                                          int4 &rf, uint32_t key[4]) {
-  const int4 *np = s.nodes + 4 * node;
-  const float4 a = __builtin_bit_cast(float4, np[0]);
-  rf = np[1];
-  const int4 qa = np[2];
-  const int2 qb = *reinterpret_cast<const int2 *>(np + 3);
-  return wide_node_order(r, a.x, a.y, a.z, __float_as_uint(a.w), (uint32_t)qa.x, (uint32_t)qa.y, (uint32_t)qa.z,
-                         (uint32_t)qa.w, (uint32_t)qb.x, (uint32_t)qb.y, tbest, key);
+                                          int32_t c[4]) {
+#if !MTX_NODE48
+  {
+    const int4 *np = s.nodes + 4 * node;
+    const int4 a = np[0], rf = np[1], qa = np[2];
+    const int2 qb = *reinterpret_cast<const int2 *>(np + 3);
+    uint32_t key[4];
+    const int n = wide_node_order(r, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z), (uint32_t)a.w,
+                                  (uint32_t)qa.x, (uint32_t)qa.y, (uint32_t)qa.z, (uint32_t)qa.w, (uint32_t)qb.x,
+                                  (uint32_t)qb.y, tbest, key);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[i] = wide_ref(key[i], rf.x, rf.y, rf.z, rf.w);
+    return n;
+  }
+#endif
+  const int4 *np = s.nodes + 3 * node;
+  const int4 a = np[0], b = np[1], q = np[2];
+  const uint32_t w3 = (uint32_t)a.w, w4 = (uint32_t)b.x, w5 = (uint32_t)b.y;
+  uint32_t key[4];
+  const int n = wide_node_order_e(r, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z),
+                                  __builtin_amdgcn_sbfe((int)w3, 0, 6), __builtin_amdgcn_sbfe((int)w3, 6, 6),
+                                  __builtin_amdgcn_sbfe((int)w3, 12, 6), (int)__builtin_amdgcn_ubfe(w3, 18, 2) + 1,
+                                  (uint32_t)b.z, (uint32_t)b.w, (uint32_t)q.x, (uint32_t)q.y, (uint32_t)q.z,
+                                  (uint32_t)q.w, tbest, key);
+  const uint32_t ends = (w3 >> 20) | ((w4 >> 24) << 12) | ((w5 >> 24) << 20);
+  const uint32_t nb = w4 & 0xffffffu, tb = w5 & 0xffffffu;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = wide_dref(key[i], ends, nb, tb);
+  return n;
 }
 
 // ---------------------------------------------------------------------------
@@ -263,18 +299,17 @@ __device__ __forceinline__ bool traverse(const DevScene &s, int32_t *stk, const 
   bool hit_any = false;
   while (true) {
     if (node >= 0) {
-      int4 rf;
-      uint32_t key[4];
+      int32_t cr[4];
       ++nv;
-      const int n = wide_visit(s, r, node, tbest, rf, key);
+      const int n = wide_visit(s, r, node, tbest, cr);
       if (n > 0) {
 #pragma unroll
         for (int rr = 3; rr >= 1; --rr)
           if (rr < n) {
-            stk[sp * kTraceBlock] = wide_ref(key[rr], rf.x, rf.y, rf.z, rf.w);
+            stk[sp * kTraceBlock] = cr[rr];
             ++sp;
           }
-        node = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
+        node = cr[0];
         continue;
       }
     } else {
@@ -474,17 +509,14 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
           const uint64_t m = __ballot(true);
           if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[0];
         }
-        int4 rf;
-        uint32_t key[4];
+        int32_t cr[4];
         ++nv;
-        const int n = wide_visit(s, r, node, tbest, rf, key);
+        const int n = wide_visit(s, r, node, tbest, cr);
         if (n > 0) {
           // far children pushed farthest first: entries sp .. sp+n-2 hold
-          // key[n-1] .. key[1]. Branch-free: three stores, the ones beyond
+          // cr[n-1] .. cr[1]. Branch-free: three stores, the ones beyond
           // the new top are dead (capacity 3*depth+1 covers them).
-          const int32_t c1 = wide_ref(key[1], rf.x, rf.y, rf.z, rf.w);
-          const int32_t c2 = wide_ref(key[2], rf.x, rf.y, rf.z, rf.w);
-          const int32_t c3 = wide_ref(key[3], rf.x, rf.y, rf.z, rf.w);
+          const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
           const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
           if (!MTX_PUSH_BRANCHY && sp + 3 <= lds_n) {
             stk[sp * kTraceBlock] = e0;
@@ -503,7 +535,7 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
               }
           }
           sp += n - 1;
-          node = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
+          node = cr[0];
         } else {
           node = pop(sp);
         }
@@ -686,14 +718,11 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         const uint64_t m = __ballot(true);
         if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[0];
       }
-      int4 rf;
-      uint32_t key[4];
+      int32_t cr[4];
       ++nv;
-      const int n = wide_visit(s, r, node, tbest, rf, key);
+      const int n = wide_visit(s, r, node, tbest, cr);
       if (n > 0) {
-        const int32_t c1 = wide_ref(key[1], rf.x, rf.y, rf.z, rf.w);
-        const int32_t c2 = wide_ref(key[2], rf.x, rf.y, rf.z, rf.w);
-        const int32_t c3 = wide_ref(key[3], rf.x, rf.y, rf.z, rf.w);
+        const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
         const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
         if (sp + 3 <= lds_n) {
           stk[sp * kTraceBlock] = e0;
@@ -712,7 +741,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
             }
         }
         sp += n - 1;
-        const int32_t c0 = wide_ref(key[0], rf.x, rf.y, rf.z, rf.w);
+        const int32_t c0 = cr[0];
         if (c0 >= 0) {
           node = c0;
         } else {

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 3
+MTX_ABI_VERSION = 4
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -259,6 +259,7 @@ EXPORTS = [
     "mtx_ctx_create",
     "mtx_ctx_destroy",
     "mtx_bvh_build",
+    "mtx_bvh_device_nodes",
     "mtx_roughplastic_tables",
     "mtx_scene_upload",
     "mtx_render",

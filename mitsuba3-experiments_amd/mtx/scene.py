@@ -270,6 +270,7 @@ class Scene:
         self.tri_geom = geom
         self.tri_vidx = np.ascontiguousarray(tri_vidx.reshape(-1, 3)[perm].reshape(-1))
         self.tri_shape = np.ascontiguousarray(tri_shape[perm])
+        self.tri_perm = perm  # input triangle of each leaf-order triangle
         self.n_tris = n
         self.bvh_depth = depth.value
 

@@ -271,16 +271,21 @@ def test_training_reduces_loss(nscene):
     tr = FieldTrainer(nscene, field, batch_size=2048, M=8)
     val = Integrator(field, batch_size=4096, M=64)
 
+    # The residual is (LHS - RHS)^2 with a Monte-Carlo RHS: its floor is the
+    # M = 64 RHS variance of the batch's points. A batch holding a few
+    # high-variance points (seeds 900001/900002: floor ~0.53 of an initial
+    # 0.58-0.71 for field seeds 2-5, tools/nerad_train_probe.py) hides the
+    # fit; this one starts at 0.09-0.23 and falls 2-5x in 60 steps.
     def residual():
-        lhs = tr.isampler.sample(900001, 4096, ctx=tr.ctx)
-        rhs = val.sample_rhs(nscene, tr.isampler, 900001, 900002, ctx=tr.ctx)
+        lhs = tr.isampler.sample(123457, 4096, ctx=tr.ctx)
+        rhs = val.sample_rhs(nscene, tr.isampler, 123457, 123458, ctx=tr.ctx)
         return float(np.mean((val.sample_lhs(nscene, lhs, ctx=tr.ctx) - rhs) ** 2))
 
     before = residual()
     losses = [tr.step()["loss"] for _ in range(60)]
     after = residual()
     assert np.isfinite(losses).all()
-    assert after < 0.7 * before, (before, after, losses)
+    assert after < 0.5 * before, (before, after, losses)
     tab, ws = tr.params()
     rng = np.random.default_rng(3)
     v = np.asarray(nscene.vpos, np.float32).reshape(-1, 3)

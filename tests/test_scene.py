@@ -128,6 +128,50 @@ def _check_bvh(nodes, tri_geom, n_tris, bvh_depth):
         boxes[i] = (blo, bhi)
     assert (seen == 1).all() or ((seen >= 1).all() and n_tris == 1)
     assert max_depth <= 40 and max_depth == bvh_depth
+    _check_device_nodes(nodes, n_tris)
+
+
+def _check_device_nodes(nodes, n_tris):
+    """The builder's layout (mtx.h) and the 48-B device form decoded here in
+    numpy (bvh_build.cpp mtx_bvh_device_nodes; device_common.h wide_dref)
+    give every child reference of the 64-B node."""
+    import ctypes as C
+
+    from mtx import _lib
+
+    u = nodes.view(np.uint32)
+    for i in range(len(nodes)):
+        nch = int(u[i, 3] >> 24)
+        refs = [int(nodes[i, 4 + k]) for k in range(nch)]
+        n_in = sum(r >= 0 for r in refs)
+        assert all(r >= 0 for r in refs[:n_in]) and all(r < 0 for r in refs[n_in:])  # inner first
+        assert refs[:n_in] == list(range(refs[0], refs[0] + n_in)) if n_in else True
+        first = [(~r) >> 3 for r in refs[n_in:]]
+        cnt = [((~r) & 7) + 1 for r in refs[n_in:]]
+        assert all(first[j + 1] == first[j] + cnt[j] for j in range(len(first) - 1))
+        assert all(-32 <= np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)) <= 31 for a in range(3))
+    L = _lib.lib()
+    out = np.zeros((len(nodes), 12), np.int32)
+    assert L.mtx_bvh_device_nodes(np.ascontiguousarray(nodes).ctypes.data, len(nodes), n_tris, out.ctypes.data) == 0
+    w = out.view(np.uint32)
+    assert np.array_equal(out[:, 0:3], nodes[:, 0:3]) and np.array_equal(out[:, 6:12], nodes[:, 8:14])
+    ends = (w[:, 3] >> 20) | ((w[:, 4] >> 24) << 12) | ((w[:, 5] >> 24) << 20)
+    nb, tb = w[:, 4] & 0xFFFFFF, w[:, 5] & 0xFFFFFF
+    for i in range(len(nodes)):
+        nch = int((w[i, 3] >> 18) & 3) + 1
+        assert nch == int(u[i, 3] >> 24)
+        for a in range(3):
+            e6 = int((w[i, 3] >> (6 * a)) & 63)
+            assert (e6 - 64 if e6 >= 32 else e6) == int(np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)))
+        for k in range(nch):
+            e1 = int(ends[i] >> (6 * k)) & 63
+            e0 = int((int(ends[i]) << 6) >> (6 * k)) & 63
+            ref = int(nb[i]) + k if e1 == 0 else ~(((int(tb[i]) + e0) << 3) | (e1 - e0 - 1))
+            assert ref == int(nodes[i, 4 + k]), (i, k)
+    bad = nodes.copy()
+    bad[0, 4], bad[0, 5] = bad[0, 5], bad[0, 4]  # slot order broken
+    if int(u[0, 3] >> 24) >= 2 and bad[0, 4] != nodes[0, 4]:
+        assert L.mtx_bvh_device_nodes(bad.ctypes.data, len(bad), n_tris, out.ctypes.data) != 0
 
 
 def test_bvh_closest_hit_equals_brute_force(small_scene, oracle):
