@@ -608,7 +608,10 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     mtx_set_error("mtx_bvh_build: child box quantisation failed (non-finite or huge coordinates?)");
     return MTX_E_ARG;
   }
-  b.relayout();
+  // MTX_BVH_RELAYOUT=0 keeps the collapse's depth-first order (A/B only: the
+  // 48-B device node form needs the breadth-first layout)
+  const char *rl = getenv("MTX_BVH_RELAYOUT");
+  if (!rl || atoi(rl) != 0) b.relayout();
   if (b.order.size() != n_tris) {
     mtx_set_error("mtx_bvh_build: internal error (%zu triangles after the relayout for %u)", b.order.size(), n_tris);
     return MTX_E_ARG;
