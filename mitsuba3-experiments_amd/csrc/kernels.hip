@@ -241,7 +241,12 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   const float4 ro = b.ray_o[path], rd = b.ray_d[path];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
   const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
-  const float4 pv = bounce == 0 ? kInitPrev : b.prev[path];
+  // prev (previous vertex, NRC spread): path-mis / path read it only for the
+  // emission MIS of an emitter hit (pdf_emitter_direction is 0 otherwise), so
+  // they load it below once the hit's emitter is known
+  constexpr bool kPrevOnEmitter = INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH;
+  float4 pv = kInitPrev;
+  if (!kPrevOnEmitter && bounce != 0) pv = b.prev[path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -251,10 +256,11 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   float eta = th.w;
   V3 L = V3{Lr.x, Lr.y, Lr.z};
   float prev_pdf = Lr.w;
-  V3 prev_p = V3{pv.x, pv.y, pv.z};
-  float spread = pv.w, a0 = rd.w;
   const V3 ray_d = V3{rd.x, rd.y, rd.z};
   const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
+  if (kPrevOnEmitter && bounce != 0 && si.emitter >= 0) pv = b.prev[path];
+  V3 prev_p = V3{pv.x, pv.y, pv.z};
+  float spread = pv.w, a0 = rd.w;
   io.emit = false;
   io.query = false;
 
@@ -263,9 +269,12 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   if (INT == MTX_INT_PATH_MIS) {
     // Direct emission with MIS against the previous BSDF sample (:75-86)
     const bool prev_delta = (flags & PF_PREV_DELTA) != 0;
-    const V3 rel = si.p - prev_p;
-    const float dist = norm(rel);
-    const float em_pdf = prev_delta ? 0.f : pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    float em_pdf = 0.f;
+    if (!prev_delta && si.emitter >= 0) {
+      const V3 rel = si.p - prev_p;
+      const float dist = norm(rel);
+      em_pdf = pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    }
     const float mis_bsdf = mis_weight_b(prev_pdf, em_pdf);
     const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
     L = fma3v(T, le * mis_bsdf, L);
@@ -297,9 +306,12 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     }
     // path.py:283-300 / nrc.py:79-100: emission of the BSDF-sampled hit
     const bool bsdf_delta = (flags & PF_PREV_DELTA) != 0;
-    const V3 rel = si.p - prev_p;
-    const float dist = norm(rel);
-    const float em_pdf = bsdf_delta ? 0.f : pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    float em_pdf = 0.f;
+    if (!bsdf_delta && si.emitter >= 0) {
+      const V3 rel = si.p - prev_p;
+      const float dist = norm(rel);
+      em_pdf = pdf_emitter_direction(sv, si.emitter, rel / dist, dist, si.sh.n);
+    }
     const float mis_bsdf =
         INT == MTX_INT_PATH ? mis_weight_a(prev_pdf, em_pdf) : mis_weight_b(prev_pdf, em_pdf);
     const V3 le = (prev_pdf > 0.f) ? emitter_eval(sv, si.emitter, si.wi) : v3s(0.f);
@@ -334,7 +346,13 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   }
 
   // ------------------------------ body ------------------------------------
+#if MTX_DIAG_DIFFUSE  // timing diagnostic only (wrong images): every material diffuse
+  mtx_material mat = sv.materials[si.material];
+  mat.type = MTX_MAT_DIFFUSE;
+  mat.flags = MTX_MF_TWOSIDED;
+#else
   const mtx_material mat = sv.materials[si.material];
+#endif
   const bool smooth = (bsdf_flags(mat) & BF_SMOOTH) != 0;
   bool active_em = (INT == MTX_INT_PATH_MIS ? active_next : true) && smooth;
   const V2 u_em = rng.next_2d();

@@ -217,7 +217,19 @@ __global__ void k_minmax(const float *__restrict__ p, uint64_t n3, float2 *parti
   float lo = INFINITY, hi = -INFINITY;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float4 *p4 = reinterpret_cast<const float4 *>(p);  // 256-B aligned device buffer
-  for (uint64_t i = t0; i < n3 / 4; i += stride) {
+  const uint64_t n4 = n3 / 4;
+  uint64_t i = t0;
+  for (; i + 3 * stride < n4; i += 4 * stride) {  // four loads in flight per thread
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = p4[i + k * stride];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lo = fminf(lo, fminf(fminf(v[k].x, v[k].y), fminf(v[k].z, v[k].w)));
+      hi = fmaxf(hi, fmaxf(fmaxf(v[k].x, v[k].y), fmaxf(v[k].z, v[k].w)));
+    }
+  }
+  for (; i < n4; i += stride) {
     const float4 v = p4[i];
     lo = fminf(lo, fminf(fminf(v.x, v.y), fminf(v.z, v.w)));
     hi = fmaxf(hi, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
