@@ -1059,7 +1059,9 @@ __global__ void k_mlt_init(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   if (i >= p.n_paths) return;
   const Pcg32 rng = sampler_lane(p.seed, p.px0 * p.spp + i);
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
-  b.mlt_cur[i] = make_float4(0.5f, 0.5f, 0.f, 0.f);  // offset = 0.5, cumulative_weight = 0 (:198-200)
+  // offset = 0.5, cumulative_weight = 0 (:198-200); w: vertex depths that may
+  // differ between the proposed and current buffers (k_mlt_end)
+  b.mlt_cur[i] = make_float4(0.5f, 0.5f, 0.f, 0.f);
   b.mlt_L[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (uint32_t d = 0; d < max_depth; ++d) {
     b.vpath[(size_t)d * b.capacity + i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1125,17 +1127,25 @@ __global__ void k_mlt_end(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   } else {
     cur.z += 1.f - a;
   }
+  // The reference copies all max_depth proposed vertices on acceptance
+  // (dr.tile(accept, max_depth), :155-158). A proposal writes depths
+  // 0..depth only (its final depth is in misc), so the two vertex buffers can
+  // differ only below the largest such bound since the chain's last
+  // acceptance (cur.w): copying those depths gives the same current path.
+  uint32_t dirty = max((uint32_t)cur.w, min(max_depth, (mi.w & 0xffffu) + 1u));
   if (accept) {
     const float2 po = b.mlt_prop[i];
     cur.x = po.x;
     cur.y = po.y;
     b.mlt_L[i] = make_float4(Lp.x, Lp.y, Lp.z, 0.f);
-    for (uint32_t d = 0; d < max_depth; ++d)
+    for (uint32_t d = 0; d < dirty; ++d)
       b.vpath[(size_t)d * b.capacity + i] = b.vprop[(size_t)d * b.capacity + i];
     if (p.integrator == MTX_INT_PSSMLT_PATH)
-      for (uint32_t d = 0; d < max_depth; ++d)
+      for (uint32_t d = 0; d < dirty; ++d)
         b.vpath_es[(size_t)d * b.capacity + i] = b.vprop_es[(size_t)d * b.capacity + i];
+    dirty = 0;
   }
+  cur.w = (float)dirty;
   b.mlt_cur[i] = cur;
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
 }
