@@ -47,7 +47,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured 
 # workgroup, served from the XCD's L2: 16.8-18.8 TB/s chip-wide (upper end).
 L2_GATHER_PEAK_GBS = 18800.0
 L2_STREAM_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate
-NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES, OCC_BYTES = 64, 48, 32, 16, 4
+# node and triangle records as the device reads them (triangles packed to 36 B, mtx_scene_upload)
+NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES, OCC_BYTES = 64, 36, 32, 16, 4
 # SURVEY §8d wavefront path state per lane per bounce, read + written
 SHADE_BYTES_PER_PATH_BOUNCE = 2 * 108 + 32
 
