@@ -138,8 +138,7 @@ struct mtx_ctx {
   uint32_t trace_batch = 256;
   uint32_t refill_lanes = 16;
   uint32_t urefill = 16;
-  uint32_t tri_min = 0;
-  bool trace_pair = false;  // MTX_TRACE_PAIR: shadow rays of bounce b with the closest hits of b + 1  // trace_loop_u: triangle step deferred until this many lanes wait on one
+  uint32_t tri_min = 0;  // trace_loop_u: triangle step deferred until this many lanes wait on one
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
@@ -194,7 +193,6 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_TRACE_PAIR")) c->trace_pair = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRI_MIN")) c->tri_min = (uint32_t)std::max(0, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
@@ -651,17 +649,6 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
   // nerad RHS lanes start at their surface point (no bounce-0 trace) and
   // trace NEE rays at that point only
   const bool nerad = p.integrator == MTX_INT_NERAD_RHS, nerad_render = p.integrator == MTX_INT_NERAD;
-  // MTX_TRACE_PAIR: a bounce's shadow rays are traced in one launch with the
-  // next bounce's closest-hit rays (k_trace_pair); not with the visit counters
-  const bool pair = c->trace_pair && !p.stats && !nerad && !nerad_render && p.integrator != MTX_INT_PSSMLT_SIMPLE &&
-                    p.integrator != MTX_INT_SIMPLE;
-  bool shadow_pending = false;
-  auto flush_shadow = [&](uint32_t sb) {
-    hipEvent_t e = tm.begin(1);
-    mtxd::launch_trace_shadow(s, b, sb, p.stats, c->trace_grid, c->stream);
-    tm.end(1, e);
-    ++*n_shadow;
-  };
   for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
     hipEvent_t e;
     // past its second vertex the nerad RHS chain only continues through
@@ -669,14 +656,7 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     // an eighth of the persistent grid (dispatching the full grid of
     // immediately-exiting blocks costs more than the work)
     const int div = (nerad && bounce >= 2) ? 8 : 1;
-    if (shadow_pending) {  // closest hits of this bounce + the previous bounce's shadow rays
-      e = tm.begin(0);
-      mtxd::launch_trace_pair(s, b, bounce, c->trace_grid, c->stream);
-      tm.end(0, e);
-      ++*n_trace;
-      ++*n_shadow;
-      shadow_pending = false;
-    } else if (!(nerad && bounce == 0)) {
+    if (!(nerad && bounce == 0)) {
       e = tm.begin(0);
       mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), c->stream);
       tm.end(0, e);
@@ -687,10 +667,10 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     tm.end(2, e);
     if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
         !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays
-      if (pair && bounce + 1 < depth_iters)
-        shadow_pending = true;
-      else
-        flush_shadow(bounce);
+      e = tm.begin(1);
+      mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
+      tm.end(1, e);
+      ++*n_shadow;
     }
     // Deep paths (max_depth 65, scene.xml:6): stop launching once the queue
     // has drained (checked every 8 bounces).
@@ -698,14 +678,9 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
       uint32_t cnt = 0;
       hipMemcpyAsync(&cnt, b.counters + 4 * (bounce + 1), 4, hipMemcpyDeviceToHost, c->stream);
       hipStreamSynchronize(c->stream);
-      if (cnt == 0) {
-        if (shadow_pending) flush_shadow(bounce);
-        shadow_pending = false;
-        break;
-      }
+      if (cnt == 0) break;
     }
   }
-  if (shadow_pending) flush_shadow(depth_iters - 1);
 }
 
 int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_t n_trace, uint64_t n_shadow,

@@ -127,21 +127,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_shadow(DevScene s, WaveBu
   }
 }
 
-// The closest-hit rays of bounce `bounce` and then the shadow rays of bounce
-// - 1 in one persistent launch (MTX_TRACE_PAIR): the two are independent
-// (hit records vs L), so waves done with the closest-hit queue continue on
-// the shadow queue instead of idling through the kernel's tail.
-__global__ __launch_bounds__(kTraceBlock) void k_trace_pair(DevScene s, WaveBuffers b, uint32_t bounce) {
-  extern __shared__ int32_t stack[];
-  uint32_t nv = 0, tv = 0, nr = 0;
-  const ClosestSrc src{b, b.queue[bounce & 1]};
-  trace_loop<false>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, stack + threadIdx.x,
-                    nv, tv, nr);
-  const ShadowSrc ssrc{b};
-  trace_loop<true>(s, ssrc, b.counters[4 * bounce + 1], b.xheads + (2 * (bounce - 1) + 1) * kXSlotWords,
-                   stack + threadIdx.x, nv, tv, nr);
-}
-
 // ---------------------------------------------------------------------------
 // Ray generation
 // ---------------------------------------------------------------------------
@@ -1226,9 +1211,6 @@ void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounc
     hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
   else
     hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
-}
-void launch_trace_pair(const DevScene &s, const WaveBuffers &b, uint32_t bounce, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_trace_pair, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
 }
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
                   hipStream_t st) {

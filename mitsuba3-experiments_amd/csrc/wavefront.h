@@ -164,7 +164,6 @@ void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t boun
                           hipStream_t st);
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st);
-void launch_trace_pair(const DevScene &s, const WaveBuffers &b, uint32_t bounce, int grid, hipStream_t st);
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
                   hipStream_t st);
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
