@@ -42,11 +42,6 @@ struct BsdfData {
   const float *tables;
 };
 
-// Rough microfacet base BSDF (the device shades these in a second pass).
-MTX_HD bool bsdf_is_rough(const mtx_material &m) {
-  return m.type == MTX_MAT_ROUGHPLASTIC || m.type == MTX_MAT_ROUGHCONDUCTOR || m.type == MTX_MAT_ROUGHDIELECTRIC;
-}
-
 MTX_HD uint32_t bsdf_flags(const mtx_material &m) {
   uint32_t f = 0;
   switch (m.type) {
@@ -144,16 +139,10 @@ MTX_HD void roughplastic_eval_pdf(const BsdfData &d, const mtx_material &m, V2 u
 }
 
 // eval + pdf together (upstream eval_pdf)
-// ROUGH = false compiles the rough microfacet cases out (the device's first
-// shade pass, which never sees those materials); the oracle uses the default.
-template <bool ROUGH = true>
 MTX_HD void base_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
   float ci = wi.z, co = wo.z;
   *val = v3s(0.f);
   *pdf = 0.f;
-  if (!ROUGH && (m.type == MTX_MAT_ROUGHPLASTIC || m.type == MTX_MAT_ROUGHCONDUCTOR ||
-                 m.type == MTX_MAT_ROUGHDIELECTRIC))
-    return;
   switch (m.type) {
     case MTX_MAT_DIFFUSE: {
       if (ci > 0.f && co > 0.f) {
@@ -164,10 +153,9 @@ MTX_HD void base_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
       break;
     }
     case MTX_MAT_ROUGHPLASTIC:
-      if constexpr (ROUGH) roughplastic_eval_pdf(d, m, uv, wi, wo, val, pdf);
+      roughplastic_eval_pdf(d, m, uv, wi, wo, val, pdf);
       break;
     case MTX_MAT_ROUGHCONDUCTOR: {
-      if constexpr (!ROUGH) break;
       if (!(ci > 0.f && co > 0.f)) break;
       Microfacet distr = mat_distr(m);
       V3 H = normalize(wo + wi);
@@ -185,7 +173,6 @@ MTX_HD void base_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
       break;
     }
     case MTX_MAT_ROUGHDIELECTRIC: {
-      if constexpr (!ROUGH) break;
       if (ci == 0.f) break;
       Microfacet distr = mat_distr(m);
       bool refl = ci * co > 0.f;
@@ -218,7 +205,6 @@ MTX_HD void base_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
   }
 }
 
-template <bool ROUGH = true>
 MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
   float ci = wi.z;
   bs->wo = v3s(0.f);
@@ -229,11 +215,11 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
   // The rough materials draw their microfacet normal in one shared call (one
   // inlined copy of the visible-normal sampler instead of three); same inputs,
   // same arithmetic as calling it inside each case.
-  bool need_mf = ROUGH && (m.type == MTX_MAT_ROUGHCONDUCTOR || m.type == MTX_MAT_ROUGHDIELECTRIC);
+  bool need_mf = m.type == MTX_MAT_ROUGHCONDUCTOR || m.type == MTX_MAT_ROUGHDIELECTRIC;
   V3 wi_mf = m.type == MTX_MAT_ROUGHDIELECTRIC ? mulsign3(wi, ci) : wi;
   float rp_prob_specular = 0.f;
   bool rp_specular = false;
-  if (ROUGH && m.type == MTX_MAT_ROUGHPLASTIC && ci > 0.f) {
+  if (m.type == MTX_MAT_ROUGHPLASTIC && ci > 0.f) {
     const float *tab = d.tables + m.table;
     float t_i = lerp_table(tab, ci);
     float prob_specular = (1.f - t_i) * m.spec_weight;
@@ -244,9 +230,7 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
   }
   float mf_pdf = 0.f;
   V3 mf_n = v3s(0.f);
-  if constexpr (ROUGH) {
-    if (need_mf) mf_n = mat_distr(m).sample(wi_mf, u2, &mf_pdf);
-  }
+  if (need_mf) mf_n = mat_distr(m).sample(wi_mf, u2, &mf_pdf);
   switch (m.type) {
     case MTX_MAT_DIFFUSE: {
       bs->wo = square_to_cosine_hemisphere(u2);
@@ -282,7 +266,6 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
       break;
     }
     case MTX_MAT_ROUGHCONDUCTOR: {
-      if constexpr (!ROUGH) break;
       Microfacet distr = mat_distr(m);
       float pdf = mf_pdf;
       V3 mn = mf_n;
@@ -300,7 +283,6 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
       break;
     }
     case MTX_MAT_ROUGHDIELECTRIC: {
-      if constexpr (!ROUGH) break;
       Microfacet distr = mat_distr(m);
       float pdf = mf_pdf;
       V3 mn = mf_n;
@@ -330,7 +312,6 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
       break;
     }
     case MTX_MAT_ROUGHPLASTIC: {
-      if constexpr (!ROUGH) break;
       if (!(ci > 0.f)) break;
       bs->eta = 1.f;
       if (rp_specular) {
@@ -356,7 +337,6 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
 // Wrapped BSDFs: mask(opacity, twosided(base)) / twosided(base) / base.
 // ---------------------------------------------------------------------------
 
-template <bool ROUGH = true>
 MTX_HD void twosided_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
   // one call of the base BSDF (flipped to the front side when wi.z < 0)
   const bool two = (m.flags & MTX_MF_TWOSIDED) != 0, flip = two && wi.z < 0.f;
@@ -365,10 +345,9 @@ MTX_HD void twosided_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V
     *pdf = 0.f;
     return;
   }
-  base_eval_pdf<ROUGH>(d, m, uv, flip ? V3{wi.x, wi.y, -wi.z} : wi, flip ? V3{wo.x, wo.y, -wo.z} : wo, val, pdf);
+  base_eval_pdf(d, m, uv, flip ? V3{wi.x, wi.y, -wi.z} : wi, flip ? V3{wo.x, wo.y, -wo.z} : wo, val, pdf);
 }
 
-template <bool ROUGH = true>
 MTX_HD V3 twosided_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
   const bool two = (m.flags & MTX_MF_TWOSIDED) != 0, flip = two && wi.z < 0.f;
   if (two && !(wi.z > 0.f) && !flip) {
@@ -378,7 +357,7 @@ MTX_HD V3 twosided_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
     bs->type = 0;
     return v3s(0.f);
   }
-  const V3 w = base_sample<ROUGH>(d, m, uv, flip ? V3{wi.x, wi.y, -wi.z} : wi, u1, u2, bs);
+  const V3 w = base_sample(d, m, uv, flip ? V3{wi.x, wi.y, -wi.z} : wi, u1, u2, bs);
   if (flip) bs->wo.z = -bs->wo.z;
   return w;
 }
@@ -392,9 +371,8 @@ MTX_HD V3 twosided_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
 #define MTX_BSDF_ENTRY MTX_HD
 #endif
 
-template <bool ROUGH = true>
 MTX_BSDF_ENTRY void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
-  twosided_eval_pdf<ROUGH>(d, m, uv, wi, wo, val, pdf);
+  twosided_eval_pdf(d, m, uv, wi, wo, val, pdf);
   if (m.flags & MTX_MF_MASK) {
     *val = *val * m.opacity;
     *pdf = *pdf * m.opacity;
@@ -402,13 +380,12 @@ MTX_BSDF_ENTRY void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 u
 }
 
 // BSDF::sample -> (BSDFSample, weight = value/pdf)
-template <bool ROUGH = true>
 MTX_BSDF_ENTRY V3 bsdf_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
   // mask: nested lobe with probability `opacity`, else a Null pass-through.
   // The factors opacity / (1 - opacity) cancel in the weight and are not
   // included in bs.pdf (upstream mask.cpp).
   const bool mask = (m.flags & MTX_MF_MASK) != 0;
-  if (!mask || u1 < m.opacity) return twosided_sample<ROUGH>(d, m, uv, wi, mask ? u1 / m.opacity : u1, u2, bs);
+  if (!mask || u1 < m.opacity) return twosided_sample(d, m, uv, wi, mask ? u1 / m.opacity : u1, u2, bs);
   bs->wo = -wi;
   bs->eta = 1.f;
   bs->pdf = 1.f;

@@ -132,10 +132,6 @@ struct mtx_ctx {
   // scratch for sample_rays / trace / primitives
   DevBuf s0, s1, s2, s3, s4, s5;
   int trace_grid = 0, shade_grid = 0;
-  bool shade_split = false;  // MTX_SHADE_SPLIT: path-mis shade in two passes (rough microfacet BSDFs second)
-  int shade_grid1 = 0;       // first-pass grid (one deferral region per block)
-  DevBuf defer_q, defer_cnt;
-  uint32_t defer_region = 0;
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
@@ -192,13 +188,11 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   // grid is recomputed per scene: its LDS stack depends on the BVH depth).
   c->trace_grid = c->n_cu * 8;
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
-  c->shade_grid1 = c->n_cu * mtxd::shade_split_blocks_per_cu();
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_SHADE_SPLIT")) c->shade_split = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRI_MIN")) c->tri_min = (uint32_t)std::max(0, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
@@ -221,7 +215,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_nbr, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5,
-                    &c->cq_keys, &c->cq_perm, &c->cq_ws, &c->defer_q, &c->defer_cnt,
+                    &c->cq_keys, &c->cq_perm, &c->cq_ws,
                     &c->field_w16, &c->tr_p, &c->tr_m, &c->tr_v, &c->tr_g, &c->tr_wpart, &c->tr_loss, &c->tr_out,
                     &c->tr_dfeat, &c->tr_feat, &c->tr_flag, &c->tr_target, &c->nr_shape_pmf, &c->nr_shape_cdf,
                     &c->nr_tri_off, &c->nr_tri_pmf, &c->nr_tri_cdf, &c->nr_tri_prim, &c->nr_dists, &c->nr_lhs,
@@ -463,14 +457,6 @@ int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     if ((rc = dalloc(c->q1, 4ull * cap))) return rc;
     if ((rc = dalloc(c->shadow, sizeof(mtxd::ShadowRec) * (size_t)cap))) return rc;
     c->capacity = cap;
-    if (c->shade_split) {
-      // a first-pass block defers at most its grid-stride share of a bounce
-      const uint64_t per = 256ull * (uint64_t)c->shade_grid1;
-      c->defer_region = (uint32_t)(((uint64_t)cap + per - 1) / per * 256ull);
-      if ((rc = dalloc(c->defer_q, 4ull * c->defer_region * (uint64_t)c->shade_grid1))) return rc;
-      if ((rc = dalloc(c->defer_cnt, 4ull * (uint64_t)c->shade_grid1))) return rc;
-      HIP_TRY(hipMemset(c->defer_cnt.p, 0, 4ull * (uint64_t)c->shade_grid1));
-    }
   }
   if ((rc = dalloc(c->counters, 16ull * (max_depth + 2)))) return rc;
   if ((rc = dalloc(c->xheads, 8ull * mtxd::kXSlotWords * (max_depth + 2)))) return rc;
@@ -506,9 +492,6 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.cq_d = (float4 *)c->cq_d.p;
   b.cq_t = (float4 *)c->cq_t.p;
   b.cq_count = (uint32_t *)c->cq_count.p;
-  b.defer_q = (uint32_t *)c->defer_q.p;
-  b.defer_cnt = (uint32_t *)c->defer_cnt.p;
-  b.defer_region = c->defer_region;
   return b;
 }
 
@@ -680,10 +663,7 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
       ++*n_trace;
     }
     e = tm.begin(2);
-    if (c->shade_split && p.integrator == MTX_INT_PATH_MIS && div == 1 && b.defer_q)
-      mtxd::launch_shade_split(s, b, p, bounce, c->shade_grid1, c->shade_grid, c->stream);
-    else
-      mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), c->stream);
+    mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), c->stream);
     tm.end(2, e);
     if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
         !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays

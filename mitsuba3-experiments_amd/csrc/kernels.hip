@@ -202,7 +202,6 @@ __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const fl
 struct ShadeIO {
   ShadowRec rec;
   bool emit;
-  bool defer;  // split shade, first pass: a rough microfacet material, shaded by the second pass
   bool query;  // NRC radiance-cache query at this hit (field.hip)
   float4 qp, qd, qt;
 };
@@ -235,25 +234,10 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
 }
 
-// PASS (MTX_SHADE_SPLIT, path-mis): 0 = every material; 1 = all but the rough
-// microfacet BSDFs, which are left untouched and deferred (their code is
-// compiled out: fewer registers, more waves); 2 = the deferred paths.
-template <int INT, int PASS = 0>
+template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h,
                                            ShadeIO &io) {
-  constexpr bool kRough = PASS != 1;
-  if constexpr (PASS == 1) {
-    // defer before anything else is loaded: the hit's material type only
-    const uint32_t prim = __float_as_uint(h.y);
-    if (prim != 0xffffffffu) {
-      const uint32_t mid = __float_as_uint(s.shade_rec[8 * (size_t)prim].w);
-      if (bsdf_is_rough(sv.materials[mid])) {
-        io.defer = true;
-        return false;
-      }
-    }
-  }
   const float4 ro = b.ray_o[path], rd = b.ray_d[path];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
   const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
@@ -390,8 +374,8 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   float bsdf_pdf = 0.f;
   BSDFSample bs;
   // eval / pdf only feed the NEE contribution (no draws, no side effects)
-  if (active_em) bsdf_eval_pdf<kRough>(sv.bsdf, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
-  const V3 bsdf_weight = bsdf_sample<kRough>(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+  if (active_em) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
+  const V3 bsdf_weight = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
 
   if (INT == MTX_INT_PATH_MIS) {
     const float mi_em = mis_weight_b(ds.pdf, bsdf_pdf);
@@ -794,16 +778,9 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   return false;
 }
 
-template <int INT, int PASS = 0>
-__global__ __launch_bounds__(kShadeBlock, PASS == 1 ? 4 : MTX_SHADE_MIN_BLOCKS) void k_shade(DevScene s, WaveBuffers b,
-                                                                                        ChunkParams p,
-                                                                                        uint32_t bounce) {
+template <int INT>
+__global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
-  __shared__ uint32_t s_defer;  // PASS 1: paths this block deferred (its region of b.defer_q)
-  if (PASS == 1) {
-    if (threadIdx.x == 0) s_defer = 0;
-    __syncthreads();
-  }
   const uint32_t count = b.counters[4 * bounce + 0];
   const uint32_t *in_q = b.queue[bounce & 1];
   uint32_t *out_q = b.queue[(bounce + 1) & 1];
@@ -828,7 +805,6 @@ __global__ __launch_bounds__(kShadeBlock, PASS == 1 ? 4 : MTX_SHADE_MIN_BLOCKS) 
     ShadeIO io;
     io.emit = false;
     io.query = false;
-    io.defer = false;
     bool cont = false;
     bool valid = i < count;
     if (s.shade_sort) {
@@ -855,7 +831,7 @@ __global__ __launch_bounds__(kShadeBlock, PASS == 1 ? 4 : MTX_SHADE_MIN_BLOCKS) 
       else if constexpr (INT == MTX_INT_NERAD)
         cont = shade_nerad<true>(s, sv, b, bounce, path, h, io);
       else
-        cont = shade_path<INT, PASS>(s, sv, b, p, bounce, path, h, io);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, h, io);
     }
     const uint32_t path_c = path;
     if (MTX_SHADE_PREFETCH) {
@@ -866,18 +842,6 @@ __global__ __launch_bounds__(kShadeBlock, PASS == 1 ? 4 : MTX_SHADE_MIN_BLOCKS) 
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path_c;
     if (io.emit) b.shadow[sslot] = io.rec;
-    if constexpr (PASS == 1) {  // one LDS atomic per wave, no barrier
-      const uint64_t dm = __ballot(io.defer);
-      if (dm) {
-        const uint32_t lead = (uint32_t)(__ffsll((unsigned long long)dm) - 1);
-        uint32_t base = 0;
-        if ((threadIdx.x & 63u) == lead) base = atomicAdd(&s_defer, (uint32_t)__popcll(dm));
-        base = __builtin_amdgcn_readlane(base, lead);
-        const uint32_t rank =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-        if (io.defer) b.defer_q[(size_t)blockIdx.x * b.defer_region + base + rank] = path_c;
-      }
-    }
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
       if (INT != MTX_INT_NRC || p.nrc_cache) {
         const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);
@@ -892,46 +856,6 @@ __global__ __launch_bounds__(kShadeBlock, PASS == 1 ? 4 : MTX_SHADE_MIN_BLOCKS) 
       path = in_q[inext];
       h = b.hit[path];
     }
-  }
-  if (PASS == 1) {
-    __syncthreads();
-    if (threadIdx.x == 0) b.defer_cnt[blockIdx.x] = s_defer;
-  }
-}
-
-// Second pass of the split shade (MTX_SHADE_SPLIT): the paths the first pass
-// deferred (rough microfacet materials), region by region, with every BSDF;
-// appends to the same next-bounce and shadow queues. Resets the region counts.
-template <int INT>
-__global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade_deferred(DevScene s, WaveBuffers b,
-                                                                                 ChunkParams p, uint32_t bounce,
-                                                                                 uint32_t n_regions) {
-  const SceneView sv = make_view(s);
-  uint32_t *out_q = b.queue[(bounce + 1) & 1];
-  uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
-  uint32_t parity = 0;
-  for (uint32_t r = blockIdx.x; r < n_regions; r += gridDim.x) {
-    const uint32_t cnt = b.defer_cnt[r];
-    const uint32_t *q = b.defer_q + (size_t)r * b.defer_region;
-    for (uint32_t base = 0; base < cnt; base += kShadeBlock, parity ^= 1u) {
-      const uint32_t i = base + threadIdx.x;
-      ShadeIO io;
-      io.emit = false;
-      io.query = false;
-      io.defer = false;
-      bool cont = false;
-      uint32_t path = 0;
-      if (i < cnt) {
-        path = q[i];
-        cont = shade_path<INT, 2>(s, sv, b, p, bounce, path, b.hit[path], io);
-      }
-      uint32_t slot, sslot;
-      block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
-      if (cont) out_q[slot] = path;
-      if (io.emit) b.shadow[sslot] = io.rec;
-    }
-    __syncthreads();  // every thread has read cnt
-    if (threadIdx.x == 0) b.defer_cnt[r] = 0;
   }
 }
 
@@ -1324,19 +1248,6 @@ int trace_blocks_per_cu(const DevScene &s) {
       nb <= 0)
     nb = 4;
   return nb;
-}
-int shade_split_blocks_per_cu() {
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<MTX_INT_PATH_MIS, 1>, kShadeBlock, 0) != hipSuccess ||
-      nb <= 0)
-    nb = 2;
-  return nb;
-}
-void launch_shade_split(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid1,
-                        int grid2, hipStream_t st) {
-  hipLaunchKernelGGL((k_shade<MTX_INT_PATH_MIS, 1>), dim3(grid1), dim3(kShadeBlock), 0, st, s, b, p, bounce);
-  hipLaunchKernelGGL(k_shade_deferred<MTX_INT_PATH_MIS>, dim3(grid2), dim3(kShadeBlock), 0, st, s, b, p, bounce,
-                     (uint32_t)grid1);
 }
 int shade_blocks_per_cu() {
   int nb = 0;

@@ -105,11 +105,6 @@ struct WaveBuffers {
   // by the bounce-0 shade (path order).
   float4 *rs_xs;
   float4 *rs_ns;
-  // split shade (MTX_SHADE_SPLIT): paths deferred by the first pass, one
-  // region of defer_region entries per first-pass block, and their counts
-  uint32_t *defer_q;
-  uint32_t *defer_cnt;
-  uint32_t defer_region;
   // NRC radiance-cache queries (compacted): p, -d, (T, path), count
   float4 *cq_p, *cq_d, *cq_t;
   uint32_t *cq_count;
@@ -162,10 +157,6 @@ struct ChunkParams {
 // -------- launch wrappers (kernels.hip) --------
 int trace_blocks_per_cu(const DevScene &s);
 int shade_blocks_per_cu();
-int shade_split_blocks_per_cu();
-// split shade: k_shade<PATH_MIS, 1> over grid1 blocks, then k_shade_deferred over grid2
-void launch_shade_split(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid1,
-                        int grid2, hipStream_t st);
 void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
                         const uint32_t *lanes, uint32_t rng_skip, hipStream_t st);
