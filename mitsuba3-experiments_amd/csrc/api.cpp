@@ -132,7 +132,6 @@ struct mtx_ctx {
   // scratch for sample_rays / trace / primitives
   DevBuf s0, s1, s2, s3, s4, s5;
   int trace_grid = 0, shade_grid = 0;
-  uint32_t tail_paths = 0;  // MTX_TAIL: run the remaining bounces per lane once a queue holds fewer paths
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
@@ -194,7 +193,6 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_TAIL")) c->tail_paths = (uint32_t)std::max(0, atoi(e));
   if (const char *e = getenv("MTX_TRI_MIN")) c->tri_min = (uint32_t)std::max(0, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
@@ -673,22 +671,6 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
       mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
       tm.end(1, e);
       ++*n_shadow;
-    }
-    // short queue: the remaining bounces in one per-lane launch (k_tail)
-    if (c->tail_paths && !p.stats && bounce >= 1 && bounce + 1 < depth_iters &&
-        (p.integrator == MTX_INT_PATH_MIS || p.integrator == MTX_INT_PATH)) {
-      uint32_t cnt = 0;
-      hipMemcpyAsync(&cnt, b.counters + 4 * (bounce + 1), 4, hipMemcpyDeviceToHost, c->stream);
-      hipStreamSynchronize(c->stream);
-      if (cnt < c->tail_paths) {
-        if (cnt) {
-          e = tm.begin(0);
-          mtxd::launch_tail(s, b, p, bounce + 1, depth_iters, cnt, c->stream);
-          tm.end(0, e);
-          ++*n_trace;
-        }
-        break;
-      }
     }
     // Deep paths (max_depth 65, scene.xml:6): stop launching once the queue
     // has drained (checked every 8 bounces).

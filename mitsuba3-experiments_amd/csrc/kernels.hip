@@ -77,31 +77,6 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveB
 // Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
 // contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
 // form).
-// ShadowSrc::finish's contribution of a traced shadow ray to its path's L.
-__device__ __forceinline__ void apply_shadow(const WaveBuffers &b, const float4 rd, const float4 rt, const float4 rx,
-                                             bool occluded) {
-  const uint32_t path = __float_as_uint(rd.w);
-  const uint32_t fl = __float_as_uint(rt.w);
-  float4 L = b.L[path];
-  if (!occluded) {
-    if (fl & 1u) {
-      L.x = fmaf(rt.x, rx.x, L.x);
-      L.y = fmaf(rt.y, rx.y, L.y);
-      L.z = fmaf(rt.z, rx.z, L.z);
-    } else {
-      L.x = L.x + rx.x;
-      L.y = L.y + rx.y;
-      L.z = L.z + rx.z;
-    }
-  } else {
-    const float qnan = __uint_as_float(0x7fc00000u);
-    if (fl & 2u) L.x = qnan;
-    if (fl & 4u) L.y = qnan;
-    if (fl & 8u) L.z = qnan;
-  }
-  b.L[path] = L;
-}
-
 struct ShadowSrc {
   WaveBuffers b;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
@@ -112,7 +87,27 @@ struct ShadowSrc {
   }
   __device__ __forceinline__ void finish(uint32_t k, bool occluded, float, uint32_t, float, float) const {
     const ShadowRec &rec = b.shadow[k];
-    apply_shadow(b, rec.d, rec.t, rec.x, occluded);
+    const float4 rd = rec.d, rt = rec.t, rx = rec.x;
+    const uint32_t path = __float_as_uint(rd.w);
+    const uint32_t fl = __float_as_uint(rt.w);
+    float4 L = b.L[path];
+    if (!occluded) {
+      if (fl & 1u) {
+        L.x = fmaf(rt.x, rx.x, L.x);
+        L.y = fmaf(rt.y, rx.y, L.y);
+        L.z = fmaf(rt.z, rx.z, L.z);
+      } else {
+        L.x = L.x + rx.x;
+        L.y = L.y + rx.y;
+        L.z = L.z + rx.z;
+      }
+    } else {
+      const float qnan = __uint_as_float(0x7fc00000u);
+      if (fl & 2u) L.x = qnan;
+      if (fl & 4u) L.y = qnan;
+      if (fl & 8u) L.z = qnan;
+    }
+    b.L[path] = L;
   }
 };
 
@@ -864,46 +859,6 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
   }
 }
 
-// The remaining bounces of a chunk in one launch (MTX_TAIL): once a bounce's
-// queue is short, every lane takes one path and runs its closest hit, shade
-// and NEE shadow ray bounce after bounce (the per-lane traversal `traverse`,
-// the same shade_path and the same shadow contribution, in the same order
-// per path), so the late bounces do not each wait out a latency-bound launch.
-template <int INT>
-__global__ __launch_bounds__(kTraceBlock) void k_tail(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce0,
-                                                      uint32_t bounce_end) {
-  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
-  int32_t *stk = stack + threadIdx.x;
-  const SceneView sv = make_view(s);
-  const uint32_t count = b.counters[4 * bounce0 + 0];
-  const uint32_t *in_q = b.queue[bounce0 & 1];
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += gridDim.x * blockDim.x) {
-    const uint32_t path = in_q[i];
-    for (uint32_t bounce = bounce0; bounce < bounce_end; ++bounce) {
-      const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
-      const TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
-      float tbest = o4.w, bu = 0.f, bv = 0.f;
-      uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
-      traverse<false>(s, stk, r, tbest, prim, bu, bv, nv, tv);
-      const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
-      b.hit[path] = h;
-      ShadeIO io;
-      io.emit = false;
-      io.query = false;
-      const bool cont = shade_path<INT>(s, sv, b, p, bounce, path, h, io);
-      if (io.emit) {
-        const TraceRay sr = make_trace_ray(V3{io.rec.o.x, io.rec.o.y, io.rec.o.z},
-                                           V3{io.rec.d.x, io.rec.d.y, io.rec.d.z}, io.rec.o.w);
-        float st = io.rec.o.w, su = 0.f, sv2 = 0.f;
-        uint32_t sp = 0xffffffffu, snv = 0, stv = 0;
-        const bool occ = traverse<true>(s, stk, sr, st, sp, su, sv2, snv, stv);
-        apply_shadow(b, io.rec.d, io.rec.t, io.rec.x, occ);
-      }
-      if (!cont) break;
-    }
-  }
-}
-
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
 // plain sum: L = L + T * out, as the oracle-side composition in the tests).
 __global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *perm) {
@@ -1293,16 +1248,6 @@ int trace_blocks_per_cu(const DevScene &s) {
       nb <= 0)
     nb = 4;
   return nb;
-}
-void launch_tail(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce0, uint32_t bounce_end,
-                 uint32_t count, hipStream_t st) {
-  const unsigned blocks = (unsigned)std::max<uint64_t>(1, (count + kTraceBlock - 1) / kTraceBlock);
-  if (p.integrator == MTX_INT_PATH)
-    hipLaunchKernelGGL(k_tail<MTX_INT_PATH>, dim3(blocks), dim3(kTraceBlock), stack_bytes(s), st, s, b, p, bounce0,
-                       bounce_end);
-  else
-    hipLaunchKernelGGL(k_tail<MTX_INT_PATH_MIS>, dim3(blocks), dim3(kTraceBlock), stack_bytes(s), st, s, b, p,
-                       bounce0, bounce_end);
 }
 int shade_blocks_per_cu() {
   int nb = 0;

@@ -157,9 +157,6 @@ struct ChunkParams {
 // -------- launch wrappers (kernels.hip) --------
 int trace_blocks_per_cu(const DevScene &s);
 int shade_blocks_per_cu();
-// the bounces [bounce0, bounce_end) of the `count` paths queued for bounce0, one lane per path (path / path-mis)
-void launch_tail(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce0, uint32_t bounce_end,
-                 uint32_t count, hipStream_t st);
 void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
                         const uint32_t *lanes, uint32_t rng_skip, hipStream_t st);
