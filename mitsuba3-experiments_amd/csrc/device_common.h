@@ -614,9 +614,6 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
 // the plain front-to-back order of `traverse` (the oracle's), with or
 // without STATS.
 // ---------------------------------------------------------------------------
-#ifndef MTX_ULEAF
-#define MTX_ULEAF 0
-#endif
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                              int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
@@ -771,27 +768,23 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         const uint64_t m = __ballot(true);
         if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
       }
-      // MTX_ULEAF (bit 0 closest hit, bit 1 any-hit): test the whole leaf in
-      // this step instead of one triangle per iteration
-      do {
-        const uint32_t pr = tri;
-        const TriGeom g = load_tri(s, pr);
-        float t, u, v;
-        ++tv;
-        ++tri;
-        if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
-          if (ANY) {
-            hit = true;
-            tri = tri_end;
-            sp = 0;
-          } else if (t < tbest || (t == tbest && pr < prim)) {
-            tbest = t;
-            prim = pr;
-            bu = u;
-            bv = v;
-          }
+      const uint32_t pr = tri;
+      const TriGeom g = load_tri(s, pr);
+      float t, u, v;
+      ++tv;
+      ++tri;
+      if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
+        if (ANY) {
+          hit = true;
+          tri = tri_end;
+          sp = 0;
+        } else if (t < tbest || (t == tbest && pr < prim)) {
+          tbest = t;
+          prim = pr;
+          bu = u;
+          bv = v;
         }
-      } while (((MTX_ULEAF >> (ANY ? 1 : 0)) & 1) && tri < tri_end);
+      }
       if (tri >= tri_end) pop_next();
     }
     if (has && node < 0 && tri >= tri_end) {
