@@ -839,28 +839,8 @@ __global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(Dev
       if (inext < count) h = b.hit[path];
     }
     uint32_t slot, sslot;
-    if (s.ray_sort) {
-      // the block's continuing paths ordered by the direction cone of their
-      // next ray (octant x dominant axis): the trace kernel's waves then hold
-      // neighbouring origins with similar directions. Per-path results do not
-      // depend on queue order.
-      uint32_t key = kShadeClasses - 1;
-      if (cont) {
-        const float4 d = b.ray_d[path_c];
-        const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-        const uint32_t dom = ax >= ay && ax >= az ? 0u : (ay >= az ? 1u : 2u);
-        const uint32_t oct = (d.x < 0.f ? 1u : 0u) | (d.y < 0.f ? 2u : 0u) | (d.z < 0.f ? 4u : 0u);
-        key = s.ray_sort == 2 ? oct : oct * 3u + dom;
-      }
-      const uint32_t n_cont = (uint32_t)__syncthreads_count(cont);
-      const uint32_t sorted = block_sort_by_key<kShadeBlock>(key, path_c);
-      const bool c2 = threadIdx.x < n_cont;
-      block_append2<kShadeBlock>(c2, io.emit, out_cnt, parity, slot, sslot);
-      if (c2) out_q[slot] = sorted;
-    } else {
-      block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
-      if (cont) out_q[slot] = path_c;
-    }
+    block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
+    if (cont) out_q[slot] = path_c;
     if (io.emit) b.shadow[sslot] = io.rec;
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
       if (INT != MTX_INT_NRC || p.nrc_cache) {
