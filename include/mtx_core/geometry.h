@@ -86,9 +86,11 @@ MTX_HD float wide_ldexp(float x, int e) {
 // qlx.. hold the four children's 8-bit bounds, child k in bits [8k, 8k+8).
 // wide_node_order_e takes the axis exponents and child count decoded (the
 // device's 48-B node keeps them in 6-bit fields, mtx_scene_upload).
-MTX_HD int wide_node_order_e(const TraceRay &r, float ox, float oy, float oz, int ex, int ey, int ez, int nch,
-                             uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
-                             float tfar, uint32_t key[4]) {
+// wide_node_keys_e: the four keys in slot order (unsorted), for callers that
+// sort them together with the child references.
+MTX_HD int wide_node_keys_e(const TraceRay &r, float ox, float oy, float oz, int ex, int ey, int ez, int nch,
+                            uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
+                            float tfar, uint32_t key[4]) {
   const float ax = wide_ldexp(r.idir.x, ex), bx = (ox - r.o.x) * r.idir.x;
   const float ay = wide_ldexp(r.idir.y, ey), by = (oy - r.o.y) * r.idir.y;
   const float az = wide_ldexp(r.idir.z, ez), bz = (oz - r.o.z) * r.idir.z;
@@ -124,6 +126,13 @@ MTX_HD int wide_node_order_e(const TraceRay &r, float ox, float oy, float oz, in
     key[k] = hit ? ((f2u(tmin) & 0x7ffffffcu) | (uint32_t)k) : (0x7f800000u | (uint32_t)k);
     n += hit ? 1 : 0;
   }
+  return n;
+}
+
+MTX_HD int wide_node_order_e(const TraceRay &r, float ox, float oy, float oz, int ex, int ey, int ez, int nch,
+                             uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
+                             float tfar, uint32_t key[4]) {
+  const int n = wide_node_keys_e(r, ox, oy, oz, ex, ey, ez, nch, qlx, qhx, qly, qhy, qlz, qhz, tfar, key);
 #define MTX_CAS(i, j)                                   \
   {                                                     \
     const uint32_t lo_ = key[i] < key[j] ? key[i] : key[j]; \

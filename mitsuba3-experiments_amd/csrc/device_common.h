@@ -256,6 +256,9 @@ __device__ __forceinline__ int32_t wide_dref(uint32_t key, uint32_t ends, uint32
 // mtx_core/geometry.h wide_node_order_e. Returns the number of children hit;
 // c[0..n) are their references in visit order (the same order and refs as
 // the 64-B node gives the oracle).
+#ifndef MTX_PAIR_SORT
+#define MTX_PAIR_SORT 1  // A/B: 0 = sort the keys, then pick each reference by its key's slot bits
+#endif
 #ifndef MTX_NODE48
 #define MTX_NODE48 0  // A/B: 1 = the 48-B node (three loads, references decoded): slower, DESIGN.md
 #endif
@@ -267,12 +270,43 @@ __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, 
     const int4 a = np[0], rf = np[1], qa = np[2];
     const int2 qb = *reinterpret_cast<const int2 *>(np + 3);
     uint32_t key[4];
-    const int n = wide_node_order(r, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z), (uint32_t)a.w,
+    const uint32_t eb = (uint32_t)a.w;
+#if MTX_PAIR_SORT
+    // the references ride along the compare-exchange network (one compare +
+    // four selects per exchange, the keys' dead selects dropped) instead of
+    // being picked by the sorted keys' slot bits afterwards: the keys are
+    // distinct (slot in the low bits), so the order and the references are
+    // those of wide_node_order + wide_ref
+    const int n = wide_node_keys_e(r, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z),
+                                   (int)(int8_t)(uint8_t)(eb & 0xffu), (int)(int8_t)(uint8_t)((eb >> 8) & 0xffu),
+                                   (int)(int8_t)(uint8_t)((eb >> 16) & 0xffu), (int)(eb >> 24), (uint32_t)qa.x,
+                                   (uint32_t)qa.y, (uint32_t)qa.z, (uint32_t)qa.w, (uint32_t)qb.x, (uint32_t)qb.y,
+                                   tbest, key);
+    c[0] = rf.x;
+    c[1] = rf.y;
+    c[2] = rf.z;
+    c[3] = rf.w;
+#define MTX_CAS2(i, j)                                   \
+  {                                                      \
+    const bool sw_ = key[j] < key[i];                    \
+    const uint32_t ki_ = key[i], kj_ = key[j];           \
+    const int32_t ci_ = c[i], cj_ = c[j];                \
+    key[i] = sw_ ? kj_ : ki_;                            \
+    key[j] = sw_ ? ki_ : kj_;                            \
+    c[i] = sw_ ? cj_ : ci_;                              \
+    c[j] = sw_ ? ci_ : cj_;                              \
+  }
+    MTX_CAS2(0, 1) MTX_CAS2(2, 3) MTX_CAS2(0, 2) MTX_CAS2(1, 3) MTX_CAS2(1, 2)
+#undef MTX_CAS2
+    return n;
+#else
+    const int n = wide_node_order(r, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z), eb,
                                   (uint32_t)qa.x, (uint32_t)qa.y, (uint32_t)qa.z, (uint32_t)qa.w, (uint32_t)qb.x,
                                   (uint32_t)qb.y, tbest, key);
 #pragma unroll
     for (int i = 0; i < 4; ++i) c[i] = wide_ref(key[i], rf.x, rf.y, rf.z, rf.w);
     return n;
+#endif
   }
 #endif
   const int4 *np = s.nodes + 3 * node;

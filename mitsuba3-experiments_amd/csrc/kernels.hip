@@ -54,8 +54,20 @@ struct ClosestSrc {
   }
 };
 
+// 8 waves/SIMD for the trace kernels (their grid is sized for 8): left alone
+// the compiler takes 66 VGPRs for the any-hit kernel (7 waves); asked for 8 it
+// fits 55 without spills. Shadow 56.4 -> 55.6 ms per step (A/B, one box, 3
+// rounds). MTX_SHADOW_WAVES=0 builds the unconstrained form.
+#ifndef MTX_SHADOW_WAVES
+#define MTX_SHADOW_WAVES 8
+#endif
+#if MTX_SHADOW_WAVES
+#define MTX_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(MTX_SHADOW_WAVES)))
+#else
+#define MTX_SHADOW_ATTR
+#endif
 template <bool STATS>
-__global__ __launch_bounds__(kTraceBlock) void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
+__global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
   const ClosestSrc src{b, b.queue[bounce & 1]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
@@ -111,17 +123,6 @@ struct ShadowSrc {
   }
 };
 
-// 8 waves/SIMD for the any-hit kernel: left alone the compiler takes 66 VGPRs
-// (7 waves); asked for 8 it fits 55 without spills. Shadow 56.4 -> 55.6 ms per
-// step (A/B, one box, 3 rounds). MTX_SHADOW_WAVES=0 builds the unconstrained form.
-#ifndef MTX_SHADOW_WAVES
-#define MTX_SHADOW_WAVES 8
-#endif
-#if MTX_SHADOW_WAVES
-#define MTX_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(MTX_SHADOW_WAVES)))
-#else
-#define MTX_SHADOW_ATTR
-#endif
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
