@@ -237,6 +237,21 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(sc, integ, args)
+        kernels = {
+            "trace_closest": _kernel_entry(trace_ms, launches, tc, alg_closest, L2_GATHER_PEAK_GBS, "l2"),
+            "trace_shadow": dict(_kernel_entry(agg["shadow_ms"] / K, cnt["shadow_launches"], traffic[names["shadow"]],
+                                               alg_shadow, L2_GATHER_PEAK_GBS, "l2"),
+                                 rays_per_step=int(cnt["rays_shadow"]),
+                                 node_visits_per_ray=round(cnt["nodes_shadow"] / max(1, cnt["rays_shadow"]), 2),
+                                 tri_visits_per_ray=round(cnt["tris_shadow"] / max(1, cnt["rays_shadow"]), 2)),
+            "shade": _kernel_entry(agg["shade_ms"] / K, cnt["trace_launches"], traffic[names["shade"]],
+                                   cnt["rays_closest"] * SHADE_BYTES_PER_PATH_BOUNCE, HBM_PEAK_GBS, "hbm"),
+        }
+        # the roofline object follows north_star's traversal kernel; the
+        # kernel with the most time per step is named beside it
+        big = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
+        largest = {"kernel": big, "ms_per_step": kernels[big]["ms_per_step"], "bound": kernels[big].get("alg_bound"),
+                   "alg_frac": kernels[big].get("alg_frac"), "hbm_frac": kernels[big].get("hbm_frac")}
         out = {
             "metric": "Mpaths/sec on bedroom@1280×720 spp=256, 1/2/4/8 GPUs; HBM GB/s vs peak",
             "value": round(value, 3),
@@ -285,18 +300,11 @@ def main():
                 "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2),
                 "active_lane_frac_node_phase": round(cnt["nodes_closest"] / max(1, 64 * cnt["wave_node_iters"]), 3),
                 "tris_per_lane_leaf_step": round(cnt["tris_closest"] / max(1, 64 * cnt["wave_leaf_iters"]), 3),
+                "kernel_choice": "north_star's traversal kernel (closest hit); the kernel with the most time "
+                                 "per step is `largest_kernel`",
+                "largest_kernel": largest,
             },
-            "kernels": {
-                "trace_closest": _kernel_entry(trace_ms, launches, tc, alg_closest, L2_GATHER_PEAK_GBS, "l2"),
-                "trace_shadow": dict(_kernel_entry(agg["shadow_ms"] / K, cnt["shadow_launches"], traffic[names["shadow"]],
-                                                   alg_shadow, L2_GATHER_PEAK_GBS, "l2"),
-                                     rays_per_step=int(cnt["rays_shadow"]),
-                                     node_visits_per_ray=round(cnt["nodes_shadow"] / max(1, cnt["rays_shadow"]), 2),
-                                     tri_visits_per_ray=round(cnt["tris_shadow"] / max(1, cnt["rays_shadow"]), 2)),
-                "shade": _kernel_entry(agg["shade_ms"] / K, cnt["trace_launches"], traffic[names["shade"]],
-                                       cnt["rays_closest"] * SHADE_BYTES_PER_PATH_BOUNCE, HBM_PEAK_GBS, "hbm"),
-                "other_ms_per_step": round(agg["other_ms"] / K, 3),
-            },
+            "kernels": dict(kernels, other_ms_per_step=round(agg["other_ms"] / K, 3)),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
