@@ -40,6 +40,10 @@ struct BsdfData {
   const mtx_texture *textures;
   const float *texels;
   const float *tables;
+  // the material colour at the shading point when a caller looked it up
+  // already (one texture fetch per shading point instead of one per BSDF call)
+  V3 col = V3{0.f, 0.f, 0.f};
+  bool has_col = false;
 };
 
 MTX_HD uint32_t bsdf_flags(const mtx_material &m) {
@@ -57,6 +61,16 @@ MTX_HD uint32_t bsdf_flags(const mtx_material &m) {
   return f;
 }
 
+// Repeat wrap ((i % w) + w) % w for w > 0; the integer division (about 25
+// instructions on the device) only for i outside [-w, 2w), which a texture
+// coordinate in [0, 1] never reaches. Same integers in every case.
+MTX_HD int wrap_repeat(int i, int w) {
+  if (i >= 0 && i < w) return i;
+  if (i < 0 && i >= -w) return i + w;
+  if (i >= w && i - w < w) return i - w;
+  return ((i % w) + w) % w;
+}
+
 // Bilinear bitmap lookup with repeat wrapping (upstream BitmapTexture::eval).
 MTX_HD V3 texture_eval(const BsdfData &d, int32_t tex, V2 uv) {
   const mtx_texture t = d.textures[tex];
@@ -67,8 +81,8 @@ MTX_HD V3 texture_eval(const BsdfData &d, int32_t tex, V2 uv) {
   int ix = (int)fx, iy = (int)fy;
   float w1x = ux - fx, w1y = uy - fy;
   float w0x = 1.f - w1x, w0y = 1.f - w1y;
-  int x0 = ((ix % w) + w) % w, y0 = ((iy % h) + h) % h;
-  int x1 = (((ix + 1) % w) + w) % w, y1 = (((iy + 1) % h) + h) % h;
+  int x0 = wrap_repeat(ix, w), y0 = wrap_repeat(iy, h);
+  int x1 = wrap_repeat(ix + 1, w), y1 = wrap_repeat(iy + 1, h);
   const float *base = d.texels + t.offset;
   const float *f00 = base + 3 * ((uint64_t)y0 * w + x0);
   const float *f10 = base + 3 * ((uint64_t)y0 * w + x1);
@@ -82,6 +96,10 @@ MTX_HD V3 texture_eval(const BsdfData &d, int32_t tex, V2 uv) {
 }
 
 MTX_HD V3 mat_color(const BsdfData &d, const mtx_material &m, V2 uv) {
+  if (d.has_col) return d.col;
+#if defined(MTX_DEVICE_COMPILE) && defined(MTX_DIAG_NOTEX) && MTX_DIAG_NOTEX  // timing diagnostic only (wrong images)
+  return V3{m.rgb[0], m.rgb[1], m.rgb[2]};
+#endif
   if (m.tex >= 0) return texture_eval(d, m.tex, uv);
   return V3{m.rgb[0], m.rgb[1], m.rgb[2]};
 }

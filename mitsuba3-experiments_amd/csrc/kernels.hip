@@ -246,6 +246,9 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
 }
 
+#ifndef MTX_EARLY_COLOR
+#define MTX_EARLY_COLOR 1  // A/B: 0 = each BSDF call looks the texture up itself
+#endif
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h,
@@ -365,6 +368,18 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
 #else
   const mtx_material mat = sv.materials[si.material];
 #endif
+#if MTX_EARLY_COLOR
+  // the textured colour of the diffuse and roughplastic lobes, fetched once
+  // and before the emitter sample (its latency overlaps that work; the NEE
+  // eval and the BSDF sample of roughplastic both read it)
+  BsdfData bd = sv.bsdf;
+  if (mat.tex >= 0 && (mat.type == MTX_MAT_DIFFUSE || mat.type == MTX_MAT_ROUGHPLASTIC)) {
+    bd.col = texture_eval(sv.bsdf, mat.tex, si.uv);
+    bd.has_col = true;
+  }
+#else
+  const BsdfData &bd = sv.bsdf;
+#endif
   const bool smooth = (bsdf_flags(mat) & BF_SMOOTH) != 0;
   bool active_em = (INT == MTX_INT_PATH_MIS ? active_next : true) && smooth;
   const V2 u_em = rng.next_2d();
@@ -386,8 +401,8 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   float bsdf_pdf = 0.f;
   BSDFSample bs;
   // eval / pdf only feed the NEE contribution (no draws, no side effects)
-  if (active_em) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
-  const V3 bsdf_weight = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+  if (active_em) bsdf_eval_pdf(bd, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
+  const V3 bsdf_weight = bsdf_sample(bd, mat, si.uv, si.wi, s1, s2, &bs);
 
   if (INT == MTX_INT_PATH_MIS) {
     const float mi_em = mis_weight_b(ds.pdf, bsdf_pdf);
