@@ -71,9 +71,10 @@ MTX_HD int wrap_repeat(int i, int w) {
   return ((i % w) + w) % w;
 }
 
-// Bilinear bitmap lookup with repeat wrapping (upstream BitmapTexture::eval)
-// of the w x h RGB bitmap at texels + offset.
-MTX_HD V3 texture_eval_at(const BsdfData &d, int w, int h, uint64_t offset, V2 uv) {
+// Bilinear bitmap lookup with repeat wrapping (upstream BitmapTexture::eval).
+MTX_HD V3 texture_eval(const BsdfData &d, int32_t tex, V2 uv) {
+  const mtx_texture t = d.textures[tex];
+  const int w = (int)t.width, h = (int)t.height;
   float ux = fmaf(uv.x, (float)w, -0.5f);
   float uy = fmaf(uv.y, (float)h, -0.5f);
   float fx = floorf(ux), fy = floorf(uy);
@@ -82,7 +83,7 @@ MTX_HD V3 texture_eval_at(const BsdfData &d, int w, int h, uint64_t offset, V2 u
   float w0x = 1.f - w1x, w0y = 1.f - w1y;
   int x0 = wrap_repeat(ix, w), y0 = wrap_repeat(iy, h);
   int x1 = wrap_repeat(ix + 1, w), y1 = wrap_repeat(iy + 1, h);
-  const float *base = d.texels + offset;
+  const float *base = d.texels + t.offset;
   const float *f00 = base + 3 * ((uint64_t)y0 * w + x0);
   const float *f10 = base + 3 * ((uint64_t)y0 * w + x1);
   const float *f01 = base + 3 * ((uint64_t)y1 * w + x0);
@@ -92,11 +93,6 @@ MTX_HD V3 texture_eval_at(const BsdfData &d, int w, int h, uint64_t offset, V2 u
   r.y = fmaf(w0x, fmaf(w0y, f00[1], w1y * f01[1]), w1x * fmaf(w0y, f10[1], w1y * f11[1]));
   r.z = fmaf(w0x, fmaf(w0y, f00[2], w1y * f01[2]), w1x * fmaf(w0y, f10[2], w1y * f11[2]));
   return r;
-}
-
-MTX_HD V3 texture_eval(const BsdfData &d, int32_t tex, V2 uv) {
-  const mtx_texture t = d.textures[tex];
-  return texture_eval_at(d, (int)t.width, (int)t.height, t.offset, uv);
 }
 
 MTX_HD V3 mat_color(const BsdfData &d, const mtx_material &m, V2 uv) {

@@ -372,21 +372,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
       // paths by it: lanes of a wave then run the same BSDF code)
       const mtx_material &m = d->materials[sh.material];
       const uint32_t cls = 1u + ((m.type & 7u) << 2 | (m.tex >= 0 ? 2u : 0u) | ((m.flags & MTX_MF_MASK) ? 1u : 0u));
-      // bit 2: the diffuse / roughplastic colour is a bitmap whose size and
-      // texel offset ride in r[30..31] (k_shade fetches the colour from the
-      // record, without the material and texture-table loads in between)
-      uint32_t tex_fl = 0;
-      if (m.tex >= 0 && (m.type == MTX_MAT_DIFFUSE || m.type == MTX_MAT_ROUGHPLASTIC) &&
-          (uint32_t)m.tex < d->n_textures) {
-        const mtx_texture &tx = d->textures[m.tex];
-        if (tx.width > 0 && tx.width < 65536u && tx.height > 0 && tx.height < 65536u && tx.offset < (1ull << 32)) {
-          const uint32_t off = (uint32_t)tx.offset, wh = (tx.width << 16) | tx.height;
-          memcpy(&r[30], &off, 4);
-          memcpy(&r[31], &wh, 4);
-          tex_fl = 4u;
-        }
-      }
-      const uint32_t mat = sh.material, fl = use_n | use_uv | tex_fl | (cls << 8);
+      const uint32_t mat = sh.material, fl = use_n | use_uv | (cls << 8);
       const int32_t em = sh.emitter;
       memcpy(&r[3], &mat, 4);
       memcpy(&r[7], &em, 4);

@@ -247,7 +247,7 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
 }
 
 #ifndef MTX_EARLY_COLOR
-#define MTX_EARLY_COLOR 2  // A/B: 0 = each BSDF call looks the texture up itself; 1 = once, via the material
+#define MTX_EARLY_COLOR 1  // A/B: 0 = each BSDF call looks the texture up itself
 #endif
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
@@ -273,20 +273,6 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   float prev_pdf = Lr.w;
   const V3 ray_d = V3{rd.x, rd.y, rd.z};
   const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
-#if MTX_EARLY_COLOR == 2
-  // the record's bitmap colour reference (api.cpp: flag bit 2, r[30..31]),
-  // read with the record so the texel loads follow the record directly
-  BsdfData bd = sv.bsdf;
-  if (si.valid) {
-    const float4 *rr = s.shade_rec + 8 * (size_t)__float_as_uint(h.y);
-    if (__float_as_uint(rr[2].w) & 4u) {
-      const float4 r7 = rr[7];
-      const uint32_t wh = __float_as_uint(r7.w);
-      bd.col = texture_eval_at(sv.bsdf, (int)(wh >> 16), (int)(wh & 0xffffu), __float_as_uint(r7.z), si.uv);
-      bd.has_col = true;
-    }
-  }
-#endif
   if (kPrevOnEmitter && bounce != 0 && si.emitter >= 0) pv = b.prev[path];
   V3 prev_p = V3{pv.x, pv.y, pv.z};
   float spread = pv.w, a0 = rd.w;
@@ -382,7 +368,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
 #else
   const mtx_material mat = sv.materials[si.material];
 #endif
-#if MTX_EARLY_COLOR == 1
+#if MTX_EARLY_COLOR
   // the textured colour of the diffuse and roughplastic lobes, fetched once
   // and before the emitter sample (its latency overlaps that work; the NEE
   // eval and the BSDF sample of roughplastic both read it)
@@ -391,8 +377,6 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     bd.col = texture_eval(sv.bsdf, mat.tex, si.uv);
     bd.has_col = true;
   }
-#elif MTX_EARLY_COLOR == 2
-  // (bd: the record's bitmap colour, fetched right after the record above)
 #else
   const BsdfData &bd = sv.bsdf;
 #endif
