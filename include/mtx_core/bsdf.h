@@ -44,9 +44,6 @@ struct BsdfData {
   // already (one texture fetch per shading point instead of one per BSDF call)
   V3 col = V3{0.f, 0.f, 0.f};
   bool has_col = false;
-  // roughplastic: the transmittance-table value at the (front-side) cos of wi
-  float t_i = 0.f;
-  bool has_ti = false;
 };
 
 MTX_HD uint32_t bsdf_flags(const mtx_material &m) {
@@ -141,7 +138,7 @@ MTX_HD void roughplastic_eval_pdf(const BsdfData &d, const mtx_material &m, V2 u
   float G = distr.G(wi, wo, H);
   float spec = F * D * G / (4.f * ci);
   V3 result = v3s(spec);
-  float t_i = d.has_ti ? d.t_i : lerp_table(tab, ci), t_o = lerp_table(tab, co);
+  float t_i = lerp_table(tab, ci), t_o = lerp_table(tab, co);
   V3 diff = mat_color(d, m, uv);
   V3 denom = (m.flags & MTX_MF_NONLINEAR) ? (v3s(1.f) - diff * m.internal_refl) : v3s(1.f - m.internal_refl);
   diff = diff / denom;
@@ -242,7 +239,7 @@ MTX_HD V3 base_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, fl
   bool rp_specular = false;
   if (m.type == MTX_MAT_ROUGHPLASTIC && ci > 0.f) {
     const float *tab = d.tables + m.table;
-    float t_i = d.has_ti ? d.t_i : lerp_table(tab, ci);
+    float t_i = lerp_table(tab, ci);
     float prob_specular = (1.f - t_i) * m.spec_weight;
     float prob_diffuse = t_i * (1.f - m.spec_weight);
     rp_prob_specular = prob_specular / (prob_specular + prob_diffuse);

@@ -246,9 +246,6 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
 }
 
-#ifndef MTX_EARLY_TI
-#define MTX_EARLY_TI 1  // A/B: 0 = every roughplastic call reads its table at cos(wi) itself
-#endif
 #ifndef MTX_EARLY_COLOR
 #define MTX_EARLY_COLOR 1  // A/B: 0 = each BSDF call looks the texture up itself
 #endif
@@ -380,18 +377,6 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     bd.col = texture_eval(sv.bsdf, mat.tex, si.uv);
     bd.has_col = true;
   }
-#if MTX_EARLY_TI
-  // roughplastic's table value at cos(wi), as the base BSDF sees wi (the
-  // twosided wrapper flips a back-side wi): read once instead of once in the
-  // sample's lobe choice and once per eval
-  if (mat.type == MTX_MAT_ROUGHPLASTIC) {
-    const float ci = ((mat.flags & MTX_MF_TWOSIDED) && si.wi.z < 0.f) ? -si.wi.z : si.wi.z;
-    if (ci > 0.f) {
-      bd.t_i = lerp_table(sv.bsdf.tables + mat.table, ci);
-      bd.has_ti = true;
-    }
-  }
-#endif
 #else
   const BsdfData &bd = sv.bsdf;
 #endif
