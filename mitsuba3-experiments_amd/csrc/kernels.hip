@@ -249,6 +249,19 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
 #ifndef MTX_EARLY_COLOR
 #define MTX_EARLY_COLOR 1  // A/B: 0 = each BSDF call looks the texture up itself
 #endif
+// BSDF data for one shading point: the textured colour of the diffuse and
+// roughplastic lobes fetched once (and early: its latency overlaps the work
+// before the first BSDF call), read by every BSDF call at this point.
+__device__ __forceinline__ BsdfData bsdf_at(const SceneView &sv, const mtx_material &mat, V2 uv) {
+  BsdfData bd = sv.bsdf;
+#if MTX_EARLY_COLOR
+  if (mat.tex >= 0 && (mat.type == MTX_MAT_DIFFUSE || mat.type == MTX_MAT_ROUGHPLASTIC)) {
+    bd.col = texture_eval(sv.bsdf, mat.tex, uv);
+    bd.has_col = true;
+  }
+#endif
+  return bd;
+}
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h,
@@ -368,18 +381,8 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
 #else
   const mtx_material mat = sv.materials[si.material];
 #endif
-#if MTX_EARLY_COLOR
-  // the textured colour of the diffuse and roughplastic lobes, fetched once
-  // and before the emitter sample (its latency overlaps that work; the NEE
-  // eval and the BSDF sample of roughplastic both read it)
-  BsdfData bd = sv.bsdf;
-  if (mat.tex >= 0 && (mat.type == MTX_MAT_DIFFUSE || mat.type == MTX_MAT_ROUGHPLASTIC)) {
-    bd.col = texture_eval(sv.bsdf, mat.tex, si.uv);
-    bd.has_col = true;
-  }
-#else
-  const BsdfData &bd = sv.bsdf;
-#endif
+  // before the emitter sample; the NEE eval and the BSDF sample both read it
+  const BsdfData bd = bsdf_at(sv, mat, si.uv);
   const bool smooth = (bsdf_flags(mat) & BF_SMOOTH) != 0;
   bool active_em = (INT == MTX_INT_PATH_MIS ? active_next : true) && smooth;
   const V2 u_em = rng.next_2d();
@@ -506,9 +509,11 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   bs.type = 0;
   V3 w = v3s(0.f);
   mtx_material mat;
+  BsdfData bd = sv.bsdf;
   if (si.valid) {
     mat = sv.materials[si.material];
-    w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+    bd = bsdf_at(sv, mat, si.uv);
+    w = bsdf_sample(bd, mat, si.uv, si.wi, s1, s2, &bs);
   }
   if (!active_next) w = v3s(0.f);
   const float4 o4 = b.vpath[(size_t)depth * b.capacity + path];
@@ -516,7 +521,7 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   V3 vwo = p.large_step ? bs.wo : normalize(old * 0.9f + bs.wo * 0.1f);
   V3 val = v3s(0.f);
   float pdf = 0.f;
-  if (si.valid) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, vwo, &val, &pdf);
+  if (si.valid) bsdf_eval_pdf(bd, mat, si.uv, si.wi, vwo, &val, &pdf);
   if (pdf <= 0.f) vwo = bs.wo;
   if (pdf > 0.f) w = val / pdf;
   b.vprop[(size_t)depth * b.capacity + path] = make_float4(vwo.x, vwo.y, vwo.z, 0.f);
@@ -632,9 +637,11 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   bs.type = 0;
   V3 w = v3s(0.f);
   mtx_material mat;
+  BsdfData bd = sv.bsdf;
   if (si.valid) {
     mat = sv.materials[si.material];
-    w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);
+    bd = bsdf_at(sv, mat, si.uv);
+    w = bsdf_sample(bd, mat, si.uv, si.wi, s1, s2, &bs);
   }
   // mutate (:170-190): a = 0.01 on the direction, sqrt(0.01) on the emitter sample
   const V2 um = rng.next_2d();
@@ -653,7 +660,7 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   }
   V3 val = v3s(0.f);
   float pdf = 0.f;
-  if (si.valid) bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, vwo, &val, &pdf);  // :107
+  if (si.valid) bsdf_eval_pdf(bd, mat, si.uv, si.wi, vwo, &val, &pdf);  // :107
   if (pdf <= 0.f) vwo = bs.wo;                                                // :109
   if (pdf > 0.f) w = val / pdf;                                               // :110
   const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, vwo));               // :114
@@ -665,7 +672,7 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
     const V3 wo = to_local(si.sh, ds.d);
     V3 ev;
     float epdf;
-    bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, wo, &ev, &epdf);
+    bsdf_eval_pdf(bd, mat, si.uv, si.wi, wo, &ev, &epdf);
     const float mi_em = mis_weight_b(ds.pdf, epdf);
     make_shadow(io, si, ds, path, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true);
   }
@@ -805,8 +812,16 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   return false;
 }
 
+// blocks per CU the shade kernels are built for (their register budget)
+#ifndef MTX_PSP_BLOCKS
+#define MTX_PSP_BLOCKS 3  // PSSMLT with NEE (pssmltpath.py): A/B 2 = no spills at 2 waves/SIMD
+#endif
 template <int INT>
-__global__ __launch_bounds__(kShadeBlock, MTX_SHADE_MIN_BLOCKS) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
+constexpr int shade_min_blocks() {
+  return INT == MTX_INT_PSSMLT_PATH ? MTX_PSP_BLOCKS : MTX_SHADE_MIN_BLOCKS;
+}
+template <int INT>
+__global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
   const uint32_t count = b.counters[4 * bounce + 0];
   const uint32_t *in_q = b.queue[bounce & 1];
@@ -1254,8 +1269,10 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
     case MTX_INT_SIMPLE:
       hipLaunchKernelGGL(k_shade<MTX_INT_SIMPLE>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
-    case MTX_INT_PSSMLT_PATH:
-      hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
+    case MTX_INT_PSSMLT_PATH:  // the grid follows its own blocks per CU
+      hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>,
+                         dim3(std::max(1, grid * shade_min_blocks<MTX_INT_PSSMLT_PATH>() / MTX_SHADE_MIN_BLOCKS)),
+                         dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
     case MTX_INT_NERAD_RHS:
       hipLaunchKernelGGL(k_shade<MTX_INT_NERAD_RHS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
