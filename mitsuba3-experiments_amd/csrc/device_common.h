@@ -416,8 +416,9 @@ __device__ __forceinline__ int32_t stack_read(const int32_t *stk, const int32_t 
   return v;
 }
 
-// Src provides: load(k, TraceRay&, float &tmax, uint32_t &payload) and
-// finish(payload, bool any_hit, float t, uint32_t prim, float u, float v).
+// Src provides: a Payload type (what a lane carries for its ray), load(k,
+// TraceRay&, float &tmax, Payload &) and finish(const Payload &, bool any_hit,
+// float t, uint32_t prim, float u, float v).
 // XCD of the executing wave (0-7): speed only (which L2 the wave fills).
 __device__ __forceinline__ uint32_t xcc_id() {
   uint32_t x;
@@ -444,7 +445,8 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
   const int lds_n = (int)s.lds_entries;
   bool has = false, exhausted = false, hit = false, drained = false;
   uint32_t res_lo = 0, res_hi = 0;
-  uint32_t payload = 0, prim = 0xffffffffu;
+  typename Src::Payload payload{};
+  uint32_t prim = 0xffffffffu;
   TraceRay r;
   float tbest = 0.f, bu = 0.f, bv = 0.f;
   int32_t node = kTravDone, leaf = 0;
@@ -661,7 +663,8 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
   const int lds_n = (int)s.lds_entries;
   bool has = false, exhausted = false, hit = false, drained = false;
   uint32_t res_lo = 0, res_hi = 0;
-  uint32_t payload = 0, prim = 0xffffffffu;
+  typename Src::Payload payload{};
+  uint32_t prim = 0xffffffffu;
   TraceRay r;
   float tbest = 0.f, bu = 0.f, bv = 0.f;
   int32_t node = -1;          // >= 0: inner node to visit next

@@ -40,6 +40,7 @@ namespace mtxd {
 
 // Closest-hit queries of bounce `bounce`: queue entries are path indices.
 struct ClosestSrc {
+  using Payload = uint32_t;  // the path
   WaveBuffers b;
   const uint32_t *queue;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
@@ -89,18 +90,39 @@ __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(D
 // Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
 // contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
 // form).
+#ifndef MTX_SHADOW_CARRY
+#define MTX_SHADOW_CARRY 1  // A/B: 0 = the finish re-reads the record
+#endif
 struct ShadowSrc {
+  // the lane carries its path and the record's contribution from the ray's
+  // start (MTX_SHADOW_CARRY), so the finish is one L load + store instead of
+  // a record load followed by the dependent L load
+  struct Payload {
+    uint32_t k, path;
+#if MTX_SHADOW_CARRY
+    float4 t, x;
+#endif
+  };
   WaveBuffers b;
-  __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
+  __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, Payload &pl) const {
     const float4 o4 = b.shadow[k].o, d4 = b.shadow[k].d;
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
-    payload = k;
+    pl.k = k;
+    pl.path = __float_as_uint(d4.w);
+#if MTX_SHADOW_CARRY
+    pl.t = b.shadow[k].t;
+    pl.x = b.shadow[k].x;
+#endif
   }
-  __device__ __forceinline__ void finish(uint32_t k, bool occluded, float, uint32_t, float, float) const {
-    const ShadowRec &rec = b.shadow[k];
-    const float4 rd = rec.d, rt = rec.t, rx = rec.x;
-    const uint32_t path = __float_as_uint(rd.w);
+  __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
+#if MTX_SHADOW_CARRY
+    const float4 rt = pl.t, rx = pl.x;
+#else
+    const ShadowRec &rec = b.shadow[pl.k];
+    const float4 rt = rec.t, rx = rec.x;
+#endif
+    const uint32_t path = pl.path;
     const uint32_t fl = __float_as_uint(rt.w);
     float4 L = b.L[path];
     if (!occluded) {
