@@ -137,7 +137,7 @@ struct mtx_ctx {
   uint32_t lds_stack = mtxd::kLdsStack;
   uint32_t trace_batch = 256;
   uint32_t refill_lanes = 16;
-  uint32_t urefill = 16;
+  uint32_t urefill = 24;  // unified loop: refill once 24 lanes are idle (16: closest +1.3 %, 32: +2 %)
   uint32_t tri_min = 0;  // trace_loop_u: triangle step deferred until this many lanes wait on one
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
