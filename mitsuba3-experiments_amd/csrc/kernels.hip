@@ -835,9 +835,6 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
 }
 
 // blocks per CU the shade kernels are built for (their register budget)
-#ifndef MTX_SHADE_PIPE
-#define MTX_SHADE_PIPE 1  // A/B: 0 = each block step waits for its own reservation (block_append2)
-#endif
 #ifndef MTX_PSP_BLOCKS
 #define MTX_PSP_BLOCKS 3  // PSSMLT with NEE (pssmltpath.py): A/B 2 = no spills at 2 waves/SIMD
 #endif
@@ -856,14 +853,6 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
   uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
   const uint32_t stride = gridDim.x * kShadeBlock;
   uint32_t parity = 0;
-#if MTX_SHADE_PIPE
-  __shared__ uint32_t s_q[2][kShadeBlock];
-  __shared__ ShadowRec s_rec[2][kShadeBlock];
-  __shared__ uint32_t s_wc[2][2][kShadeBlock / 64];
-  __shared__ uint32_t s_prev[4];
-  unsigned long long pend = 0;  // thread 0: the reply of the last step's reservation
-  uint32_t pend_n0 = 0, pend_n1 = 0;
-#endif
   // software pipeline over the persistent loop: the next step's queue entry
   // loads during this step, its hit record before this step's appends
   uint32_t path = 0;
@@ -913,51 +902,10 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       path = path_n;
       if (inext < count) h = b.hit[path];
     }
-#if MTX_SHADE_PIPE
-    {
-      // this step's outputs staged in LDS in block order; thread 0 reserves
-      // their slots with one atomic and does not wait for it: the reply is
-      // used one step later, when the block writes the staged outputs out
-      const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-      const uint64_t m0 = __ballot(cont), m1 = __ballot(io.emit);
-      if (lane == 0) {
-        s_wc[parity][0][wave] = (uint32_t)__popcll(m0);
-        s_wc[parity][1][wave] = (uint32_t)__popcll(m1);
-      }
-      __syncthreads();
-      uint32_t o0 = 0, o1 = 0, t0 = 0, t1 = 0;
-#pragma unroll
-      for (uint32_t w = 0; w < kShadeBlock / 64; ++w) {
-        const uint32_t c0 = s_wc[parity][0][w], c1 = s_wc[parity][1][w];
-        o0 += w < wave ? c0 : 0u;
-        o1 += w < wave ? c1 : 0u;
-        t0 += c0;
-        t1 += c1;
-      }
-      if (cont) s_q[parity][o0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u))] = path_c;
-      if (io.emit) s_rec[parity][o1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u))] = io.rec;
-      if (threadIdx.x == 0) {
-        s_prev[0] = (uint32_t)pend;  // the previous step's reservation
-        s_prev[1] = (uint32_t)(pend >> 32);
-        s_prev[2] = pend_n0;
-        s_prev[3] = pend_n1;
-        pend = (t0 | t1) ? atomicAdd(reinterpret_cast<unsigned long long *>(out_cnt),
-                                     ((unsigned long long)t1 << 32) | t0)
-                         : 0ull;
-        pend_n0 = t0;
-        pend_n1 = t1;
-      }
-      __syncthreads();
-      const uint32_t pb0 = s_prev[0], pb1 = s_prev[1], pn0 = s_prev[2], pn1 = s_prev[3];
-      for (uint32_t j = threadIdx.x; j < pn0; j += kShadeBlock) out_q[pb0 + j] = s_q[parity ^ 1u][j];
-      for (uint32_t j = threadIdx.x; j < pn1; j += kShadeBlock) b.shadow[pb1 + j] = s_rec[parity ^ 1u][j];
-    }
-#else
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path_c;
     if (io.emit) b.shadow[sslot] = io.rec;
-#endif
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
       if (INT != MTX_INT_NRC || p.nrc_cache) {
         const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);
@@ -973,21 +921,6 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       h = b.hit[path];
     }
   }
-#if MTX_SHADE_PIPE
-  // the last step's outputs (staged under parity ^ 1)
-  if (threadIdx.x == 0) {
-    s_prev[0] = (uint32_t)pend;
-    s_prev[1] = (uint32_t)(pend >> 32);
-    s_prev[2] = pend_n0;
-    s_prev[3] = pend_n1;
-  }
-  __syncthreads();
-  {
-    const uint32_t pb0 = s_prev[0], pb1 = s_prev[1], pn0 = s_prev[2], pn1 = s_prev[3];
-    for (uint32_t j = threadIdx.x; j < pn0; j += kShadeBlock) out_q[pb0 + j] = s_q[parity ^ 1u][j];
-    for (uint32_t j = threadIdx.x; j < pn1; j += kShadeBlock) b.shadow[pb1 + j] = s_rec[parity ^ 1u][j];
-  }
-#endif
 }
 
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
