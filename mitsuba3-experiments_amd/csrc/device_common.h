@@ -654,9 +654,6 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
 // the plain front-to-back order of `traverse` (the oracle's), with or
 // without STATS.
 // ---------------------------------------------------------------------------
-#ifndef MTX_QUEUE_PREFETCH
-#define MTX_QUEUE_PREFETCH 1  // A/B: 0 = a refilled lane reads its queue entry, then its ray
-#endif
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                              int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
@@ -675,7 +672,6 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
   int sp = 0;
   const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
   const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
-  uint32_t pf = 0;  // MTX_QUEUE_PREFETCH: queue entry res_lo + lane
   if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + batch - 1) / batch) return;
   uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
   // next work item of a lane from its stack: an inner node, a leaf's
@@ -736,14 +732,6 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
           k = base2 + (rk - left);
           ok = true;
         }
-        uint32_t entry = 0;
-        if constexpr (Src::kIndirect && MTX_QUEUE_PREFETCH) {
-          // entries res_lo + lane were read at the previous refill: a lane
-          // taking res_lo + rk reads lane rk's copy (no queue round trip);
-          // entries of a batch claimed just now are read here
-          const uint32_t pq = __shfl(pf, (int)(rk & 63u));
-          entry = rk < left ? pq : (ok ? src.entry(k) : 0u);
-        }
         if (n <= left) {
           res_lo += n;
         } else {
@@ -751,13 +739,8 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
           res_lo = base2 + used2;
           res_hi = base2 + got2;
         }
-        if constexpr (Src::kIndirect && MTX_QUEUE_PREFETCH)
-          pf = res_lo + lane < res_hi ? src.entry(res_lo + lane) : 0u;  // for the next refill
         if (!has && ok) {
-          if constexpr (Src::kIndirect && MTX_QUEUE_PREFETCH)
-            src.load_entry(entry, r, tbest, payload);
-          else
-            src.load(k, r, tbest, payload);
+          src.load(k, r, tbest, payload);
           prim = 0xffffffffu;
           bu = bv = 0.f;
           hit = false;

@@ -41,18 +41,14 @@ namespace mtxd {
 // Closest-hit queries of bounce `bounce`: queue entries are path indices.
 struct ClosestSrc {
   using Payload = uint32_t;  // the path
-  static constexpr bool kIndirect = true;  // rays are reached through the queue
   WaveBuffers b;
   const uint32_t *queue;
-  __device__ __forceinline__ uint32_t entry(uint32_t k) const { return queue[k]; }
-  __device__ __forceinline__ void load_entry(uint32_t path, TraceRay &r, float &tmax, uint32_t &payload) const {
+  __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
+    const uint32_t path = queue[k];
     const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
     payload = path;
-  }
-  __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
-    load_entry(queue[k], r, tmax, payload);
   }
   __device__ __forceinline__ void finish(uint32_t path, bool, float t, uint32_t prim, float u, float v) const {
     b.hit[path] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
@@ -101,10 +97,6 @@ struct ShadowSrc {
   // the lane carries its path and the record's contribution from the ray's
   // start (MTX_SHADOW_CARRY), so the finish is one L load + store instead of
   // a record load followed by the dependent L load
-  static constexpr bool kIndirect = false;
-  __device__ __forceinline__ uint32_t entry(uint32_t k) const { return k; }
-  template <class P>
-  __device__ __forceinline__ void load_entry(uint32_t, TraceRay &, float &, P &) const {}
   struct Payload {
     uint32_t k, path;
 #if MTX_SHADOW_CARRY

@@ -393,9 +393,6 @@ __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
 // Any-hit traversal of the compacted visibility tests; occ[base + slot].
 struct TestSrc {
   using Payload = uint32_t;  // the test slot
-  static constexpr bool kIndirect = false;
-  __device__ __forceinline__ uint32_t entry(uint32_t k) const { return k; }
-  __device__ __forceinline__ void load_entry(uint32_t, TraceRay &, float &, uint32_t &) const {}
   RestirBuffers r;
   uint32_t occ_base;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &tr, float &tmax, uint32_t &payload) const {
