@@ -142,7 +142,6 @@ struct mtx_ctx {
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
-  uint32_t ww_bounce0 = 0;
   uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
   DevBuf cq_keys, cq_perm, cq_ws;
   uint32_t sample_major = 0;
@@ -198,7 +197,6 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
-  if (const char *e = getenv("MTX_WW_BOUNCE0")) c->ww_bounce0 = atoi(e) != 0;
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
   *out = c;
   return MTX_OK;
@@ -411,7 +409,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
   s.shade_sort = c->shade_sort;
-  s.ww_bounce0 = c->ww_bounce0;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {

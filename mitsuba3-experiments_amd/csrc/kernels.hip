@@ -87,17 +87,6 @@ __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(D
   }
 }
 
-// Closest hit with the while-while loop (camera rays, MTX_WW_BOUNCE0): their
-// lanes stay coherent, so the per-iteration refill and triangle-step checks
-// of the unified loop buy less there.
-__global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest_ww(DevScene s, WaveBuffers b, uint32_t bounce) {
-  extern __shared__ int32_t stack[];
-  const ClosestSrc src{b, b.queue[bounce & 1]};
-  uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop_ww<false, false>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords,
-                              stack + threadIdx.x, nv, tv, nr, nullptr);
-}
-
 // Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
 // contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
 // form).
@@ -1277,8 +1266,6 @@ void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t boun
                           hipStream_t st) {
   if (stats)
     hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
-  else if (bounce == 0 && s.ww_bounce0)
-    hipLaunchKernelGGL(k_trace_closest_ww, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
   else
     hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
 }

@@ -67,7 +67,6 @@ struct DevScene {
   uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   uint32_t shade_sort;     // k_shade: order a block's paths by the hit's shading class
-  uint32_t ww_bounce0;     // closest hit of the camera rays with the while-while loop (A/B)
   mtx_camera camera;
 };
 
