@@ -153,6 +153,10 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         sys.exit(2)
+    if args.workload == "path_mis" and args.spp < world:
+        # checked on every rank before any collective (no rank waits in a gather)
+        print(f"bench.py: --spp {args.spp} < {world} ranks: every rank needs >= 1 sample per pixel", file=sys.stderr)
+        sys.exit(2)
     if args.workload != "path_mis":
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         import bench_workloads

@@ -23,6 +23,7 @@
 //   fold per target in LDS-bucket order: every target receives its values
 //   in ascending index order (deterministic), with no host round trips and
 //   no global atomics.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -1227,21 +1228,27 @@ __global__ void k_sorted_fold(const uint32_t *__restrict__ keys, const uint32_t 
   target[t] = acc;
 }
 
-// Self-check of the lane-ordered LDS atomic property the RANK kernels use:
-// random keys with many collisions per wave instruction; counts returns
-// that differ from (base + number of lower lanes with the same key).
+// Self-check of the lane-ordered LDS atomic property the RANK kernels use, in
+// their exact access pattern: per-wave rows of u16 counters packed two per
+// word (digits d and d^1 share a word), up to 4096 digits, random keys with
+// 2..4096 distinct values per wave instruction (many same-word collisions).
+// Counts returns whose u16 half differs from (first return of the key + number
+// of lower lanes with the same key).
 __global__ __launch_bounds__(512) void k_lds_order_probe(uint32_t seed, uint32_t *bad) {
-  __shared__ uint32_t cnt[8][64];
+  __shared__ uint32_t cnt[8][2048];  // [wave][4096 digits / 2]
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  cnt[w][lane] = 0;
+  for (uint32_t i = lane; i < 2048; i += 64) cnt[w][i] = 0;
   __syncthreads();
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t x = seed ^ (blockIdx.x * 7919u + threadIdx.x * 104729u);
-  for (int r = 0; r < 64; ++r) {
+  constexpr uint32_t kinds[6] = {2u, 3u, 16u, 64u, 512u, 4096u};
+  for (int r = 0; r < 60; ++r) {  // <= 60 * 64 increments per digit: no u16 carry
     x = x * 1664525u + 1013904223u;
-    const uint32_t k = (x >> 20) % (1u + (uint32_t)r % 16u);  // 1..16 distinct keys per round
-    const uint32_t old = atomicAdd(&cnt[w][k], 1u);
-    const uint64_t m = ms_match(k, 4, ~0ull);
+    const uint32_t K = kinds[r % 6];
+    const uint32_t k = (x >> 8) % K;
+    const uint32_t sh = (k & 1u) << 4;
+    const uint32_t old = (atomicAdd(&cnt[w][k >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    const uint64_t m = ms_match(k, 12, ~0ull);
     const uint32_t base = __shfl(old, __ffsll((unsigned long long)m) - 1);
     if (old != base + (uint32_t)__popcll(m & lt)) atomicAdd(bad, 1u);
   }
@@ -1358,13 +1365,14 @@ uint32_t bucket_lds(int s, bool slow) {
 // in ascending lane order (observed on gfx950; not a documented guarantee):
 // the RANK kernels rely on it, the ballot-match kernels do not.
 bool lds_lane_order(hipStream_t st) {
-  static int state[64];  // 0 unknown, 1 holds, 2 fails
+  static std::atomic<int> state[64];  // 0 unknown, 1 holds, 2 fails (a racing first call probes twice: same answer)
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
-  if (state[dev]) return state[dev] == 1;
+  const int known = state[dev].load(std::memory_order_acquire);
+  if (known) return known == 1;
   const char *env = getenv("MTX_LDS_RANK");  // "0": always the ballot-match kernels
   if (env && env[0] == '0') {
-    state[dev] = 2;
+    state[dev].store(2, std::memory_order_release);
     return false;
   }
   uint32_t *d_bad = nullptr, bad = 1;
@@ -1377,7 +1385,7 @@ bool lds_lane_order(hipStream_t st) {
     }
     hipFree(d_bad);
   }
-  state[dev] = bad == 0 ? 1 : 2;
+  state[dev].store(bad == 0 ? 1 : 2, std::memory_order_release);
   return bad == 0;
 }
 

@@ -41,7 +41,7 @@ constexpr uint32_t kXHeadStride = 32;
 constexpr uint32_t kXSlotWords = kXcds * kXHeadStride;
 
 struct DevScene {
-  const int4 *nodes;  // 3 x int4 per node (48-B device form, bvh_build.cpp mtx_bvh_device_nodes)
+  const int4 *nodes;  // 4 x int4 per node: the 64-B ABI node (mtx.h); 3 x int4 only in the MTX_NODE48=1 A/B build
   const float *tri;   // 9 floats per triangle (v0, e1, e2; device_common.h load_tri)
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;

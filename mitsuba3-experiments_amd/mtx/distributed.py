@@ -39,7 +39,13 @@ def row_bands(height: int, world: int):
 def sample_range(spp: int, world: int, rank: int):
     """Strong-scaling sample shard: rank r traces the global samples
     [r*spp//N, (r+1)*spp//N) of every pixel (global-lane seeding keeps each
-    path identical to the single-GPU render, path.py:156-161)."""
+    path identical to the single-GPU render, path.py:156-161).
+
+    Every rank needs at least one sample (mtx_render rejects spp = 0): with
+    spp < world this raises on every rank alike, before any collective, so no
+    rank is left waiting in a gather."""
+    if spp < world:
+        raise ValueError(f"sample shards: spp={spp} < world size {world} (every rank needs >= 1 sample per pixel)")
     return rank * spp // world, (rank + 1) * spp // world
 
 

@@ -64,11 +64,23 @@ def develop(film: np.ndarray) -> np.ndarray:
     return np.where(w != 0, inner[..., :3] / np.where(w != 0, w, 1), 0).astype(np.float32)
 
 
-def _rows3(v) -> np.ndarray:
-    """A wavefront of 3-vectors as (N, 3) float32 from (N, 3) or (3, N)."""
+def _rows3(v, drjit_layout: bool = False) -> np.ndarray:
+    """A wavefront of 3-vectors as (N, 3) float32.
+
+    `drjit_layout`: the field comes from a ray object, whose Array3f is (3, N)
+    in Dr.Jit's layout at every N. A bare array is (N, 3) or (3, N); a 3x3
+    array is ambiguous (3 rays either way) and is refused."""
     a = np.asarray(v, np.float32)
-    if a.ndim == 2 and a.shape[0] == 3 and a.shape[1] != 3:
-        a = a.T
+    if a.ndim == 2 and a.shape[0] == 3:
+        if drjit_layout:
+            a = a.T
+        elif a.shape[1] == 3:
+            raise MtxError("ambiguous 3x3 ray array: pass a ray object (Dr.Jit (3, N) fields) "
+                           "or (N, 3) arrays with N != 3")
+        else:
+            a = a.T
+    elif drjit_layout and a.ndim == 1 and a.size == 3:
+        a = a.reshape(3, 1).T
     return a.reshape(-1, 3)
 
 
@@ -137,8 +149,9 @@ class SamplingIntegrator:
         `ray` is an (o, d) pair or a ray object with `.o` / `.d` fields (the
         RayDifferential3f of path.py:195-202); each field is (N, 3) or (3, N)
         (Dr.Jit's Array3f layout)."""
-        o, d = (ray.o, ray.d) if hasattr(ray, "o") and hasattr(ray, "d") else ray
-        rays = np.ascontiguousarray(np.concatenate([_rows3(o), _rows3(d)], 1))
+        obj = hasattr(ray, "o") and hasattr(ray, "d")
+        o, d = (ray.o, ray.d) if obj else ray
+        rays = np.ascontiguousarray(np.concatenate([_rows3(o, obj), _rows3(d, obj)], 1))
         n = len(rays)
         if len(sampler.lanes) != n:
             raise MtxError("sampler lanes and rays differ in length")

@@ -80,8 +80,7 @@ def test_bsdf_sample_matches_eval(oracle, small_scene, materials):
             val2 = val2 / opacity
             pdf2 = pdf2 / opacity
         np.testing.assert_allclose(w[ok], val2[ok] / pdf2[ok, None], rtol=2e-3, atol=1e-5)
-        if mtype != _abi.MTX_MAT_ROUGHPLASTIC:
-            np.testing.assert_allclose(spdf[ok], pdf2[ok], rtol=2e-3)
+        np.testing.assert_allclose(spdf[ok], pdf2[ok], rtol=2e-3)
 
 
 def test_bsdf_energy_and_pdf_normalisation(oracle, small_scene, materials):

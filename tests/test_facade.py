@@ -61,3 +61,11 @@ def test_ray_layouts():
     assert np.array_equal(_rows3(a), a)
     assert np.array_equal(_rows3(a.T), a)  # Dr.Jit Array3f layout (3, N)
     assert _rows3(np.zeros(3, np.float32)).shape == (1, 3)
+    # a 3x3 bare array is ambiguous and refused; from a ray object it is (3, N)
+    from mtx import MtxError
+
+    sq = np.arange(9, dtype=np.float32).reshape(3, 3)
+    with pytest.raises(MtxError):
+        _rows3(sq)
+    assert np.array_equal(_rows3(sq, drjit_layout=True), sq.T)
+    assert np.array_equal(_rows3(a.T, drjit_layout=True), a)
