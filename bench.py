@@ -69,7 +69,8 @@ def parse():
     p.add_argument("--workload", default="path_mis", choices=["path_mis", "pssmlt", "pssmltpath", "restir", "nrc", "prims", "field", "nerad"],
                    help="path_mis = the driver's headline line (default); the others measure the remaining "
                         "SURVEY §8 configurations on one GPU (C3 PSSMLT, C4 ReSTIR GI, C5 NRC, primitives)")
-    p.add_argument("--iterations", type=int, default=20, help="PSSMLT Metropolis iterations (C3 short variant)")
+    p.add_argument("--iterations", type=int, default=200,
+                   help="PSSMLT Metropolis iterations (pssmlt.py:208: 200, aggregation when i %% 50 > 40)")
     p.add_argument("--frames", type=int, default=10, help="ReSTIR GI timed frames")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="N>1 ranks: nccl (RCCL, the measurement) or gloo (host-staged device tensors; lets "

@@ -942,10 +942,6 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   }
   const bool mlt = a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH;
   if (mlt) {
-    if (a->sample_offset != 0 || a->spp_total != a->spp) {
-      mtx_set_error("mtx_render: PSSMLT chains cannot be split by sample range (use row bands)");
-      return MTX_E_ARG;
-    }
     if ((rc = ensure_mlt(c, cap, std::max<uint32_t>(a->max_depth, 1), a->integrator == MTX_INT_PSSMLT_PATH)))
       return rc;
     HIP_TRY(hipMemsetAsync(c->contrib.p, 0, 9ull * 16 * band_px, c->stream));

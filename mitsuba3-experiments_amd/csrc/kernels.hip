@@ -1116,12 +1116,16 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const flo
 // ---------------------------------------------------------------------------
 // PSSMLT chain kernels (pssmlt.py:167-228). Chains of a chunk keep their
 // state in HBM across all Metropolis iterations; chain i of the chunk is
-// sampler lane px0*spp + i (pssmlt.py:188-193).
+// chain s = sample_offset + i % spp of pixel px0 + i / spp, sampler lane
+// pixel * spp_total + s (pssmlt.py:188-193 with wavefront W*H*spp_total): a
+// chain range [sample_offset, sample_offset + spp) of every pixel is a shard
+// of the spp_total-chain render (multi-GPU, chains never leave their pixel).
 // ---------------------------------------------------------------------------
 __global__ void k_mlt_init(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_paths) return;
-  const Pcg32 rng = sampler_lane(p.seed, p.px0 * p.spp + i);
+  const uint32_t q = i / p.spp;
+  const Pcg32 rng = sampler_lane(p.seed, (p.px0 + q) * p.spp_total + p.sample_offset + (i - q * p.spp));
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
   // offset = 0.5, cumulative_weight = 0 (:198-200); w: vertex depths that may
   // differ between the proposed and current buffers (k_mlt_end)

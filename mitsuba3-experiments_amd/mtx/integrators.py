@@ -273,7 +273,9 @@ class PssmltSimple(SamplingIntegrator):
     (large step every 50, aggregation when i % 50 > 40, pssmlt.py:206-210),
     BSDF-only proposals whose local directions are mutated as
     normalize(0.9 old + 0.1 new) (pssmltsimple.py:135-142). Chains are
-    independent, so multi-GPU sharding is by row bands."""
+    independent and never leave their pixel, so a multi-GPU render shards
+    the chains of every pixel by range (``spp_total`` / ``sample_offset``,
+    :func:`mtx.distributed.render_sharded` mode "samples"), or by row bands."""
 
     integrator_id = _abi.MTX_INT_PSSMLT_SIMPLE
     name = "pssmlt_simple"

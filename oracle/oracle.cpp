@@ -736,7 +736,10 @@ int orc_pssmlt_render(const mtx_scene_desc *d, const mtx_render_args *a, uint32_
     std::vector<V2> off(spp, V2{0.5f, 0.5f});
     std::vector<V3> Lc(spp, v3s(0.f));
     std::vector<float> cw(spp, 0.f);
-    for (uint32_t k = 0; k < spp; ++k) rng[k] = sampler_lane(a->seed, (uint32_t)(((uint64_t)y * W + x) * spp + k));
+    // chains [sample_offset, sample_offset + spp) of the pixel's spp_total (a chain shard)
+    const uint32_t spp_total = a->spp_total ? a->spp_total : spp;
+    for (uint32_t k = 0; k < spp; ++k)
+      rng[k] = sampler_lane(a->seed, (uint32_t)(((uint64_t)y * W + x) * spp_total + a->sample_offset + k));
     float *ac = &acc[36 * (size_t)p];
     for (uint32_t it = 0; it < iterations; ++it) {
       const bool large = it % 50 == 0, agg = it % 50 > 40;

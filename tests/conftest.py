@@ -22,6 +22,14 @@ def small_scene():
 
 
 @pytest.fixture(scope="session")
+def full_scene():
+    """The benchmark's bedroom proxy: 1,832,004 triangles, 1280x720 film."""
+    from mtx import scene
+
+    return scene.bedroom()
+
+
+@pytest.fixture(scope="session")
 def oracle():
     import binding
 

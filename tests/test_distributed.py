@@ -31,20 +31,29 @@ def _worker(rank, world, port, mode, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sc = scene.bedroom(width=48, height=27, scale=0.02, tex_res=32)
-    integ = load_dict({"type": "path_test"})
+    if mode == "chains":  # PSSMLT: chain range of every pixel per rank
+        sc = sc.with_film(24, 12)
+        integ = load_dict({"type": "pssmlt_simple", "iterations": 45})
 
-    def render(spp, spp_total, off, y0, y1):
-        a = integ.render_args(sc, 4, spp, y0, y1, spp_total, off)
-        return oracle.render(sc, a)
+        def render(spp, spp_total, off, y0, y1):
+            return oracle.pssmlt_render(sc, integ.render_args(sc, 4, spp, y0, y1, spp_total, off), 45)
 
-    full = distributed.render_sharded(render, sc.height, 8 if mode == "samples" else 4, mode)
+        full = distributed.render_sharded(render, sc.height, 4, "samples")
+    else:
+        integ = load_dict({"type": "path_test"})
+
+        def render(spp, spp_total, off, y0, y1):
+            a = integ.render_args(sc, 4, spp, y0, y1, spp_total, off)
+            return oracle.render(sc, a)
+
+        full = distributed.render_sharded(render, sc.height, 8 if mode == "samples" else 4, mode)
     if rank == 0:
         np.save(out_path, full.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["samples", "rows"])
+@pytest.mark.parametrize("mode", ["samples", "rows", "chains"])
 def test_two_rank_combine(tmp_path, oracle, mode):
     from mtx import load_dict, scene
 
@@ -53,6 +62,18 @@ def test_two_rank_combine(tmp_path, oracle, mode):
     got = np.load(out)
     sc = scene.bedroom(width=48, height=27, scale=0.02, tex_res=32)
     integ = load_dict({"type": "path_test"})
+    if mode == "chains":
+        # pssmlt.py chains [2r, 2r+2) of every pixel on rank r (4 chains), 45
+        # iterations (aggregation window 41-44 included): the sum of the shards
+        # equals the one-rank film up to the summation order (rtol 2e-6)
+        sc = sc.with_film(24, 12)
+        integ = load_dict({"type": "pssmlt_simple", "iterations": 45})
+        parts = [oracle.pssmlt_render(sc, integ.render_args(sc, 4, 2, 0, sc.height, 4, 2 * r), 45) for r in range(2)]
+        assert np.array_equal(got, parts[0] + parts[1])  # rank-order sum, bit-exact
+        ref = oracle.pssmlt_render(sc, integ.render_args(sc, 4, 4, 0, sc.height), 45)
+        assert ref[..., 3].sum() > 0
+        np.testing.assert_allclose(got, ref, rtol=2e-6, atol=1e-6)
+        return
     if mode == "samples":
         parts = [oracle.render(sc, integ.render_args(sc, 4, 4, 0, sc.height, 8, 4 * r)) for r in range(2)]
         assert np.array_equal(got, parts[0] + parts[1])  # rank-order sum, bit-exact
@@ -118,6 +139,18 @@ def test_restir_halo_exchange(tmp_path, world, height, halo):
                        join=True, start_method="spawn")
     for r in range(world):
         assert bool(np.load(os.path.join(tmp_path, f"ok{r}.npy"))[0]), f"rank {r}"
+
+
+def test_sample_range_needs_a_sample_per_rank():
+    """spp < world would leave a rank with an empty range (mtx_render
+    rejects spp 0) while the others wait in the gather: every rank raises alike."""
+    from mtx import distributed
+
+    assert [distributed.sample_range(256, 8, r) for r in (0, 7)] == [(0, 32), (224, 256)]
+    assert [distributed.sample_range(3, 2, r) for r in range(2)] == [(0, 1), (1, 3)]
+    for r in range(4):
+        with pytest.raises(ValueError):
+            distributed.sample_range(3, 4, r)
 
 
 def test_halo_plan_edges():

@@ -37,13 +37,6 @@ def _rays(scene, n, seed):
     return rays
 
 
-@pytest.fixture(scope="module")
-def full_scene():
-    from mtx import scene
-
-    return scene.bedroom()
-
-
 def test_full_bedroom_trace_bit_exact(full_scene, oracle):
     from test_gpu_parity import _trace_gpu
 

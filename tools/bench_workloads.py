@@ -3,7 +3,7 @@ headline path-mis line (run through `python bench.py --workload X`; this
 module is imported by bench.py, which sets up sys.path):
 
   pssmlt  C3  pssmltsimple.py PSSMLT, bedroom 1280x720, 256 chains/pixel,
-              --iterations Metropolis iterations (20 = the SURVEY's CI variant)
+              --iterations Metropolis iterations (200 = pssmlt.py:208, default)
   pssmltpath  the same chains with pssmltpath.py's NEE + MIS proposals
   restir  C4  restirgi.py ReSTIR GI, bedroom 1920x1080, props of
               restirgi.py:610-620, --frames timed frames
@@ -29,10 +29,17 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
-def _trace_roofline(cnt, trace_ms_per_unit, units_label):
+def _trace_roofline(cnt, trace_ms_per_unit, units_label, timed_launches=None):
+    """`cnt`: visit counters of one untimed run. When that run is shorter than
+    the timed unit (PSSMLT: 20 of 200 iterations), `timed_launches` is the
+    timed unit's launch count: the bytes per launch come from the counter run
+    and are scaled to the timed launches."""
     alg = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
            + cnt["tris_closest"] * TRI_BYTES)
     launches = max(1, cnt["trace_launches"])
+    if timed_launches:
+        alg = alg / launches * timed_launches
+        launches = max(1, int(round(timed_launches)))
     s = trace_ms_per_unit / 1e3
     ach = alg / s / 1e9 if s > 0 else 0.0
     # stated against the level that serves the traversal's bytes (bench.py docstring)
@@ -131,56 +138,70 @@ def _sum_stats(a, b):
 
 # --------------------------------------------------------------- PSSMLT (C3) --
 def pssmlt(args, with_nee=False):
+    """Pssmlt.render (pssmlt.py:167-228) on the reference's own schedule: 200
+    iterations by default (large step every 50, aggregation + block.put when
+    i % 50 > 40, :206-219), so the splat phase is inside the timed region.
+    N > 1: every rank runs the chain range [r*spp/N, (r+1)*spp/N) of every
+    pixel (chains never leave their pixel, pssmlt.py:250-254; global-lane
+    seeding keeps each chain identical to the one-GPU render), films are
+    gathered to rank 0 and summed in rank order: the same work split as the
+    headline's sample shards, balanced whatever the scene's row costs."""
     import binding as oracle
     import torch
-    from mtx import PssmltPath, PssmltSimple, scene
+    from mtx import PssmltPath, PssmltSimple, distributed, scene
 
     sc = scene.bedroom(1280, 720)
     rk = Ranks(args, sc.height)
-    y0, y1 = rk.y0, rk.y1
     spp, it = args.spp, args.iterations
+    s0, s1 = distributed.sample_range(spp, rk.world, rk.rank)
     cls = PssmltPath if with_nee else PssmltSimple
     integ = cls({"iterations": it})
-    film = torch.empty((y1 - y0 + 2, sc.width + 2, 4), dtype=torch.float32, device=f"cuda:{rk.dev}")
-    cls({"iterations": 1}).render_film(sc, seed=99, spp=spp, y0=y0, y1=y1, out=film, device=rk.dev)  # warm-up
+    film = torch.empty((sc.height + 2, sc.width + 2, 4), dtype=torch.float32, device=f"cuda:{rk.dev}")
+    shard = dict(spp=s1 - s0, spp_total=spp, sample_offset=s0, out=film, device=rk.dev)
+    cls({"iterations": 1}).render_film(sc, seed=99, **shard)  # warm-up
     rk.barrier()
     t0 = time.perf_counter()
     st = None
     for k in range(args.steps):
-        st = _sum_stats(st, integ.render_film(sc, seed=k, spp=spp, y0=y0, y1=y1, out=film, stats=True,
-                                              device=rk.dev)[1])
-        rk.gather(film, sc.height)
+        st = _sum_stats(st, integ.render_film(sc, seed=k, stats=True, **shard)[1])
+        if rk.world > 1:
+            distributed.gather_sum(film)
     rk.barrier()
     dt = rk.max_elapsed(time.perf_counter() - t0) / args.steps
     st = {x: v / args.steps for x, v in st.items()}
-    cnt = integ.render_film(sc, seed=0, spp=spp, y0=y0, y1=y1, out=film, stats=True, counters=True,
-                            device=rk.dev)[1]
+    # visit counters (untimed): one short render of the same chains
+    cnt = cls({"iterations": min(it, 20)}).render_film(sc, seed=0, stats=True, counters=True, **shard)[1]
     chains = sc.width * sc.height * spp
     cpu = None
     if rk.world == 1:
-        # CPU: the oracle on a band of rows, same chains per pixel and iterations
+        # CPU: the oracle on whole film rows at 16 chains per pixel (the cost
+        # per chain-iteration does not depend on the chain count), same
+        # iterations, rows sized to the CPU budget
         oracle.build()
-        a1 = integ.render_args(sc, 0, spp, 0, 1)
+        cs = min(spp, 16)
+        a1 = integ.render_args(sc, 0, cs, 0, 1)
         t1 = time.perf_counter()
         oracle.pssmlt_render(sc, a1, it)
         c1 = time.perf_counter() - t1
         rows = max(1, min(sc.height, int(args.cpu_seconds / max(c1, 1e-3))))
-        a = integ.render_args(sc, 0, spp, 0, rows)
+        a = integ.render_args(sc, 0, cs, 0, rows)
         t1 = time.perf_counter()
         oracle.pssmlt_render(sc, a, it)
         c = time.perf_counter() - t1
-        cpu = {"value": round(sc.width * rows * spp * it / c / 1e6, 4), "unit": "Mchain-iterations/s",
+        cpu = {"value": round(sc.width * rows * cs * it / c / 1e6, 4), "unit": "Mchain-iterations/s",
                "cores": _threads(), "kind": "port",
-               "sample": f"{rows} of {sc.height} rows x {sc.width} px x {spp} chains x {it} iterations ({c:.1f} s); "
+               "sample": f"{rows} of {sc.height} rows x {sc.width} px x {cs} chains x {it} iterations ({c:.1f} s); "
                          "oracle/oracle.cpp orc_pssmlt_render (OpenMP)"}
     if rk.rank == 0:
         script = "pssmltpath.py (NEE + MIS)" if with_nee else "pssmltsimple.py"
+        par = f"chain-range shards x{rk.world}" + (", RCCL gather of films to rank 0" if rk.world > 1 else "")
         _line(f"PSSMLT{'-path' if with_nee else ''} Mchain-iterations/sec on bedroom@1280x720, {spp} chains/pixel (C3)",
               chains * it / dt / 1e6, "Mchain-iterations/s", args.steps, 1, dt * 1e3,
               {"workload": f"{script} + pssmlt.py render, {it} iterations (large step every 50, aggregate "
                            f"i%50>40), max_depth 16, rr_depth 4, {chains} chains", "chains": chains,
-               "iterations": it, "parallelism": rk.parallelism()},
-              _trace_roofline(cnt, st["trace_ms"], "step"), cpu,
+               "iterations": it, "aggregation_iterations": sum(1 for i in range(it) if i % 50 > 40),
+               "chains_per_rank": sc.width * sc.height * (s1 - s0), "parallelism": par},
+              _trace_roofline(cnt, st["trace_ms"], "step", st["trace_launches"]), cpu,
               {"kernels_ms_per_step": {"trace_closest": round(st["trace_ms"], 3), "shade": round(st["shade_ms"], 3),
                                        "trace_shadow": round(st["shadow_ms"], 3), "other": round(st["other_ms"], 3)},
                "n_gpus": rk.world, "scaling": "strong" if rk.world > 1 else "weak"})
