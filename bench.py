@@ -17,17 +17,23 @@ GPU) and exits with their status; under torchrun WORLD_SIZE must equal N.
 
 Prints ONE JSON line on rank 0 (contract in the task statement) with
 `roofline` for the closest-hit traversal kernel and `cpu_baseline` (the
-oracle/ CPU restatement on a bounded sample, N=1 only). The roofline is
-stated against the memory level that serves the traversal's bytes: the
-algorithmic bytes (32 + 16 + 64 N_node + 48 N_tri per ray, exact
-visit counts from the in-kernel counters of one extra, untimed step) divided
-by the HIP-event time of the launches, against the L2-resident random-gather
-rate of MI355X_MICROARCH.md ("Indexed rows: gather into LDS", 16.8-18.8 TB/s).
-Its `hbm` sub-object is the DRAM/fabric side: the committed rocprofv3 PMC
-traffic of the same kernel (FETCH_SIZE x2 + WRITE_SIZE per launch,
-profiles/*_pmc_traffic.json) over the same launch time, against the 8 TB/s
-HBM peak; the PMC file is used only when its recorded source hash and bench
-arguments match this build and this run (otherwise `traffic` is null).
+oracle/ CPU restatement on a bounded sample, N=1 only).
+
+The roofline names the unit that bounds the traversal: its vector-memory
+address path (TA/TCP, "vmem"). The achieved rate is the algorithmic bytes
+(32 + 16 + 64 N_node + 36 N_tri per ray, exact visit counts from
+the in-kernel counters of one extra, untimed step) over the HIP-event time of
+the launches; the peak is that path's byte rate (64 B per CU-cycle, measured
+by tools/probes/ta_rate.hip: 1 KiB wave-loads in <= 16 lines at 17 cycles). The
+committed rocprofv3 unit counters of the same build (profiles/*_pmc_units.json,
+tools/pmc_units.py) give the occupancy beside it: TA busy ~0.8 of the
+kernel's cycles at ~0.3 of the byte peak, because a divergent gather costs
+the TA one cycle per distinct 128-B line per instruction (the probe: 64
+lanes on 64 L1 lines 65 cycles, on L2 lines 142), so the bound is the line
+rate of gathers, not bytes. The `hbm` sub-object is the DRAM/fabric side
+(FETCH_SIZE x2 + WRITE_SIZE per launch, profiles/*_pmc_traffic.json) against
+the 8 TB/s HBM peak. PMC files are used only when their recorded source hash
+and bench arguments match this build and this run (otherwise null).
 """
 import argparse
 import hashlib
@@ -46,7 +52,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured 
 # MI355X_MICROARCH.md "Indexed rows: gather into LDS": rows shared by every
 # workgroup, served from the XCD's L2: 16.8-18.8 TB/s chip-wide (upper end).
 L2_GATHER_PEAK_GBS = 18800.0
-L2_STREAM_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md "L2 (per XCD)": ~34.5 TB/s aggregate
+# vector-memory (TA/TCP) byte path: 1 KiB per 16.9 CU-cycles for a wave64
+# dwordx4 load touching <= 16 lines (tools/probes/ta_rate.hip, profiles/r3_ta_rate.txt),
+# x 256 CUs x 2.4 GHz
+VMEM_PEAK_GBS = round(1024 / 16.9 * 256 * 2.4, 0)
 # node and triangle records as the device reads them (triangles packed to 36 B, mtx_scene_upload)
 NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES, OCC_BYTES = 64, 36, 32, 16, 4
 # SURVEY §8d wavefront path state per lane per bounce, read + written
@@ -127,6 +136,28 @@ def measured_traffic(kernels, key):
         ks = d.get("kernels", {})
         return {k: (int(ks[k]["hbm_bytes_per_launch"]) if k in ks else None) for k in kernels}, \
             os.path.relpath(f, ROOT)
+    return {k: None for k in kernels}, reason
+
+
+def measured_units(kernels, key):
+    """Unit occupancy per launch of each kernel in `kernels` (TA busy, VALU
+    busy, ...) from the newest committed profiles/*_pmc_units.json
+    (tools/pmc_units.py) whose src_sha and bench key match. Returns
+    ({kernel: dict or None}, source or reason)."""
+    sha = src_sha()
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_units.json")), key=os.path.getmtime)
+    reason = "no profiles/*_pmc_units.json"
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("src_sha") != sha:
+            reason = f"stale: {os.path.basename(f)} src_sha {d.get('src_sha')} != {sha}"
+            continue
+        if d.get("bench_key") != key:
+            reason = f"{os.path.basename(f)}: bench args differ"
+            continue
+        ks = d.get("kernels", {})
+        keep = ("ta_busy", "valu_busy", "salu_busy", "l1_l2_read_bytes_per_launch", "ta_cycles_per_vmem")
+        return {k: ({x: ks[k][x] for x in keep} if k in ks else None) for k in kernels}, os.path.relpath(f, ROOT)
     return {k: None for k in kernels}, reason
 
 
@@ -235,7 +266,10 @@ def main():
              "shade": "mtxd::k_shade<2>"}
     traffic, traffic_src = (measured_traffic(list(names.values()), traffic_key(args)) if world == 1
                             else ({k: None for k in names.values()}, "N>1: PMC profiles are N=1"))
+    units, units_src = (measured_units(list(names.values()), traffic_key(args)) if world == 1
+                        else ({k: None for k in names.values()}, "N>1: PMC profiles are N=1"))
     tc = traffic[names["closest"]]
+    uc = units[names["closest"]]
     launch_s = trace_s / launches
     hbm_ach = tc / launch_s / 1e9 if (tc is not None and launch_s > 0) else None
     if rank == 0:
@@ -243,15 +277,17 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(sc, integ, args)
         kernels = {
-            "trace_closest": _kernel_entry(trace_ms, launches, tc, alg_closest, L2_GATHER_PEAK_GBS, "l2"),
+            "trace_closest": _kernel_entry(trace_ms, launches, tc, alg_closest, VMEM_PEAK_GBS, "vmem"),
             "trace_shadow": dict(_kernel_entry(agg["shadow_ms"] / K, cnt["shadow_launches"], traffic[names["shadow"]],
-                                               alg_shadow, L2_GATHER_PEAK_GBS, "l2"),
+                                               alg_shadow, VMEM_PEAK_GBS, "vmem"),
                                  rays_per_step=int(cnt["rays_shadow"]),
                                  node_visits_per_ray=round(cnt["nodes_shadow"] / max(1, cnt["rays_shadow"]), 2),
                                  tri_visits_per_ray=round(cnt["tris_shadow"] / max(1, cnt["rays_shadow"]), 2)),
             "shade": _kernel_entry(agg["shade_ms"] / K, cnt["trace_launches"], traffic[names["shade"]],
                                    cnt["rays_closest"] * SHADE_BYTES_PER_PATH_BOUNCE, HBM_PEAK_GBS, "hbm"),
         }
+        for kk, nn in names.items():
+            kernels[kk]["units"] = units[nn]
         # the roofline object follows north_star's traversal kernel; the
         # kernel with the most time per step is named beside it
         big = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
@@ -281,18 +317,22 @@ def main():
                 "parallelism": f"sample-range shards x{world}" + (", RCCL gather of films to rank 0" if world > 1 else ""),
             },
             "roofline": {
-                "bound": "l2",
+                "bound": "vmem",
                 "kernel": "k_trace_closest (4-wide quantised BVH, closest hit)",
                 "achieved": round(achieved, 1),
-                "peak": L2_GATHER_PEAK_GBS,
+                "peak": VMEM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": round(achieved / L2_GATHER_PEAK_GBS, 4),
+                "frac": round(achieved / VMEM_PEAK_GBS, 4),
                 "traffic": tc,
                 "traffic_source": traffic_src,
-                "peak_source": "MI355X_MICROARCH.md 'Indexed rows: gather into LDS': L2-served random row "
-                               "gathers 16.8-18.8 TB/s chip-wide (node array + triangles stay in L2 / Infinity "
-                               "Cache: PMC fabric traffic << algorithmic bytes)",
-                "frac_vs_l2_stream_peak": round(achieved / L2_STREAM_PEAK_GBS, 4),
+                "peak_source": "vector-memory (TA/TCP) byte path, 64 B/CU-cycle: tools/probes/ta_rate.hip "
+                               "(profiles/r3_ta_rate.txt) x 256 CUs x 2.4 GHz",
+                "units": uc,
+                "units_source": units_src,
+                "bound_reason": "TA (vector-memory address path) is the busiest unit of the kernel (units.ta_busy "
+                                "vs units.valu_busy); gathers cost the TA one cycle per distinct 128-B line per "
+                                "instruction, so it saturates at a fraction of its byte peak",
+                "frac_vs_l2_gather_peak": round(achieved / L2_GATHER_PEAK_GBS, 4),
                 "hbm": None if hbm_ach is None else {
                     "achieved": round(hbm_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(hbm_ach / HBM_PEAK_GBS, 4),

@@ -272,8 +272,12 @@ int mtx_set_camera(mtx_ctx *ctx, const mtx_camera *camera);
 /* Copy rows [row0, row0+nrows) of the ReSTIR GI state to (to_state = 0) or
  * from (to_state = 1) a device buffer, plane-major (planes x rows x W*spp
  * float4): which = 0 the current frame's samples (5 planes), 1 the temporal
- * reservoirs (6 planes). The halo exchange of a row-banded frame
- * (restirgi.py:301-313 reads up to search_radius rows away). */
+ * reservoirs (6 planes), 2 the previous frame's samples (5 planes; between
+ * frames only: the buffer temporal resampling reprojects into,
+ * restirgi.py:374-383). The halo exchange of a row-banded frame
+ * (restirgi.py:301-313 reads up to search_radius rows away; a
+ * moving camera reprojects arbitrarily far, so a banded caller gathers the
+ * whole previous-sample buffer with which = 2 before stage A). */
 int mtx_restir_rows(mtx_ctx *ctx, int which, uint32_t row0, uint32_t nrows, void *buf, int to_state);
 
 /* Read back ReSTIR GI frame state (test / debugging hook for restirgi.py's

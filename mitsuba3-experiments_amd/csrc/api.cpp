@@ -135,10 +135,10 @@ struct mtx_ctx {
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
+  uint32_t lds_top = MTX_LDS_TOP;  // wide nodes of the tree top kept in LDS per block (MTX_LDS_TOP env: A/B)
   uint32_t trace_batch = 256;
   uint32_t refill_lanes = 16;
   uint32_t urefill = 24;  // unified loop: refill once 24 lanes are idle (16: closest +1.3 %, 32: +2 %)
-  uint32_t tri_min = 0;  // trace_loop_u: triangle step deferred until this many lanes wait on one
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
@@ -189,11 +189,11 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   c->trace_grid = c->n_cu * 8;
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
+  if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_TRI_MIN")) c->tri_min = (uint32_t)std::max(0, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
@@ -402,10 +402,12 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.stack_entries = 3 * bvh_depth + 1;
   s.camera = d->camera;
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
+  // LDS copy of the tree top (64-B nodes only): with 16 stack entries per
+  // lane and 16 blocks of 128 threads per CU, 32 nodes fill the 160 KB
+  s.lds_top = MTX_NODE48 ? 0u : std::min<uint32_t>(d->n_nodes, c->lds_top);
   s.trace_batch = c->trace_batch;
   s.refill_lanes = c->refill_lanes;
   s.urefill = c->urefill;
-  s.tri_min = c->tri_min;
   s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
   s.shade_sort = c->shade_sort;
@@ -1020,7 +1022,7 @@ int mtx_set_camera(mtx_ctx *c, const mtx_camera *cam) {
 }
 
 int mtx_restir_rows(mtx_ctx *c, int which, uint32_t row0, uint32_t nrows, void *buf, int to_state) {
-  if (!c || !buf || which < 0 || which > 1) {
+  if (!c || !buf || which < 0 || which > 2) {
     mtx_set_error("mtx_restir_rows: bad argument");
     return MTX_E_ARG;
   }
@@ -1035,9 +1037,15 @@ int mtx_restir_rows(mtx_ctx *c, int which, uint32_t row0, uint32_t nrows, void *
   }
   const size_t n = c->rs_n, per_row = n / H;  // lanes per row (W * spp)
   (void)W;
-  const int planes = which == 0 ? 5 : 6;
-  // which = 0: the current frame's samples (before stage B swaps them)
-  char *state = (char *)(which == 0 ? c->rs_samp[c->rs_cur].p : c->rs_tres.p);
+  if (which == 2 && (!c->rs_valid || c->rs_pending_b)) {
+    mtx_set_error("mtx_restir_rows: the previous frame's samples exist between complete frames only");
+    return MTX_E_ARG;
+  }
+  const int planes = which == 1 ? 6 : 5;
+  // which = 0: the current frame's samples (before stage B swaps them);
+  // 2: the previous frame's (what k_rs_temporal reads through prev_cam)
+  char *state = (char *)(which == 0 ? c->rs_samp[c->rs_cur].p
+                                    : which == 2 ? c->rs_samp[c->rs_cur ^ 1].p : c->rs_tres.p);
   char *dev = (char *)buf;
   HIP_TRY(hipSetDevice(c->device));
   for (int k = 0; k < planes; ++k) {

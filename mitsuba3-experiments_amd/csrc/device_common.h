@@ -21,8 +21,10 @@ inline size_t stack_bytes(const DevScene &s) { return (size_t)s.stack_entries * 
 // The persistent kernels keep only the top s.lds_entries entries in LDS (so
 // LDS does not cap occupancy) and spill deeper entries to a per-thread global
 // area ([entry - lds_entries][thread], coalesced per depth), rarely touched.
+// Behind the stack columns each block holds an LDS copy of the first
+// s.lds_top wide nodes (the top of the breadth-first tree, 64 B each).
 inline size_t persistent_stack_bytes(const DevScene &s) {
-  return (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t);
+  return (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t) + (size_t)s.lds_top * 64;
 }
 constexpr int kShadeBlock = 256;
 
@@ -263,12 +265,41 @@ __device__ __forceinline__ int32_t wide_dref(uint32_t key, uint32_t ends, uint32
 #define MTX_NODE48 0  // A/B: 1 = the 48-B node (three loads, references decoded): slower, DESIGN.md
 #endif
 __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
-                                          int32_t c[4]) {
+                                          int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
 #if !MTX_NODE48
   {
-    const int4 *np = s.nodes + 4 * node;
-    const int4 a = np[0], rf = np[1], qa = np[2];
-    const int2 qb = *reinterpret_cast<const int2 *>(np + 3);
+    // nodes [0, top_n) from the block's LDS copy of the tree top (40-47 % of
+    // the visits, tools/top_visits.py), the others from global memory
+    // (the LDS reads are inline asm: as plain loads the compiler merges the
+    // two branches into flat loads through a selected generic pointer, which
+    // take the vector-memory path for every lane)
+    int4 a, rf, qa;
+    int2 qb;
+    if (node < top_n) {
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      typedef int v2i __attribute__((ext_vector_type(2)));
+      v4i x0, x1, x2;
+      v2i x3;
+      const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 64u * (uint32_t)node;
+      asm volatile(
+          "ds_read_b128 %0, %4\n\t"
+          "ds_read_b128 %1, %4 offset:16\n\t"
+          "ds_read_b128 %2, %4 offset:32\n\t"
+          "ds_read_b64 %3, %4 offset:48\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+          : "v"(la));
+      a = make_int4(x0.x, x0.y, x0.z, x0.w);
+      rf = make_int4(x1.x, x1.y, x1.z, x1.w);
+      qa = make_int4(x2.x, x2.y, x2.z, x2.w);
+      qb = make_int2(x3.x, x3.y);
+    } else {
+      const int4 *np = s.nodes + 4 * node;
+      a = np[0];
+      rf = np[1];
+      qa = np[2];
+      qb = *reinterpret_cast<const int2 *>(np + 3);
+    }
     uint32_t key[4];
     const uint32_t eb = (uint32_t)a.w;
 #if MTX_PAIR_SORT
@@ -438,8 +469,8 @@ __device__ __forceinline__ uint32_t xseg_bound(uint32_t count, uint32_t k) {
 // wave on to the next XCD's segment.
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
-                                              int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
-                                              uint32_t *wave_iters = nullptr) {
+                                              int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
+                                              uint32_t &nr, uint32_t *wave_iters = nullptr) {
   const uint32_t lane = lane_id();
   int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
   const int lds_n = (int)s.lds_entries;
@@ -451,6 +482,7 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
   float tbest = 0.f, bu = 0.f, bv = 0.f;
   int32_t node = kTravDone, leaf = 0;
   bool has_leaf = false;
+  const int top_n = (int)s.lds_top;
   int sp = 0;
   const bool spec = !STATS && s.speculate;
   // more waves than batches: the surplus exits at once (a near-empty queue
@@ -551,7 +583,7 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
         }
         int32_t cr[4];
         ++nv;
-        const int n = wide_visit(s, r, node, tbest, cr);
+        const int n = wide_visit(s, r, node, tbest, cr, top, top_n);
         if (n > 0) {
           // far children pushed farthest first: entries sp .. sp+n-2 hold
           // cr[n-1] .. cr[1]. Branch-free: three stores, the ones beyond
@@ -654,10 +686,13 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
 // the plain front-to-back order of `traverse` (the oracle's), with or
 // without STATS.
 // ---------------------------------------------------------------------------
+#ifndef MTX_TRI_MIN
+#define MTX_TRI_MIN 0
+#endif
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
-                                             int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
-                                             uint32_t *wave_iters = nullptr) {
+                                             int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
+                                             uint32_t &nr, uint32_t *wave_iters = nullptr) {
   const uint32_t lane = lane_id();
   int32_t *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
   const int lds_n = (int)s.lds_entries;
@@ -668,6 +703,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
   TraceRay r;
   float tbest = 0.f, bu = 0.f, bv = 0.f;
   int32_t node = -1;          // >= 0: inner node to visit next
+  const int top_n = (int)s.lds_top;
   uint32_t tri = 0, tri_end = 0;  // triangles [tri, tri_end) of the current leaf
   int sp = 0;
   const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
@@ -761,7 +797,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
       }
       int32_t cr[4];
       ++nv;
-      const int n = wide_visit(s, r, node, tbest, cr);
+      const int n = wide_visit(s, r, node, tbest, cr, top, top_n);
       if (n > 0) {
         const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
         const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
@@ -796,13 +832,14 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         pop_next();
       }
     }
-    // ---- one triangle test. Deferred (s.tri_min > 0) until enough lanes
-    // wait on a triangle or no lane has a node to visit: the step then runs
-    // with more lanes busy; every ray's own visit sequence is unchanged.
+    // ---- one triangle test. Deferred (MTX_TRI_MIN > 0, an A/B build that
+    // measured slower at every threshold) until enough lanes wait
+    // on a triangle or no lane has a node to visit; every ray's own visit
+    // sequence is unchanged.
     bool tri_step = true;
-    if (s.tri_min) {
+    if (MTX_TRI_MIN) {
       const uint32_t nt = (uint32_t)__popcll(__ballot(has && tri < tri_end));
-      tri_step = nt >= s.tri_min || __ballot(has && node >= 0) == 0;
+      tri_step = nt >= MTX_TRI_MIN || __ballot(has && node >= 0) == 0;
     }
     if (tri_step && has && tri < tri_end) {
       if (STATS) {
@@ -840,14 +877,19 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
 #ifndef MTX_TRAV_UNIFIED
 #define MTX_TRAV_UNIFIED 1
 #endif
+// stk: this thread's stack column (dynamic LDS + threadIdx.x). Every thread
+// of the block calls this (the LDS tree top is filled behind a barrier).
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                            int32_t *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
                                            uint32_t *wave_iters = nullptr) {
+  int4 *top = reinterpret_cast<int4 *>(stk - threadIdx.x + s.lds_entries * kTraceBlock);
+  for (uint32_t i = threadIdx.x; i < 4 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
+  __syncthreads();
   if ((MTX_TRAV_UNIFIED >> (ANY ? 1 : 0)) & 1)
-    trace_loop_u<ANY, STATS>(s, src, count, heads, stk, nv, tv, nr, wave_iters);
+    trace_loop_u<ANY, STATS>(s, src, count, heads, stk, top, nv, tv, nr, wave_iters);
   else
-    trace_loop_ww<ANY, STATS>(s, src, count, heads, stk, nv, tv, nr, wave_iters);
+    trace_loop_ww<ANY, STATS>(s, src, count, heads, stk, top, nv, tv, nr, wave_iters);
 }
 
 }  // namespace mtxd

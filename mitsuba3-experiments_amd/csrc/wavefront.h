@@ -33,6 +33,9 @@ enum : uint32_t {
 
 constexpr int kTraceBlock = 128;     // threads per traversal block
 constexpr uint32_t kLdsStack = 16;   // default LDS part of the persistent traversal stack (entries per lane)
+#ifndef MTX_LDS_TOP
+#define MTX_LDS_TOP 32  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
+#endif
 
 // Per-XCD claim cursors of the persistent trace kernels: kXcds words,
 // kXHeadStride words (128 B) apart; one slot per trace launch of a chunk.
@@ -58,12 +61,12 @@ struct DevScene {
   uint32_t n_tris, n_emitters;
   uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane)
   uint32_t lds_entries;    // persistent kernels: stack entries kept in LDS
+  uint32_t lds_top;        // persistent kernels: wide nodes [0, lds_top) read from a per-block LDS copy
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
   int32_t *stack_ovf;      // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
   uint32_t refill_lanes;   // persistent kernels: refill a wave once this many lanes are idle
   uint32_t urefill;        // unified single-step traversal (trace_loop_u): the same, its own threshold
-  uint32_t tri_min;        // trace_loop_u: run the triangle step once this many lanes wait on one (or no lane has a node)
   uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   uint32_t shade_sort;     // k_shade: order a block's paths by the hit's shading class

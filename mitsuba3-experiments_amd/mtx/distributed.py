@@ -142,7 +142,9 @@ def render_sharded(render, height: int, spp: int, mode: str = "samples", group=N
 def restir_halo(integ) -> int:
     """Halo rows a band needs from each neighbour: the spatial taps reach
     trunc(radius) <= initial_search_radius rows (the radius only shrinks), the
-    temporal reprojection of a static camera one row."""
+    temporal reprojection of a static camera one row. A camera that moved
+    since the previous frame reprojects arbitrarily far: render_restir_sharded
+    then gathers the whole previous-sample buffer (gather_prev_samples)."""
     import math
 
     return max(1, int(math.ceil(float(integ.initial_search_radius))))
@@ -208,7 +210,7 @@ def device_row_io(integ, scene, spp: int = 1, ctx=None):
     dev = torch.device("cuda", (ctx.device if ctx is not None else torch.cuda.current_device()))
 
     def export_rows(which, row0, nrows):
-        planes = 5 if which == "sample" else 6
+        planes = 6 if which == "temporal" else 5
         t = torch.empty((planes, nrows, lanes_per_row, 4), dtype=torch.float32, device=dev)
         integ.rows(which, row0, nrows, t, to_state=False, ctx=ctx)
         return t
@@ -219,17 +221,53 @@ def device_row_io(integ, scene, spp: int = 1, ctx=None):
     return export_rows, import_rows
 
 
+def gather_prev_samples(export_rows, import_rows, y0: int, y1: int, height: int, group=None):
+    """Give every rank the previous frame's samples of the whole film: each
+    rank contributes its band rows [y0, y1) (what its last stage A wrote), one
+    all_gather (bands padded to the tallest), then the other ranks' rows are
+    imported. Temporal resampling (restirgi.py:374-383) gathers prev_sample at
+    the pixel the current hit reprojects to through the previous camera; with
+    a moving camera that pixel can lie in any band. Costs 80 B per lane."""
+    import torch
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    bands = row_bands(height, world)
+    maxrows = max(b1 - b0 for b0, b1 in bands)
+    mine = export_rows("prev_sample", y0, y1 - y0)
+    dev = mine.device
+    mine = _comm(mine, group)
+    buf = torch.zeros((mine.shape[0], maxrows) + tuple(mine.shape[2:]), dtype=mine.dtype, device=mine.device)
+    buf[:, : y1 - y0] = mine
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    for r, (b0, b1) in enumerate(bands):
+        if r != rank and b1 > b0:
+            import_rows("prev_sample", b0, parts[r][:, : b1 - b0].contiguous().to(dev))
+
+
 def render_restir_sharded(integ, scene, seed: int, spp: int = 1, group=None):
     """Row-banded ReSTIR GI frame over torch.distributed (one rank per GPU):
-    returns the stitched film on rank 0 (None elsewhere)."""
+    returns the stitched film on rank 0 (None elsewhere).
+
+    Static camera: one halo exchange of ceil(initial_search_radius) rows of
+    samples and temporal reservoirs between stage A and stage B. When the
+    camera moved since the previous frame (test-restir-dynamic.py:25-32), the
+    previous frame's samples of the whole film are gathered first
+    (gather_prev_samples), so the reprojection reads the same samples as a
+    single-GPU frame wherever it lands."""
     import torch.distributed as dist
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     y0, y1 = row_bands(scene.height, world)[rank]
     halo = restir_halo(integ)
     ex, im = device_row_io(integ, scene, spp)
+    cam = bytes(scene.camera)
+    if integ.n > 0 and getattr(integ, "_shard_prev_cam", cam) != cam:
+        gather_prev_samples(ex, im, y0, y1, scene.height, group)
     film = restir_band_frame(integ, scene, seed, y0, y1,
                              lambda: exchange_halos(ex, im, y0, y1, scene.height, halo, group), spp)
+    integ._shard_prev_cam = cam
     return gather_bands(film, y0, y1, scene.height, group)
 
 

@@ -384,10 +384,12 @@ class RestirIntegrator(SamplingIntegrator):
 
     def rows(self, which: str, row0: int, nrows: int, buf, to_state: bool, ctx=None) -> None:
         """Copy state rows to / from a device tensor (halo exchange):
-        which = 'sample' (5 planes) or 'temporal' (6 planes); buf is a
+        which = 'sample' (5 planes), 'temporal' (6 planes) or 'prev_sample'
+        (5 planes: the previous frame's samples, between frames; a moving
+        camera's reprojection reads them anywhere in the film); buf is a
         contiguous [planes, nrows, W*spp, 4] float32 tensor on the device."""
         ctx = ctx or getattr(self, "_ctx", None) or context()
-        idx = {"sample": 0, "temporal": 1}[which]
+        idx = {"sample": 0, "temporal": 1, "prev_sample": 2}[which]
         check(lib().mtx_restir_rows(ctx.handle, idx, int(row0), int(nrows), C.c_void_p(buf.data_ptr()),
                                     int(bool(to_state))), "mtx_restir_rows")
 

@@ -36,6 +36,7 @@ def lib():
         SD, RA = C.POINTER(_abi.SceneDesc), C.POINTER(_abi.RenderArgs)
         sig = {
             "orc_trace": [SD, u64, vp, C.c_int, C.c_int, vp, vp],
+            "orc_node_visit_hist": [SD, u64, vp, C.c_int, vp, C.c_uint32],
             "orc_sample_rays": [SD, RA, u64, vp, vp, u32, vp, vp],
             "orc_render_samples": [SD, RA, vp, vp],
             "orc_render_samples_q": [SD, RA, vp, vp, vp],
@@ -125,6 +126,15 @@ def trace(scene, rays, any_hit=False, brute=False):
     lib().orc_trace(C.byref(d), n, np.ascontiguousarray(rays, np.float32).ctypes.data, int(any_hit), int(brute),
                     hits.ctypes.data, visits.ctypes.data)
     return hits, visits.reshape(n, 2)
+
+
+def node_visit_hist(scene, rays, hist_len, any_hit=False):
+    """Visits per node index < hist_len over `rays` (diagnostic for tools/)."""
+    hist = np.zeros(hist_len, np.uint64)
+    d = scene.desc()
+    lib().orc_node_visit_hist(C.byref(d), len(rays), np.ascontiguousarray(rays, np.float32).ctypes.data,
+                              int(any_hit), hist.ctypes.data, int(hist_len))
+    return hist
 
 
 def rng_stream(seed, lane0, n_lanes, n_draws):

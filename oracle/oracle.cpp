@@ -84,6 +84,12 @@ struct Hit {
 // ascending entry distance (near-ties by slot); the nearest is visited next,
 // the others are pushed farthest first. Closest-hit ties on t go to the smaller prim, so the
 // hit does not depend on the order; the visit counts do, and match the device.
+// Diagnostic (tools/ only): visits per node index < g_hist_len are counted
+// into g_hist while orc_node_visit_hist runs (the top-of-tree share of node
+// fetches that an LDS-resident tree top would serve).
+static uint64_t *g_hist = nullptr;
+static uint32_t g_hist_len = 0;
+
 template <bool ANY>
 bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *nodes_visited,
                 uint32_t *tris_visited) {
@@ -100,6 +106,10 @@ bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *
       const int32_t *w = s.nodes + 16 * (size_t)node;
       const float *f = reinterpret_cast<const float *>(w);
       ++nv;
+      if (g_hist && (uint32_t)node < g_hist_len) {
+#pragma omp atomic
+        ++g_hist[node];
+      }
       uint32_t key[4];
       const int n = wide_node_order(r, f[0], f[1], f[2], (uint32_t)w[3], (uint32_t)w[8], (uint32_t)w[9],
                                     (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], tbest, key);
@@ -590,6 +600,18 @@ int orc_trace(const mtx_scene_desc *d, uint64_t n, const float *rays, int any_hi
     }
   }
   return 0;
+}
+
+// orc_trace with the per-node visit histogram of nodes [0, hist_len) (tools/ diagnostic)
+int orc_node_visit_hist(const mtx_scene_desc *d, uint64_t n, const float *rays, int any_hit, uint64_t *hist,
+                        uint32_t hist_len) {
+  std::vector<uint32_t> hits(any_hit ? n : 4 * n);
+  g_hist = hist;
+  g_hist_len = hist_len;
+  const int rc = orc_trace(d, n, rays, any_hit, 0, hits.data(), nullptr);
+  g_hist = nullptr;
+  g_hist_len = 0;
+  return rc;
 }
 
 // SamplingIntegrator.sample() for given rays (see mtx_sample_rays).

@@ -141,6 +141,49 @@ def test_restir_halo_exchange(tmp_path, world, height, halo):
         assert bool(np.load(os.path.join(tmp_path, f"ok{r}.npy"))[0]), f"rank {r}"
 
 
+def _prev_worker(rank, world, port, height, out_dir):
+    """gather_prev_samples with a fake state: each rank holds only its band of
+    the previous frame's samples; afterwards every rank holds the whole film's."""
+    import sys
+
+    sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd")]
+    import torch
+    import torch.distributed as dist
+
+    from mtx import distributed
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    y0, y1 = distributed.row_bands(height, world)[rank]
+    lanes = 3
+    truth = torch.arange(5 * height * lanes * 4, dtype=torch.float32).view(5, height, lanes, 4)
+    state = torch.full_like(truth, -1.0)
+    state[:, y0:y1] = truth[:, y0:y1]
+
+    def export_rows(which, row0, nrows):
+        assert which == "prev_sample"
+        return state[:, row0:row0 + nrows].contiguous()
+
+    def import_rows(which, row0, t):
+        assert which == "prev_sample" and not (y0 <= row0 < y1)
+        state[:, row0:row0 + t.shape[1]] = t
+
+    distributed.gather_prev_samples(export_rows, import_rows, y0, y1, height)
+    np.save(os.path.join(out_dir, f"ok{rank}.npy"), np.array([bool(torch.equal(state, truth))]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,height", [(2, 27), (3, 10)])
+def test_restir_moving_camera_gathers_prev_samples(tmp_path, world, height):
+    """A moving camera reprojects into any band (restirgi.py:374-383): the
+    previous frame's samples of the whole film reach every rank (ragged bands)."""
+    mp.start_processes(_prev_worker, args=(world, _free_port(), height, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        assert bool(np.load(os.path.join(tmp_path, f"ok{r}.npy"))[0]), f"rank {r}"
+
+
 def test_sample_range_needs_a_sample_per_rank():
     """spp < world would leave a rank with an empty range (mtx_render
     rejects spp 0) while the others wait in the gather: every rank raises alike."""

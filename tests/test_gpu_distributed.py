@@ -17,6 +17,25 @@ RESTIR_PROPS = {"jacobian": False, "bias_correction": True, "max_M_spatial": 500
                 "initial_search_radius": 6.0}
 
 
+# small search radius (2-row halo) and a camera that rises 0.4 along its up
+# axis per frame (test-restir-dynamic.py:25-32 moves the sensor every frame):
+# reprojections land well outside a 13-row band's halo
+RESTIR_MOVING = {"jacobian": False, "bias_correction": False, "max_M_spatial": 500, "max_M_temporal": 30,
+                 "initial_search_radius": 2.0}
+
+
+def _moving_cameras(sc, frames=4):
+    from mtx import _abi
+
+    cams = []
+    for fr in range(frames):
+        c = _abi.Camera.from_buffer_copy(bytes(sc.camera))
+        for k in range(3):
+            c.origin[k] += 0.4 * fr * c.axis_y[k]
+        cams.append(c)
+    return cams
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -80,6 +99,13 @@ def _worker(rank, world, port, kind, out_dir):
         integ = load_dict({"type": "restirgi", **RESTIR_PROPS})
         for fr in range(3):
             films.append(distributed.render_restir_sharded(integ, sc, seed=fr))
+    elif kind.startswith("restir_moving"):
+        if kind.endswith("nogather"):  # sensitivity check: the halo alone
+            distributed.gather_prev_samples = lambda *a, **k: None
+        integ = load_dict({"type": "restirgi", **RESTIR_MOVING})
+        for fr, cam in enumerate(_moving_cameras(sc)):
+            sc.camera = cam
+            films.append(distributed.render_restir_sharded(integ, sc, seed=fr))
     if rank == 0:
         np.save(os.path.join(out_dir, "films.npy"), np.stack([f.cpu().numpy() for f in films]))
     dist.barrier()
@@ -140,6 +166,28 @@ def test_two_rank_restir_frames(tmp_path):
     for fr in range(3):
         ref = integ.render_film(sc, seed=fr, spp=1)
         np.testing.assert_allclose(got[fr], ref, rtol=2e-6, atol=1e-6, err_msg=f"frame {fr}")
+
+
+@pytest.mark.gpu
+def test_two_rank_restir_moving_camera(tmp_path):
+    """row-banded ReSTIR GI with a camera that moves every frame.
+    Temporal resampling reprojects into the previous camera (restirgi.py:374-383),
+    beyond the spatial halo; render_restir_sharded gathers the previous frame's
+    samples of the whole film first, so every sharded frame equals the
+    single-GPU frame (rtol 2e-6). Without that gather (the halo alone) the
+    frames differ: the test sees the reprojection leave the halo."""
+    from mtx import load_dict
+
+    got = _run("restir_moving", tmp_path)
+    sc = _scene()
+    integ = load_dict({"type": "restirgi", **RESTIR_MOVING})
+    refs = []
+    for fr, cam in enumerate(_moving_cameras(sc)):
+        sc.camera = cam
+        refs.append(integ.render_film(sc, seed=fr, spp=1))
+        np.testing.assert_allclose(got[fr], refs[fr], rtol=2e-6, atol=1e-6, err_msg=f"frame {fr}")
+    bad = _run("restir_moving_nogather", tmp_path)
+    assert any(not np.allclose(bad[fr], refs[fr], rtol=2e-6, atol=1e-6) for fr in range(1, len(refs)))
 
 
 @pytest.mark.gpu

@@ -14,7 +14,8 @@ the full bedroom proxy (1,832,004 triangles), bit-exact against the oracle.
   quarter of that on the GPU box's 16 (3 Mchain-it/s, profiles/r2j_workloads.jsonl).
   Also the chain-range shards of a multi-GPU render (chains [0, 128) and
   [128, 256) of every pixel): the upper one bit-exact (another ~15 s of
-  oracle), their sum equal to the whole film up to summation order.
+  oracle), their sum equal to the whole film up to summation order (rtol
+  5e-5, derived at the assertion).
 """
 import numpy as np
 import pytest
@@ -67,9 +68,12 @@ def test_pssmlt_band_256_chains_60_iterations_bit_exact(full_scene, oracle, name
     if name == "pssmlt_simple":
         # chain-range shards (multi-GPU C3): the upper shard (sample_offset 128)
         # bit-exact against the oracle, the sum of both shards close to the
-        # one-rank film (different summation order: rtol 2e-6)
+        # one-rank film. Only the summation order differs: a pixel accumulates
+        # ~2,300 splats (256 chains x 9 aggregation iterations) of values up to
+        # ~10^3 in fp32, so the reordering error is ~sqrt(n)*u ~ 3e-6 typically
+        # and n*u ~ 1.4e-4 at worst; measured max 7.1e-6 -> rtol 5e-5
         parts = [integ.render_film(full_scene, seed=5, spp=128, y0=y0, y1=y1, spp_total=spp, sample_offset=s0)
                  for s0 in (0, 128)]
         c = oracle.pssmlt_render(full_scene, integ.render_args(full_scene, 5, 128, y0, y1, spp, 128), it)
         np.testing.assert_array_equal(parts[1], c)
-        np.testing.assert_allclose(parts[0] + parts[1], film, rtol=2e-6, atol=1e-6)
+        np.testing.assert_allclose(parts[0] + parts[1], film, rtol=5e-5, atol=1e-6)

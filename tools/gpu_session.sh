@@ -10,7 +10,7 @@ mkdir -p $OUT
 cd $R
 echo "== smoke"; timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1
 rc=$?; tail -3 $OUT/smoke_$TAG.log; [ $rc -ne 0 ] && { echo "smoke rc=$rc"; exit $rc; }
-echo "== pytest -m gpu"; timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
+echo "== pytest -m gpu"; timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
 rc=$?; tail -15 $OUT/pytest_gpu_$TAG.log; [ $rc -gt 1 ] && { echo "pytest rc=$rc"; exit $rc; }
 [ "$MODE" = "tests" ] && exit 0
 echo "== bench"; timeout -k 10 600 python3 bench.py --steps 3 --warmup 1 > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err

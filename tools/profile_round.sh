@@ -23,7 +23,12 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $c -d $OUT/prof_${TAG}_$c -o pmc --output-format csv -- python3 $R/bench.py $BARGS > $OUT/prof_${TAG}_$c.log 2>&1
   rc=$?; [ $rc -ne 0 ] && { echo "pmc rc=$rc"; tail -5 $OUT/prof_${TAG}_$c.log; exit $rc; }
 done
+UNITS="GRBM_GUI_ACTIVE TA_TA_BUSY_sum TCP_TCC_READ_REQ_sum SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
+echo "== pmc units"
+timeout -s KILL 300 rocprofv3 --pmc $UNITS -d $OUT/prof_${TAG}_units -o pmc --output-format csv -- python3 $R/bench.py $BARGS > $OUT/prof_${TAG}_units.log 2>&1
+rc=$?; [ $rc -ne 0 ] && { echo "pmc units rc=$rc"; tail -5 $OUT/prof_${TAG}_units.log; exit $rc; }
 cd $R
 python3 tools/pmc_summary.py $OUT/prof_${TAG}_FETCH_SIZE $OUT/prof_${TAG}_WRITE_SIZE $OUT/${TAG}_pmc_traffic.json "$BARGS"
+python3 tools/pmc_units.py $OUT/prof_${TAG}_units $OUT/${TAG}_pmc_units.json "$BARGS"
 find $OUT/prof_$TAG -name "*stats*"
 exit 0
