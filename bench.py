@@ -286,7 +286,8 @@ def main():
             "shade": _kernel_entry(agg["shade_ms"] / K, cnt["trace_launches"], traffic[names["shade"]],
                                    cnt["rays_closest"] * SHADE_BYTES_PER_PATH_BOUNCE, HBM_PEAK_GBS, "hbm"),
         }
-        for kk, nn in names.items():
+        for kk, nn in (("trace_closest", names["closest"]), ("trace_shadow", names["shadow"]),
+                       ("shade", names["shade"])):
             kernels[kk]["units"] = units[nn]
         # the roofline object follows north_star's traversal kernel; the
         # kernel with the most time per step is named beside it
@@ -317,7 +318,9 @@ def main():
                 "parallelism": f"sample-range shards x{world}" + (", RCCL gather of films to rank 0" if world > 1 else ""),
             },
             "roofline": {
-                "bound": "vmem",
+                # the busier of the two units the traversal can saturate, from the
+                # build's unit counters (TA 0.75 vs VALU 0.54 in profiles/r3d_pmc_units.json)
+                "bound": "vmem" if (uc is None or uc["ta_busy"] >= uc["valu_busy"]) else "valu",
                 "kernel": "k_trace_closest (4-wide quantised BVH, closest hit)",
                 "achieved": round(achieved, 1),
                 "peak": VMEM_PEAK_GBS,
