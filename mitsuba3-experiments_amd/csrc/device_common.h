@@ -264,6 +264,9 @@ __device__ __forceinline__ int32_t wide_dref(uint32_t key, uint32_t ends, uint32
 #ifndef MTX_NODE48
 #define MTX_NODE48 0  // A/B: 1 = the 48-B node (three loads, references decoded): slower, DESIGN.md
 #endif
+#ifndef MTX_SCALAR_NODE
+#define MTX_SCALAR_NODE 0  // A/B: 1 = wave-uniform node visits fetch the node with scalar loads
+#endif
 __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
                                           int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
 #if !MTX_NODE48
@@ -294,11 +297,28 @@ __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, 
       qa = make_int4(x2.x, x2.y, x2.z, x2.w);
       qb = make_int2(x3.x, x3.y);
     } else {
-      const int4 *np = s.nodes + 4 * node;
-      a = np[0];
-      rf = np[1];
-      qa = np[2];
-      qb = *reinterpret_cast<const int2 *>(np + 3);
+#if MTX_SCALAR_NODE
+      // every active lane on one node (coherent camera rays): one scalar
+      // fetch through the scalar cache instead of four vector loads (A/B)
+      const int32_t n0 = __builtin_amdgcn_readfirstlane(node);
+      if (__ballot(node != n0) == 0) {
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const __attribute__((address_space(4))) v4i *sp =
+            (const __attribute__((address_space(4))) v4i *)s.nodes + 4 * n0;
+        const v4i x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];
+        a = make_int4(x0.x, x0.y, x0.z, x0.w);
+        rf = make_int4(x1.x, x1.y, x1.z, x1.w);
+        qa = make_int4(x2.x, x2.y, x2.z, x2.w);
+        qb = make_int2(x3.x, x3.y);
+      } else
+#endif
+      {
+        const int4 *np = s.nodes + 4 * node;
+        a = np[0];
+        rf = np[1];
+        qa = np[2];
+        qb = *reinterpret_cast<const int2 *>(np + 3);
+      }
     }
     uint32_t key[4];
     const uint32_t eb = (uint32_t)a.w;
@@ -462,6 +482,33 @@ __device__ __forceinline__ uint32_t xseg_bound(uint32_t count, uint32_t k) {
   return (uint32_t)(((uint64_t)count * k) >> 3);
 }
 
+// Claim of the next queue entries for a wave (wave-uniform; the leader lane
+// does the atomic): [base2, base2 + got2) from the own XCD's segment first,
+// then the next segments; returns true once every segment is drained.
+// (Guided sizes -- each claim its fair share of what the segment has left,
+// read with an atomic load before the add -- measured much slower: closest
+// 61.3 -> 74.0 ms/step at spp 256, 9.45 -> 15.3 at spp 32)
+__device__ __forceinline__ bool claim_rays(const DevScene &s, uint32_t *heads, uint32_t count, uint32_t batch,
+                                           uint32_t leader, uint32_t lane, uint32_t &seg, uint32_t &tries,
+                                           uint32_t &base2, uint32_t &got2) {
+  while (true) {
+    const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
+    const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
+    uint32_t b = 0xffffffffu;
+    if (hi > lo) {
+      if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
+      b = __builtin_amdgcn_readlane(b, leader);
+    }
+    if (hi > lo && b < hi - lo) {
+      base2 = lo + b;
+      got2 = min(batch, hi - lo - b);
+      return false;
+    }
+    if (++tries >= kXcds) return true;
+    seg = (seg + 1) & (kXcds - 1u);
+  }
+}
+
 // heads: kXcds claim cursors (kXHeadStride words apart), zeroed before the
 // launch. A wave claims rays from the queue segment of its own XCD first,
 // so the rays an XCD traces come from one band of the (pixel-ordered)
@@ -510,28 +557,9 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
         const uint32_t n = (uint32_t)__popcll(idle);
         const uint32_t left = res_hi - res_lo;
         uint32_t base2 = 0, got2 = 0;
-        if (left < n && !drained) {
-          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
-          while (true) {  // wave-uniform
-            const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
-            const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
-            uint32_t b = 0xffffffffu;
-            if (hi > lo) {
-              if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
-              b = __builtin_amdgcn_readlane(b, leader);
-            }
-            if (hi > lo && b < hi - lo) {
-              base2 = lo + b;
-              got2 = min(batch, hi - lo - b);
-              break;
-            }
-            if (++tries >= kXcds) {
-              drained = true;
-              break;
-            }
-            seg = (seg + 1) & (kXcds - 1u);
-          }
-        }
+        if (left < n && !drained)
+          drained = claim_rays(s, heads, count, batch, (uint32_t)(__ffsll((unsigned long long)idle) - 1), lane, seg,
+                               tries, base2, got2);
         const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         uint32_t k = 0;
@@ -735,28 +763,9 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
       if (n >= s.urefill || idle == ~0ull) {
         const uint32_t left = res_hi - res_lo;
         uint32_t base2 = 0, got2 = 0;
-        if (left < n && !drained) {
-          const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
-          while (true) {  // wave-uniform
-            const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
-            const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
-            uint32_t b = 0xffffffffu;
-            if (hi > lo) {
-              if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
-              b = __builtin_amdgcn_readlane(b, leader);
-            }
-            if (hi > lo && b < hi - lo) {
-              base2 = lo + b;
-              got2 = min(batch, hi - lo - b);
-              break;
-            }
-            if (++tries >= kXcds) {
-              drained = true;
-              break;
-            }
-            seg = (seg + 1) & (kXcds - 1u);
-          }
-        }
+        if (left < n && !drained)
+          drained = claim_rays(s, heads, count, batch, (uint32_t)(__ffsll((unsigned long long)idle) - 1), lane, seg,
+                               tries, base2, got2);
         const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
         uint32_t k = 0;

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Interleaved A/B of library variants at several spp (the per-rank work of
+# the strong-scaling curve). Usage: tools/ab_spp.sh TAG ROUNDS "SPPS" v1 v2 ...
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
+TAG=$1; ROUNDS=$2; SPPS=$3; shift 3
+for i in $(seq 1 $ROUNDS); do
+  for spp in $SPPS; do
+    for v in "$@"; do
+      if [ "$v" = base ]; then V=""; else V=$v; fi
+      MTX_LIB_VARIANT=$V timeout -k 10 300 python3 bench.py --no-cpu-baseline --spp $spp --steps 5 --warmup 2 > $OUT/abspp_$TAG.tmp 2>> $OUT/abspp_$TAG.err
+      rc=$?; [ $rc -ne 0 ] && { tail -5 $OUT/abspp_$TAG.err; exit $rc; }
+      python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); k=d['kernels']; print(json.dumps({'variant': sys.argv[2], 'spp': int(sys.argv[4]), 'round': int(sys.argv[3]), 'ms': d['ms_per_step'], 'closest': k['trace_closest']['ms_per_step'], 'shadow': k['trace_shadow']['ms_per_step'], 'shade': k['shade']['ms_per_step']}))" $OUT/abspp_$TAG.tmp "$v" $i $spp | tee -a $OUT/abspp_$TAG.jsonl
+    done
+  done
+done
+exit 0
