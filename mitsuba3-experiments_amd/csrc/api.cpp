@@ -136,12 +136,11 @@ struct mtx_ctx {
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
   uint32_t lds_top = MTX_LDS_TOP;  // wide nodes of the tree top kept in LDS per block (MTX_LDS_TOP env: A/B)
-  uint32_t trace_batch = 256;
+  uint32_t trace_batch = 128;  // queue entries per claim (256: +0.6 % closest, +1 % at spp 32; 64: +5 %)
   uint32_t refill_lanes = 16;
   uint32_t urefill = 24;  // unified loop: refill once 24 lanes are idle (16: closest +1.3 %, 32: +2 %)
   uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
-  uint32_t shade_sort = 0;  // measured slower (extra dependent loads before shading)
   uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
   DevBuf cq_keys, cq_perm, cq_ws;
   uint32_t sample_major = 0;
@@ -196,7 +195,6 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
-  if (const char *e = getenv("MTX_SHADE_SORT")) c->shade_sort = atoi(e) != 0;
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
   *out = c;
   return MTX_OK;
@@ -368,8 +366,8 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
           r[24 + 2 * k + 1] = d->vuv[2 * (size_t)vi + 1];
         }
       }
-      // bits 8..12: shading class of the material (k_shade sorts a block's
-      // paths by it: lanes of a wave then run the same BSDF code)
+      // bits 8..12: shading class of the material (read by no kernel since
+      // the block-level material sort was measured slower and removed)
       const mtx_material &m = d->materials[sh.material];
       const uint32_t cls = 1u + ((m.type & 7u) << 2 | (m.tex >= 0 ? 2u : 0u) | ((m.flags & MTX_MF_MASK) ? 1u : 0u));
       const uint32_t mat = sh.material, fl = use_n | use_uv | (cls << 8);
@@ -410,7 +408,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.urefill = c->urefill;
   s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
-  s.shade_sort = c->shade_sort;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {

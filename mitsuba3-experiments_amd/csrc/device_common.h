@@ -196,48 +196,6 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c, uin
   s1 = o1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
 }
 
-// Stable block-wide counting sort of one value per thread by a key in
-// [0, kShadeClasses): returns the value of rank threadIdx.x. Deterministic
-// (ranks from ballots, no LDS atomics). Every thread of the block calls it.
-constexpr uint32_t kShadeClasses = 32;
-template <int BLOCK>
-__device__ __forceinline__ uint32_t block_sort_by_key(uint32_t key, uint32_t value) {
-  constexpr int W = BLOCK / 64;
-  __shared__ uint32_t cnt[W][kShadeClasses];
-  __shared__ uint32_t off[kShadeClasses];
-  __shared__ uint32_t vals[BLOCK];
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint32_t j = threadIdx.x; j < W * kShadeClasses; j += BLOCK) (&cnt[0][0])[j] = 0u;
-  __syncthreads();
-  uint32_t rank = 0;
-  uint64_t pending = __ballot(true);
-  while (pending) {  // one round per distinct key in the wave
-    const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)pending) - 1);
-    const uint32_t k = __builtin_amdgcn_readlane(key, leader);
-    const uint64_t m = __ballot(key == k);
-    if (key == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane == leader) cnt[wave][k] = (uint32_t)__popcll(m);
-    pending &= ~m;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (uint32_t k = 0; k < kShadeClasses; ++k) {
-      off[k] = t;
-#pragma unroll
-      for (int w = 0; w < W; ++w) t += cnt[w][k];
-    }
-  }
-  __syncthreads();
-  uint32_t dst = off[key] + rank;
-  for (uint32_t w = 0; w < wave; ++w) dst += cnt[w][key];
-  vals[dst] = value;
-  __syncthreads();
-  const uint32_t out = vals[threadIdx.x];
-  __syncthreads();
-  return out;
-}
-
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   return v;
@@ -263,9 +221,6 @@ __device__ __forceinline__ int32_t wide_dref(uint32_t key, uint32_t ends, uint32
 #endif
 #ifndef MTX_NODE48
 #define MTX_NODE48 0  // A/B: 1 = the 48-B node (three loads, references decoded): slower, DESIGN.md
-#endif
-#ifndef MTX_SCALAR_NODE
-#define MTX_SCALAR_NODE 0  // A/B: 1 = wave-uniform node visits fetch the node with scalar loads
 #endif
 __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
                                           int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
@@ -297,28 +252,11 @@ __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, 
       qa = make_int4(x2.x, x2.y, x2.z, x2.w);
       qb = make_int2(x3.x, x3.y);
     } else {
-#if MTX_SCALAR_NODE
-      // every active lane on one node (coherent camera rays): one scalar
-      // fetch through the scalar cache instead of four vector loads (A/B)
-      const int32_t n0 = __builtin_amdgcn_readfirstlane(node);
-      if (__ballot(node != n0) == 0) {
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        const __attribute__((address_space(4))) v4i *sp =
-            (const __attribute__((address_space(4))) v4i *)s.nodes + 4 * n0;
-        const v4i x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];
-        a = make_int4(x0.x, x0.y, x0.z, x0.w);
-        rf = make_int4(x1.x, x1.y, x1.z, x1.w);
-        qa = make_int4(x2.x, x2.y, x2.z, x2.w);
-        qb = make_int2(x3.x, x3.y);
-      } else
-#endif
-      {
-        const int4 *np = s.nodes + 4 * node;
-        a = np[0];
-        rf = np[1];
-        qa = np[2];
-        qb = *reinterpret_cast<const int2 *>(np + 3);
-      }
+      const int4 *np = s.nodes + 4 * node;
+      a = np[0];
+      rf = np[1];
+      qa = np[2];
+      qb = *reinterpret_cast<const int2 *>(np + 3);
     }
     uint32_t key[4];
     const uint32_t eb = (uint32_t)a.w;

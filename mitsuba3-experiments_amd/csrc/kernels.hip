@@ -39,8 +39,14 @@ using namespace mtx;
 namespace mtxd {
 
 // Closest-hit queries of bounce `bounce`: queue entries are path indices.
+// The hit record goes to the queue position k (not the path): the shade
+// kernel, which walks the same queue, then reads it coalesced and without
+// waiting for its queue entry (MTX_HIT_BY_PATH=1: the path-indexed form).
+#ifndef MTX_HIT_BY_PATH
+#define MTX_HIT_BY_PATH 0
+#endif
 struct ClosestSrc {
-  using Payload = uint32_t;  // the path
+  using Payload = uint32_t;  // the queue position (the path with MTX_HIT_BY_PATH)
   WaveBuffers b;
   const uint32_t *queue;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
@@ -48,10 +54,10 @@ struct ClosestSrc {
     const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
-    payload = path;
+    payload = MTX_HIT_BY_PATH ? path : k;
   }
-  __device__ __forceinline__ void finish(uint32_t path, bool, float t, uint32_t prim, float u, float v) const {
-    b.hit[path] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
+  __device__ __forceinline__ void finish(uint32_t slot, bool, float t, uint32_t prim, float u, float v) const {
+    b.hit[slot] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
   }
 };
 
@@ -862,12 +868,15 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
   const uint32_t stride = gridDim.x * kShadeBlock;
   uint32_t parity = 0;
   // software pipeline over the persistent loop: the next step's queue entry
-  // loads during this step, its hit record before this step's appends
+  // loads during this step, its hit record before this step's appends. Hit
+  // records are stored by queue position (ClosestSrc), so they load
+  // coalesced and in parallel with the queue entry.
   uint32_t path = 0;
   float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
   if (blockIdx.x * kShadeBlock + threadIdx.x < count) {
-    path = in_q[blockIdx.x * kShadeBlock + threadIdx.x];
-    h = b.hit[path];
+    const uint32_t i0 = blockIdx.x * kShadeBlock + threadIdx.x;
+    path = in_q[i0];
+    h = b.hit[MTX_HIT_BY_PATH ? path : i0];
   }
   for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += stride, parity ^= 1u) {
     const uint32_t i = base + threadIdx.x;
@@ -878,19 +887,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     io.emit = false;
     io.query = false;
     bool cont = false;
-    bool valid = i < count;
-    if (s.shade_sort) {
-      // the block's paths ordered by the shading class of their hit: waves
-      // then run one or two BSDF branches instead of all of them
-      uint32_t key = kShadeClasses - 1;  // slots past the queue end sort last
-      if (valid) {
-        const uint32_t prim = __float_as_uint(h.y);
-        key = prim == 0xffffffffu ? 0u : (__float_as_uint(s.shade_rec[8 * (size_t)prim + 2].w) >> 8) & 31u;
-      }
-      path = block_sort_by_key<kShadeBlock>(key, path);
-      valid = threadIdx.x < min(count - base, (uint32_t)kShadeBlock);
-      if (valid) h = b.hit[path];
-    }
+    const bool valid = i < count;
     if (valid) {
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
         cont = shade_pssmlt(s, sv, b, p, path, h);
@@ -908,7 +905,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     const uint32_t path_c = path;
     if (MTX_SHADE_PREFETCH) {
       path = path_n;
-      if (inext < count) h = b.hit[path];
+      if (inext < count) h = b.hit[MTX_HIT_BY_PATH ? path : inext];
     }
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
@@ -926,7 +923,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     }
     if (!MTX_SHADE_PREFETCH && inext < count) {
       path = in_q[inext];
-      h = b.hit[path];
+      h = b.hit[MTX_HIT_BY_PATH ? path : inext];
     }
   }
 }

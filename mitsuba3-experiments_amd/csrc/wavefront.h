@@ -69,7 +69,6 @@ struct DevScene {
   uint32_t urefill;        // unified single-step traversal (trace_loop_u): the same, its own threshold
   uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
-  uint32_t shade_sort;     // k_shade: order a block's paths by the hit's shading class
   mtx_camera camera;
 };
 
