@@ -83,10 +83,24 @@ int upload(DevBuf &b, const T *src, size_t count, hipStream_t st) {
 
 }  // namespace
 
+// Second wavefront of the two-stream render (mtx_render's path / path-mis /
+// nrc / simple integrators): its own path state, queues, counters, claim
+// cursors and traversal spill area, on its own stream. The film's chunks
+// alternate between the two wavefronts, so one chunk's kernels fill the
+// GPU while the other's persistent trace launches drain their tails.
+struct Wave2 {
+  hipStream_t stream = nullptr;
+  hipEvent_t start = nullptr, done = nullptr;
+  DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, xheads, stack_ovf;
+  uint32_t capacity = 0;
+};
+
 struct mtx_ctx {
   int device = 0;
   int n_cu = 256;
   hipStream_t stream = nullptr;
+  Wave2 w2;
+  uint32_t streams = MTX_STREAMS;  // 1: every chunk on `stream` (MTX_STREAMS env: A/B)
   bool has_scene = false;
   // scene
   DevBuf stack_ovf;  // traversal stack entries beyond the LDS part
@@ -189,6 +203,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
+  if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
@@ -204,6 +219,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->w2.stream) hipStreamSynchronize(c->w2.stream);
   DevBuf *bufs[] = {&c->nodes,  &c->tri,     &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
@@ -219,6 +235,13 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->nr_tri_off, &c->nr_tri_pmf, &c->nr_tri_cdf, &c->nr_tri_prim, &c->nr_dists, &c->nr_lhs,
                     &c->nr_qp, &c->nr_qd, &c->nr_Lrhs, &c->nr_lanes};
   for (DevBuf *b : bufs) dfree(*b);
+  Wave2 &w = c->w2;
+  for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.L, &w.prev, &w.misc, &w.pos, &w.hit, &w.q0, &w.q1, &w.shadow,
+                    &w.counters, &w.xheads, &w.stack_ovf})
+    dfree(*b);
+  if (w.start) hipEventDestroy(w.start);
+  if (w.done) hipEventDestroy(w.done);
+  if (w.stream) hipStreamDestroy(w.stream);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
   for (hipEvent_t ev : c->prim_ev)
     if (ev) hipEventDestroy(ev);
@@ -494,6 +517,54 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   return b;
 }
 
+// The second wavefront (Wave2): buffers for `cap` paths, its stream and
+// events, and a traversal spill area of its own (two trace launches may run
+// at once).
+int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
+  int rc;
+  Wave2 &w = c->w2;
+  if (!w.stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&w.start, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+  }
+  if (cap > w.capacity) {
+    for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.L, &w.prev, &w.misc, &w.hit})
+      if ((rc = dalloc(*b, 16ull * cap))) return rc;
+    if ((rc = dalloc(w.pos, 8ull * cap))) return rc;
+    if ((rc = dalloc(w.q0, 4ull * cap))) return rc;
+    if ((rc = dalloc(w.q1, 4ull * cap))) return rc;
+    if ((rc = dalloc(w.shadow, sizeof(mtxd::ShadowRec) * (size_t)cap))) return rc;
+    w.capacity = cap;
+  }
+  if ((rc = dalloc(w.counters, 16ull * (max_depth + 2)))) return rc;
+  if ((rc = dalloc(w.xheads, 8ull * mtxd::kXSlotWords * (max_depth + 2)))) return rc;
+  const mtxd::DevScene &s = c->scene;
+  const size_t deep = s.stack_entries - s.lds_entries;
+  if ((rc = dalloc(w.stack_ovf, std::max<size_t>(4, deep * s.ovf_threads * sizeof(int32_t))))) return rc;
+  return MTX_OK;
+}
+
+mtxd::WaveBuffers buffers2(mtx_ctx *c) {
+  mtxd::WaveBuffers b = buffers(c);  // shared: stats, the PSSMLT / cache planes (unused by this path)
+  Wave2 &w = c->w2;
+  b.ray_o = (float4 *)w.ray_o.p;
+  b.ray_d = (float4 *)w.ray_d.p;
+  b.thr = (float4 *)w.thr.p;
+  b.L = (float4 *)w.L.p;
+  b.prev = (float4 *)w.prev.p;
+  b.misc = (uint4 *)w.misc.p;
+  b.pos = (float2 *)w.pos.p;
+  b.hit = (float4 *)w.hit.p;
+  b.queue[0] = (uint32_t *)w.q0.p;
+  b.queue[1] = (uint32_t *)w.q1.p;
+  b.shadow = (mtxd::ShadowRec *)w.shadow.p;
+  b.counters = (uint32_t *)w.counters.p;
+  b.xheads = (uint32_t *)w.xheads.p;
+  b.capacity = w.capacity;
+  return b;
+}
+
 // Zeroes a chunk's queue counters and the per-XCD claim cursors.
 hipError_t reset_counters(const mtxd::WaveBuffers &b, uint32_t depth, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b.counters, 0, 16ull * (depth + 2), st);
@@ -578,16 +649,16 @@ struct Timer {
     }
     return c->events[next++];
   }
-  hipEvent_t begin(int k) {
+  hipEvent_t begin(int k, hipStream_t st = nullptr) {
     if (!on) return nullptr;
     hipEvent_t e0 = get();
-    hipEventRecord(e0, c->stream);
+    hipEventRecord(e0, st ? st : c->stream);
     return e0;
   }
-  void end(int k, hipEvent_t e0) {
+  void end(int k, hipEvent_t e0, hipStream_t st = nullptr) {
     if (!on) return;
     hipEvent_t e1 = get();
-    hipEventRecord(e1, c->stream);
+    hipEventRecord(e1, st ? st : c->stream);
     pairs[k].push_back({e0, e1});
   }
   double total(int k) {
@@ -641,8 +712,10 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
 
 // Runs one chunk's bounce loop (rays already generated, counters[0] set).
 void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
-                 uint64_t *n_trace, uint64_t *n_shadow) {
-  const mtxd::DevScene &s = c->scene;
+                 uint64_t *n_trace, uint64_t *n_shadow, const mtxd::DevScene *scene = nullptr,
+                 hipStream_t stream = nullptr) {
+  const mtxd::DevScene &s = scene ? *scene : c->scene;
+  hipStream_t st = stream ? stream : c->stream;
   // an NRC cache query needs one more trace + shade after the last segment
   const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1) + (p.nrc_cache ? 1u : 0u);
   // nerad RHS lanes start at their surface point (no bounce-0 trace) and
@@ -656,27 +729,27 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     // immediately-exiting blocks costs more than the work)
     const int div = (nerad && bounce >= 2) ? 8 : 1;
     if (!(nerad && bounce == 0)) {
-      e = tm.begin(0);
-      mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), c->stream);
-      tm.end(0, e);
+      e = tm.begin(0, st);
+      mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), st);
+      tm.end(0, e, st);
       ++*n_trace;
     }
-    e = tm.begin(2);
-    mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), c->stream);
-    tm.end(2, e);
+    e = tm.begin(2, st);
+    mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), st);
+    tm.end(2, e, st);
     if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
         !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays
-      e = tm.begin(1);
-      mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, c->stream);
-      tm.end(1, e);
+      e = tm.begin(1, st);
+      mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, st);
+      tm.end(1, e, st);
       ++*n_shadow;
     }
     // Deep paths (max_depth 65, scene.xml:6): stop launching once the queue
     // has drained (checked every 8 bounces).
     if (depth_iters > 16 && (bounce & 7) == 7 && bounce + 1 < depth_iters) {
       uint32_t cnt = 0;
-      hipMemcpyAsync(&cnt, b.counters + 4 * (bounce + 1), 4, hipMemcpyDeviceToHost, c->stream);
-      hipStreamSynchronize(c->stream);
+      hipMemcpyAsync(&cnt, b.counters + 4 * (bounce + 1), 4, hipMemcpyDeviceToHost, st);
+      hipStreamSynchronize(st);
       if (cnt == 0) break;
     }
   }
@@ -915,10 +988,24 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   uint32_t px_per_chunk = std::max<uint32_t>(1, chunk_paths / a->spp);
   const uint32_t band_px = (a->y1 - a->y0) * W;
   px_per_chunk = std::min(px_per_chunk, band_px);
-  const uint32_t cap = px_per_chunk * a->spp;
-  if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
   const bool nerad_render = a->integrator == MTX_INT_NERAD;
+  const bool mlt = a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH;
+  // two wavefronts on two streams (Wave2): the band splits into at least two
+  // chunks that alternate between them (the caller's chunk size still caps a
+  // chunk), so one chunk's kernels fill the tails of the other's persistent
+  // trace launches (~0.2 ms per launch that does not shrink with the rays).
+  // Renders of 2^16 .. 2^26 paths: the bench's per-rank share at N >= 4
+  // (spp 32: 26.8 -> 25.9 ms per step); at spp 256 (2^27.8 paths) it gains
+  // nothing and would only blur the per-kernel event times. Path-state
+  // integrators without a per-chunk cache pass only.
+  const uint64_t n_paths_all = (uint64_t)band_px * a->spp;
+  const bool two = c->streams > 1 && !mlt && !nrc_cache && !nerad_render && a->integrator != MTX_INT_RESTIR_GI &&
+                   n_paths_all >= (1u << 16) && n_paths_all <= (1u << 26);
+  if (two) px_per_chunk = std::min(px_per_chunk, (band_px + 1) / 2);
+  const uint32_t cap = px_per_chunk * a->spp;
+  if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
+  if (two && (rc = ensure_wavefront2(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   if ((nrc_cache || nerad_render) && (rc = ensure_cache(c, cap))) return rc;
   if ((rc = dalloc(c->contrib, 9ull * 16 * band_px))) return rc;
   const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
@@ -939,7 +1026,6 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     HIP_TRY(hipStreamSynchronize(c->stream));
     return fill_stats(c, stats, want_stats, tm, n_trace, n_shadow, (uint64_t)W * H * a->spp);
   }
-  const bool mlt = a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH;
   if (mlt) {
     if ((rc = ensure_mlt(c, cap, std::max<uint32_t>(a->max_depth, 1), a->integrator == MTX_INT_PSSMLT_PATH)))
       return rc;
@@ -949,7 +1035,22 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   if (want_stats) HIP_TRY(hipMemsetAsync(b.stats, 0, 64, c->stream));
   uint64_t n_trace = 0, n_shadow = 0;
   hipEvent_t e_all = tm.begin(3);
-  for (uint32_t px0 = a->y0 * W; px0 < a->y1 * W; px0 += px_per_chunk) {
+  mtxd::WaveBuffers b2{};
+  mtxd::DevScene s2{};
+  if (two) {
+    // the second stream starts after everything queued on the first
+    b2 = buffers2(c);
+    s2 = c->scene;
+    s2.stack_ovf = (int32_t *)c->w2.stack_ovf.p;
+    HIP_TRY(hipEventRecord(c->w2.start, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
+  }
+  uint32_t chunk_index = 0;
+  for (uint32_t px0 = a->y0 * W; px0 < a->y1 * W; px0 += px_per_chunk, ++chunk_index) {
+    const bool second = two && (chunk_index & 1u);
+    hipStream_t st = second ? c->w2.stream : c->stream;
+    const mtxd::WaveBuffers &bc = second ? b2 : b;
+    const mtxd::DevScene &sc = second ? s2 : c->scene;
     mtxd::ChunkParams p{};
     p.integrator = a->integrator;
     p.max_depth = a->max_depth;
@@ -983,13 +1084,17 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       }
       continue;
     }
-    HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
+    HIP_TRY(reset_counters(bc, std::max<uint32_t>(a->max_depth, 1), st));
     if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
-    mtxd::launch_raygen_camera(c->scene, b, p, c->stream);
-    run_bounces(c, b, p, tm, &n_trace, &n_shadow);
+    mtxd::launch_raygen_camera(sc, bc, p, st);
+    run_bounces(c, bc, p, tm, &n_trace, &n_shadow, &sc, st);
     if (nrc_cache) run_cache(c, b, p.n_paths, tm);
     if (nerad_render) run_cache(c, b, p.n_paths, tm, true);
-    mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, c->stream);
+    mtxd::launch_film_src(bc, p, (float4 *)c->contrib.p, st);
+  }
+  if (two) {  // the film gather reads both wavefronts' contributions
+    HIP_TRY(hipEventRecord(c->w2.done, c->w2.stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->w2.done, 0));
   }
   mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, c->stream);
   tm.end(3, e_all);

@@ -36,6 +36,9 @@ constexpr uint32_t kLdsStack = 16;   // default LDS part of the persistent trave
 #ifndef MTX_LDS_TOP
 #define MTX_LDS_TOP 32  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
 #endif
+#ifndef MTX_STREAMS
+#define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)
+#endif
 
 // Per-XCD claim cursors of the persistent trace kernels: kXcds words,
 // kXHeadStride words (128 B) apart; one slot per trace launch of a chunk.

@@ -122,6 +122,24 @@ def test_render_film_bit_exact(small_scene, oracle, name):
     assert film[..., 3].sum() > 0
 
 
+@pytest.mark.parametrize("name", ["path_test", "mypath", "nrc"])
+def test_two_stream_chunks_bit_exact(small_scene, oracle, name):
+    """Renders of >= 2^16 paths alternate their chunks between two wavefronts
+    on two HIP streams (api.cpp Wave2): 7 chunks of 5 rows (boundaries inside
+    the sample range of no pixel, an odd count, a short last chunk) give the
+    oracle's film bit for bit, as does the default two-chunk split."""
+    from mtx import load_dict
+
+    integ = load_dict({"type": name, "max_depth": 6} if name != "nrc" else {"type": name})
+    spp = 32  # 64 x 36 x 32 = 73,728 paths
+    a = integ.render_args(small_scene, 7, spp)
+    ref = oracle.render(small_scene, a)
+    for chunk in (64 * 5 * spp, 0):
+        film = integ.render_film(small_scene, seed=7, spp=spp, chunk_paths=chunk)
+        np.testing.assert_array_equal(film, ref, err_msg=f"chunk_paths={chunk}")
+    assert ref[..., 3].sum() > 0
+
+
 def test_rank_shards_and_row_bands(small_scene, oracle):
     """Sample-range shards (weak-scaling bench) and row bands (strong) combine
     to the single-call film up to float summation order (rtol 2e-6)."""
