@@ -424,7 +424,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.camera = d->camera;
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
   // LDS copy of the tree top (64-B nodes only): with 16 stack entries per
-  // lane and 16 blocks of 128 threads per CU, 32 nodes fill the 160 KB
+  // lane and 8 blocks of 256 threads per CU, 64 nodes fill the 160 KB
   s.lds_top = MTX_NODE48 ? 0u : std::min<uint32_t>(d->n_nodes, c->lds_top);
   s.trace_batch = c->trace_batch;
   s.refill_lanes = c->refill_lanes;

@@ -55,9 +55,6 @@ __device__ __forceinline__ SceneView make_view(const DevScene &s) {
 // arithmetic (si_from_vertices), so identical to the host compute_si.
 //   r0 p0.xyz material | r1 p1.xyz emitter | r2 p2.xyz use flags (bit0 vertex
 //   normals, bit1 uvs) | r3..r5 n0..n2 | r6 uv0, uv1 | r7 uv2
-#ifndef MTX_REC_ALL
-#define MTX_REC_ALL 0  // A/B: 1 = normals and uvs loaded with the positions, not after the flags
-#endif
 __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, float t, uint32_t prim, float u,
                                                              float v, V3 ray_d) {
   if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
@@ -71,21 +68,6 @@ __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, 
   const bool use_n = (fl & 1u) != 0, use_uv = (fl & 2u) != 0;
   V3 n0 = v3s(0.f), n1 = v3s(0.f), n2 = v3s(0.f);
   V2 t0 = V2{0.f, 0.f}, t1 = t0, t2 = t0;
-#if MTX_REC_ALL
-  // the whole 128-B record in one round trip (same line: no extra traffic);
-  // the flags only select what is used
-  const float4 x3 = r[3], y4 = r[4], z5 = r[5], x6 = r[6], y7 = r[7];
-  if (use_n) {
-    n0 = V3{x3.x, x3.y, x3.z};
-    n1 = V3{y4.x, y4.y, y4.z};
-    n2 = V3{z5.x, z5.y, z5.z};
-  }
-  if (use_uv) {
-    t0 = V2{x6.x, x6.y};
-    t1 = V2{x6.z, x6.w};
-    t2 = V2{y7.x, y7.y};
-  }
-#else
   if (use_n) {
     const float4 x = r[3], y = r[4], z = r[5];
     n0 = V3{x.x, x.y, x.z};
@@ -98,7 +80,6 @@ __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, 
     t1 = V2{x.z, x.w};
     t2 = V2{y.x, y.y};
   }
-#endif
   return si_from_vertices(t, prim, u, v, ray_d, V3{a.x, a.y, a.z}, V3{b.x, b.y, b.z}, V3{c.x, c.y, c.z},
                           __float_as_uint(a.w), (int32_t)__float_as_uint(b.w), use_n, n0, n1, n2, use_uv, t0, t1, t2);
 }
@@ -245,8 +226,8 @@ __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, 
                                           int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
 #if !MTX_NODE48
   {
-    // nodes [0, top_n) from the block's LDS copy of the tree top (40-47 % of
-    // the visits, tools/top_visits.py), the others from global memory
+    // nodes [0, top_n) from the block's LDS copy of the tree top (64 nodes:
+    // about half of the visits, tools/top_visits.py), the others from global memory
     // (the LDS reads are inline asm: as plain loads the compiler merges the
     // two branches into flat loads through a selected generic pointer, which
     // take the vector-memory path for every lane)

@@ -31,10 +31,13 @@ enum : uint32_t {
   PF_CACHE_QUERY = 8u,  // NRC: the next hit is the radiance-cache query
 };
 
-constexpr int kTraceBlock = 128;     // threads per traversal block
+#ifndef MTX_TRACE_BLOCK
+#define MTX_TRACE_BLOCK 256  // 8 blocks of 4 waves per CU: LDS room for a 64-node tree top (128: 32 nodes, -0.5 %)
+#endif
+constexpr int kTraceBlock = MTX_TRACE_BLOCK;  // threads per traversal block
 constexpr uint32_t kLdsStack = 16;   // default LDS part of the persistent traversal stack (entries per lane)
 #ifndef MTX_LDS_TOP
-#define MTX_LDS_TOP 32  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
+#define MTX_LDS_TOP 64  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
 #endif
 #ifndef MTX_STREAMS
 #define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)
