@@ -655,6 +655,9 @@ __device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src,
 #ifndef MTX_TRI_MIN
 #define MTX_TRI_MIN 0
 #endif
+// (A per-lane ray prefetch -- the next ray's raw data held in registers so a
+// refill starts without a load round trip -- measured slower: closest +2.3 %
+// with batched swaps, +16 % swapping every iteration)
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                              int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
@@ -694,45 +697,55 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
       return;
     }
   };
+  // claim one queue index for every lane in `want` from the wave's
+  // reservoir (topped up by claim_rays): k is this lane's, ok if it got one
+  auto take = [&](uint64_t want, uint32_t &k, bool &ok) {
+    const uint32_t n = (uint32_t)__popcll(want);
+    const uint32_t left = res_hi - res_lo;
+    uint32_t base2 = 0, got2 = 0;
+    if (left < n && !drained)
+      drained = claim_rays(s, heads, count, batch, (uint32_t)(__ffsll((unsigned long long)want) - 1), lane, seg,
+                           tries, base2, got2);
+    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+    k = 0;
+    ok = false;
+    if (rk < left) {
+      k = res_lo + rk;
+      ok = true;
+    } else if (rk - left < got2) {
+      k = base2 + (rk - left);
+      ok = true;
+    }
+    if (n <= left) {
+      res_lo += n;
+    } else {
+      const uint32_t used2 = min(n - left, got2);
+      res_lo = base2 + used2;
+      res_hi = base2 + got2;
+    }
+    exhausted = drained && res_lo >= res_hi;
+  };
+  auto begin_ray = [&]() {
+    prim = 0xffffffffu;
+    bu = bv = 0.f;
+    hit = false;
+    node = 0;
+    tri = tri_end = 0;
+    sp = 0;
+    has = true;
+  };
   while (true) {
     if (!exhausted) {
       const uint64_t idle = __ballot(!has);
-      const uint32_t n = (uint32_t)__popcll(idle);
-      if (n >= s.urefill || idle == ~0ull) {
-        const uint32_t left = res_hi - res_lo;
-        uint32_t base2 = 0, got2 = 0;
-        if (left < n && !drained)
-          drained = claim_rays(s, heads, count, batch, (uint32_t)(__ffsll((unsigned long long)idle) - 1), lane, seg,
-                               tries, base2, got2);
-        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-        uint32_t k = 0;
-        bool ok = false;
-        if (rk < left) {
-          k = res_lo + rk;
-          ok = true;
-        } else if (rk - left < got2) {
-          k = base2 + (rk - left);
-          ok = true;
-        }
-        if (n <= left) {
-          res_lo += n;
-        } else {
-          const uint32_t used2 = min(n - left, got2);
-          res_lo = base2 + used2;
-          res_hi = base2 + got2;
-        }
+      if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
+        uint32_t k;
+        bool ok;
+        take(idle, k, ok);
         if (!has && ok) {
           src.load(k, r, tbest, payload);
-          prim = 0xffffffffu;
-          bu = bv = 0.f;
-          hit = false;
-          node = 0;
-          tri = tri_end = 0;
-          sp = 0;
-          has = true;
+          begin_ray();
         }
-        exhausted = drained && res_lo >= res_hi;
       }
     }
     if (__ballot(has) == 0) break;

@@ -293,6 +293,18 @@ __device__ __forceinline__ BsdfData bsdf_at(const SceneView &sv, const mtx_mater
 #endif
   return bd;
 }
+// path-mis: once a path ends, L.w (its prev_bsdf_pdf until then) holds
+// valid_ray as 1 / 0 (path-mis.py:155), so the film reads L and pos only,
+// not the 16-B misc record for one flag (MTX_FILM_FLAG_IN_L=0: misc).
+#ifndef MTX_FILM_FLAG_IN_L
+#define MTX_FILM_FLAG_IN_L 1
+#endif
+__device__ __forceinline__ float end_w(uint32_t flags, float prev_pdf) {
+  return MTX_FILM_FLAG_IN_L ? ((flags & PF_VALID_RAY) ? 1.f : 0.f) : prev_pdf;
+}
+__device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, float lw) {
+  return MTX_FILM_FLAG_IN_L ? lw != 0.f : ((b.misc[path].w >> 16) & PF_VALID_RAY) != 0;
+}
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h,
@@ -396,7 +408,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     // escaped path: nothing after this point is observable (valid_ray,
     // result unchanged; throughput becomes 0 -> inactive) -- except the
     // sampler position, which ReSTIR keeps using (6 draws per iteration)
-    b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+    b.L[path] = make_float4(L.x, L.y, L.z, end_w(flags, prev_pdf));
     if (p.restir) {
       rng.advance(6);
       b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
@@ -505,7 +517,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     b.thr[path] = make_float4(T.x, T.y, T.z, eta);
     b.prev[path] = make_float4(prev_p.x, prev_p.y, prev_p.z, spread);
   }
-  b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+  b.L[path] = make_float4(L.x, L.y, L.z, (INT == MTX_INT_PATH_MIS && !active) ? end_w(flags, prev_pdf) : prev_pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
 }
@@ -950,10 +962,7 @@ __global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *p
 __device__ __forceinline__ V3 final_L(const WaveBuffers &b, const ChunkParams &p, uint32_t path) {
   const float4 l = b.L[path];
   V3 L = V3{l.x, l.y, l.z};
-  if (p.integrator == MTX_INT_PATH_MIS) {
-    const uint32_t flags = b.misc[path].w >> 16;
-    if (!(flags & PF_VALID_RAY)) L = v3s(0.f);  // path-mis.py:155
-  }
+  if (p.integrator == MTX_INT_PATH_MIS && !end_valid(b, path, l.w)) L = v3s(0.f);  // path-mis.py:155
   return L;
 }
 
@@ -1000,7 +1009,7 @@ __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkPara
       if (q0 + j < p.n_px && sm < ns) {
         const uint32_t path = (q0 + j) * p.spp + s0 + sm;
         float4 l = b.L[path];
-        if (mask_valid && !((b.misc[path].w >> 16) & PF_VALID_RAY)) l = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (mask_valid && !end_valid(b, path, l.w)) l = make_float4(0.f, 0.f, 0.f, 0.f);
         const float2 ps = b.pos[path];
         sv[0][j][sm] = l.x;
         sv[1][j][sm] = l.y;
