@@ -167,6 +167,11 @@ extern "C" {
 
 int mtx_abi_version(void) { return MTX_ABI_VERSION; }
 
+// Diagnostic export (not in mtx.h): the shade kernel's per-phase stamp sums of
+// an MTX_DIAG_STAMPS build (tools/shade_stamps.py); returns the segment
+// count, or -1 in production builds.
+int mtx_diag_shade_stamps(unsigned long long *out) { return mtxd::shade_stamps(out); }
+
 const char *mtx_last_error(void) { return g_err; }
 
 int mtx_ctx_create(int hip_device, mtx_ctx **out) {

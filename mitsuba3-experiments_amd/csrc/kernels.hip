@@ -239,11 +239,38 @@ __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const fl
 #define kInitL make_float4(0.f, 0.f, 0.f, 1.f)
 #define kInitPrev make_float4(0.f, 0.f, 0.f, 0.f)
 
+// Diagnostic build only (MTX_DIAG_STAMPS=1, tools/shade_stamps.py): s_memtime
+// stamps between the phases of a shade step, summed per wave in scalar
+// registers and added to g_shade_stamps at the kernel's end. Read shares, not
+// the build's run time (cdna_hip_programming.md "In-kernel stamps").
+#ifndef MTX_DIAG_STAMPS
+#define MTX_DIAG_STAMPS 0
+#endif
+constexpr int kStampSegs = 8;
+struct Stamps {
+  unsigned long long prev, acc[kStampSegs];
+};
+#if MTX_DIAG_STAMPS
+__device__ unsigned long long g_shade_stamps[kStampSegs + 2];
+#define MTX_STAMP(st, i)                                                                  \
+  do {                                                                                    \
+    unsigned long long t_;                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    (st).acc[i] += t_ - (st).prev;                                                        \
+    (st).prev = t_;                                                                       \
+  } while (0)
+#endif
+
 struct ShadeIO {
   ShadowRec rec;
   bool emit;
   bool query;  // NRC radiance-cache query at this hit (field.hip)
   float4 qp, qd, qt;
+#if MTX_DIAG_STAMPS
+  Stamps st;
+#endif
 };
 
 // Builds the shadow record for an NEE contribution. fma_form: value = (T, X)
@@ -329,6 +356,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   float prev_pdf = Lr.w;
   const V3 ray_d = V3{rd.x, rd.y, rd.z};
   const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
+#if MTX_DIAG_STAMPS
+  MTX_STAMP(io.st, 1);
+#endif
   if (kPrevOnEmitter && bounce != 0 && si.emitter >= 0) pv = b.prev[path];
   V3 prev_p = V3{pv.x, pv.y, pv.z};
   float spread = pv.w, a0 = rd.w;
@@ -426,6 +456,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
 #endif
   // before the emitter sample; the NEE eval and the BSDF sample both read it
   const BsdfData bd = bsdf_at(sv, mat, si.uv);
+#if MTX_DIAG_STAMPS
+  MTX_STAMP(io.st, 2);
+#endif
   const bool smooth = (bsdf_flags(mat) & BF_SMOOTH) != 0;
   bool active_em = (INT == MTX_INT_PATH_MIS ? active_next : true) && smooth;
   const V2 u_em = rng.next_2d();
@@ -439,6 +472,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   V3 em_weight = v3s(0.f);
   const bool do_nee = (INT == MTX_INT_NRC) ? true : active_em;  // nrc.py:51-53 samples with `active`
   if (do_nee) em_weight = sample_emitter_direction(sv, si.p, u_em, &ds);
+#if MTX_DIAG_STAMPS
+  MTX_STAMP(io.st, 3);
+#endif
   if (INT != MTX_INT_PATH_MIS) active_em = active_em && ds.pdf != 0.f;
   const V3 wo = to_local(si.sh, ds.d);
   const float s1 = rng.next_1d();
@@ -449,6 +485,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   // eval / pdf only feed the NEE contribution (no draws, no side effects)
   if (active_em) bsdf_eval_pdf(bd, mat, si.uv, si.wi, wo, &bsdf_val, &bsdf_pdf);
   const V3 bsdf_weight = bsdf_sample(bd, mat, si.uv, si.wi, s1, s2, &bs);
+#if MTX_DIAG_STAMPS
+  MTX_STAMP(io.st, 4);
+#endif
 
   if (INT == MTX_INT_PATH_MIS) {
     const float mi_em = mis_weight_b(ds.pdf, bsdf_pdf);
@@ -519,6 +558,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   }
   b.L[path] = make_float4(L.x, L.y, L.z, (INT == MTX_INT_PATH_MIS && !active) ? end_w(flags, prev_pdf) : prev_pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+#if MTX_DIAG_STAMPS
+  MTX_STAMP(io.st, 5);
+#endif
   return active;
 }
 
@@ -890,6 +932,11 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     path = in_q[i0];
     h = b.hit[MTX_HIT_BY_PATH ? path : i0];
   }
+#if MTX_DIAG_STAMPS
+  Stamps stp{};
+  unsigned long long steps = 0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stp.prev)::"memory");
+#endif
   for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += stride, parity ^= 1u) {
     const uint32_t i = base + threadIdx.x;
     const uint32_t inext = i + stride;
@@ -898,6 +945,11 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     ShadeIO io;
     io.emit = false;
     io.query = false;
+#if MTX_DIAG_STAMPS
+    ++steps;
+    MTX_STAMP(stp, 0);
+    io.st = stp;
+#endif
     bool cont = false;
     const bool valid = i < count;
     if (valid) {
@@ -919,10 +971,16 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       path = path_n;
       if (inext < count) h = b.hit[MTX_HIT_BY_PATH ? path : inext];
     }
+#if MTX_DIAG_STAMPS
+    stp = io.st;
+#endif
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
     if (cont) out_q[slot] = path_c;
     if (io.emit) b.shadow[sslot] = io.rec;
+#if MTX_DIAG_STAMPS
+    MTX_STAMP(stp, 6);
+#endif
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
       if (INT != MTX_INT_NRC || p.nrc_cache) {
         const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);
@@ -937,7 +995,17 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       path = in_q[inext];
       h = b.hit[MTX_HIT_BY_PATH ? path : inext];
     }
+#if MTX_DIAG_STAMPS
+    MTX_STAMP(stp, 7);
+#endif
   }
+#if MTX_DIAG_STAMPS
+  if ((threadIdx.x & 63u) == 0) {
+    for (int k = 0; k < kStampSegs; ++k) atomicAdd(&g_shade_stamps[k], stp.acc[k]);
+    atomicAdd(&g_shade_stamps[kStampSegs], steps);
+    atomicAdd(&g_shade_stamps[kStampSegs + 1], 1ull);
+  }
+#endif
 }
 
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
@@ -1332,6 +1400,21 @@ int trace_blocks_per_cu(const DevScene &s) {
       nb <= 0)
     nb = 4;
   return nb;
+}
+// MTX_DIAG_STAMPS builds: read (and zero) the shade stamp sums; -1 otherwise.
+int shade_stamps(unsigned long long *out) {
+#if MTX_DIAG_STAMPS
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_shade_stamps), sizeof(unsigned long long) * (kStampSegs + 2)) !=
+      hipSuccess)
+    return -1;
+  unsigned long long z[kStampSegs + 2] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_shade_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  return kStampSegs;
+#else
+  (void)out;
+  return -1;
+#endif
 }
 int shade_blocks_per_cu() {
   int nb = 0;

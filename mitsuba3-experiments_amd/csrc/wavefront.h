@@ -165,6 +165,7 @@ struct ChunkParams {
 // -------- launch wrappers (kernels.hip) --------
 int trace_blocks_per_cu(const DevScene &s);
 int shade_blocks_per_cu();
+int shade_stamps(unsigned long long *out);  // diagnostic builds (MTX_DIAG_STAMPS)
 void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
                         const uint32_t *lanes, uint32_t rng_skip, hipStream_t st);
