@@ -451,11 +451,11 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
 
 namespace {
 
-// Default wavefront: up to 256 Mi paths (~200 B of state each, ~50 GB) so a
+// Default wavefront: up to 256 Mi paths (~232 B of state each, ~58 GB) so a
 // 1280x720 spp=256 frame runs as one chunk (fewer queue tails), bounded by
 // 40 % of the free HBM.
 constexpr uint32_t kDefaultChunk = 1u << 28;
-constexpr size_t kPathStateBytes = 200;
+constexpr size_t kPathStateBytes = 232;
 uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
@@ -472,8 +472,8 @@ uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
 int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   int rc;
   if (cap > c->capacity) {
-    if ((rc = dalloc(c->ray_o, 16ull * cap))) return rc;
-    if ((rc = dalloc(c->ray_d, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->ray_o, 32ull * cap))) return rc;  // two planes (bounce parity), wavefront.h
+    if ((rc = dalloc(c->ray_d, 32ull * cap))) return rc;
     if ((rc = dalloc(c->thr, 16ull * cap))) return rc;
     if ((rc = dalloc(c->L, 16ull * cap))) return rc;
     if ((rc = dalloc(c->prev, 16ull * cap))) return rc;
@@ -493,8 +493,11 @@ int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
 
 mtxd::WaveBuffers buffers(mtx_ctx *c) {
   mtxd::WaveBuffers b;
-  b.ray_o = (float4 *)c->ray_o.p;
-  b.ray_d = (float4 *)c->ray_d.p;
+  b.ray_o[0] = (float4 *)c->ray_o.p;
+  b.ray_o[1] = b.ray_o[0] + c->capacity;
+  b.ray_d[0] = (float4 *)c->ray_d.p;
+  b.ray_d[1] = b.ray_d[0] + c->capacity;
+  b.ray_par = 0;
   b.thr = (float4 *)c->thr.p;
   b.L = (float4 *)c->L.p;
   b.prev = (float4 *)c->prev.p;
@@ -534,7 +537,9 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
   }
   if (cap > w.capacity) {
-    for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.L, &w.prev, &w.misc, &w.hit})
+    for (DevBuf *b : {&w.ray_o, &w.ray_d})
+      if ((rc = dalloc(*b, 32ull * cap))) return rc;
+    for (DevBuf *b : {&w.thr, &w.L, &w.prev, &w.misc, &w.hit})
       if ((rc = dalloc(*b, 16ull * cap))) return rc;
     if ((rc = dalloc(w.pos, 8ull * cap))) return rc;
     if ((rc = dalloc(w.q0, 4ull * cap))) return rc;
@@ -553,8 +558,10 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
 mtxd::WaveBuffers buffers2(mtx_ctx *c) {
   mtxd::WaveBuffers b = buffers(c);  // shared: stats, the PSSMLT / cache planes (unused by this path)
   Wave2 &w = c->w2;
-  b.ray_o = (float4 *)w.ray_o.p;
-  b.ray_d = (float4 *)w.ray_d.p;
+  b.ray_o[0] = (float4 *)w.ray_o.p;
+  b.ray_o[1] = b.ray_o[0] + w.capacity;
+  b.ray_d[0] = (float4 *)w.ray_d.p;
+  b.ray_d[1] = b.ray_d[0] + w.capacity;
   b.thr = (float4 *)w.thr.p;
   b.L = (float4 *)w.L.p;
   b.prev = (float4 *)w.prev.p;
@@ -928,7 +935,9 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     ++*n_trace;
     HIP_TRY(reset_counters(b, depth, st));
     mtxd::launch_restir_begin(c->scene, b, p, r, st);
-    run_bounces(c, b, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
+    mtxd::WaveBuffers b1 = b;  // k_rs_begin left the secondary rays in the parity-1 planes
+    b1.ray_par = 1;
+    run_bounces(c, b1, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
     mtxd::launch_restir_collect(b, p, r, st);
     mtxd::launch_restir_temporal(r, p, st);
   }

@@ -49,12 +49,12 @@ struct ClosestSrc {
   using Payload = uint32_t;  // the queue position (the path with MTX_HIT_BY_PATH)
   WaveBuffers b;
   const uint32_t *queue;
+  const float4 *ro, *rd;  // this bounce's ray planes, by queue position
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
-    const uint32_t path = queue[k];
-    const float4 o4 = b.ray_o[path], d4 = b.ray_d[path];
+    const float4 o4 = ro[k], d4 = rd[k];
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
-    payload = MTX_HIT_BY_PATH ? path : k;
+    payload = MTX_HIT_BY_PATH ? queue[k] : k;
   }
   __device__ __forceinline__ void finish(uint32_t slot, bool, float t, uint32_t prim, float u, float v) const {
     b.hit[slot] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
@@ -76,7 +76,8 @@ struct ClosestSrc {
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
-  const ClosestSrc src{b, b.queue[bounce & 1]};
+  const uint32_t rp = (bounce + b.ray_par) & 1u;
+  const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
   trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, stack + threadIdx.x, nv,
                            tv, nr, wi);
@@ -183,8 +184,8 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   }
   // throughput = 1, eta = 1, L = 0, prev_bsdf_pdf = 1 (path-mis.py:45), prev_p = 0 are
   // not stored: the bounce-0 shade uses these constants (kInitThr / kInitL / kInitPrev)
-  b.ray_o[i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
-  b.ray_d[i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+  b.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);  // queue position i (identity)
+  b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   b.pos[i] = pos;
   b.queue[0][i] = i;
@@ -268,6 +269,7 @@ struct ShadeIO {
   bool emit;
   bool query;  // NRC radiance-cache query at this hit (field.hip)
   float4 qp, qd, qt;
+  float4 nro, nrd;  // the next ray: k_shade stores it at the path's append slot
 #if MTX_DIAG_STAMPS
   Stamps st;
 #endif
@@ -334,9 +336,10 @@ __device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, f
 }
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                           const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h,
-                                           ShadeIO &io) {
-  const float4 ro = b.ray_o[path], rd = b.ray_d[path];
+                                           const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
+                                           const float4 h, ShadeIO &io) {
+  const uint32_t rp = (bounce + b.ray_par) & 1u;
+  const float4 ro = b.ray_o[rp][qi], rd = b.ray_d[rp][qi];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
   const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
   // prev (previous vertex, NRC spread): path-mis / path read it only for the
@@ -550,9 +553,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   // a path that ends here is read only through L and misc afterwards (film,
   // k_rs_collect): its ray, throughput and previous vertex stay unwritten
   // (64 of 96 B; 39 % of the path-bounces of a bench step end the path)
+  io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, a0);
   if (MTX_SHADE_ALL_PLANES || active) {
-    b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
-    b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, a0);
     b.thr[path] = make_float4(T.x, T.y, T.z, eta);
     b.prev[path] = make_float4(prev_p.x, prev_p.y, prev_p.z, spread);
   }
@@ -574,8 +577,9 @@ __device__ __forceinline__ float dr_clamp(float x, float lo, float hi) { return 
 // executed bounce consumes 4 draws: the chain's RNG stream continues across
 // the Metropolis iterations.
 __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                             const ChunkParams &p, uint32_t path, const float4 h) {
-  const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path];
+                                             const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
+                                             const float4 h, ShadeIO &io) {
+  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi], th = b.thr[path], Lr = b.L[path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -626,8 +630,8 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   const bool rr_continue = rng.next_1d() < rr_prob;
   if (rr_active) T = T * rcp(rr_prob);
   const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
-  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
-  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+  io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
   b.thr[path] = make_float4(T.x, T.y, T.z, eta);
   b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
@@ -641,8 +645,9 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
 // pssmltsimple.py:60-131 without the mutation; bounce 0 starts from the
 // constant initial state (f = 1, eta = 1, L = 0, prev_bsdf_pdf = 1).
 __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                             const ChunkParams &p, uint32_t bounce, uint32_t path, const float4 h) {
-  const float4 rd = b.ray_d[path];
+                                             const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
+                                             const float4 h, ShadeIO &io) {
+  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi];
   const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
@@ -677,8 +682,8 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
   const bool rr_continue = rng.next_1d() < rr_prob;
   if (rr_active) T = T * rcp(rr_prob);
   const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
-  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
-  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+  io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
   b.thr[path] = make_float4(T.x, T.y, T.z, eta);
   b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
@@ -693,8 +698,9 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
 // (:118-134, shadow ray), proposed vertex write (:138), RR (:154-166).
 // Draws per bounce: 1 + 2 (BSDF) + 2 (mutation) + 1 (RR).
 __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                                  const ChunkParams &p, uint32_t path, const float4 h, ShadeIO &io) {
-  const float4 rd = b.ray_d[path], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
+                                                  const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
+                                                  const float4 h, ShadeIO &io) {
+  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -779,8 +785,8 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   const bool rr_continue = rng.next_1d() < rr_prob;
   if (rr_active) T = T * rcp(rr_prob);
   const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
-  b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
-  b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+  io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+  io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
   b.thr[path] = make_float4(T.x, T.y, T.z, eta);
   b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
   b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
@@ -805,8 +811,9 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
 // L = Field(si) * f + Le(si) (applied by k_nerad_apply after the field).
 template <bool RENDER>
 __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
-                                            uint32_t bounce, uint32_t path, const float4 h, ShadeIO &io) {
-  const float4 rd = b.ray_d[path];
+                                            uint32_t bounce, uint32_t path, uint32_t qi, const float4 h,
+                                            ShadeIO &io) {
+  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi];
   // a rendered lane's bounce-0 state is the camera raygen's (nothing stored)
   const float4 Lr = (RENDER && bounce == 0) ? kInitL : b.L[path];
   const float4 pv = (RENDER && bounce == 0) ? kInitPrev : b.prev[path];
@@ -842,8 +849,8 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     BSDFSample bs;
     const V3 w = bsdf_sample(sv.bsdf, mat, si.uv, si.wi, s1, s2, &bs);  // :204-206
     const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));   // :208
-    b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
-    b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+    io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+    io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
     b.thr[path] = make_float4(w.x, w.y, w.z, 1.f);
     b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
     b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
@@ -874,8 +881,8 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   if (chain) {
     f2 = f2 * w;  // :150
     const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
-    b.ray_o[path] = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
-    b.ray_d[path] = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
+    io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
+    io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
     b.thr[path] = make_float4(f.x, f.y, f.z, 1.f);
     b.prev[path] = make_float4(f2.x, f2.y, f2.z, 0.f);
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
@@ -919,6 +926,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
   // [4(bounce+1)] next queue count, [4(bounce+1)+1] this bounce's shadow
   // rays: one 64-bit pair, reserved by one atomic per block step
   uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
+  const uint32_t rp = (bounce + b.ray_par) & 1u;  // this bounce's ray planes; the next ray goes to rp ^ 1
   const uint32_t stride = gridDim.x * kShadeBlock;
   uint32_t parity = 0;
   // software pipeline over the persistent loop: the next step's queue entry
@@ -954,17 +962,17 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     const bool valid = i < count;
     if (valid) {
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
-        cont = shade_pssmlt(s, sv, b, p, path, h);
+        cont = shade_pssmlt(s, sv, b, p, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_SIMPLE)
-        cont = shade_simple(s, sv, b, p, bounce, path, h);
+        cont = shade_simple(s, sv, b, p, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
-        cont = shade_pssmlt_path(s, sv, b, p, path, h, io);
+        cont = shade_pssmlt_path(s, sv, b, p, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_NERAD_RHS)
-        cont = shade_nerad<false>(s, sv, b, bounce, path, h, io);
+        cont = shade_nerad<false>(s, sv, b, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_NERAD)
-        cont = shade_nerad<true>(s, sv, b, bounce, path, h, io);
+        cont = shade_nerad<true>(s, sv, b, bounce, path, i, h, io);
       else
-        cont = shade_path<INT>(s, sv, b, p, bounce, path, h, io);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io);
     }
     const uint32_t path_c = path;
     if (MTX_SHADE_PREFETCH) {
@@ -976,7 +984,11 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
 #endif
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
-    if (cont) out_q[slot] = path_c;
+    if (cont) {
+      out_q[slot] = path_c;
+      b.ray_o[rp ^ 1u][slot] = io.nro;
+      b.ray_d[rp ^ 1u][slot] = io.nrd;
+    }
     if (io.emit) b.shadow[sslot] = io.rec;
 #if MTX_DIAG_STAMPS
     MTX_STAMP(stp, 6);
@@ -1247,8 +1259,8 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   const V2 sp = V2{((float)x + po.x) / (float)p.width, ((float)y + po.y) / (float)p.height};
   const Ray ray = camera_ray(s.camera, sp);
   b.mlt_prop[i] = make_float2(po.x, po.y);
-  b.ray_o[i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
-  b.ray_d[i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+  b.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);  // queue position i (identity)
+  b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
   b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
   // pssmltpath.py:42-44: prev_si zero, prev_bsdf_delta = True

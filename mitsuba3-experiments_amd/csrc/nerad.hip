@@ -42,8 +42,8 @@ __global__ void k_nerad_raygen(WaveBuffers b, ChunkParams p, const float4 *lhs, 
   const float4 a = lhs[3 * (size_t)pt], c = lhs[3 * (size_t)pt + 1], d = lhs[3 * (size_t)pt + 2];
   const Pcg32 rng = sampler_lane(p.seed, i);
   b.hit[i] = make_float4(1.f, a.w, c.w, d.x);
-  b.ray_o[i] = make_float4(a.x, a.y, a.z, 0.f);
-  b.ray_d[i] = make_float4(-c.x, -c.y, -c.z, 0.f);
+  b.ray_o[0][i] = make_float4(a.x, a.y, a.z, 0.f);  // queue position i (identity)
+  b.ray_d[0][i] = make_float4(-c.x, -c.y, -c.z, 0.f);
   b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
   b.L[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -109,9 +109,10 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t i = r.lane0 + t;
   bool enq = false;
+  float4 nro = make_float4(0.f, 0.f, 0.f, 0.f), nrd = nro;
   const uint32_t path = t < r.nb ? path_of(t, p) : 0u;
   if (t < r.nb) {
-    const float4 h = b.hit[path], d4 = b.ray_d[path];
+    const float4 h = b.hit[path], d4 = b.ray_d[0][path];  // bounce-0 queue is the identity
     r.prim_hit[i] = h;
     r.prim_dir[i] = d4;
     const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
@@ -137,8 +138,8 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
     r.cur[n + i] = si.valid ? f4(si.n, pdf) : make_float4(0.f, 0.f, 0.f, pdf);
     if (si.valid) {
       const Ray nr = spawn_ray(si.p, si.n, to_world(si.sh, wo));
-      b.ray_o[path] = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
-      b.ray_d[path] = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
+      nro = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
+      nrd = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
       // throughput 1, L 0, prev_bsdf_pdf 1, prev_p 0: the bounce-0 shade's constants
       b.misc[path] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
       enq = true;
@@ -151,7 +152,13 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
     }
   }
   const uint32_t slot = block_reserve<kRsBlock>(enq ? 1u : 0u, &b.counters[0]);
-  if (enq) b.queue[0][slot] = path;
+  if (enq) {
+    // the secondary loop runs with ray_par = 1: its bounce-0 rays are the
+    // parity-1 planes (the primary rays, still read above, are parity 0)
+    b.queue[0][slot] = path;
+    b.ray_o[1][slot] = nro;
+    b.ray_d[1][slot] = nrd;
+  }
 }
 
 // L_o = select(valid_ray, result, 0) (:588) and the sampler position.

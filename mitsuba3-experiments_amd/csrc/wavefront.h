@@ -3,8 +3,8 @@
 //
 // A chunk of C paths lives in HBM as SoA arrays of 16-byte records (one
 // dwordx4 load/store per field group per lane):
-//   ray_o  float4  o.xyz, maxt
-//   ray_d  float4  d.xyz, a0 (NRC footprint, nrc.py:121)
+//   ray_o  float4  o.xyz, maxt                       } by QUEUE position, two
+//   ray_d  float4  d.xyz, a0 (NRC footprint, nrc.py:121) } planes by bounce parity
 //   thr    float4  throughput.xyz, eta
 //   L      float4  result.xyz, prev_bsdf_pdf
 //   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93)
@@ -90,7 +90,12 @@ struct ShadowRec {
 };
 
 struct WaveBuffers {
-  float4 *ray_o, *ray_d, *thr, *L, *prev;
+  // rays of bounce b at ray_o / ray_d[(b + ray_par) & 1][k] for queue position
+  // k: the trace loads them coalesced, the shade writes the next ray at its
+  // append slot (no path-indexed scatter on either side)
+  float4 *ray_o[2], *ray_d[2];
+  uint32_t ray_par;
+  float4 *thr, *L, *prev;
   uint4 *misc;
   float2 *pos;
   float4 *hit;
