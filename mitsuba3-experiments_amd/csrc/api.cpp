@@ -451,11 +451,11 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
 
 namespace {
 
-// Default wavefront: up to 256 Mi paths (~232 B of state each, ~58 GB) so a
+// Default wavefront: up to 256 Mi paths (~264 B of state each, ~66 GB) so a
 // 1280x720 spp=256 frame runs as one chunk (fewer queue tails), bounded by
 // 40 % of the free HBM.
 constexpr uint32_t kDefaultChunk = 1u << 28;
-constexpr size_t kPathStateBytes = 232;
+constexpr size_t kPathStateBytes = 264;
 uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
@@ -474,9 +474,9 @@ int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   if (cap > c->capacity) {
     if ((rc = dalloc(c->ray_o, 32ull * cap))) return rc;  // two planes (bounce parity), wavefront.h
     if ((rc = dalloc(c->ray_d, 32ull * cap))) return rc;
-    if ((rc = dalloc(c->thr, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->thr, 32ull * cap))) return rc;
     if ((rc = dalloc(c->L, 16ull * cap))) return rc;
-    if ((rc = dalloc(c->prev, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->prev, 32ull * cap))) return rc;
     if ((rc = dalloc(c->misc, 16ull * cap))) return rc;
     if ((rc = dalloc(c->pos, 8ull * cap))) return rc;
     if ((rc = dalloc(c->hit, 16ull * cap))) return rc;
@@ -498,9 +498,11 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.ray_d[0] = (float4 *)c->ray_d.p;
   b.ray_d[1] = b.ray_d[0] + c->capacity;
   b.ray_par = 0;
-  b.thr = (float4 *)c->thr.p;
+  b.thr[0] = (float4 *)c->thr.p;
+  b.thr[1] = b.thr[0] + c->capacity;
   b.L = (float4 *)c->L.p;
-  b.prev = (float4 *)c->prev.p;
+  b.prev[0] = (float4 *)c->prev.p;
+  b.prev[1] = b.prev[0] + c->capacity;
   b.misc = (uint4 *)c->misc.p;
   b.pos = (float2 *)c->pos.p;
   b.hit = (float4 *)c->hit.p;
@@ -537,9 +539,9 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     HIP_TRY(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
   }
   if (cap > w.capacity) {
-    for (DevBuf *b : {&w.ray_o, &w.ray_d})
+    for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.prev})
       if ((rc = dalloc(*b, 32ull * cap))) return rc;
-    for (DevBuf *b : {&w.thr, &w.L, &w.prev, &w.misc, &w.hit})
+    for (DevBuf *b : {&w.L, &w.misc, &w.hit})
       if ((rc = dalloc(*b, 16ull * cap))) return rc;
     if ((rc = dalloc(w.pos, 8ull * cap))) return rc;
     if ((rc = dalloc(w.q0, 4ull * cap))) return rc;
@@ -562,9 +564,11 @@ mtxd::WaveBuffers buffers2(mtx_ctx *c) {
   b.ray_o[1] = b.ray_o[0] + w.capacity;
   b.ray_d[0] = (float4 *)w.ray_d.p;
   b.ray_d[1] = b.ray_d[0] + w.capacity;
-  b.thr = (float4 *)w.thr.p;
+  b.thr[0] = (float4 *)w.thr.p;
+  b.thr[1] = b.thr[0] + w.capacity;
   b.L = (float4 *)w.L.p;
-  b.prev = (float4 *)w.prev.p;
+  b.prev[0] = (float4 *)w.prev.p;
+  b.prev[1] = b.prev[0] + w.capacity;
   b.misc = (uint4 *)w.misc.p;
   b.pos = (float2 *)w.pos.p;
   b.hit = (float4 *)w.hit.p;

@@ -269,7 +269,7 @@ struct ShadeIO {
   bool emit;
   bool query;  // NRC radiance-cache query at this hit (field.hip)
   float4 qp, qd, qt;
-  float4 nro, nrd;  // the next ray: k_shade stores it at the path's append slot
+  float4 nro, nrd, nthr, nprev;  // the next ray and state: k_shade stores them at the path's append slot
 #if MTX_DIAG_STAMPS
   Stamps st;
 #endif
@@ -303,9 +303,6 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
 }
 
-#ifndef MTX_SHADE_ALL_PLANES
-#define MTX_SHADE_ALL_PLANES 0  // A/B: 1 = a path that ends still writes its ray / throughput / prev planes
-#endif
 #ifndef MTX_EARLY_COLOR
 #define MTX_EARLY_COLOR 1  // A/B: 0 = each BSDF call looks the texture up itself
 #endif
@@ -341,13 +338,13 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const float4 ro = b.ray_o[rp][qi], rd = b.ray_d[rp][qi];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
-  const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
+  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[path];
   // prev (previous vertex, NRC spread): path-mis / path read it only for the
   // emission MIS of an emitter hit (pdf_emitter_direction is 0 otherwise), so
   // they load it below once the hit's emitter is known
   constexpr bool kPrevOnEmitter = INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH;
   float4 pv = kInitPrev;
-  if (!kPrevOnEmitter && bounce != 0) pv = b.prev[path];
+  if (!kPrevOnEmitter && bounce != 0) pv = b.prev[rp][qi];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -362,7 +359,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
 #if MTX_DIAG_STAMPS
   MTX_STAMP(io.st, 1);
 #endif
-  if (kPrevOnEmitter && bounce != 0 && si.emitter >= 0) pv = b.prev[path];
+  if (kPrevOnEmitter && bounce != 0 && si.emitter >= 0) pv = b.prev[rp][qi];
   V3 prev_p = V3{pv.x, pv.y, pv.z};
   float spread = pv.w, a0 = rd.w;
   io.emit = false;
@@ -550,15 +547,13 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     flags = (bs.type & BF_DELTA) ? (flags | PF_PREV_DELTA) : (flags & ~PF_PREV_DELTA);
   }
 
-  // a path that ends here is read only through L and misc afterwards (film,
-  // k_rs_collect): its ray, throughput and previous vertex stay unwritten
-  // (64 of 96 B; 39 % of the path-bounces of a bench step end the path)
+  // ray, throughput and previous vertex travel with the queue entry (k_shade
+  // stores them at the append slot, coalesced, for continuing paths only);
+  // a path that ends is read afterwards through L and misc alone
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, a0);
-  if (MTX_SHADE_ALL_PLANES || active) {
-    b.thr[path] = make_float4(T.x, T.y, T.z, eta);
-    b.prev[path] = make_float4(prev_p.x, prev_p.y, prev_p.z, spread);
-  }
+  io.nthr = make_float4(T.x, T.y, T.z, eta);
+  io.nprev = make_float4(prev_p.x, prev_p.y, prev_p.z, spread);
   b.L[path] = make_float4(L.x, L.y, L.z, (INT == MTX_INT_PATH_MIS && !active) ? end_w(flags, prev_pdf) : prev_pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
 #if MTX_DIAG_STAMPS
@@ -579,7 +574,8 @@ __device__ __forceinline__ float dr_clamp(float x, float lo, float hi) { return 
 __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                              const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                              const float4 h, ShadeIO &io) {
-  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi], th = b.thr[path], Lr = b.L[path];
+  const uint32_t rp = (bounce + b.ray_par) & 1u;
+  const float4 rd = b.ray_d[rp][qi], th = b.thr[rp][qi], Lr = b.L[path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -632,7 +628,7 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
-  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  io.nthr = make_float4(T.x, T.y, T.z, eta);
   b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
@@ -647,8 +643,9 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
 __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                              const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                              const float4 h, ShadeIO &io) {
-  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi];
-  const float4 th = bounce == 0 ? kInitThr : b.thr[path], Lr = bounce == 0 ? kInitL : b.L[path];
+  const uint32_t rp = (bounce + b.ray_par) & 1u;
+  const float4 rd = b.ray_d[rp][qi];
+  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -684,7 +681,7 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
   const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
-  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  io.nthr = make_float4(T.x, T.y, T.z, eta);
   b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
@@ -700,7 +697,8 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
 __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                                   const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                                   const float4 h, ShadeIO &io) {
-  const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi], th = b.thr[path], Lr = b.L[path], pv = b.prev[path];
+  const uint32_t rp = (bounce + b.ray_par) & 1u;
+  const float4 rd = b.ray_d[rp][qi], th = b.thr[rp][qi], Lr = b.L[path], pv = b.prev[rp][qi];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -787,9 +785,9 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   const bool active = active_next && (!rr_active || rr_continue) && (fmax_ != 0.f);
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
-  b.thr[path] = make_float4(T.x, T.y, T.z, eta);
+  io.nthr = make_float4(T.x, T.y, T.z, eta);
   b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
-  b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
+  io.nprev = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
   b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
 }
@@ -816,8 +814,9 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi];
   // a rendered lane's bounce-0 state is the camera raygen's (nothing stored)
   const float4 Lr = (RENDER && bounce == 0) ? kInitL : b.L[path];
-  const float4 pv = (RENDER && bounce == 0) ? kInitPrev : b.prev[path];
-  const float4 th = (RENDER && bounce == 0) ? kInitThr : b.thr[path];
+  // thr / prev path-indexed in plane 0 (k_nerad_apply reads prev by path)
+  const float4 pv = (RENDER && bounce == 0) ? kInitPrev : b.prev[0][path];
+  const float4 th = (RENDER && bounce == 0) ? kInitThr : b.thr[0][path];
   const uint4 mi = b.misc[path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
@@ -851,9 +850,9 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));   // :208
     io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
     io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
-    b.thr[path] = make_float4(w.x, w.y, w.z, 1.f);
+    b.thr[0][path] = make_float4(w.x, w.y, w.z, 1.f);
     b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
-    b.prev[path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
+    b.prev[0][path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
     return true;  // traced unconditionally (:209)
   }
@@ -883,8 +882,8 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     const Ray nray = spawn_ray(si.p, si.n, to_world(si.sh, bs.wo));
     io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
     io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
-    b.thr[path] = make_float4(f.x, f.y, f.z, 1.f);
-    b.prev[path] = make_float4(f2.x, f2.y, f2.z, 0.f);
+    b.thr[0][path] = make_float4(f.x, f.y, f.z, 1.f);
+    b.prev[0][path] = make_float4(f2.x, f2.y, f2.z, 0.f);
     b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
     return true;
   }
@@ -901,7 +900,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     io.qp = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
     io.qd = make_float4(wi.x, wi.y, wi.z, 0.f);
     io.qt = make_float4(f.x, f.y, f.z, __uint_as_float(path));
-    b.prev[path] = make_float4(le.x, le.y, le.z, 0.f);
+    b.prev[0][path] = make_float4(le.x, le.y, le.z, 0.f);
   } else {
     L = L + f * (le + v3s(0.f));
     b.L[path] = make_float4(L.x, L.y, L.z, Lr.w);
@@ -988,6 +987,9 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       out_q[slot] = path_c;
       b.ray_o[rp ^ 1u][slot] = io.nro;
       b.ray_d[rp ^ 1u][slot] = io.nrd;
+      if constexpr (INT != MTX_INT_NERAD_RHS && INT != MTX_INT_NERAD) b.thr[rp ^ 1u][slot] = io.nthr;
+      if constexpr (INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH || INT == MTX_INT_NRC || INT == MTX_INT_PSSMLT_PATH)
+        b.prev[rp ^ 1u][slot] = io.nprev;
     }
     if (io.emit) b.shadow[sslot] = io.rec;
 #if MTX_DIAG_STAMPS
@@ -1261,11 +1263,11 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   b.mlt_prop[i] = make_float2(po.x, po.y);
   b.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);  // queue position i (identity)
   b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
-  b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+  b.thr[0][i] = make_float4(1.f, 1.f, 1.f, 1.f);
   b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
   // pssmltpath.py:42-44: prev_si zero, prev_bsdf_delta = True
   const uint32_t fl = p.integrator == MTX_INT_PSSMLT_PATH ? (PF_PREV_DELTA << 16) : 0u;
-  if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
   b.queue[0][i] = i;
 }

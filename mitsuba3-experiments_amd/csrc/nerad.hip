@@ -44,9 +44,9 @@ __global__ void k_nerad_raygen(WaveBuffers b, ChunkParams p, const float4 *lhs, 
   b.hit[i] = make_float4(1.f, a.w, c.w, d.x);
   b.ray_o[0][i] = make_float4(a.x, a.y, a.z, 0.f);  // queue position i (identity)
   b.ray_d[0][i] = make_float4(-c.x, -c.y, -c.z, 0.f);
-  b.thr[i] = make_float4(1.f, 1.f, 1.f, 1.f);
+  b.thr[0][i] = make_float4(1.f, 1.f, 1.f, 1.f);
   b.L[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  b.prev[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
   b.queue[0][i] = i;
 }
@@ -58,7 +58,7 @@ __global__ void k_nerad_apply(WaveBuffers b, const float *out, uint32_t render) 
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
     const float4 t = b.cq_t[q];
     const uint32_t path = __float_as_uint(t.w);
-    const float4 le = b.prev[path];
+    const float4 le = b.prev[0][path];
     float4 L = b.L[path];
     if (render) {
       L.x = out[3 * (size_t)q] * t.x + le.x;

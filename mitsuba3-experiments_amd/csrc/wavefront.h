@@ -5,9 +5,9 @@
 // dwordx4 load/store per field group per lane):
 //   ray_o  float4  o.xyz, maxt                       } by QUEUE position, two
 //   ray_d  float4  d.xyz, a0 (NRC footprint, nrc.py:121) } planes by bounce parity
-//   thr    float4  throughput.xyz, eta
+//   thr    float4  throughput.xyz, eta                } by queue position too
 //   L      float4  result.xyz, prev_bsdf_pdf
-//   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93)
+//   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93) } (thr, prev)
 //   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16
 //   pos    float2  film sample position (block.put position, path.py:101)
 //   hit    float4  t, prim, u, v (written by the closest-hit traversal)
@@ -95,7 +95,10 @@ struct WaveBuffers {
   // append slot (no path-indexed scatter on either side)
   float4 *ray_o[2], *ray_d[2];
   uint32_t ray_par;
-  float4 *thr, *L, *prev;
+  // throughput and previous vertex move with the ray the same way (the nerad
+  // integrators keep them path-indexed in plane 0: k_nerad_apply reads them)
+  float4 *thr[2], *prev[2];
+  float4 *L;
   uint4 *misc;
   float2 *pos;
   float4 *hit;
