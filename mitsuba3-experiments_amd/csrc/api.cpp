@@ -451,11 +451,11 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
 
 namespace {
 
-// Default wavefront: up to 256 Mi paths (~264 B of state each, ~66 GB) so a
+// Default wavefront: up to 256 Mi paths (~328 B of state each, ~82 GB) so a
 // 1280x720 spp=256 frame runs as one chunk (fewer queue tails), bounded by
 // 40 % of the free HBM.
 constexpr uint32_t kDefaultChunk = 1u << 28;
-constexpr size_t kPathStateBytes = 264;
+constexpr size_t kPathStateBytes = 328;
 uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
@@ -475,9 +475,10 @@ int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     if ((rc = dalloc(c->ray_o, 32ull * cap))) return rc;  // two planes (bounce parity), wavefront.h
     if ((rc = dalloc(c->ray_d, 32ull * cap))) return rc;
     if ((rc = dalloc(c->thr, 32ull * cap))) return rc;
-    if ((rc = dalloc(c->L, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->L, 48ull * cap))) return rc;  // queue planes 0 / 1 + the per-path plane
+
     if ((rc = dalloc(c->prev, 32ull * cap))) return rc;
-    if ((rc = dalloc(c->misc, 16ull * cap))) return rc;
+    if ((rc = dalloc(c->misc, 48ull * cap))) return rc;
     if ((rc = dalloc(c->pos, 8ull * cap))) return rc;
     if ((rc = dalloc(c->hit, 16ull * cap))) return rc;
     if ((rc = dalloc(c->q0, 4ull * cap))) return rc;
@@ -500,10 +501,10 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.ray_par = 0;
   b.thr[0] = (float4 *)c->thr.p;
   b.thr[1] = b.thr[0] + c->capacity;
-  b.L = (float4 *)c->L.p;
+  for (int k = 0; k < 3; ++k) b.L[k] = (float4 *)c->L.p + (size_t)k * c->capacity;
   b.prev[0] = (float4 *)c->prev.p;
   b.prev[1] = b.prev[0] + c->capacity;
-  b.misc = (uint4 *)c->misc.p;
+  for (int k = 0; k < 3; ++k) b.misc[k] = (uint4 *)c->misc.p + (size_t)k * c->capacity;
   b.pos = (float2 *)c->pos.p;
   b.hit = (float4 *)c->hit.p;
   b.queue[0] = (uint32_t *)c->q0.p;
@@ -541,8 +542,9 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   if (cap > w.capacity) {
     for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.prev})
       if ((rc = dalloc(*b, 32ull * cap))) return rc;
-    for (DevBuf *b : {&w.L, &w.misc, &w.hit})
-      if ((rc = dalloc(*b, 16ull * cap))) return rc;
+    for (DevBuf *b : {&w.L, &w.misc})
+      if ((rc = dalloc(*b, 48ull * cap))) return rc;
+    if ((rc = dalloc(w.hit, 16ull * cap))) return rc;
     if ((rc = dalloc(w.pos, 8ull * cap))) return rc;
     if ((rc = dalloc(w.q0, 4ull * cap))) return rc;
     if ((rc = dalloc(w.q1, 4ull * cap))) return rc;
@@ -566,10 +568,10 @@ mtxd::WaveBuffers buffers2(mtx_ctx *c) {
   b.ray_d[1] = b.ray_d[0] + w.capacity;
   b.thr[0] = (float4 *)w.thr.p;
   b.thr[1] = b.thr[0] + w.capacity;
-  b.L = (float4 *)w.L.p;
+  for (int k = 0; k < 3; ++k) b.L[k] = (float4 *)w.L.p + (size_t)k * w.capacity;
   b.prev[0] = (float4 *)w.prev.p;
   b.prev[1] = b.prev[0] + w.capacity;
-  b.misc = (uint4 *)w.misc.p;
+  for (int k = 0; k < 3; ++k) b.misc[k] = (uint4 *)w.misc.p + (size_t)k * w.capacity;
   b.pos = (float2 *)w.pos.p;
   b.hit = (float4 *)w.hit.p;
   b.queue[0] = (uint32_t *)w.q0.p;
@@ -766,9 +768,11 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
       uint32_t cnt = 0;
       hipMemcpyAsync(&cnt, b.counters + 4 * (bounce + 1), 4, hipMemcpyDeviceToHost, st);
       hipStreamSynchronize(st);
-      if (cnt == 0) break;
+      if (cnt == 0) return;
     }
   }
+  // paths a depth limit left queued keep their result in a queue plane
+  if (!nerad && !nerad_render) mtxd::launch_flush_tail(b, depth_iters, b.capacity, st);
 }
 
 int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_t n_trace, uint64_t n_shadow,

@@ -129,9 +129,9 @@ struct ShadowSrc {
     const ShadowRec &rec = b.shadow[pl.k];
     const float4 rt = rec.t, rx = rec.x;
 #endif
-    const uint32_t path = pl.path;
+    const uint32_t li = pl.path;  // L index (plane * capacity + position)
     const uint32_t fl = __float_as_uint(rt.w);
-    float4 L = b.L[path];
+    float4 L = b.L[0][li];
     if (!occluded) {
       if (fl & 1u) {
         L.x = fmaf(rt.x, rx.x, L.x);
@@ -148,7 +148,7 @@ struct ShadowSrc {
       if (fl & 4u) L.y = qnan;
       if (fl & 8u) L.z = qnan;
     }
-    b.L[path] = L;
+    b.L[0][li] = L;
   }
 };
 
@@ -186,7 +186,7 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   // not stored: the bounce-0 shade uses these constants (kInitThr / kInitL / kInitPrev)
   b.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);  // queue position i (identity)
   b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
-  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   b.pos[i] = pos;
   b.queue[0][i] = i;
 }
@@ -270,6 +270,8 @@ struct ShadeIO {
   bool query;  // NRC radiance-cache query at this hit (field.hip)
   float4 qp, qd, qt;
   float4 nro, nrd, nthr, nprev;  // the next ray and state: k_shade stores them at the path's append slot
+  float4 nL;                     // result and sampler state: at the append slot, or by path once the path ends
+  uint4 nmisc;
 #if MTX_DIAG_STAMPS
   Stamps st;
 #endif
@@ -329,7 +331,7 @@ __device__ __forceinline__ float end_w(uint32_t flags, float prev_pdf) {
   return MTX_FILM_FLAG_IN_L ? ((flags & PF_VALID_RAY) ? 1.f : 0.f) : prev_pdf;
 }
 __device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, float lw) {
-  return MTX_FILM_FLAG_IN_L ? lw != 0.f : ((b.misc[path].w >> 16) & PF_VALID_RAY) != 0;
+  return MTX_FILM_FLAG_IN_L ? lw != 0.f : ((b.misc[kFinal][path].w >> 16) & PF_VALID_RAY) != 0;
 }
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
@@ -338,14 +340,16 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const float4 ro = b.ray_o[rp][qi], rd = b.ray_d[rp][qi];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
-  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[path];
+  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[rp][qi];
   // prev (previous vertex, NRC spread): path-mis / path read it only for the
   // emission MIS of an emitter hit (pdf_emitter_direction is 0 otherwise), so
   // they load it below once the hit's emitter is known
   constexpr bool kPrevOnEmitter = INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH;
   float4 pv = kInitPrev;
   if (!kPrevOnEmitter && bounce != 0) pv = b.prev[rp][qi];
-  const uint4 mi = b.misc[path];
+  const uint4 mi = b.misc[rp][qi];
+  io.nL = Lr;  // an exit that changes neither keeps them
+  io.nmisc = mi;
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -384,7 +388,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     if (INT == MTX_INT_PATH) {
       L = L + emitter_eval(sv, si.emitter, si.wi);  // path.py:239
       if (!(depth < p.max_depth)) {                // path.py:235
-        b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+        io.nL = make_float4(L.x, L.y, L.z, prev_pdf);
         return false;
       }
     } else {  // NRC primary (nrc.py:117-121)
@@ -425,8 +429,8 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   const bool head_ok =
       (INT == MTX_INT_NRC && bounce == 0) ? si.valid : (depth < p.max_depth && si.valid);
   if (INT != MTX_INT_PATH_MIS && !head_ok) {
-    b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
-    if (INT == MTX_INT_NRC) b.misc[path] = make_uint4(mi.x, mi.y, mi.z, depth | (flags << 16));
+    io.nL = make_float4(L.x, L.y, L.z, prev_pdf);
+    if (INT == MTX_INT_NRC) io.nmisc = make_uint4(mi.x, mi.y, mi.z, depth | (flags << 16));
     return false;
   }
   if (INT == MTX_INT_PATH_MIS && p.restir && bounce == 0) {
@@ -438,10 +442,10 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     // escaped path: nothing after this point is observable (valid_ray,
     // result unchanged; throughput becomes 0 -> inactive) -- except the
     // sampler position, which ReSTIR keeps using (6 draws per iteration)
-    b.L[path] = make_float4(L.x, L.y, L.z, end_w(flags, prev_pdf));
+    io.nL = make_float4(L.x, L.y, L.z, end_w(flags, prev_pdf));
     if (p.restir) {
       rng.advance(6);
-      b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+      io.nmisc = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
     }
     return false;
   }
@@ -554,8 +558,8 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, a0);
   io.nthr = make_float4(T.x, T.y, T.z, eta);
   io.nprev = make_float4(prev_p.x, prev_p.y, prev_p.z, spread);
-  b.L[path] = make_float4(L.x, L.y, L.z, (INT == MTX_INT_PATH_MIS && !active) ? end_w(flags, prev_pdf) : prev_pdf);
-  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  io.nL = make_float4(L.x, L.y, L.z, (INT == MTX_INT_PATH_MIS && !active) ? end_w(flags, prev_pdf) : prev_pdf);
+  io.nmisc = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
 #if MTX_DIAG_STAMPS
   MTX_STAMP(io.st, 5);
 #endif
@@ -575,8 +579,8 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
                                              const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                              const float4 h, ShadeIO &io) {
   const uint32_t rp = (bounce + b.ray_par) & 1u;
-  const float4 rd = b.ray_d[rp][qi], th = b.thr[rp][qi], Lr = b.L[path];
-  const uint4 mi = b.misc[path];
+  const float4 rd = b.ray_d[rp][qi], th = b.thr[rp][qi], Lr = b.L[rp][qi];
+  const uint4 mi = b.misc[rp][qi];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -629,8 +633,8 @@ __device__ __forceinline__ bool shade_pssmlt(const DevScene &s, const SceneView 
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
   io.nthr = make_float4(T.x, T.y, T.z, eta);
-  b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
-  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  io.nL = make_float4(L.x, L.y, L.z, prev_pdf);
+  io.nmisc = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
 }
 
@@ -645,8 +649,8 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
                                              const float4 h, ShadeIO &io) {
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const float4 rd = b.ray_d[rp][qi];
-  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[path];
-  const uint4 mi = b.misc[path];
+  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[rp][qi];
+  const uint4 mi = b.misc[rp][qi];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -682,8 +686,8 @@ __device__ __forceinline__ bool shade_simple(const DevScene &s, const SceneView 
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
   io.nthr = make_float4(T.x, T.y, T.z, eta);
-  b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
-  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  io.nL = make_float4(L.x, L.y, L.z, bs.pdf);
+  io.nmisc = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
 }
 
@@ -698,8 +702,8 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
                                                   const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                                   const float4 h, ShadeIO &io) {
   const uint32_t rp = (bounce + b.ray_par) & 1u;
-  const float4 rd = b.ray_d[rp][qi], th = b.thr[rp][qi], Lr = b.L[path], pv = b.prev[rp][qi];
-  const uint4 mi = b.misc[path];
+  const float4 rd = b.ray_d[rp][qi], th = b.thr[rp][qi], Lr = b.L[rp][qi], pv = b.prev[rp][qi];
+  const uint4 mi = b.misc[rp][qi];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -786,9 +790,9 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
   io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
   io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
   io.nthr = make_float4(T.x, T.y, T.z, eta);
-  b.L[path] = make_float4(L.x, L.y, L.z, prev_pdf);
+  io.nL = make_float4(L.x, L.y, L.z, prev_pdf);
   io.nprev = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
-  b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  io.nmisc = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   return active;
 }
 
@@ -813,11 +817,12 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
                                             ShadeIO &io) {
   const float4 rd = b.ray_d[(bounce + b.ray_par) & 1u][qi];
   // a rendered lane's bounce-0 state is the camera raygen's (nothing stored)
-  const float4 Lr = (RENDER && bounce == 0) ? kInitL : b.L[path];
+  const float4 Lr = (RENDER && bounce == 0) ? kInitL : b.L[kFinal][path];
   // thr / prev path-indexed in plane 0 (k_nerad_apply reads prev by path)
   const float4 pv = (RENDER && bounce == 0) ? kInitPrev : b.prev[0][path];
   const float4 th = (RENDER && bounce == 0) ? kInitThr : b.thr[0][path];
-  const uint4 mi = b.misc[path];
+  // a rendered lane's bounce-0 sampler state is the camera raygen's (queue plane 0, identity)
+  const uint4 mi = (RENDER && bounce == 0) ? b.misc[0][path] : b.misc[kFinal][path];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -851,9 +856,9 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     io.nro = make_float4(nray.o.x, nray.o.y, nray.o.z, nray.maxt);
     io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
     b.thr[0][path] = make_float4(w.x, w.y, w.z, 1.f);
-    b.L[path] = make_float4(L.x, L.y, L.z, bs.pdf);
+    b.L[kFinal][path] = make_float4(L.x, L.y, L.z, bs.pdf);
     b.prev[0][path] = make_float4(si.p.x, si.p.y, si.p.z, 0.f);
-    b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+    b.misc[kFinal][path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
     return true;  // traced unconditionally (:209)
   }
   if (!RENDER && bounce == 1) {
@@ -884,7 +889,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     io.nrd = make_float4(nray.d.x, nray.d.y, nray.d.z, 0.f);
     b.thr[0][path] = make_float4(f.x, f.y, f.z, 1.f);
     b.prev[0][path] = make_float4(f2.x, f2.y, f2.z, 0.f);
-    b.misc[path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
+    b.misc[kFinal][path] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth);
     return true;
   }
   // stop vertex (:219-229; render: :250-252)
@@ -893,7 +898,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   const V3 le = emitter_eval(sv, si.emitter, si.wi);
   if (RENDER && !si.valid) {
     L = v3s(0.f) * f + le;
-    b.L[path] = make_float4(L.x, L.y, L.z, Lr.w);
+    b.L[kFinal][path] = make_float4(L.x, L.y, L.z, Lr.w);
   } else if (si.valid) {
     io.query = true;
     const V3 wi = to_world(si.sh, si.wi);  // Field.__call__ wi (nerad.py:100)
@@ -903,7 +908,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     b.prev[0][path] = make_float4(le.x, le.y, le.z, 0.f);
   } else {
     L = L + f * (le + v3s(0.f));
-    b.L[path] = make_float4(L.x, L.y, L.z, Lr.w);
+    b.L[kFinal][path] = make_float4(L.x, L.y, L.z, Lr.w);
   }
   return false;
 }
@@ -926,6 +931,8 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
   // rays: one 64-bit pair, reserved by one atomic per block step
   uint32_t *out_cnt = &b.counters[4 * (bounce + 1) + 0];
   const uint32_t rp = (bounce + b.ray_par) & 1u;  // this bounce's ray planes; the next ray goes to rp ^ 1
+  // the nerad integrators keep thr / prev / L / misc by path (plane 0 / kFinal)
+  constexpr bool kNerad = INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD;
   const uint32_t stride = gridDim.x * kShadeBlock;
   uint32_t parity = 0;
   // software pipeline over the persistent loop: the next step's queue entry
@@ -987,11 +994,24 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       out_q[slot] = path_c;
       b.ray_o[rp ^ 1u][slot] = io.nro;
       b.ray_d[rp ^ 1u][slot] = io.nrd;
-      if constexpr (INT != MTX_INT_NERAD_RHS && INT != MTX_INT_NERAD) b.thr[rp ^ 1u][slot] = io.nthr;
+      if constexpr (!kNerad) b.thr[rp ^ 1u][slot] = io.nthr;
       if constexpr (INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH || INT == MTX_INT_NRC || INT == MTX_INT_PSSMLT_PATH)
         b.prev[rp ^ 1u][slot] = io.nprev;
+      if constexpr (!kNerad) {
+        b.L[rp ^ 1u][slot] = io.nL;
+        b.misc[rp ^ 1u][slot] = io.nmisc;
+      }
+    } else if (!kNerad && valid) {
+      b.L[kFinal][path_c] = io.nL;
+      b.misc[kFinal][path_c] = io.nmisc;
     }
-    if (io.emit) b.shadow[sslot] = io.rec;
+    if (io.emit) {
+      // the contribution goes to the path's L where the next shade (or the
+      // film) reads it
+      const uint32_t li = (kNerad || !cont) ? kFinal * b.capacity + path_c : (rp ^ 1u) * b.capacity + slot;
+      io.rec.d.w = __uint_as_float(li);
+      b.shadow[sslot] = io.rec;
+    }
 #if MTX_DIAG_STAMPS
     MTX_STAMP(stp, 6);
 #endif
@@ -1022,6 +1042,20 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
 #endif
 }
 
+// Paths still queued after a chunk's last bounce (its depth limit stops
+// every integrator's paths first; kept so that no loop bound can leave a
+// result in a queue plane): their L / misc move to the per-path plane.
+__global__ void k_flush_tail(WaveBuffers b, uint32_t bounce) {
+  const uint32_t n = b.counters[4 * bounce];
+  const uint32_t *q = b.queue[bounce & 1];
+  const uint32_t rp = (bounce + b.ray_par) & 1u;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const uint32_t path = q[k];
+    b.L[kFinal][path] = b.L[rp][k];
+    b.misc[kFinal][path] = b.misc[rp][k];
+  }
+}
+
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
 // plain sum: L = L + T * out, as the oracle-side composition in the tests).
 __global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *perm) {
@@ -1029,11 +1063,11 @@ __global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *p
   for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
     const float4 t = b.cq_t[perm ? perm[q] : q];  // out row q belongs to query perm[q]
     const uint32_t path = __float_as_uint(t.w);
-    float4 L = b.L[path];
+    float4 L = b.L[kFinal][path];
     L.x = L.x + t.x * out[3 * (size_t)q];
     L.y = L.y + t.y * out[3 * (size_t)q + 1];
     L.z = L.z + t.z * out[3 * (size_t)q + 2];
-    b.L[path] = L;
+    b.L[kFinal][path] = L;
   }
 }
 
@@ -1042,7 +1076,7 @@ __global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *p
 // stage 2 per film pixel (9 neighbours in fixed order). See DESIGN.md.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ V3 final_L(const WaveBuffers &b, const ChunkParams &p, uint32_t path) {
-  const float4 l = b.L[path];
+  const float4 l = b.L[kFinal][path];
   V3 L = V3{l.x, l.y, l.z};
   if (p.integrator == MTX_INT_PATH_MIS && !end_valid(b, path, l.w)) L = v3s(0.f);  // path-mis.py:155
   return L;
@@ -1090,7 +1124,7 @@ __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkPara
       const uint32_t e = (uint32_t)it * 64 + lane, j = e / S, sm = e % S;
       if (q0 + j < p.n_px && sm < ns) {
         const uint32_t path = (q0 + j) * p.spp + s0 + sm;
-        float4 l = b.L[path];
+        float4 l = b.L[kFinal][path];
         if (mask_valid && !end_valid(b, path, l.w)) l = make_float4(0.f, 0.f, 0.f, 0.f);
         const float2 ps = b.pos[path];
         sv[0][j][sm] = l.x;
@@ -1174,11 +1208,11 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
   L_out[3 * (size_t)i] = L.x;
   L_out[3 * (size_t)i + 1] = L.y;
   L_out[3 * (size_t)i + 2] = L.z;
-  const uint32_t flags = b.misc[i].w >> 16;
+  const uint32_t flags = b.misc[kFinal][i].w >> 16;
   uint8_t v = 1;
   if (p.integrator == MTX_INT_PATH_MIS) v = (flags & PF_VALID_RAY) ? 1 : 0;
   if (p.integrator == MTX_INT_NRC) v = (flags & PF_PRIMARY_VALID) ? 1 : 0;
-  if (p.integrator == MTX_INT_SIMPLE) v = (b.misc[i].w & 0xffffu) != 0 ? 1 : 0;  // simple.py:118
+  if (p.integrator == MTX_INT_SIMPLE) v = (b.misc[kFinal][i].w & 0xffffu) != 0 ? 1 : 0;  // simple.py:118
   valid_out[i] = v;
 }
 
@@ -1222,7 +1256,7 @@ __global__ void k_mlt_init(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   if (i >= p.n_paths) return;
   const uint32_t q = i / p.spp;
   const Pcg32 rng = sampler_lane(p.seed, (p.px0 + q) * p.spp_total + p.sample_offset + (i - q * p.spp));
-  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+  b.misc[kFinal][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
   // offset = 0.5, cumulative_weight = 0 (:198-200); w: vertex depths that may
   // differ between the proposed and current buffers (k_mlt_end)
   b.mlt_cur[i] = make_float4(0.5f, 0.5f, 0.f, 0.f);
@@ -1242,7 +1276,7 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) b.counters[0] = p.n_paths;
   if (i >= p.n_paths) return;
-  const uint4 mi = b.misc[i];
+  const uint4 mi = b.misc[kFinal][i];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
@@ -1264,11 +1298,11 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   b.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);  // queue position i (identity)
   b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.thr[0][i] = make_float4(1.f, 1.f, 1.f, 1.f);
-  b.L[i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1
+  b.L[0][i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1 (queue position i)
   // pssmltpath.py:42-44: prev_si zero, prev_bsdf_delta = True
   const uint32_t fl = p.integrator == MTX_INT_PSSMLT_PATH ? (PF_PREV_DELTA << 16) : 0u;
   if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
+  b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
   b.queue[0][i] = i;
 }
 
@@ -1276,11 +1310,11 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
 __global__ void k_mlt_end(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n_paths) return;
-  const uint4 mi = b.misc[i];
+  const uint4 mi = b.misc[kFinal][i];
   Pcg32 rng;
   rng.state = ((uint64_t)mi.y << 32) | (uint64_t)mi.x;
   rng.seq = mi.z;
-  const float4 lp4 = b.L[i];
+  const float4 lp4 = b.L[kFinal][i];
   const V3 Lp = V3{lp4.x, lp4.y, lp4.z};
   float4 cur = b.mlt_cur[i];
   const float4 lc4 = b.mlt_L[i];
@@ -1311,7 +1345,7 @@ __global__ void k_mlt_end(WaveBuffers b, ChunkParams p, uint32_t max_depth) {
   }
   cur.w = (float)dirty;
   b.mlt_cur[i] = cur;
-  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+  b.misc[kFinal][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
 }
 
 // block.put(pos, L / cw) at the integer pixel position (:161-165), running
@@ -1441,6 +1475,10 @@ void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacit
                         const uint32_t *perm) {
   const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 16384);
   hipLaunchKernelGGL(k_cache_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out, perm);
+}
+void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, hipStream_t st) {
+  const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_flush_tail, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, bounce);
 }
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
   hipLaunchKernelGGL(k_mlt_init, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);

@@ -45,9 +45,9 @@ __global__ void k_nerad_raygen(WaveBuffers b, ChunkParams p, const float4 *lhs, 
   b.ray_o[0][i] = make_float4(a.x, a.y, a.z, 0.f);  // queue position i (identity)
   b.ray_d[0][i] = make_float4(-c.x, -c.y, -c.z, 0.f);
   b.thr[0][i] = make_float4(1.f, 1.f, 1.f, 1.f);
-  b.L[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  b.L[kFinal][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  b.misc[i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
+  b.misc[kFinal][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, 0u);
   b.queue[0][i] = i;
 }
 
@@ -59,7 +59,7 @@ __global__ void k_nerad_apply(WaveBuffers b, const float *out, uint32_t render) 
     const float4 t = b.cq_t[q];
     const uint32_t path = __float_as_uint(t.w);
     const float4 le = b.prev[0][path];
-    float4 L = b.L[path];
+    float4 L = b.L[kFinal][path];
     if (render) {
       L.x = out[3 * (size_t)q] * t.x + le.x;
       L.y = out[3 * (size_t)q + 1] * t.y + le.y;
@@ -69,7 +69,7 @@ __global__ void k_nerad_apply(WaveBuffers b, const float *out, uint32_t render) 
       L.y = L.y + t.y * (le.y + out[3 * (size_t)q + 1]);
       L.z = L.z + t.z * (le.z + out[3 * (size_t)q + 2]);
     }
-    b.L[path] = L;
+    b.L[kFinal][path] = L;
   }
 }
 
@@ -80,7 +80,7 @@ __global__ void k_nerad_mean(WaveBuffers b, uint32_t n, uint32_t M, float *L_rhs
   float x = 0.f, y = 0.f, z = 0.f;
   for (uint32_t j = 0; j < M; ++j) {
     const uint32_t k = i * M + j;
-    const float4 L = b.L[k];
+    const float4 L = b.L[kFinal][k];
     x = x + L.x;
     y = y + L.y;
     z = z + L.z;

@@ -110,6 +110,7 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   const uint32_t i = r.lane0 + t;
   bool enq = false;
   float4 nro = make_float4(0.f, 0.f, 0.f, 0.f), nrd = nro;
+  uint4 nmi = make_uint4(0u, 0u, 0u, 0u);
   const uint32_t path = t < r.nb ? path_of(t, p) : 0u;
   if (t < r.nb) {
     const float4 h = b.hit[path], d4 = b.ray_d[0][path];  // bounce-0 queue is the identity
@@ -117,7 +118,7 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
     r.prim_dir[i] = d4;
     const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
     r.emit[i] = f4(emitter_eval(sv, si.emitter, si.wi), 0.f);
-    Pcg32 rng = ld_rng(b.misc[path]);
+    Pcg32 rng = ld_rng(b.misc[0][path]);
     V3 wo;
     float pdf;
     if (r.flags & MTX_RESTIR_BSDF_SAMPLING) {
@@ -141,12 +142,12 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
       nro = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
       nrd = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
       // throughput 1, L 0, prev_bsdf_pdf 1, prev_p 0: the bounce-0 shade's constants
-      b.misc[path] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
+      nmi = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
       enq = true;
     } else {
       rng.advance(6);
-      b.L[path] = make_float4(0.f, 0.f, 0.f, 1.f);
-      b.misc[path] = st_rng(rng, 0u);
+      b.L[kFinal][path] = make_float4(0.f, 0.f, 0.f, 1.f);
+      b.misc[kFinal][path] = st_rng(rng, 0u);
       b.rs_xs[path] = make_float4(0.f, 0.f, 0.f, 0.f);
       b.rs_ns[path] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -158,6 +159,7 @@ __global__ void k_rs_begin(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
     b.queue[0][slot] = path;
     b.ray_o[1][slot] = nro;
     b.ray_d[1][slot] = nrd;
+    b.misc[1][slot] = nmi;
   }
 }
 
@@ -166,8 +168,8 @@ __global__ void k_rs_collect(WaveBuffers b, ChunkParams p, RestirBuffers r) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= r.nb) return;
   const uint32_t i = r.lane0 + t, path = path_of(t, p);
-  const float4 l = b.L[path];
-  const uint4 m = b.misc[path];
+  const float4 l = b.L[kFinal][path];
+  const uint4 m = b.misc[kFinal][path];
   const bool valid_ray = ((m.w >> 16) & PF_VALID_RAY) != 0;
   r.cur[2 * (size_t)r.n + i] = b.rs_xs[path];
   r.cur[3 * (size_t)r.n + i] = b.rs_ns[path];
@@ -392,7 +394,7 @@ __global__ void k_rs_final(DevScene s, WaveBuffers b, ChunkParams p, RestirBuffe
   const float4 em = r.emit[i];
   const V3 res = beta * R.z.L_o * R.W + V3{em.x, em.y, em.z};
   const uint32_t path = path_of(t, p);
-  b.L[path] = make_float4(res.x, res.y, res.z, 0.f);
+  b.L[kFinal][path] = make_float4(res.x, res.y, res.z, 0.f);
   const uint32_t x = i / p.spp % p.width, y = i / p.width / p.spp;
   b.pos[path] = make_float2((float)x, (float)y);
 }

@@ -8,7 +8,7 @@
 //   thr    float4  throughput.xyz, eta                } by queue position too
 //   L      float4  result.xyz, prev_bsdf_pdf
 //   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93) } (thr, prev)
-//   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16
+//   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16 (L, misc: queue-ordered planes + a per-path final plane)
 //   pos    float2  film sample position (block.put position, path.py:101)
 //   hit    float4  t, prim, u, v (written by the closest-hit traversal)
 // Paths of a chunk are stored sample-major: path = s * n_px + q for sample s
@@ -78,10 +78,13 @@ struct DevScene {
   mtx_camera camera;
 };
 
-// Shadow-ray record (64 B): o.xyz maxt | d.xyz path | T.xyz flags | X.xyz 0
+// Shadow-ray record (64 B): o.xyz maxt | d.xyz L index | T.xyz flags | X.xyz 0
+// (L index = plane * capacity + position of the path's L, WaveBuffers)
 // flags bit0: fma form L = fma(T, X, L) (path-mis.py:117) else L = L + X
 // (path.py:259, nrc.py:62); bits 1..3: the occluded-case contribution of that
 // channel is NaN (non-finite BSDF value / MIS weight), see DESIGN.md.
+constexpr int kFinal = 2;  // the per-path plane of L / misc
+
 struct ShadowRec {
   float4 o;
   float4 d;
@@ -98,8 +101,14 @@ struct WaveBuffers {
   // throughput and previous vertex move with the ray the same way (the nerad
   // integrators keep them path-indexed in plane 0: k_nerad_apply reads them)
   float4 *thr[2], *prev[2];
-  float4 *L;
-  uint4 *misc;
+  // result and sampler state: planes 0 / 1 by queue position (bounce parity,
+  // as the rays), plane kFinal by path -- a path's state lands there when it
+  // ends (k_shade; k_flush_tail for paths still queued after the last
+  // bounce), where the film, k_collect and the PSSMLT / ReSTIR / nerad
+  // kernels read it. The three L planes are contiguous (capacity apart):
+  // a shadow record addresses its target as plane * capacity + index.
+  float4 *L[3];
+  uint4 *misc[3];
   float2 *pos;
   float4 *hit;
   uint32_t *queue[2];
@@ -190,6 +199,7 @@ void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st)
 void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
+void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, hipStream_t st);
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st);
 // perm (optional): MLP row q belongs to cache query perm[q]
 void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st,
