@@ -6,10 +6,12 @@ A step renders ONE 1280x720 film at a fixed global spp=256 (strong scaling:
 the job's work is the same at every N). Rank r of N traces the global sample
 range [r*256/N, (r+1)*256/N) of every pixel with global-lane seeding
 (path.py:156-161: lane = pixel*spp + sample), so the N=1 and N>1 films hold
-the same paths; the per-rank films are gathered to rank 0 over RCCL and
-summed in rank order (deterministic). Inputs (scene, BVH) are resident in HBM
-before the timed region; the film stays in HBM and only the gather crosses
-GPUs. The timed region includes the gather.
+the same paths; the per-rank films are combined on rank 0 over RCCL by an
+all_to_all of film slices, a rank-order sum of each slice on its rank and a
+gather of the summed slices (deterministic, the same bits as gathering the
+films and summing them in rank order). Inputs (scene, BVH) are resident in
+HBM before the timed region; the film stays in HBM and only the combine
+crosses GPUs. The timed region includes it.
 
 `python bench.py --gpus N` without a torchrun environment starts the N rank
 processes itself (torch.distributed.run, before this process touches the
@@ -221,7 +223,7 @@ def main():
         r = integ.render_film(sc, seed=i, spp=s1 - s0, spp_total=spp, sample_offset=s0, out=film,
                               stats=stats, chunk_paths=args.chunk, counters=counters)
         if world > 1:
-            combined[0] = distributed.gather_sum(film)  # RCCL gather to rank 0, rank-order sum
+            combined[0] = distributed.reduce_sum(film)  # RCCL all_to_all of slices, slice sums, gather to rank 0
         return r[1] if stats else None
 
     for i in range(args.warmup):
@@ -315,7 +317,7 @@ def main():
                 "global_spp": spp,
                 "spp_per_rank": s1 - s0,
                 "paths_per_step": W * H * spp,
-                "parallelism": f"sample-range shards x{world}" + (", RCCL gather of films to rank 0" if world > 1 else ""),
+                "parallelism": f"sample-range shards x{world}" + (", RCCL slice-reduce of films to rank 0" if world > 1 else ""),
             },
             "roofline": {
                 # the busier of the two units the traversal can saturate, from the

@@ -93,6 +93,38 @@ def gather_sum(film, group=None):
     return total.to(t.device)
 
 
+def reduce_sum(film, group=None):
+    """`gather_sum` with the sum spread over the ranks: an all_to_all hands
+    every rank one 1/N slice of every film, each rank sums its slice in rank
+    order, and rank 0 gathers the N summed slices (None on other ranks).
+    Bit-identical to `gather_sum` (the same additions, elementwise, in the
+    same order); rank 0 receives (N-1)/N of one film instead of N-1 films
+    and adds 1/N of them, and every xGMI link carries 2/N of a film."""
+    import torch
+    import torch.distributed as dist
+
+    t = _to_tensor(film)
+    c = _comm(t, group)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world == 1:
+        return (torch.zeros_like(c) + c).to(t.device)
+    flat = c.reshape(-1)
+    n = flat.numel()
+    chunk = -(-n // world)
+    send = flat if chunk * world == n else torch.cat([flat, flat.new_zeros(chunk * world - n)])
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    part = torch.zeros(chunk, dtype=c.dtype, device=c.device)
+    for r in range(world):
+        part.add_(recv[r * chunk:(r + 1) * chunk])
+    parts = [torch.empty_like(part) for _ in range(world)] if rank == 0 else None
+    dist.gather(part, parts, dst=0, group=group)
+    if rank != 0:
+        return None
+    return torch.cat(parts)[:n].reshape(c.shape).to(t.device)
+
+
 def gather_bands(band, y0: int, y1: int, height: int, group=None):
     """Stitch row-band films (with halos) into the full film on rank 0."""
     import torch
@@ -130,7 +162,7 @@ def render_sharded(render, height: int, spp: int, mode: str = "samples", group=N
     if mode == "samples":
         s0, s1 = sample_range(spp, world, rank)
         film = render(s1 - s0, spp, s0, 0, height)
-        return gather_sum(film, group)
+        return reduce_sum(film, group)
     if mode == "rows":
         y0, y1 = row_bands(height, world)[rank]
         film = render(spp, spp, 0, y0, y1)

@@ -165,7 +165,7 @@ def pssmlt(args, with_nee=False):
     for k in range(args.steps):
         st = _sum_stats(st, integ.render_film(sc, seed=k, stats=True, **shard)[1])
         if rk.world > 1:
-            distributed.gather_sum(film)
+            distributed.reduce_sum(film)
     rk.barrier()
     dt = rk.max_elapsed(time.perf_counter() - t0) / args.steps
     st = {x: v / args.steps for x, v in st.items()}
