@@ -101,6 +101,7 @@ struct mtx_ctx {
   hipStream_t stream = nullptr;
   Wave2 w2;
   uint32_t streams = MTX_STREAMS;  // 1: every chunk on `stream` (MTX_STREAMS env: A/B)
+  uint32_t streams_max_log2 = 27;  // two streams for renders of <= 2^this paths (MTX_STREAMS_MAX_LOG2: A/B)
   bool has_scene = false;
   // scene
   DevBuf stack_ovf;  // traversal stack entries beyond the LDS part
@@ -208,6 +209,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
+  if (const char *e = getenv("MTX_STREAMS_MAX_LOG2")) c->streams_max_log2 = (uint32_t)std::max(16, std::min(31, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
@@ -1017,13 +1019,14 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   // chunks that alternate between them (the caller's chunk size still caps a
   // chunk), so one chunk's kernels fill the tails of the other's persistent
   // trace launches (~0.2 ms per launch that does not shrink with the rays).
-  // Renders of 2^16 .. 2^26 paths: the bench's per-rank share at N >= 4
-  // (spp 32: 26.8 -> 25.9 ms per step); at spp 256 (2^27.8 paths) it gains
-  // nothing and would only blur the per-kernel event times. Path-state
-  // integrators without a per-chunk cache pass only.
+  // Renders of 2^16 .. 2^27 paths: the bench's per-rank share at N >= 2
+  // (spp 32: 26.8 -> 25.9 ms per step; spp 128: 91.6 -> 90.2 ms); at spp 256
+  // (2^27.8 paths) it gains 0.5 % and would blur the per-kernel event times
+  // the N = 1 roofline is measured with. Path-state integrators without a
+  // per-chunk cache pass only.
   const uint64_t n_paths_all = (uint64_t)band_px * a->spp;
   const bool two = c->streams > 1 && !mlt && !nrc_cache && !nerad_render && a->integrator != MTX_INT_RESTIR_GI &&
-                   n_paths_all >= (1u << 16) && n_paths_all <= (1u << 26);
+                   n_paths_all >= (1u << 16) && n_paths_all <= (1ull << c->streams_max_log2);
   if (two) px_per_chunk = std::min(px_per_chunk, (band_px + 1) / 2);
   const uint32_t cap = px_per_chunk * a->spp;
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
