@@ -936,20 +936,56 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   if (want_stats) HIP_TRY(hipMemsetAsync(c->stats.p, 0, 64, c->stream));
   hipEvent_t e;
   if (run_a) {
-    // sample_initial: primary rays and their closest hits
-    HIP_TRY(reset_counters(b, depth, st));
-    mtxd::launch_raygen_camera(c->scene, b, p, st);
-    e = tm.begin(0);
-    mtxd::launch_trace_closest(c->scene, b, 0, p.stats, c->trace_grid, st);
-    tm.end(0, e);
-    ++*n_trace;
-    HIP_TRY(reset_counters(b, depth, st));
-    mtxd::launch_restir_begin(c->scene, b, p, r, st);
-    mtxd::WaveBuffers b1 = b;  // k_rs_begin left the secondary rays in the parity-1 planes
-    b1.ray_par = 1;
-    run_bounces(c, b1, p, tm, n_trace, n_shadow);  // sample_ray (path-mis loop)
-    mtxd::launch_restir_collect(b, p, r, st);
-    mtxd::launch_restir_temporal(r, p, st);
+    // Stage A is per lane up to and including the temporal resampling (which
+    // reads this frame's lane and the complete previous frame), so the band's
+    // rows split into two halves traced on two wavefronts / streams: one
+    // half's kernels fill the tails of the other's short (~2 M-ray)
+    // persistent launches. Same lanes, same draws: bit-identical.
+    const uint32_t rows = a->y1 - a->y0;
+    const bool two = c->streams > 1 && rows >= 2 && nb >= (1u << 16);
+    const uint32_t ym = two ? a->y0 + rows / 2 : a->y1;
+    mtxd::DevScene s2 = c->scene;
+    mtxd::WaveBuffers bw2{};
+    if (two) {
+      if ((rc = ensure_wavefront2(c, (a->y1 - ym) * W * spp, depth))) return rc;
+      bw2 = buffers2(c);
+      s2.stack_ovf = (int32_t *)c->w2.stack_ovf.p;
+      HIP_TRY(hipEventRecord(c->w2.start, st));  // after the frame-0 clears
+      HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
+    }
+    for (int h = 0; h < (two ? 2 : 1); ++h) {
+      const uint32_t ya = h ? ym : a->y0, yb = h ? a->y1 : ym;
+      hipStream_t sh = h ? c->w2.stream : st;
+      const mtxd::DevScene &sc = h ? s2 : c->scene;
+      mtxd::WaveBuffers bh = h ? bw2 : b;
+      bh.rs_xs = b.rs_xs + (size_t)(ya - a->y0) * W * spp;  // path-indexed within the half
+      bh.rs_ns = b.rs_ns + (size_t)(ya - a->y0) * W * spp;
+      mtxd::ChunkParams ph = p;
+      ph.px0 = ya * W;
+      ph.n_px = (yb - ya) * W;
+      ph.n_paths = ph.n_px * spp;
+      mtxd::RestirBuffers rh = r;
+      rh.lane0 = ya * W * spp;
+      rh.nb = ph.n_paths;
+      // sample_initial: primary rays and their closest hits
+      HIP_TRY(reset_counters(bh, depth, sh));
+      mtxd::launch_raygen_camera(sc, bh, ph, sh);
+      e = tm.begin(0, sh);
+      mtxd::launch_trace_closest(sc, bh, 0, ph.stats, c->trace_grid, sh);
+      tm.end(0, e, sh);
+      ++*n_trace;
+      HIP_TRY(reset_counters(bh, depth, sh));
+      mtxd::launch_restir_begin(sc, bh, ph, rh, sh);
+      mtxd::WaveBuffers b1 = bh;  // k_rs_begin left the secondary rays in the parity-1 planes
+      b1.ray_par = 1;
+      run_bounces(c, b1, ph, tm, n_trace, n_shadow, &sc, sh);  // sample_ray (path-mis loop)
+      mtxd::launch_restir_collect(bh, ph, rh, sh);
+      mtxd::launch_restir_temporal(rh, ph, sh);
+    }
+    if (two) {  // stage B reads every lane of the band
+      HIP_TRY(hipEventRecord(c->w2.done, c->w2.stream));
+      HIP_TRY(hipStreamWaitEvent(st, c->w2.done, 0));
+    }
   }
   if (run_b) {
     // spatial_resampling (reads samples / temporal reservoirs of rows outside
