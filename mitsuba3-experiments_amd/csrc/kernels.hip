@@ -105,7 +105,7 @@ struct ShadowSrc {
   // start (MTX_SHADOW_CARRY), so the finish is one L load + store instead of
   // a record load followed by the dependent L load
   struct Payload {
-    uint32_t k, path;
+    uint32_t k, li;  // record, L index of the target (plane * capacity + position)
 #if MTX_SHADOW_CARRY
     float4 t, x;
 #endif
@@ -116,7 +116,7 @@ struct ShadowSrc {
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
     pl.k = k;
-    pl.path = __float_as_uint(d4.w);
+    pl.li = __float_as_uint(d4.w);
 #if MTX_SHADOW_CARRY
     pl.t = b.shadow[k].t;
     pl.x = b.shadow[k].x;
@@ -129,7 +129,7 @@ struct ShadowSrc {
     const ShadowRec &rec = b.shadow[pl.k];
     const float4 rt = rec.t, rx = rec.x;
 #endif
-    const uint32_t li = pl.path;  // L index (plane * capacity + position)
+    const uint32_t li = pl.li;
     const uint32_t fl = __float_as_uint(rt.w);
     float4 L = b.L[0][li];
     if (!occluded) {
@@ -281,7 +281,7 @@ struct ShadeIO {
 // applied as fma(T, X, L); otherwise X is added. Xo is the contribution the
 // reference forms when the shadow ray is occluded (em_weight = 0).
 __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteraction &si, const DirectionSample &ds,
-                                            uint32_t path, V3 T, V3 X, V3 Xo, bool fma_form) {
+                                            V3 T, V3 X, V3 Xo, bool fma_form) {
   uint32_t fl = fma_form ? 1u : 0u;
   bool vis_noop, occ_noop;
   if (fma_form) {
@@ -300,7 +300,7 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   if (!io.emit) return;
   const Ray sr = spawn_ray_to(si.p, si.n, ds.p);
   io.rec.o = make_float4(sr.o.x, sr.o.y, sr.o.z, sr.maxt);
-  io.rec.d = make_float4(sr.d.x, sr.d.y, sr.d.z, __uint_as_float(path));
+  io.rec.d = make_float4(sr.d.x, sr.d.y, sr.d.z, 0.f);  // .w: the L index, set by k_shade after its append
   io.rec.t = make_float4(T.x, T.y, T.z, __uint_as_float(fl));
   io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
 }
@@ -498,14 +498,14 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     if (active_em) {
       const V3 X = bsdf_val * em_weight * mi_em;
       const V3 Xo = bsdf_val * v3s(0.f) * mi_em;
-      make_shadow(io, si, ds, path, T, X, Xo, true);
+      make_shadow(io, si, ds, T, X, Xo, true);
     }
   } else {
     const float mis_em = INT == MTX_INT_PATH ? mis_weight_a(ds.pdf, bsdf_pdf) : mis_weight_b(ds.pdf, bsdf_pdf);
     if (active_em) {
       const V3 P = T * bsdf_val * em_weight * mis_em;
       const V3 Po = T * bsdf_val * v3s(0.f) * mis_em;
-      make_shadow(io, si, ds, path, T, P, Po, false);
+      make_shadow(io, si, ds, T, P, Po, false);
     }
   }
 
@@ -772,7 +772,7 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
     float epdf;
     bsdf_eval_pdf(bd, mat, si.uv, si.wi, wo, &ev, &epdf);
     const float mi_em = mis_weight_b(ds.pdf, epdf);
-    make_shadow(io, si, ds, path, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true);
+    make_shadow(io, si, ds, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true);
   }
   b.vprop[vi] = make_float4(vwo.x, vwo.y, vwo.z, 0.f);  // :138
   b.vprop_es[vi] = make_float2(es.x, es.y);
@@ -847,7 +847,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     float pdf;
     bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :198
     const float mis = mis_weight_b(ds.pdf, pdf);
-    make_shadow(io, si, ds, path, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :200
+    make_shadow(io, si, ds, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :200
     const float s1 = rng.next_1d();
     const V2 s2 = rng.next_2d();
     BSDFSample bs;

@@ -3,18 +3,24 @@
 //
 // A chunk of C paths lives in HBM as SoA arrays of 16-byte records (one
 // dwordx4 load/store per field group per lane):
-//   ray_o  float4  o.xyz, maxt                       } by QUEUE position, two
-//   ray_d  float4  d.xyz, a0 (NRC footprint, nrc.py:121) } planes by bounce parity
-//   thr    float4  throughput.xyz, eta                } by queue position too
+//   ray_o  float4  o.xyz, maxt
+//   ray_d  float4  d.xyz, a0 (NRC footprint, nrc.py:121)
+//   thr    float4  throughput.xyz, eta
+//   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93)
 //   L      float4  result.xyz, prev_bsdf_pdf
-//   prev   float4  prev_si.p.xyz, spread (NRC, nrc.py:91-93) } (thr, prev)
-//   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16 (L, misc: queue-ordered planes + a per-path final plane)
+//   misc   uint4   rng.state lo/hi, rng.seq, depth | flags << 16
 //   pos    float2  film sample position (block.put position, path.py:101)
 //   hit    float4  t, prim, u, v (written by the closest-hit traversal)
-// Paths of a chunk are stored sample-major: path = s * n_px + q for sample s
-// of the chunk's pixel q (raygen_camera, film_src).
-// Queues are u32 path indices compacted with wave64 ballot + mbcnt and one
-// atomic per wave; shadow rays are 64-byte records.
+// ray_o / ray_d / thr / prev / L / misc travel with the path's queue entry:
+// two planes each, by bounce parity, indexed by queue position (the trace
+// and shade kernels read them coalesced; the shade stores a continuing
+// path's next state at its append slot). L and misc have a third, per-path
+// plane that an ending path's state lands in (film, chain and ReSTIR
+// kernels). pos is per path, hit per queue position. Paths of a chunk are
+// pixel-major by default: path = q * spp + s for sample s of the chunk's
+// pixel q (sample-major q + s * n_px with MTX_SAMPLE_MAJOR=1).
+// Queues are u32 path indices compacted per 256-thread block (ballot + mbcnt
+// + LDS, one atomic per block step); shadow rays are 64-byte records.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
