@@ -114,7 +114,10 @@ def reduce_sum(film, group=None):
     chunk = -(-n // world)
     send = flat if chunk * world == n else torch.cat([flat, flat.new_zeros(chunk * world - n)])
     recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
+    try:
+        dist.all_to_all_single(recv, send, group=group)
+    except (RuntimeError, NotImplementedError):  # a backend without all_to_all: every rank raises alike
+        return gather_sum(film, group)
     part = torch.zeros(chunk, dtype=c.dtype, device=c.device)
     for r in range(world):
         part.add_(recv[r * chunk:(r + 1) * chunk])
