@@ -92,6 +92,7 @@ struct Wave2 {
   hipStream_t stream = nullptr;
   hipEvent_t start = nullptr, done = nullptr;
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, xheads, stack_ovf;
+  DevBuf cq_p, cq_d, cq_t, cq_count, f_feat, f_out;  // NRC radiance-cache queries of its chunks
   uint32_t capacity = 0;
 };
 
@@ -100,6 +101,7 @@ struct mtx_ctx {
   int n_cu = 256;
   hipStream_t stream = nullptr;
   Wave2 w2;
+  uint32_t *q_pinned = nullptr;  // per-chunk cache-query counts of a stats render (pinned, kQSlots)
   uint32_t streams = MTX_STREAMS;  // 1: every chunk on `stream` (MTX_STREAMS env: A/B)
   uint32_t streams_max_log2 = 27;  // two streams for renders of <= 2^this paths (MTX_STREAMS_MAX_LOG2: A/B)
   bool has_scene = false;
@@ -244,12 +246,14 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   for (DevBuf *b : bufs) dfree(*b);
   Wave2 &w = c->w2;
   for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.L, &w.prev, &w.misc, &w.pos, &w.hit, &w.q0, &w.q1, &w.shadow,
-                    &w.counters, &w.xheads, &w.stack_ovf})
+                    &w.counters, &w.xheads, &w.stack_ovf, &w.cq_p, &w.cq_d, &w.cq_t, &w.cq_count, &w.f_feat,
+                    &w.f_out})
     dfree(*b);
   if (w.start) hipEventDestroy(w.start);
   if (w.done) hipEventDestroy(w.done);
   if (w.stream) hipStreamDestroy(w.stream);
   for (hipEvent_t ev : c->events) hipEventDestroy(ev);
+  if (c->q_pinned) hipHostFree(c->q_pinned);
   for (hipEvent_t ev : c->prim_ev)
     if (ev) hipEventDestroy(ev);
   if (c->stream) hipStreamDestroy(c->stream);
@@ -582,6 +586,10 @@ mtxd::WaveBuffers buffers2(mtx_ctx *c) {
   b.counters = (uint32_t *)w.counters.p;
   b.xheads = (uint32_t *)w.xheads.p;
   b.capacity = w.capacity;
+  b.cq_p = (float4 *)w.cq_p.p;  // null unless ensure_cache2
+  b.cq_d = (float4 *)w.cq_d.p;
+  b.cq_t = (float4 *)w.cq_t.p;
+  b.cq_count = (uint32_t *)w.cq_count.p;
   return b;
 }
 
@@ -631,6 +639,18 @@ int ensure_cache(mtx_ctx *c, uint32_t cap) {
   return MTX_OK;
 }
 
+// The second wavefront's cache-query buffers (two-stream NRC + cache render).
+int ensure_cache2(mtx_ctx *c, uint32_t cap) {
+  int rc;
+  Wave2 &w = c->w2;
+  if ((rc = dalloc(w.cq_p, 16ull * cap))) return rc;
+  if ((rc = dalloc(w.cq_d, 16ull * cap))) return rc;
+  if ((rc = dalloc(w.cq_t, 16ull * cap))) return rc;
+  if ((rc = dalloc(w.cq_count, 16))) return rc;
+  if ((rc = dalloc(w.f_feat, 128ull * cap))) return rc;
+  if ((rc = dalloc(w.f_out, 12ull * cap))) return rc;
+  return MTX_OK;
+}
 
 int check_args(mtx_ctx *c, const mtx_render_args *a) {
   if (!c || !a) {
@@ -654,12 +674,15 @@ int check_args(mtx_ctx *c, const mtx_render_args *a) {
   return MTX_OK;
 }
 
+constexpr uint32_t kQSlots = 4096;  // chunks whose cache-query counts one stats render records
+
 // Event-pair timer per kernel class.
 struct Timer {
   mtx_ctx *c;
   bool on;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs[6];  // trace, shadow, shade, all, encode, mlp
   uint64_t cache_queries = 0;
+  uint32_t q_used = 0;  // chunk query counts copied (asynchronously) into c->q_pinned
   size_t next = 0;
   hipEvent_t get() {
     if (next >= c->events.size()) {
@@ -692,11 +715,16 @@ struct Timer {
   }
 };
 
-// Encode + MLP + L += T * out for the chunk's compacted cache queries.
-void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false) {
+// Encode + MLP + L += T * out for the chunk's compacted cache queries (on
+// `stream` with the feature / output buffers of the chunk's wavefront: the
+// context's by default, the second wavefront's in a two-stream render).
+void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false,
+               hipStream_t stream = nullptr, DevBuf *feat = nullptr, DevBuf *out = nullptr) {
+  hipStream_t st = stream ? stream : c->stream;
+  DevBuf &f_feat = feat ? *feat : c->f_feat, &f_out = out ? *out : c->f_out;
   const uint32_t *perm = nullptr;
-  hipEvent_t e = tm.begin(4);
-  if (c->cache_sort && !nerad_render) {
+  hipEvent_t e = tm.begin(4, st);
+  if (c->cache_sort && !nerad_render && st == c->stream) {
     // encode the queries in Morton order (a stable sort of 24-bit cell codes
     // with the hash-grid group-by): the hash-grid corner gathers of
     // neighbouring rows then share table lines. The MLP row order follows;
@@ -712,21 +740,20 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
         perm = (const uint32_t *)c->cq_perm.p;
     }
   }
-  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)c->f_feat.p, c->stream, perm);
-  tm.end(4, e);
-  e = tm.begin(5);
-  mtxd::field_mlp((const uint16_t *)c->f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
-                  (float *)c->f_out.p, c->n_cu, c->stream);
-  tm.end(5, e);
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm);
+  tm.end(4, e, st);
+  e = tm.begin(5, st);
+  mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden, (float *)f_out.p,
+                  c->n_cu, st);
+  tm.end(5, e, st);
   if (nerad_render)
-    mtxd::launch_nerad_apply(b, (const float *)c->f_out.p, cap, 1, c->stream);
+    mtxd::launch_nerad_apply(b, (const float *)f_out.p, cap, 1, st);
   else
-    mtxd::launch_cache_apply(b, (const float *)c->f_out.p, cap, c->stream, perm);
-  if (tm.on) {
-    uint32_t nq = 0;
-    if (hipMemcpyAsync(&nq, b.cq_count, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
-        hipStreamSynchronize(c->stream) == hipSuccess)
-      tm.cache_queries += nq;
+    mtxd::launch_cache_apply(b, (const float *)f_out.p, cap, st, perm);
+  if (tm.on) {  // counted after the render's final synchronisation (fill_stats): no per-chunk sync
+    if (!c->q_pinned && hipHostMalloc((void **)&c->q_pinned, 4 * kQSlots) != hipSuccess) c->q_pinned = nullptr;
+    if (c->q_pinned && tm.q_used < kQSlots)
+      hipMemcpyAsync(c->q_pinned + tm.q_used++, b.cq_count, 4, hipMemcpyDeviceToHost, st);
   }
 }
 
@@ -802,6 +829,7 @@ int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_
     stats->shade_ms = tm.total(2);
     stats->cache_encode_ms = tm.total(4);
     stats->cache_mlp_ms = tm.total(5);
+    for (uint32_t i = 0; i < tm.q_used; ++i) tm.cache_queries += c->q_pinned[i];
     stats->cache_queries = tm.cache_queries;
     stats->other_ms = tm.total(3) - stats->trace_ms - stats->shadow_ms - stats->shade_ms - stats->cache_encode_ms -
                       stats->cache_mlp_ms;
@@ -1061,13 +1089,17 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   // the N = 1 roofline is measured with. Path-state integrators without a
   // per-chunk cache pass only.
   const uint64_t n_paths_all = (uint64_t)band_px * a->spp;
-  const bool two = c->streams > 1 && !mlt && !nrc_cache && !nerad_render && a->integrator != MTX_INT_RESTIR_GI &&
-                   n_paths_all >= (1u << 16) && n_paths_all <= (1ull << c->streams_max_log2);
+  // (NRC + cache: each wavefront has its own query / feature buffers, so one
+  // chunk's cache pass overlaps the other's bounces; not with the Morton sort)
+  const bool two = c->streams > 1 && !mlt && !(nrc_cache && c->cache_sort) && !nerad_render &&
+                   a->integrator != MTX_INT_RESTIR_GI && n_paths_all >= (1u << 16) &&
+                   n_paths_all <= (1ull << c->streams_max_log2);
   if (two) px_per_chunk = std::min(px_per_chunk, (band_px + 1) / 2);
   const uint32_t cap = px_per_chunk * a->spp;
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   if (two && (rc = ensure_wavefront2(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   if ((nrc_cache || nerad_render) && (rc = ensure_cache(c, cap))) return rc;
+  if (two && nrc_cache && (rc = ensure_cache2(c, cap))) return rc;
   if ((rc = dalloc(c->contrib, 9ull * 16 * band_px))) return rc;
   const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
   float4 *film_dev = (float4 *)film_rgbw;
@@ -1146,10 +1178,15 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
       continue;
     }
     HIP_TRY(reset_counters(bc, std::max<uint32_t>(a->max_depth, 1), st));
-    if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
+    if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(bc.cq_count, 0, 4, st));
     mtxd::launch_raygen_camera(sc, bc, p, st);
     run_bounces(c, bc, p, tm, &n_trace, &n_shadow, &sc, st);
-    if (nrc_cache) run_cache(c, b, p.n_paths, tm);
+    if (nrc_cache) {
+      if (second)
+        run_cache(c, bc, p.n_paths, tm, false, st, &c->w2.f_feat, &c->w2.f_out);
+      else
+        run_cache(c, b, p.n_paths, tm);
+    }
     if (nerad_render) run_cache(c, b, p.n_paths, tm, true);
     mtxd::launch_film_src(bc, p, (float4 *)c->contrib.p, st);
   }

@@ -141,6 +141,28 @@ def test_nrc_cache_film_bit_exact(small_scene, oracle, chunk):
 
 
 @pytest.mark.gpu
+def test_nrc_cache_two_streams_bit_exact(small_scene, oracle):
+    """A render of >= 2^16 paths runs on two wavefronts / streams, each chunk's
+    cache pass (encode, MLP, apply) on its wavefront's own query buffers
+    while the other chunk traces: the film still equals the oracle's
+    composition bit for bit (256x144, spp 4: 147 K paths, two chunks)."""
+    from mtx import load_dict
+    from mtx.field import Field
+
+    sc = small_scene.with_film(256, 144)
+    field = Field(sc, seed=5, table_scale=1.0)
+    integ = load_dict({"type": "nrc", "field": field})
+    spp = 4
+    film = integ.render_film(sc, seed=3, spp=spp)
+    a = integ.render_args(sc, 3, spp)
+    L, pos, q = oracle.render_samples_nrc_cache(sc, a)
+    m = q[:, 0] == 1
+    out = field(q[m, 1:4], q[m, 4:7])
+    L[m] = L[m] + q[m, 7:10] * out
+    np.testing.assert_array_equal(film, oracle.film(sc.width, 0, sc.height, spp, L, pos))
+
+
+@pytest.mark.gpu
 def test_nrc_cache_morton_order_unchanged(tmp_path):
     """MTX_CACHE_SORT=1 encodes the cache queries in Morton order (sorted with
     the hash-grid group-by; measured slower, so off by default); queue order
