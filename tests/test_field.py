@@ -141,11 +141,13 @@ def test_nrc_cache_film_bit_exact(small_scene, oracle, chunk):
 
 
 @pytest.mark.gpu
-def test_nrc_cache_two_streams_bit_exact(small_scene, oracle):
+@pytest.mark.parametrize("chunk", [0, 40000])
+def test_nrc_cache_two_streams_bit_exact(small_scene, oracle, chunk):
     """A render of >= 2^16 paths runs on two wavefronts / streams, each chunk's
     cache pass (encode, MLP, apply) on its wavefront's own query buffers
     while the other chunk traces: the film still equals the oracle's
-    composition bit for bit (256x144, spp 4: 147 K paths, two chunks)."""
+    composition bit for bit (256x144, spp 4: 147 K paths; two chunks, or four
+    alternating over the two wavefronts with chunk_paths 40000)."""
     from mtx import load_dict
     from mtx.field import Field
 
@@ -153,7 +155,7 @@ def test_nrc_cache_two_streams_bit_exact(small_scene, oracle):
     field = Field(sc, seed=5, table_scale=1.0)
     integ = load_dict({"type": "nrc", "field": field})
     spp = 4
-    film = integ.render_film(sc, seed=3, spp=spp)
+    film = integ.render_film(sc, seed=3, spp=spp, chunk_paths=chunk)
     a = integ.render_args(sc, 3, spp)
     L, pos, q = oracle.render_samples_nrc_cache(sc, a)
     m = q[:, 0] == 1

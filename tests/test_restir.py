@@ -121,6 +121,29 @@ def test_restir_moving_camera_bit_exact(small_scene, oracle):
 
 
 @pytest.mark.gpu
+def test_restir_two_wavefront_split_bit_exact(small_scene, oracle):
+    """A frame of >= 2^16 lanes runs stage A as two row halves on two
+    wavefronts / streams (api.cpp render_restir): 384x216 (82,944 lanes), a
+    moving camera, films and temporal reservoirs bit-exact vs the oracle."""
+    from mtx import _abi, load_dict
+
+    sc = small_scene.with_film(384, 216)
+    assert sc.width * sc.height >= 1 << 16
+    cams = []
+    for fr in range(2):
+        c = _abi.Camera.from_buffer_copy(bytes(sc.camera))
+        c.origin[0] += 0.03 * fr
+        cams.append(c)
+    ref, orc = _oracle_frames(oracle, sc, CONFIGS["unbiased"], 2, cameras=cams)
+    integ = load_dict({"type": "restirgi", **CONFIGS["unbiased"]})
+    for fr in range(2):
+        sc.camera = cams[fr]
+        film = integ.render_film(sc, seed=fr, spp=1)
+        np.testing.assert_array_equal(film, ref[fr], err_msg=f"frame {fr}")
+    np.testing.assert_array_equal(integ.state("temporal"), orc.tres)
+
+
+@pytest.mark.gpu
 def test_restir_errors():
     from mtx import MtxError, load_dict, scene
 
