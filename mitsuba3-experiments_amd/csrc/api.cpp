@@ -1163,6 +1163,10 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.stats = want_stats ? 1 : 0;
     p.sample_major = c->sample_major;
     p.nrc_cache = nrc_cache ? 1u : 0u;
+    // the film (and the cache apply) read an ending path's L only; PSSMLT's
+    // chain kernels read its sampler state (mtx_sample_rays' k_collect and
+    // ReSTIR's k_rs_collect build their own ChunkParams, which keep it)
+    p.drop_end_misc = mlt ? 0u : 1u;
     if (mlt) {
       // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains
       const uint32_t iters = a->iterations ? a->iterations : 200;

@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       }
     } else if (!kNerad && valid) {
       b.L[kFinal][path_c] = io.nL;
-      b.misc[kFinal][path_c] = io.nmisc;
+      if (!p.drop_end_misc) b.misc[kFinal][path_c] = io.nmisc;
     }
     if (io.emit) {
       // the contribution goes to the path's L where the next shade (or the

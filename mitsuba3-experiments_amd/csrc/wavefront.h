@@ -183,6 +183,7 @@ struct ChunkParams {
   uint32_t restir;      // ReSTIR GI secondary paths (path-mis loop, restirgi.py:459-588)
   uint32_t sample_major;  // chunk path order: 1 = s * n_px + q, 0 = q * spp + s
   uint32_t nrc_cache;     // NRC: query the radiance field where the spread criterion stops
+  uint32_t drop_end_misc; // film render: an ending path's sampler state is never read (its L is)
 };
 
 // -------- launch wrappers (kernels.hip) --------
