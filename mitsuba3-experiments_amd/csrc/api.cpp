@@ -1167,6 +1167,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     // chain kernels read its sampler state (mtx_sample_rays' k_collect and
     // ReSTIR's k_rs_collect build their own ChunkParams, which keep it)
     p.drop_end_misc = mlt ? 0u : 1u;
+    p.ident0 = 1;  // raygen_camera / mlt_begin queue every path at its own position
     if (mlt) {
       // Pssmlt.render (pssmlt.py:167-228): all iterations of this chunk's chains
       const uint32_t iters = a->iterations ? a->iterations : 200;

@@ -188,7 +188,7 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   b.pos[i] = pos;
-  b.queue[0][i] = i;
+  if (!p.ident0 || MTX_HIT_BY_PATH) b.queue[0][i] = i;
 }
 
 __global__ void k_raygen_camera(DevScene s, WaveBuffers b, ChunkParams p) {
@@ -941,9 +941,11 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
   // coalesced and in parallel with the queue entry.
   uint32_t path = 0;
   float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
+  // an identity bounce-0 queue is not stored: position i is path i
+  const bool ident = bounce == 0 && p.ident0 && !MTX_HIT_BY_PATH;
   if (blockIdx.x * kShadeBlock + threadIdx.x < count) {
     const uint32_t i0 = blockIdx.x * kShadeBlock + threadIdx.x;
-    path = in_q[i0];
+    path = ident ? i0 : in_q[i0];
     h = b.hit[MTX_HIT_BY_PATH ? path : i0];
   }
 #if MTX_DIAG_STAMPS
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     const uint32_t i = base + threadIdx.x;
     const uint32_t inext = i + stride;
     uint32_t path_n = 0;
-    if (MTX_SHADE_PREFETCH && inext < count) path_n = in_q[inext];
+    if (MTX_SHADE_PREFETCH && inext < count) path_n = ident ? inext : in_q[inext];
     ShadeIO io;
     io.emit = false;
     io.query = false;
@@ -1026,7 +1028,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
       }
     }
     if (!MTX_SHADE_PREFETCH && inext < count) {
-      path = in_q[inext];
+      path = ident ? inext : in_q[inext];
       h = b.hit[MTX_HIT_BY_PATH ? path : inext];
     }
 #if MTX_DIAG_STAMPS
@@ -1303,7 +1305,7 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   const uint32_t fl = p.integrator == MTX_INT_PSSMLT_PATH ? (PF_PREV_DELTA << 16) : 0u;
   if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
-  b.queue[0][i] = i;
+  if (!p.ident0 || MTX_HIT_BY_PATH) b.queue[0][i] = i;
 }
 
 // render_sample tail (:137-159): acceptance, cumulative weights, state swap.
