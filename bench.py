@@ -116,6 +116,8 @@ def src_sha() -> str:
 
 def traffic_key(args) -> str:
     """The bench arguments a PMC profile depends on (per-launch traffic)."""
+    if getattr(args, "workload", "path_mis") != "path_mis":
+        return f"{args.workload} spp={args.spp} iterations={args.iterations}"
     return f"path_mis {args.width}x{args.height} spp={args.spp} md={args.max_depth} rr={args.rr_depth} chunk={args.chunk}"
 
 
@@ -362,6 +364,24 @@ def main():
         dist.destroy_process_group()
 
 
+def cpu_model() -> str:
+    """The host CPU's model name as lscpu prints it."""
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.strip().startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(sc, integ, args):
     """oracle/ (the CPU restatement, OpenMP over the host cores) on a bounded
     sample of the same workload: the full 1280x720 frame at a reduced spp,
@@ -381,7 +401,7 @@ def cpu_baseline(sc, integ, args):
     dt = time.perf_counter() - t0
     n = sc.width * sc.height * spp
     return {"value": round(n / dt / 1e6, 4), "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "sample": f"full {sc.width}x{sc.height} frame at spp={spp} ({n} paths, {dt:.1f} s), same integrator, "
+            "cpu_model": cpu_model(), "sample": f"full {sc.width}x{sc.height} frame at spp={spp} ({n} paths, {dt:.1f} s), same integrator, "
                       "scene and seed scheme; oracle/oracle.cpp (OpenMP)"}
 
 

@@ -36,6 +36,21 @@ def test_nrc_full_frame_bit_exact(full_scene, oracle):
     assert film[1:-1, 1:-1, 3].min() > 0 and film[..., :3].sum() > 0
 
 
+def test_c1_mypath_256_spp4_defaults_bit_exact(full_scene, oracle):
+    """C1 at its own configuration: path.py's `mypath` (Path.sample,
+    path.py:194-302) with the Path.__init__ defaults max_depth 16 / rr_depth 4
+    (path.py:22-25), the full 1.83 M-triangle proxy at 256x256, spp 4."""
+    from mtx import load_dict
+
+    sc = full_scene.with_film(256, 256)
+    integ = load_dict({"type": "mypath"})
+    assert (integ.max_depth, integ.rr_depth) == (16, 4)
+    film = integ.render_film(sc, seed=4, spp=4)
+    ref = oracle.render(sc, integ.render_args(sc, 4, 4))
+    np.testing.assert_array_equal(film, ref)
+    assert film[1:-1, 1:-1, 3].min() > 0 and film[..., :3].sum() > 0
+
+
 def test_restir_1080p_three_frames_bit_exact(full_scene, oracle):
     from mtx import load_dict
 

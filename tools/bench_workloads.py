@@ -29,8 +29,18 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
-def _trace_roofline(cnt, trace_ms_per_unit, units_label, timed_launches=None):
-    """`cnt`: visit counters of one untimed run. When that run is shorter than
+TRACE_KERNEL = "mtxd::k_trace_closest<false>"
+
+
+def _trace_roofline(cnt, trace_ms_per_unit, units_label, timed_launches=None, args=None):
+    """The headline's roofline definition (bench.py) for a workload's
+    closest-hit launches: algorithmic bytes over HIP-event time against the
+    vector-memory byte peak, with the PMC traffic (HBM side) and unit
+    occupancy of the committed profiles/*_pmc_{traffic,units}.json whose
+    source hash and bench key (bench.traffic_key: workload, spp, iterations)
+    match this build and run, else null.
+
+    `cnt`: visit counters of one untimed run. When that run is shorter than
     the timed unit (PSSMLT: 20 of 200 iterations), `timed_launches` is the
     timed unit's launch count: the bytes per launch come from the counter run
     and are scaled to the timed launches."""
@@ -42,10 +52,26 @@ def _trace_roofline(cnt, trace_ms_per_unit, units_label, timed_launches=None):
         launches = max(1, int(round(timed_launches)))
     s = trace_ms_per_unit / 1e3
     ach = alg / s / 1e9 if s > 0 else 0.0
-    # stated against the level that serves the traversal's bytes (bench.py docstring)
-    return {"bound": "l2", "kernel": "k_trace_closest (4-wide quantised BVH, closest hit)",
-            "achieved": round(ach, 1), "peak": bench.L2_GATHER_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / bench.L2_GATHER_PEAK_GBS, 4), "traffic": None,
+    if args is not None:
+        key = bench.traffic_key(args)
+        tr, tsrc = bench.measured_traffic([TRACE_KERNEL], key)
+        un, usrc = bench.measured_units([TRACE_KERNEL], key)
+    else:
+        tr, tsrc, un, usrc = {TRACE_KERNEL: None}, "no bench key", {TRACE_KERNEL: None}, "no bench key"
+    tc, uc = tr[TRACE_KERNEL], un[TRACE_KERNEL]
+    launch_s = s / launches
+    hbm = None
+    if tc is not None and launch_s > 0:
+        hb = tc / launch_s / 1e9
+        hbm = {"achieved": round(hb, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(hb / bench.HBM_PEAK_GBS, 4), "bytes_per_launch": tc,
+               "definition": "PMC FETCH_SIZE x2 + WRITE_SIZE per launch / avg launch time"}
+    return {"bound": "vmem" if (uc is None or uc["ta_busy"] >= uc["valu_busy"]) else "valu",
+            "kernel": "k_trace_closest (closest hit)",
+            "achieved": round(ach, 1), "peak": bench.VMEM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / bench.VMEM_PEAK_GBS, 4), "traffic": tc, "traffic_source": tsrc,
+            "units": uc, "units_source": usrc, "hbm": hbm,
+            "peak_source": "vector-memory (TA/TCP) byte path, as bench.py's headline roofline",
             "avg_launch_ms": round(trace_ms_per_unit / launches, 4), "launches_per_" + units_label: int(launches),
             "alg_bytes_per_launch": int(alg / launches),
             "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
@@ -53,6 +79,8 @@ def _trace_roofline(cnt, trace_ms_per_unit, units_label, timed_launches=None):
 
 
 def _line(metric, value, unit, steps, warmup, ms, config, roofline, cpu, extra=None, dtype="f32"):
+    if isinstance(cpu, dict) and "cpu_model" not in cpu:
+        cpu = dict(cpu, cpu_model=bench.cpu_model())
     out = {"metric": metric, "value": round(value, 4), "unit": unit, "n_gpus": 1, "steps": steps, "warmup": warmup,
            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": dtype, "data": "synthetic: deterministic bedroom proxy / seeded PCG32 inputs",
@@ -201,7 +229,7 @@ def pssmlt(args, with_nee=False):
                            f"i%50>40), max_depth 16, rr_depth 4, {chains} chains", "chains": chains,
                "iterations": it, "aggregation_iterations": sum(1 for i in range(it) if i % 50 > 40),
                "chains_per_rank": sc.width * sc.height * (s1 - s0), "parallelism": par},
-              _trace_roofline(cnt, st["trace_ms"], "step", st["trace_launches"]), cpu,
+              _trace_roofline(cnt, st["trace_ms"], "step", st["trace_launches"], args), cpu,
               {"kernels_ms_per_step": {"trace_closest": round(st["trace_ms"], 3), "shade": round(st["shade_ms"], 3),
                                        "trace_shadow": round(st["shadow_ms"], 3), "other": round(st["other_ms"], 3)},
                "n_gpus": rk.world, "scaling": "strong" if rk.world > 1 else "weak"})
@@ -279,7 +307,7 @@ def restir(args):
                "frames_per_s": round(1.0 / dt, 2), "pixels": px,
                "parallelism": rk.parallelism() + (f", P2P halo of {halo} rows (samples + temporal reservoirs)"
                                                   if rk.world > 1 else "")},
-              _trace_roofline(cnt, agg["trace_ms"] / args.frames, "frame"), cpu,
+              _trace_roofline(cnt, agg["trace_ms"] / args.frames, "frame", args=args), cpu,
               {"kernels_ms_per_frame": {"trace_closest": round(agg["trace_ms"] / args.frames, 3),
                                         "trace_shadow_and_visibility": round(agg["shadow_ms"] / args.frames, 3),
                                         "shade": round(agg["shade_ms"] / args.frames, 3),
@@ -317,7 +345,7 @@ def nrc(args):
     cpu = bench.cpu_baseline(sc, integ, A)
     _line("NRC Mpaths/sec on bedroom@1280x720 spp=4 (C5)", n / dt / 1e6, "Mpaths/s", reps, 1, dt * 1e3,
           {"workload": "nrc.py NRCIntegrator.sample: NEE+MIS segments, spread heuristic c=0.01, max_depth 10",
-           "paths_per_step": n}, _trace_roofline(cnt, agg["trace_ms"] / reps, "step"), cpu)
+           "paths_per_step": n}, _trace_roofline(cnt, agg["trace_ms"] / reps, "step", args=args), cpu)
     # the same with the radiance cache: stopped segments
     # trace one more segment and query the fused fp16 MFMA field there
     from mtx.field import Field
@@ -343,7 +371,7 @@ def nrc(args):
            "cache_mlp_ms": round(agg["cache_mlp_ms"] / reps, 3),
            "trace_ms": round(agg["trace_ms"] / reps, 3), "shadow_ms": round(agg["shadow_ms"] / reps, 3),
            "shade_ms": round(agg["shade_ms"] / reps, 3)},
-          _trace_roofline(cnt, agg["trace_ms"] / reps, "step"), cpu)
+          _trace_roofline(cnt, agg["trace_ms"] / reps, "step", args=args), cpu)
 
 
 # ------------------------------------------------------------- primitives --
@@ -530,9 +558,11 @@ def nerad(args):
            + cnt["tris_closest"] * TRI_BYTES)
     tms = agg["ms_trace"] / reps
     ach = alg / (tms / 1e3) / 1e9 if tms > 0 else 0.0
-    roof = {"bound": "hbm", "kernel": "k_trace_closest (RHS BSDF rays + next_smooth_si chain)",
-            "achieved": round(ach, 1), "peak": bench.HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None, "trace_ms_per_step": round(tms, 3),
+    roof = {"bound": "vmem", "kernel": "k_trace_closest (RHS BSDF rays + next_smooth_si chain)",
+            "achieved": round(ach, 1), "peak": bench.VMEM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / bench.VMEM_PEAK_GBS, 4), "traffic": None,
+            "peak_source": "vector-memory (TA/TCP) byte path, as bench.py's headline roofline",
+            "trace_ms_per_step": round(tms, 3),
             "alg_bytes_per_step": int(alg), "rays_per_step": int(cnt["rays_closest"]),
             "node_visits_per_ray": round(cnt["nodes_closest"] / max(1, cnt["rays_closest"]), 2),
             "tri_visits_per_ray": round(cnt["tris_closest"] / max(1, cnt["rays_closest"]), 2)}
