@@ -462,16 +462,22 @@ namespace {
 // 40 % of the free HBM.
 constexpr uint32_t kDefaultChunk = 1u << 28;
 constexpr size_t kPathStateBytes = 328;
-uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a) {
+constexpr size_t kCacheQueryBytes = 16 * 3 + 128 + 12;  // ensure_cache: query planes, features, outputs
+// `ways` wavefronts of the returned size are allocated (2 for a two-stream
+// render), each with the NRC cache-query buffers when `cache`: the budget is
+// 40 % of the free HBM for all of them together. Buffers this context already
+// holds (every wavefront's) count as available.
+uint32_t default_chunk(mtx_ctx *c, const mtx_render_args *a, uint32_t ways, bool cache) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 1u << 22;
   // PSSMLT chains also keep the current and proposed path vertices
   const size_t per_path =
-      kPathStateBytes + (a->integrator == MTX_INT_PSSMLT_SIMPLE ? 32ull * std::max<uint32_t>(a->max_depth, 1) + 48
-                         : a->integrator == MTX_INT_PSSMLT_PATH ? 48ull * std::max<uint32_t>(a->max_depth, 1) + 48
-                                                                : 0);
-  // buffers this context already holds count as available
-  const size_t fit = std::max<size_t>((size_t)((double)free_b * 0.4) / per_path, c->capacity);
+      kPathStateBytes + (cache ? kCacheQueryBytes : 0) +
+      (a->integrator == MTX_INT_PSSMLT_SIMPLE ? 32ull * std::max<uint32_t>(a->max_depth, 1) + 48
+       : a->integrator == MTX_INT_PSSMLT_PATH ? 48ull * std::max<uint32_t>(a->max_depth, 1) + 48
+                                              : 0);
+  const size_t held = ways > 1 ? std::min<size_t>(c->capacity, c->w2.capacity) : c->capacity;
+  const size_t fit = std::max<size_t>((size_t)((double)free_b * 0.4) / (per_path * std::max<uint32_t>(ways, 1)), held);
   return (uint32_t)std::max<size_t>(1u << 20, std::min<size_t>(kDefaultChunk, fit));
 }
 
@@ -752,8 +758,14 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
     mtxd::launch_cache_apply(b, (const float *)f_out.p, cap, st, perm);
   if (tm.on) {  // counted after the render's final synchronisation (fill_stats): no per-chunk sync
     if (!c->q_pinned && hipHostMalloc((void **)&c->q_pinned, 4 * kQSlots) != hipSuccess) c->q_pinned = nullptr;
-    if (c->q_pinned && tm.q_used < kQSlots)
+    if (c->q_pinned && tm.q_used < kQSlots) {
       hipMemcpyAsync(c->q_pinned + tm.q_used++, b.cq_count, 4, hipMemcpyDeviceToHost, st);
+    } else {  // more chunks than pinned slots: count this one synchronously (never dropped)
+      uint32_t nq = 0;
+      if (hipMemcpyAsync(&nq, b.cq_count, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+          hipStreamSynchronize(st) == hipSuccess)
+        tm.cache_queries += nq;
+    }
   }
 }
 
@@ -801,7 +813,7 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
     }
   }
   // paths a depth limit left queued keep their result in a queue plane
-  if (!nerad && !nerad_render) mtxd::launch_flush_tail(b, depth_iters, b.capacity, st);
+  if (!nerad && !nerad_render) mtxd::launch_flush_tail(b, depth_iters, b.capacity, p.integrator, st);
 }
 
 int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_t n_trace, uint64_t n_shadow,
@@ -1072,10 +1084,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     return MTX_E_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  uint32_t chunk_paths = a->chunk_paths ? a->chunk_paths : default_chunk(c, a);
-  uint32_t px_per_chunk = std::max<uint32_t>(1, chunk_paths / a->spp);
   const uint32_t band_px = (a->y1 - a->y0) * W;
-  px_per_chunk = std::min(px_per_chunk, band_px);
   const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
   const bool nerad_render = a->integrator == MTX_INT_NERAD;
   const bool mlt = a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH;
@@ -1094,6 +1103,10 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   const bool two = c->streams > 1 && !mlt && !(nrc_cache && c->cache_sort) && !nerad_render &&
                    a->integrator != MTX_INT_RESTIR_GI && n_paths_all >= (1u << 16) &&
                    n_paths_all <= (1ull << c->streams_max_log2);
+  // the default chunk is sized for every wavefront the render allocates
+  const uint32_t chunk_paths =
+      a->chunk_paths ? a->chunk_paths : default_chunk(c, a, two ? 2u : 1u, nrc_cache || nerad_render);
+  uint32_t px_per_chunk = std::min(std::max<uint32_t>(1, chunk_paths / a->spp), band_px);
   if (two) px_per_chunk = std::min(px_per_chunk, (band_px + 1) / 2);
   const uint32_t cap = px_per_chunk * a->spp;
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
@@ -1309,7 +1322,7 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     return MTX_E_ARG;
   }
   HIP_TRY(hipSetDevice(c->device));
-  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : default_chunk(c, a);
+  const uint32_t chunk = a->chunk_paths ? a->chunk_paths : default_chunk(c, a, 1u, false);
   const uint32_t cap = (uint32_t)std::min<uint64_t>(n, chunk);
   if ((rc = ensure_wavefront(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);

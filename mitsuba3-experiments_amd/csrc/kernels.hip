@@ -323,15 +323,15 @@ __device__ __forceinline__ BsdfData bsdf_at(const SceneView &sv, const mtx_mater
 }
 // path-mis: once a path ends, L.w (its prev_bsdf_pdf until then) holds
 // valid_ray as 1 / 0 (path-mis.py:155), so the film reads L and pos only,
-// not the 16-B misc record for one flag (MTX_FILM_FLAG_IN_L=0: misc).
-#ifndef MTX_FILM_FLAG_IN_L
-#define MTX_FILM_FLAG_IN_L 1
-#endif
+// not the 16-B misc record for one flag.
 __device__ __forceinline__ float end_w(uint32_t flags, float prev_pdf) {
-  return MTX_FILM_FLAG_IN_L ? ((flags & PF_VALID_RAY) ? 1.f : 0.f) : prev_pdf;
+  (void)prev_pdf;
+  return (flags & PF_VALID_RAY) ? 1.f : 0.f;
 }
 __device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, float lw) {
-  return MTX_FILM_FLAG_IN_L ? lw != 0.f : ((b.misc[kFinal][path].w >> 16) & PF_VALID_RAY) != 0;
+  (void)b;
+  (void)path;
+  return lw != 0.f;
 }
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
@@ -1047,14 +1047,18 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
 // Paths still queued after a chunk's last bounce (its depth limit stops
 // every integrator's paths first; kept so that no loop bound can leave a
 // result in a queue plane): their L / misc move to the per-path plane.
-__global__ void k_flush_tail(WaveBuffers b, uint32_t bounce) {
+// A path-mis path's final L.w holds valid_ray (end_w), not its prev_bsdf_pdf.
+__global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator) {
   const uint32_t n = b.counters[4 * bounce];
   const uint32_t *q = b.queue[bounce & 1];
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
     const uint32_t path = q[k];
-    b.L[kFinal][path] = b.L[rp][k];
-    b.misc[kFinal][path] = b.misc[rp][k];
+    float4 L = b.L[rp][k];
+    const uint4 m = b.misc[rp][k];
+    if (integrator == MTX_INT_PATH_MIS) L.w = end_w(m.w >> 16, L.w);
+    b.L[kFinal][path] = L;
+    b.misc[kFinal][path] = m;
   }
 }
 
@@ -1478,9 +1482,10 @@ void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacit
   const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 16384);
   hipLaunchKernelGGL(k_cache_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out, perm);
 }
-void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, hipStream_t st) {
+void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, uint32_t integrator,
+                       hipStream_t st) {
   const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 1024);
-  hipLaunchKernelGGL(k_flush_tail, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, bounce);
+  hipLaunchKernelGGL(k_flush_tail, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, bounce, integrator);
 }
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st) {
   hipLaunchKernelGGL(k_mlt_init, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, p.max_depth);

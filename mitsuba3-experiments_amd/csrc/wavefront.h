@@ -207,7 +207,8 @@ void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st)
 void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
-void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, hipStream_t st);
+void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, uint32_t integrator,
+                       hipStream_t st);
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st);
 // perm (optional): MLP row q belongs to cache query perm[q]
 void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacity, hipStream_t st,

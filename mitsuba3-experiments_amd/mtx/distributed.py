@@ -93,6 +93,9 @@ def gather_sum(film, group=None):
     return total.to(t.device)
 
 
+_ALL_TO_ALL_BACKENDS = ("nccl", "gloo")  # backends with all_to_all_single (RCCL, gloo)
+
+
 def reduce_sum(film, group=None):
     """`gather_sum` with the sum spread over the ranks: an all_to_all hands
     every rank one 1/N slice of every film, each rank sums its slice in rank
@@ -104,8 +107,12 @@ def reduce_sum(film, group=None):
     import torch.distributed as dist
 
     t = _to_tensor(film)
-    c = _comm(t, group)
     world = dist.get_world_size(group)
+    # decided from the backend, identically on every rank (a communication
+    # error is raised, never turned into a different collective sequence)
+    if world > 1 and dist.get_backend(group) not in _ALL_TO_ALL_BACKENDS:
+        return gather_sum(film, group)
+    c = _comm(t, group)
     rank = dist.get_rank(group)
     if world == 1:
         return (torch.zeros_like(c) + c).to(t.device)
@@ -114,10 +121,7 @@ def reduce_sum(film, group=None):
     chunk = -(-n // world)
     send = flat if chunk * world == n else torch.cat([flat, flat.new_zeros(chunk * world - n)])
     recv = torch.empty_like(send)
-    try:
-        dist.all_to_all_single(recv, send, group=group)
-    except (RuntimeError, NotImplementedError):  # a backend without all_to_all: every rank raises alike
-        return gather_sum(film, group)
+    dist.all_to_all_single(recv, send, group=group)
     part = torch.zeros(chunk, dtype=c.dtype, device=c.device)
     for r in range(world):
         part.add_(recv[r * chunk:(r + 1) * chunk])
