@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MTX_ABI_VERSION 4
+#define MTX_ABI_VERSION 5
 
 enum {
   MTX_OK = 0,
@@ -108,29 +108,40 @@ typedef struct mtx_camera {
   uint32_t pad;
 } mtx_camera;
 
-/* BVH node (64 B): up to 4 children with 8-bit quantised boxes, collapsed
- * from a binned-SAH BVH2 (bvh_build.cpp); breadth-first, the inner children
- * of a node consecutive and first in slot order, then its leaves, whose
- * triangle ranges are consecutive (the device's 48-B node relies on it).
- * Words:
- *   f[0..2] = origin.xyz (fp32);  w[3] = bytes [ex, ey, ez, n_children],
- *             e* int8 in [-32, 31]: axis scale 2^e
- *   i[4..7] = child refs: >= 0 inner node index,
- *             < 0 leaf: ~c = (first_tri << 3) | (count - 1)
- *   w[8..13] = q_lo.x, q_hi.x, q_lo.y, q_hi.y, q_lo.z, q_hi.z: one byte per
- *             child (child k in bits 8k..8k+7); bound = origin + q * 2^e in
- *             fp32, conservative (contains the child's padded box)
- *   w[14], w[15] = 0
+/* BVH node (80 B, a compressed 8-wide node after Ylitie, Karras & Laine
+ * 2017): up to 8 children with 8-bit quantised boxes, collapsed from a
+ * binned-SAH BVH2 by dynamic programming over the 8-wide tree's SAH
+ * (bvh_build.cpp). The children of a node sit in slots chosen so that
+ * visiting slot s at position s ^ octant(ray) (octant bit a set when the
+ * direction's component a is negative) is approximately front to back: no
+ * per-visit sort. Breadth-first; a node's inner children are consecutive
+ * from child_base in slot order, its leaves' triangles consecutive from
+ * tri_base in slot order. Words:
+ *   f[0..2]  origin.xyz (fp32)
+ *   w[3]     bytes [ex, ey, ez, imask]: int8 axis exponents in [-32, 31]
+ *            (axis scale 2^e); imask bit s set: slot s holds an inner node
+ *   w[4]     child_base: node index of the first inner child; the inner
+ *            child in slot s is child_base + popcount(imask & ((1 << s) - 1))
+ *   w[5]     tri_base: first triangle (leaf order) of the node's leaves
+ *   w[6..7]  meta, one byte per slot (slot s in byte s of the 8):
+ *              0 = empty; inner: 0x20 | (24 + s);
+ *              leaf of n = 1..3 triangles: ((1 << n) - 1) << 5 | offset,
+ *              its triangles tri_base + offset .. + n - 1 (offset + n <= 24)
+ *   w[8..19] q_lo.x, q_hi.x, q_lo.y, q_hi.y, q_lo.z, q_hi.z: 8 bytes each
+ *            (two words, slot s in byte s); bound = origin + q * 2^e in
+ *            fp32, conservative (contains the child's padded box); empty
+ *            slots hold q_lo 255, q_hi 0
  * Triangles are stored in leaf order as 12 floats (48 B):
  *   v0.xyz, 0, e1 = v1-v0 .xyz, 0, e2 = v2-v0 .xyz, 0 */
-#define MTX_BVH_WIDTH 4
-#define MTX_BVH_MAX_LEAF 8
+#define MTX_BVH_WIDTH 8
+#define MTX_BVH_MAX_LEAF 3
+#define MTX_BVH_NODE_WORDS 20
 #define MTX_BVH_MAX_DEPTH 40
 
 typedef struct mtx_scene_desc {
   uint32_t n_tris, n_nodes, n_verts, n_shapes;
   uint32_t n_materials, n_emitters, n_textures, flags;
-  const int32_t *nodes;      /* 16 words per node */
+  const int32_t *nodes;      /* MTX_BVH_NODE_WORDS (20) words per node */
   const float *tri_geom;     /* 12 floats per triangle (leaf order) */
   const uint32_t *tri_vidx;  /* 3 vertex indices per triangle (leaf order) */
   const uint32_t *tri_shape; /* shape index per triangle (leaf order) */
@@ -218,6 +229,10 @@ typedef struct mtx_stats {
    * complement: other_ms excludes them) */
   uint64_t cache_queries;
   double cache_encode_ms, cache_mlp_ms;
+  /* wavefronts / HIP streams the render ran on: > 1 means the per-kernel
+   * times above are summed over overlapping launches (wall time is other_ms
+   * + the kernels only for a one-stream render) */
+  uint32_t streams, reserved;
 } mtx_stats;
 
 /* --------------------------- context ------------------------------ */
@@ -229,19 +244,15 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out);
 void mtx_ctx_destroy(mtx_ctx *ctx);
 
 /* --------------------------- scene -------------------------------- */
-/* Host-only binned-SAH BVH2 build over an indexed triangle mesh (replaces
- * Embree/OptiX acceleration-structure builds behind mi.load_file, upstream).
- * nodes_out: capacity 2*n_tris*16 words; tri_geom_out: 12*n_tris floats;
- * perm_out: n_tris (leaf order -> input triangle index). */
+/* Host-only BVH build over an indexed triangle mesh (replaces the Embree /
+ * OptiX acceleration-structure build behind mi.load_file, upstream): binned-
+ * SAH BVH2, collapsed to the 8-wide node above.
+ * nodes_out: capacity (n_tris + 1) * MTX_BVH_NODE_WORDS words; tri_geom_out:
+ * 12*n_tris floats; perm_out: n_tris (leaf order -> input triangle index);
+ * depth_out: levels of the 8-wide tree (the traversal stack's bound). */
 int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t *tri_vidx, uint32_t n_tris,
                   int32_t *nodes_out, uint32_t *n_nodes_out, float *tri_geom_out, uint32_t *perm_out,
                   uint32_t *depth_out);
-/* Host-only: the 48-B device form of mtx_bvh_build's 64-B nodes (12 words
- * per node in out; layout at bvh_build.cpp mtx_bvh_device_nodes), which
- * mtx_scene_upload builds. Fails with MTX_E_ARG unless the nodes follow the
- * builder's layout (inner children first and consecutive, leaf triangle
- * ranges consecutive in slot order, exponents in [-32, 31]). */
-int mtx_bvh_device_nodes(const int32_t *nodes, uint32_t n_nodes, uint32_t n_tris, int32_t *out);
 /* Host-only roughplastic precompute (upstream roughplastic constructor):
  * external transmittance table (64 floats) and internal reflectance. */
 int mtx_roughplastic_tables(uint32_t distribution, float alpha, float eta, float *table_out,

@@ -41,6 +41,8 @@ constexpr float kLargest = 3.40282346638528859812e+38f;
 
 MTX_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 MTX_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+MTX_HD int popc32(uint32_t x) { return __builtin_popcount(x); }
+MTX_HD int ctz32(uint32_t x) { return __builtin_ctz(x); }  // x != 0
 
 MTX_HD float mulsign(float a, float b) { return u2f(f2u(a) ^ (f2u(b) & 0x80000000u)); }
 MTX_HD float mulsign_neg(float a, float b) {

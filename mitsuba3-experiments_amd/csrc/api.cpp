@@ -154,9 +154,7 @@ struct mtx_ctx {
   uint32_t lds_stack = mtxd::kLdsStack;
   uint32_t lds_top = MTX_LDS_TOP;  // wide nodes of the tree top kept in LDS per block (MTX_LDS_TOP env: A/B)
   uint32_t trace_batch = 128;  // queue entries per claim (256: +0.6 % closest, +1 % at spp 32; 64: +5 %)
-  uint32_t refill_lanes = 16;
-  uint32_t urefill = 24;  // unified loop: refill once 24 lanes are idle (16: closest +1.3 %, 32: +2 %)
-  uint32_t speculate = 1;
+  uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
   uint32_t xcd_claim = 1;
   uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
   DevBuf cq_keys, cq_perm, cq_ws;
@@ -215,9 +213,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
-  if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
   *out = c;
@@ -270,12 +266,12 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     mtx_set_error("mtx_scene_upload: incomplete scene (need geometry, BVH, shapes, materials, >=1 emitter)");
     return MTX_E_ARG;
   }
-  // Validate indices on the host so that no kernel can read out of bounds,
-  // and find the tree depth (stack entries of the traversal kernels: each
-  // wide level pushes at most 3 entries); also rejects cycles.
+  // Validate the 8-wide nodes (mtx.h) on the host so that no kernel can
+  // read out of bounds, and find the tree depth (the traversal stack holds
+  // at most one node group per level); also rejects cycles.
   uint32_t bvh_depth = 0;
   {
-    std::vector<std::pair<int32_t, uint32_t>> todo{{0, 0u}};
+    std::vector<std::pair<uint32_t, uint32_t>> todo{{0u, 0u}};
     uint64_t visited = 0;
     while (!todo.empty()) {
       auto [nd, dep] = todo.back();
@@ -285,24 +281,23 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
         mtx_set_error("mtx_scene_upload: BVH is not a tree of depth <= %d", MTX_BVH_MAX_DEPTH);
         return MTX_E_ARG;
       }
-      const int32_t *w = d->nodes + 16 * (size_t)nd;
-      const uint32_t nch = (uint32_t)w[3] >> 24;
-      if (nch < 1 || nch > MTX_BVH_WIDTH) {
-        mtx_set_error("mtx_scene_upload: node %d has %u children", nd, nch);
-        return MTX_E_ARG;
-      }
-      for (uint32_t k = 0; k < nch; ++k) {
-        const int32_t ch = w[4 + k];
-        if (ch >= 0) {
-          if ((uint32_t)ch >= d->n_nodes) {
-            mtx_set_error("mtx_scene_upload: node %d child %d out of range", nd, ch);
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(d->nodes) + MTX_BVH_NODE_WORDS * (size_t)nd;
+      const uint32_t imask = w[3] >> 24, child_base = w[4], tri_base = w[5];
+      uint32_t inner = 0;
+      for (uint32_t sl = 0; sl < MTX_BVH_WIDTH; ++sl) {
+        const uint32_t m = (w[6 + (sl >> 2)] >> (8 * (sl & 3))) & 0xffu;
+        const bool is_inner = (imask >> sl) & 1u;
+        if (is_inner) {
+          const uint32_t ch = child_base + inner++;
+          if (m != (0x20u | (24u + sl)) || ch >= d->n_nodes) {
+            mtx_set_error("mtx_scene_upload: node %u slot %u: bad inner child", nd, sl);
             return MTX_E_ARG;
           }
           todo.push_back({ch, dep + 1});
-        } else {
-          uint32_t x = (uint32_t)(~ch), first = x >> 3, cnt = (x & 7u) + 1;
-          if ((uint64_t)first + cnt > d->n_tris) {
-            mtx_set_error("mtx_scene_upload: leaf [%u,+%u) exceeds %u triangles", first, cnt, d->n_tris);
+        } else if (m != 0) {
+          const uint32_t cb = m >> 5, off = m & 31u, cnt = cb == 1 ? 1u : cb == 3 ? 2u : cb == 7 ? 3u : 0u;
+          if (cnt == 0 || off + cnt > 24 || (uint64_t)tri_base + off + cnt > d->n_tris) {
+            mtx_set_error("mtx_scene_upload: node %u slot %u: bad leaf", nd, sl);
             return MTX_E_ARG;
           }
         }
@@ -347,18 +342,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   HIP_TRY(hipSetDevice(c->device));
   int rc = 0;
   hipStream_t st = c->stream;
-#ifndef MTX_NODE48
-#define MTX_NODE48 0
-#endif
-  if (MTX_NODE48) {
-    // the device traverses the 48-B node form (bvh_build.cpp mtx_bvh_device_nodes)
-    std::vector<int32_t> n12(12ull * d->n_nodes);
-    if ((rc = mtx_bvh_device_nodes(d->nodes, d->n_nodes, d->n_tris, n12.data()))) return rc;
-    if ((rc = upload(c->nodes, n12.data(), n12.size(), st))) return rc;
-    HIP_TRY(hipStreamSynchronize(st));  // n12 is freed at scope exit
-  } else if ((rc = upload(c->nodes, d->nodes, 16ull * d->n_nodes, st))) {
-    return rc;
-  }
+  if ((rc = upload(c->nodes, d->nodes, (size_t)MTX_BVH_NODE_WORDS * d->n_nodes, st))) return rc;
   {
     // device triangles packed to 36 B (the ABI's 48-B records carry 3 pad
     // words): 3.6 instead of 2.7 triangles per 128-B line, same load count
@@ -431,23 +415,21 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.tables = (const float *)c->tables.p;
   s.n_tris = d->n_tris;
   s.n_emitters = d->n_emitters;
-  s.stack_entries = 3 * bvh_depth + 1;
+  s.stack_entries = bvh_depth + 1;
   s.camera = d->camera;
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
-  // LDS copy of the tree top (64-B nodes only): with 16 stack entries per
-  // lane and 8 blocks of 256 threads per CU, 64 nodes fill the 160 KB
-  s.lds_top = MTX_NODE48 ? 0u : std::min<uint32_t>(d->n_nodes, c->lds_top);
+  // LDS copy of the tree top: with 8 stack entries (8 B) per lane and 8
+  // blocks of 256 threads per CU, 48 nodes (80 B) fill the 160 KB
+  s.lds_top = std::min<uint32_t>(d->n_nodes, c->lds_top);
   s.trace_batch = c->trace_batch;
-  s.refill_lanes = c->refill_lanes;
   s.urefill = c->urefill;
-  s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
   {
     const size_t deep = s.stack_entries - s.lds_entries;
-    if ((rc = dalloc(c->stack_ovf, std::max<size_t>(4, deep * s.ovf_threads * sizeof(int32_t))))) return rc;
-    s.stack_ovf = (int32_t *)c->stack_ovf.p;
+    if ((rc = dalloc(c->stack_ovf, std::max<size_t>(8, deep * s.ovf_threads * sizeof(uint2))))) return rc;
+    s.stack_ovf = (uint2 *)c->stack_ovf.p;
   }
   c->has_scene = true;
   return MTX_OK;
@@ -567,7 +549,7 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   if ((rc = dalloc(w.xheads, 8ull * mtxd::kXSlotWords * (max_depth + 2)))) return rc;
   const mtxd::DevScene &s = c->scene;
   const size_t deep = s.stack_entries - s.lds_entries;
-  if ((rc = dalloc(w.stack_ovf, std::max<size_t>(4, deep * s.ovf_threads * sizeof(int32_t))))) return rc;
+  if ((rc = dalloc(w.stack_ovf, std::max<size_t>(8, deep * s.ovf_threads * sizeof(uint2))))) return rc;
   return MTX_OK;
 }
 
@@ -689,6 +671,7 @@ struct Timer {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pairs[6];  // trace, shadow, shade, all, encode, mlp
   uint64_t cache_queries = 0;
   uint32_t q_used = 0;  // chunk query counts copied (asynchronously) into c->q_pinned
+  uint32_t streams = 1;  // wavefronts / streams of the render (mtx_stats.streams)
   size_t next = 0;
   hipEvent_t get() {
     if (next >= c->events.size()) {
@@ -834,6 +817,7 @@ int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_
   }
   stats->trace_launches = n_trace;
   stats->shadow_launches = n_shadow;
+  stats->streams = tm.streams;
   stats->paths = paths;
   if (tm.on) {
     stats->trace_ms = tm.total(0);
@@ -983,13 +967,14 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // persistent launches. Same lanes, same draws: bit-identical.
     const uint32_t rows = a->y1 - a->y0;
     const bool two = c->streams > 1 && rows >= 2 && nb >= (1u << 16);
+    if (two) tm.streams = 2;
     const uint32_t ym = two ? a->y0 + rows / 2 : a->y1;
     mtxd::DevScene s2 = c->scene;
     mtxd::WaveBuffers bw2{};
     if (two) {
       if ((rc = ensure_wavefront2(c, (a->y1 - ym) * W * spp, depth))) return rc;
       bw2 = buffers2(c);
-      s2.stack_ovf = (int32_t *)c->w2.stack_ovf.p;
+      s2.stack_ovf = (uint2 *)c->w2.stack_ovf.p;
       HIP_TRY(hipEventRecord(c->w2.start, st));  // after the frame-0 clears
       HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
     }
@@ -1122,6 +1107,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   }
   const bool want_stats = stats && (a->flags & 1u);
   Timer tm{c, stats && (a->flags & 2u)};
+  if (two) tm.streams = 2;
   if (a->integrator == MTX_INT_RESTIR_GI) {
     hipEvent_t e_all = tm.begin(3);
     uint64_t n_trace = 0, n_shadow = 0;
@@ -1147,7 +1133,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     // the second stream starts after everything queued on the first
     b2 = buffers2(c);
     s2 = c->scene;
-    s2.stack_ovf = (int32_t *)c->w2.stack_ovf.p;
+    s2.stack_ovf = (uint2 *)c->w2.stack_ovf.p;
     HIP_TRY(hipEventRecord(c->w2.start, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
   }

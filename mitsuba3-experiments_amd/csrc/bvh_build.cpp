@@ -1,18 +1,18 @@
 // bvh_build.cpp — host-side scene preprocessing for libmtx.
 //
-// * Binned-SAH BVH2 over an indexed triangle mesh, collapsed (SAH-optimal
-//   dynamic programming over the BVH2, which may also merge small subtrees
-//   into one leaf) into 4-wide nodes with 8-bit quantised child boxes (64 B, layout in mtx.h) with the
-//   triangles reordered into leaf order as {v0, e1, e2} records. Replaces the
-//   Embree / OptiX acceleration-structure build that mi.load_file performs
-//   upstream for Scene.ray_intersect (path-mis.py:69-71). The wide node
-//   halves the node fetches per ray of the memory-pipeline-bound traversal.
+// * Binned-SAH BVH2 over an indexed triangle mesh (leaves of <= 3
+//   triangles), collapsed by SAH-optimal dynamic programming into 8-wide
+//   compressed nodes (80 B, layout in mtx.h: 8-bit quantised child boxes,
+//   children in octant-ordered slots, Ylitie, Karras & Laine 2017) with the
+//   triangles reordered into leaf order as {v0, e1, e2} records. Replaces
+//   the Embree / OptiX acceleration-structure build that mi.load_file
+//   performs upstream for Scene.ray_intersect (path-mis.py:69-71).
 // * roughplastic precompute (upstream roughplastic constructor): the
 //   64-entry external transmittance table and the internal reflectance.
 //
-// Tree depth is capped at MTX_BVH_MAX_DEPTH inner levels (object-median
-// splits take over when the SAH would exceed it) so that the device
-// traversal's fixed LDS stack can never overflow.
+// BVH2 depth is capped at MTX_BVH_MAX_DEPTH inner levels (object-median
+// splits take over when the SAH would exceed it); the 8-wide tree is never
+// deeper, which bounds the device traversal's stack.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -69,7 +69,6 @@ struct Builder {
   std::vector<uint32_t> order; // leaf order -> input tri
   float ct = kDefaultCt;
   int n_bins = 32;
-  int layout = 0;
   uint32_t max_depth_seen = 0;
 
   static int ceil_log2(uint32_t c) {
@@ -216,13 +215,20 @@ struct Builder {
     return (int32_t)node;
   }
 
-  // ---- collapse to 4-wide quantised nodes --------------------------------
-  struct Child {
-    int32_t ref;  // BVH2 ref (inner index or leaf code)
-    Box box;      // padded fp32 box
-  };
-  std::vector<int32_t> wnodes;  // 16 words per wide node
-  uint32_t wide_depth = 0;
+  // ---- collapse to 8-wide compressed nodes (layout in mtx.h) -------------
+  // SAH-optimal collapse (dynamic programming over the BVH2, Ylitie et al.
+  // 2017): cost[n][j] = least SAH cost of representing BVH2 subtree n as at
+  // most j children of a wide node (j = 1..8); a child is either a wide inner
+  // node (area * c_node + the best 8-way split of its subtree) or a leaf
+  // holding the whole subtree when it has <= MTX_BVH_MAX_LEAF triangles
+  // (area * c_tri * count; BVH2 subtrees are contiguous in leaf order).
+  static constexpr int kW = MTX_BVH_WIDTH;
+  float c_node = 1.0f, c_tri = 1.0f;
+  std::vector<float> dp_cost;      // (kW + 1) per BVH2 node (index j = 1..kW)
+  std::vector<uint8_t> dp_split;   // (kW + 1) per node: 0 = use j-1 slots, k = k slots left
+  std::vector<uint8_t> dp_leaf;    // 1: the subtree as one leaf (j = 1)
+  std::vector<uint32_t> sub_first, sub_count;
+  std::vector<Box> box2;           // padded box of each BVH2 node
 
   Box child_box2(uint32_t node, int c) const {
     const float *f = reinterpret_cast<const float *>(&nodes[16 * (size_t)node]);
@@ -235,105 +241,23 @@ struct Builder {
     return b;
   }
 
-  // Opens the inner child with the largest surface area (ties: first) until
-  // the node has 4 children or only leaves remain.
-  std::vector<Child> open_children(uint32_t node2) const {
-    std::vector<Child> ch = {{nodes[16 * (size_t)node2 + 12], child_box2(node2, 0)},
-                             {nodes[16 * (size_t)node2 + 13], child_box2(node2, 1)}};
-    while (ch.size() < MTX_BVH_WIDTH) {
-      int best = -1;
-      float best_area = -1.f;
-      for (int i = 0; i < (int)ch.size(); ++i)
-        if (ch[i].ref >= 0 && ch[i].box.area() > best_area) {
-          best_area = ch[i].box.area();
-          best = i;
-        }
-      if (best < 0) break;
-      const uint32_t n2 = (uint32_t)ch[best].ref;
-      Child a{nodes[16 * (size_t)n2 + 12], child_box2(n2, 0)}, b{nodes[16 * (size_t)n2 + 13], child_box2(n2, 1)};
-      ch[best] = a;
-      ch.insert(ch.begin() + best + 1, b);
-    }
-    return ch;
-  }
-
-  // Sibling-contiguous layout: the inner children of a wide node get
-  // consecutive indices (two 64-B nodes per 128-B line), allocated before
-  // their subtrees.
-  void collapse_siblings(uint32_t w, uint32_t node2, uint32_t depth) {
-    const std::vector<Child> ch = open_children(node2);
-    wide_depth = std::max(wide_depth, depth + 1);
-    int32_t refs[MTX_BVH_WIDTH] = {0, 0, 0, 0};
-    uint32_t n_inner = 0;
-    for (const Child &c : ch) n_inner += c.ref >= 0 ? 1u : 0u;
-    const uint32_t base = (uint32_t)(wnodes.size() / 16);
-    wnodes.resize(wnodes.size() + 16 * (size_t)n_inner, 0);
-    uint32_t j = 0;
-    for (size_t k = 0; k < ch.size(); ++k) refs[k] = ch[k].ref >= 0 ? (int32_t)(base + j++) : ch[k].ref;
-    encode(w, ch, refs);
-    j = 0;
-    for (size_t k = 0; k < ch.size(); ++k)
-      if (ch[k].ref >= 0) collapse_siblings(base + j++, (uint32_t)ch[k].ref, depth + 1);
-  }
-
-  int32_t collapse(uint32_t node2, uint32_t depth) {
-    std::vector<Child> ch = {{nodes[16 * (size_t)node2 + 12], child_box2(node2, 0)},
-                             {nodes[16 * (size_t)node2 + 13], child_box2(node2, 1)}};
-    while (ch.size() < MTX_BVH_WIDTH) {
-      int best = -1;
-      float best_area = -1.f;
-      for (int i = 0; i < (int)ch.size(); ++i)
-        if (ch[i].ref >= 0 && ch[i].box.area() > best_area) {
-          best_area = ch[i].box.area();
-          best = i;
-        }
-      if (best < 0) break;
-      const uint32_t n2 = (uint32_t)ch[best].ref;
-      Child a{nodes[16 * (size_t)n2 + 12], child_box2(n2, 0)}, b{nodes[16 * (size_t)n2 + 13], child_box2(n2, 1)};
-      ch[best] = a;
-      ch.insert(ch.begin() + best + 1, b);
-    }
-    const uint32_t w = (uint32_t)(wnodes.size() / 16);
-    wnodes.resize(wnodes.size() + 16, 0);
-    wide_depth = std::max(wide_depth, depth + 1);
-    int32_t refs[MTX_BVH_WIDTH] = {0, 0, 0, 0};
-    for (size_t k = 0; k < ch.size(); ++k)
-      refs[k] = ch[k].ref >= 0 ? collapse((uint32_t)ch[k].ref, depth + 1) : ch[k].ref;
-    return encode(w, ch, refs) ? (int32_t)w : INT32_MIN;
-  }
-
-  // ---- SAH-optimal collapse (dynamic programming over the BVH2) ----------
-  // cost[n][j]: least SAH cost of representing BVH2 subtree n as at most j
-  // children of a wide node (j = 1..4); a child is either a wide inner node
-  // (area * c_node + the best 4-way split of its subtree) or a leaf holding
-  // the whole subtree when it has <= MTX_BVH_MAX_LEAF triangles (area *
-  // c_tri * count; BVH2 subtrees are contiguous in leaf order). Replaces the
-  // greedy largest-area opening (Ylitie et al. 2017, wide-BVH collapse).
-  float c_node = 1.0f, c_tri = 1.0f;  // tuned on the bedroom proxy (A/B: +1.8 % vs greedy)
-  float c_leaf = 0.f;                 // per-leaf visit cost (leaf-phase overhead)
-  std::vector<float> dp_cost;      // 5 per BVH2 node (index j = 1..4)
-  std::vector<uint8_t> dp_split;   // 5 per node: 0 = use j-1 slots, k = k slots left
-  std::vector<uint8_t> dp_leaf;    // 1: the subtree as one leaf (j = 1)
-  std::vector<uint32_t> sub_first, sub_count;
-  std::vector<Box> box2;           // padded box of each BVH2 node
-
   void ref_info(int32_t ref, float area, float *cost, uint32_t *first, uint32_t *count) const {
     if (ref >= 0) {
-      for (int j = 1; j <= 4; ++j) cost[j] = dp_cost[5 * (size_t)ref + j];
+      for (int j = 1; j <= kW; ++j) cost[j] = dp_cost[(kW + 1) * (size_t)ref + j];
       *first = sub_first[ref];
       *count = sub_count[ref];
     } else {
       const uint32_t code = ~(uint32_t)ref;
       *first = code >> 3;
       *count = (code & 7u) + 1u;
-      for (int j = 1; j <= 4; ++j) cost[j] = area * (c_leaf + c_tri * (float)*count);
+      for (int j = 1; j <= kW; ++j) cost[j] = area * c_tri * (float)*count;
     }
   }
 
   void dp_prepare() {
     const size_t n2 = nodes.size() / 16;
-    dp_cost.assign(5 * n2, 0.f);
-    dp_split.assign(5 * n2, 0);
+    dp_cost.assign((kW + 1) * n2, 0.f);
+    dp_split.assign((kW + 1) * n2, 0);
     dp_leaf.assign(n2, 0);
     sub_first.assign(n2, 0);
     sub_count.assign(n2, 0);
@@ -347,15 +271,15 @@ struct Builder {
         if (r >= 0) box2[r] = child_box2((uint32_t)n, c);
       }
     for (size_t n = n2; n-- > 0;) {
-      float cl[5], cr[5];
+      float cl[kW + 1], cr[kW + 1];
       uint32_t fl, nl, fr, nr;
       ref_info(nodes[16 * n + 12], child_box2((uint32_t)n, 0).area(), cl, &fl, &nl);
       ref_info(nodes[16 * n + 13], child_box2((uint32_t)n, 1).area(), cr, &fr, &nr);
       sub_first[n] = std::min(fl, fr);
       sub_count[n] = nl + nr;
-      float dist[5];
-      uint8_t kbest[5] = {0, 0, 0, 0, 0};
-      for (int j = 2; j <= 4; ++j) {
+      float dist[kW + 1];
+      uint8_t kbest[kW + 1] = {0};
+      for (int j = 2; j <= kW; ++j) {
         dist[j] = INFINITY;
         for (int k = 1; k < j; ++k) {
           const float c = cl[k] + cr[j - k];
@@ -366,22 +290,27 @@ struct Builder {
         }
       }
       const float area = box2[n].area();
-      const float c_inner = area * c_node + dist[4];
-      const float c_lf = sub_count[n] <= MTX_BVH_MAX_LEAF ? area * (c_leaf + c_tri * (float)sub_count[n]) : INFINITY;
-      float *C = &dp_cost[5 * n];
+      const float c_inner = area * c_node + dist[kW];
+      const float c_lf = sub_count[n] <= MTX_BVH_MAX_LEAF ? area * c_tri * (float)sub_count[n] : INFINITY;
+      float *Cn = &dp_cost[(kW + 1) * n];
       dp_leaf[n] = c_lf <= c_inner ? 1 : 0;
-      C[1] = std::min(c_lf, c_inner);
-      for (int j = 2; j <= 4; ++j) {
-        if (dist[j] < C[j - 1]) {
-          C[j] = dist[j];
-          dp_split[5 * n + j] = kbest[j];
+      Cn[1] = std::min(c_lf, c_inner);
+      for (int j = 2; j <= kW; ++j) {
+        if (dist[j] < Cn[j - 1]) {
+          Cn[j] = dist[j];
+          dp_split[(kW + 1) * n + j] = kbest[j];
         } else {
-          C[j] = C[j - 1];
-          dp_split[5 * n + j] = 0;
+          Cn[j] = Cn[j - 1];
+          dp_split[(kW + 1) * n + j] = 0;
         }
       }
     }
   }
+
+  struct Child {
+    int32_t ref;  // BVH2 ref (inner index or leaf code)
+    Box box;      // padded fp32 box
+  };
 
   // Children of the wide node made from BVH2 node n with j slots.
   void dp_expand(int32_t ref, int j, Box box, std::vector<Child> &out) const {
@@ -389,10 +318,10 @@ struct Builder {
       out.push_back({ref, box});
       return;
     }
-    int k = dp_split[5 * (size_t)ref + j];
+    int k = dp_split[(kW + 1) * (size_t)ref + j];
     while (k == 0 && j > 1) {
       --j;
-      k = j > 1 ? dp_split[5 * (size_t)ref + j] : 0;
+      k = j > 1 ? dp_split[(kW + 1) * (size_t)ref + j] : 0;
     }
     if (j == 1) {
       out.push_back({ref, box});
@@ -402,90 +331,61 @@ struct Builder {
     dp_expand(nodes[16 * (size_t)ref + 13], j - k, child_box2((uint32_t)ref, 1), out);
   }
 
-  int32_t collapse_dp(uint32_t node2, uint32_t depth) {
-    std::vector<Child> ch;
-    dp_expand((int32_t)node2, 4, box2[node2], ch);
-    if (ch.size() == 1) {  // a subtree that prefers fewer slots: still split the root in two
-      ch.clear();
-      dp_expand(nodes[16 * (size_t)node2 + 12], 1, child_box2(node2, 0), ch);
-      dp_expand(nodes[16 * (size_t)node2 + 13], 1, child_box2(node2, 1), ch);
-    }
-    const uint32_t w = (uint32_t)(wnodes.size() / 16);
-    wnodes.resize(wnodes.size() + 16, 0);
-    wide_depth = std::max(wide_depth, depth + 1);
-    int32_t refs[MTX_BVH_WIDTH] = {0, 0, 0, 0};
-    for (size_t k = 0; k < ch.size(); ++k) {
-      const int32_t r = ch[k].ref;
-      if (r < 0) {
-        refs[k] = r;
-      } else if (dp_leaf[r]) {  // the whole subtree as one leaf
-        refs[k] = ~(int32_t)((sub_first[r] << 3) | (sub_count[r] - 1u));
-      } else {
-        refs[k] = collapse_dp((uint32_t)r, depth + 1);
+  // Slot of each child: slot s is visited at position s ^ octant(ray), so
+  // the child in slot s should lie towards the corner s of the node (axis a
+  // on the + side when bit a of s is set). Greedy assignment (Ylitie et al.
+  // 2017, section 3.2): repeatedly the unassigned (child, slot) pair with the
+  // largest dot(centroid_child - centroid_node, corner_s); ties to the
+  // smaller child, then the smaller slot.
+  static void assign_slots(const std::vector<Child> &ch, int slot_of[kW]) {
+    Box u;
+    u.reset();
+    for (const Child &c : ch) u.grow(c.box);
+    double pc[3], cc[kW][3];
+    for (int a = 0; a < 3; ++a) pc[a] = 0.5 * ((double)u.lo[a] + (double)u.hi[a]);
+    for (size_t i = 0; i < ch.size(); ++i)
+      for (int a = 0; a < 3; ++a) cc[i][a] = 0.5 * ((double)ch[i].box.lo[a] + (double)ch[i].box.hi[a]) - pc[a];
+    bool used_c[kW] = {false}, used_s[kW] = {false};
+    for (size_t n = 0; n < ch.size(); ++n) {
+      double best = -INFINITY;
+      int bc = -1, bs = -1;
+      for (size_t i = 0; i < ch.size(); ++i) {
+        if (used_c[i]) continue;
+        for (int sl = 0; sl < kW; ++sl) {
+          if (used_s[sl]) continue;
+          double v = 0.0;
+          for (int a = 0; a < 3; ++a) v += ((sl >> a) & 1) ? cc[i][a] : -cc[i][a];
+          if (v > best) {
+            best = v;
+            bc = (int)i;
+            bs = sl;
+          }
+        }
       }
+      used_c[bc] = used_s[bs] = true;
+      slot_of[bc] = bs;
     }
-    return encode(w, ch, refs) ? (int32_t)w : INT32_MIN;
   }
 
   bool quant_ok = true;
   static constexpr int kEMin = -32, kEMax = 31;
+  std::vector<int32_t> wnodes;  // MTX_BVH_NODE_WORDS per wide node
+  uint32_t wide_depth = 0;
 
-  // Device layout (mtx_bvh_device_nodes): nodes in breadth-first order with
-  // the inner children of a node at consecutive indices, a node's slots
-  // ordered inner children first (each group keeps its order), and the
-  // triangles re-ordered so that a node's leaf children are consecutive
-  // ranges in slot order. A child reference is then a base + a small offset.
-  void relayout() {
-    std::vector<int32_t> out(16, 0);
-    std::vector<uint32_t> queue = {0}, tris;
-    tris.reserve(order.size());
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-      const int32_t *W = &wnodes[16 * (size_t)queue[qi]];
-      int slot[MTX_BVH_WIDTH], m = 0;
-      for (int k = 0; k < (int)((uint32_t)W[3] >> 24); ++k)
-        if (W[4 + k] >= 0) slot[m++] = k;
-      for (int k = 0; k < (int)((uint32_t)W[3] >> 24); ++k) {
-        bool dup = false;  // a one-triangle mesh's root holds its leaf twice
-        for (int j = 0; j < k; ++j) dup = dup || W[4 + j] == W[4 + k];
-        if (W[4 + k] < 0 && !dup) slot[m++] = k;
-      }
-      const int nch = m;
-      int32_t O[16] = {W[0], W[1], W[2], (int32_t)(((uint32_t)W[3] & 0xffffffu) | ((uint32_t)nch << 24)),
-                       0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int a = 0; a < 6; ++a) {
-        uint32_t q = 0;
-        for (int j = 0; j < nch; ++j) q |= (((uint32_t)W[8 + a] >> (8 * slot[j])) & 255u) << (8 * j);
-        O[8 + a] = (int32_t)q;
-      }
-      for (int j = 0; j < nch; ++j) {
-        const int32_t r = W[4 + slot[j]];
-        if (r >= 0) {
-          O[4 + j] = (int32_t)queue.size();
-          queue.push_back((uint32_t)r);
-        } else {
-          const uint32_t code = ~(uint32_t)r, first = code >> 3, cnt = (code & 7u) + 1u;
-          O[4 + j] = ~(int32_t)(((uint32_t)tris.size() << 3) | (cnt - 1u));
-          for (uint32_t t = 0; t < cnt; ++t) tris.push_back(order[first + t]);
-        }
-      }
-      out.resize(16 * queue.size(), 0);
-      std::memcpy(&out[16 * qi], O, sizeof(O));
-    }
-    wnodes.swap(out);
-    order.swap(tris);
-  }
-
-  bool encode(uint32_t w, const std::vector<Child> &ch, const int32_t *refs) {
+  // Quantised child boxes of node W in slots slot_of[k] (mtx.h layout).
+  void encode_boxes(int32_t *W, const std::vector<Child> &ch, const int *slot_of) {
     Box u;
     u.reset();
     for (const Child &c : ch) u.grow(c.box);
-    int32_t *W = &wnodes[16 * (size_t)w];
-    uint32_t q[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t q[12];
+    for (int a = 0; a < 3; ++a) {  // empty slots: q_lo 255, q_hi 0
+      q[4 * a + 0] = q[4 * a + 1] = 0xffffffffu;
+      q[4 * a + 2] = q[4 * a + 3] = 0u;
+    }
     uint32_t ebytes = 0;
     for (int a = 0; a < 3; ++a) {
       const float org = u.lo[a];
       const double ext = (double)u.hi[a] - (double)org;
-      // exponents stay in [kEMin, kEMax]: the device node keeps them in 6 bits
       int e = kEMin;
       if (ext > 0.0) {
         int ee;
@@ -504,17 +404,82 @@ struct Builder {
         while (qhi < 255 && mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a]) ++qhi;
         if (mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a] || mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a])
           quant_ok = false;
-        q[2 * a] |= qlo << (8 * k);
-        q[2 * a + 1] |= qhi << (8 * k);
+        const int sl = slot_of[k], wd = sl >> 2, sh = 8 * (sl & 3);
+        uint32_t &lo = q[4 * a + wd], &hi = q[4 * a + 2 + wd];
+        lo = (lo & ~(255u << sh)) | (qlo << sh);
+        hi = (hi & ~(255u << sh)) | (qhi << sh);
       }
       std::memcpy(&W[a], &org, 4);
       ebytes |= (uint32_t)(e & 255) << (8 * a);
     }
-    ebytes |= (uint32_t)ch.size() << 24;
-    W[3] = (int32_t)ebytes;
-    for (int k = 0; k < MTX_BVH_WIDTH; ++k) W[4 + k] = refs[k];
-    for (int k = 0; k < 6; ++k) W[8 + k] = (int32_t)q[k];
-    return true;
+    W[3] = (int32_t)((uint32_t)W[3] | ebytes);
+    for (int k = 0; k < 12; ++k) W[8 + k] = (int32_t)q[k];
+  }
+
+  // Breadth-first wide tree: node i's inner children get consecutive
+  // indices (slot order) when it is laid out, its leaves' triangles
+  // consecutive slots of the new leaf order.
+  void collapse_wide() {
+    const int NW = MTX_BVH_NODE_WORDS;
+    std::vector<uint32_t> queue = {0}, level = {1}, tris;
+    tris.reserve(order.size());
+    wnodes.assign(NW, 0);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const uint32_t n2 = queue[qi];
+      std::vector<Child> ch;
+      dp_expand((int32_t)n2, kW, box2[n2], ch);
+      if (ch.size() == 1) {  // a subtree that prefers one slot: still split the root in two
+        ch.clear();
+        dp_expand(nodes[16 * (size_t)n2 + 12], 1, child_box2(n2, 0), ch);
+        dp_expand(nodes[16 * (size_t)n2 + 13], 1, child_box2(n2, 1), ch);
+      }
+      if (qi == 0 && n == 1) ch.resize(1);  // one triangle: the root's two BVH2 children are the same leaf
+      wide_depth = std::max(wide_depth, level[qi]);
+      int slot_of[kW];
+      assign_slots(ch, slot_of);
+      int child_at[kW];
+      for (int sl = 0; sl < kW; ++sl) child_at[sl] = -1;
+      for (size_t k = 0; k < ch.size(); ++k) child_at[slot_of[k]] = (int)k;
+      uint32_t imask = 0, meta[2] = {0, 0}, off = 0;
+      const uint32_t child_base = (uint32_t)queue.size(), tri_base = (uint32_t)tris.size();
+      for (int sl = 0; sl < kW; ++sl) {
+        const int k = child_at[sl];
+        if (k < 0) continue;
+        const int32_t r = ch[k].ref;
+        uint32_t first = 0, cnt = 0, m;
+        bool leaf = r < 0;
+        if (r < 0) {
+          const uint32_t code = ~(uint32_t)r;
+          first = code >> 3;
+          cnt = (code & 7u) + 1u;
+        } else if (dp_leaf[r]) {  // the whole subtree as one leaf
+          first = sub_first[r];
+          cnt = sub_count[r];
+          leaf = true;
+        }
+        if (leaf) {
+          m = (((1u << cnt) - 1u) << 5) | off;
+          for (uint32_t t = 0; t < cnt; ++t) tris.push_back(order[first + t]);
+          off += cnt;
+        } else {
+          imask |= 1u << sl;
+          m = 0x20u | (24u + (uint32_t)sl);
+          queue.push_back((uint32_t)r);
+          level.push_back(level[qi] + 1);
+        }
+        meta[sl >> 2] |= m << (8 * (sl & 3));
+      }
+      if (off > 24) quant_ok = false;  // cannot happen: <= 8 leaves of <= 3 triangles
+      wnodes.resize((size_t)NW * queue.size(), 0);
+      int32_t *W = &wnodes[(size_t)NW * qi];
+      W[3] = (int32_t)(imask << 24);
+      W[4] = (int32_t)child_base;
+      W[5] = (int32_t)tri_base;
+      W[6] = (int32_t)meta[0];
+      W[7] = (int32_t)meta[1];
+      encode_boxes(W, ch, slot_of);
+    }
+    order.swap(tris);
   }
 
   void run() {
@@ -575,12 +540,10 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
       return MTX_E_ARG;
     }
   Builder b;
-  // build knobs (tuning experiments): SAH traversal cost relative to one
-  // triangle test, the wide-node layout (0 depth-first, 1 siblings
-  // contiguous), the collapse (MTX_BVH_COLLAPSE=0 greedy, default DP) and
-  // its node / triangle costs
+  // build knobs (tuning experiments, tools/bvh_experiment.py): SAH traversal
+  // cost relative to one triangle test, bins, and the collapse's node /
+  // triangle costs
   if (const char *e = getenv("MTX_BVH_CT")) b.ct = std::max(0.05f, (float)atof(e));
-  if (const char *e = getenv("MTX_BVH_LAYOUT")) b.layout = atoi(e);
   if (const char *e = getenv("MTX_BVH_BINS")) b.n_bins = std::max(2, std::min(kMaxBins, atoi(e)));
   b.vpos = vpos;
   b.vidx = tri_vidx;
@@ -590,33 +553,19 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     mtx_set_error("mtx_bvh_build: internal error (%zu leaf triangles for %u)", b.order.size(), n_tris);
     return MTX_E_ARG;
   }
-  b.wnodes.reserve(b.nodes.size() / 2 + 16);
   if (const char *e = getenv("MTX_BVH_CNODE")) b.c_node = (float)atof(e);
   if (const char *e = getenv("MTX_BVH_CTRI")) b.c_tri = (float)atof(e);
-  if (const char *e = getenv("MTX_BVH_CLEAF")) b.c_leaf = (float)atof(e);
-  const char *col = getenv("MTX_BVH_COLLAPSE");
-  if (b.layout == 1) {
-    b.wnodes.resize(16, 0);
-    b.collapse_siblings(0, 0, 0);
-  } else if (col && atoi(col) == 0) {  // greedy largest-area opening (A/B baseline)
-    b.collapse(0, 0);
-  } else {
-    b.dp_prepare();
-    b.collapse_dp(0, 0);
-  }
+  b.dp_prepare();
+  b.collapse_wide();
   if (!b.quant_ok) {
     mtx_set_error("mtx_bvh_build: child box quantisation failed (non-finite or huge coordinates?)");
     return MTX_E_ARG;
   }
-  // MTX_BVH_RELAYOUT=0 keeps the collapse's depth-first order (A/B only: the
-  // 48-B device node form needs the breadth-first layout)
-  const char *rl = getenv("MTX_BVH_RELAYOUT");
-  if (!rl || atoi(rl) != 0) b.relayout();
   if (b.order.size() != n_tris) {
-    mtx_set_error("mtx_bvh_build: internal error (%zu triangles after the relayout for %u)", b.order.size(), n_tris);
+    mtx_set_error("mtx_bvh_build: internal error (%zu triangles after the collapse for %u)", b.order.size(), n_tris);
     return MTX_E_ARG;
   }
-  uint32_t n_nodes = (uint32_t)(b.wnodes.size() / 16);
+  uint32_t n_nodes = (uint32_t)(b.wnodes.size() / MTX_BVH_NODE_WORDS);
   std::memcpy(nodes_out, b.wnodes.data(), b.wnodes.size() * sizeof(int32_t));
   *n_nodes_out = n_nodes;
   for (uint32_t i = 0; i < n_tris; ++i) {
@@ -631,64 +580,6 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     g[8] = p2[0] - p0[0]; g[9] = p2[1] - p0[1]; g[10] = p2[2] - p0[2]; g[11] = 0.f;
   }
   if (depth_out) *depth_out = b.wide_depth;
-  return MTX_OK;
-}
-
-// Device form of the nodes (48 B, three dwordx4 loads per visit instead of
-// four): the 64-B node's four child references become two bases and a 24-bit
-// field of per-slot leaf ends, which the builder's layout (relayout) makes
-// sufficient: inner children first, at node_base + slot; leaf slots' triangle
-// ranges consecutive from tri_base, slot k ending at tri_base + end_k. Words:
-//   0..2 origin | 3: ex, ey, ez (6-bit two's complement), nch - 1 (2 bits),
-//   ends[0..11] | 4: node_base (24 bits), ends[12..19] | 5: tri_base (24 bits),
-//   ends[20..23] | 6..11: the quantised bounds (unchanged).
-extern "C" int mtx_bvh_device_nodes(const int32_t *nodes, uint32_t n_nodes, uint32_t n_tris, int32_t *out) {
-  if (!nodes || !out || n_nodes == 0) {
-    mtx_set_error("mtx_bvh_device_nodes: null argument or no nodes");
-    return MTX_E_ARG;
-  }
-  for (uint32_t i = 0; i < n_nodes; ++i) {
-    const int32_t *W = nodes + 16 * (size_t)i;
-    const uint32_t eb = (uint32_t)W[3], nch = eb >> 24;
-    auto fail = [&](const char *why) {
-      mtx_set_error("mtx_bvh_device_nodes: node %u %s (build the BVH with mtx_bvh_build)", i, why);
-      return MTX_E_ARG;
-    };
-    if (nch < 1 || nch > MTX_BVH_WIDTH) return fail("has a bad child count");
-    uint32_t ex[3];
-    for (int a = 0; a < 3; ++a) {
-      const int e = (int)(int8_t)(uint8_t)((eb >> (8 * a)) & 0xffu);
-      if (e < -32 || e > 31) return fail("has an axis exponent outside [-32, 31]");
-      ex[a] = (uint32_t)e & 63u;
-    }
-    uint32_t node_base = 0, tri_base = 0, run = 0, ends[4] = {0, 0, 0, 0};
-    bool leaf_seen = false;
-    for (uint32_t k = 0; k < nch; ++k) {
-      const int32_t r = W[4 + k];
-      if (r >= 0) {
-        if (leaf_seen) return fail("has an inner child after a leaf");
-        if (k == 0) node_base = (uint32_t)r;
-        if ((uint32_t)r != node_base + k || (uint32_t)r >= n_nodes) return fail("has non-consecutive inner children");
-      } else {
-        const uint32_t code = ~(uint32_t)r, first = code >> 3, cnt = (code & 7u) + 1u;
-        if (!leaf_seen) tri_base = first;
-        leaf_seen = true;
-        if (first != tri_base + run || (uint64_t)first + cnt > n_tris) return fail("has non-consecutive leaf triangles");
-        run += cnt;
-        ends[k] = run;
-      }
-    }
-    if (node_base >= (1u << 24) || tri_base >= (1u << 24)) return fail("has a base beyond 2^24");
-    const uint32_t E = ends[0] | ends[1] << 6 | ends[2] << 12 | ends[3] << 18;
-    int32_t *O = out + 12 * (size_t)i;
-    O[0] = W[0];
-    O[1] = W[1];
-    O[2] = W[2];
-    O[3] = (int32_t)(ex[0] | ex[1] << 6 | ex[2] << 12 | (nch - 1u) << 18 | (E & 0xfffu) << 20);
-    O[4] = (int32_t)(node_base | ((E >> 12) & 0xffu) << 24);
-    O[5] = (int32_t)(tri_base | ((E >> 20) & 0xfu) << 24);
-    for (int a = 0; a < 6; ++a) O[6 + a] = W[8 + a];
-  }
   return MTX_OK;
 }
 

@@ -75,7 +75,7 @@ struct ClosestSrc {
 #endif
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
-  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
+  extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
@@ -154,7 +154,7 @@ struct ShadowSrc {
 
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
-  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
+  extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
   const ShadowSrc src{b};
   uint32_t nv = 0, tv = 0, nr = 0;
   trace_loop<true>(s, src, b.counters[4 * (bounce + 1) + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, stack + threadIdx.x, nv, tv, nr);
@@ -1225,8 +1225,8 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
 // Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0).
 __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const float4 *rays, uint32_t n, int any_hit,
                                                            uint32_t *hits, uint32_t *visits) {
-  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
-  int32_t *stk = stack + threadIdx.x;
+  extern __shared__ uint2 stack[];  // s.stack_entries x kTraceBlock node groups (dynamic)
+  uint2 *stk = stack + threadIdx.x;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 o4 = rays[2 * (size_t)i], d4 = rays[2 * (size_t)i + 1];

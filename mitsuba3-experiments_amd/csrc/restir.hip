@@ -416,7 +416,7 @@ struct TestSrc {
 };
 
 __global__ __launch_bounds__(kTraceBlock) void k_trace_test(DevScene s, RestirBuffers r, uint32_t occ_base) {
-  extern __shared__ int32_t stack[];  // s.stack_entries x kTraceBlock (dynamic)
+  extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
   const TestSrc src{r, occ_base};
   uint32_t nv = 0, tv = 0, nr = 0;
   trace_loop<true>(s, src, r.test_count[0], r.test_heads, stack + threadIdx.x, nv, tv, nr);

@@ -38,12 +38,12 @@ enum : uint32_t {
 };
 
 #ifndef MTX_TRACE_BLOCK
-#define MTX_TRACE_BLOCK 256  // 8 blocks of 4 waves per CU: LDS room for a 64-node tree top (128: 32 nodes, -0.5 %)
+#define MTX_TRACE_BLOCK 256  // 8 blocks of 4 waves per CU: 20 KB of LDS each (stack + tree top)
 #endif
 constexpr int kTraceBlock = MTX_TRACE_BLOCK;  // threads per traversal block
-constexpr uint32_t kLdsStack = 16;   // default LDS part of the persistent traversal stack (entries per lane)
+constexpr uint32_t kLdsStack = 8;    // default LDS part of the persistent traversal stack (8-B entries per lane)
 #ifndef MTX_LDS_TOP
-#define MTX_LDS_TOP 64  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
+#define MTX_LDS_TOP 48  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
 #endif
 #ifndef MTX_STREAMS
 #define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)
@@ -56,7 +56,7 @@ constexpr uint32_t kXHeadStride = 32;
 constexpr uint32_t kXSlotWords = kXcds * kXHeadStride;
 
 struct DevScene {
-  const int4 *nodes;  // 4 x int4 per node: the 64-B ABI node (mtx.h); 3 x int4 only in the MTX_NODE48=1 A/B build
+  const int4 *nodes;  // 5 x int4 per node: the 80-B ABI node (mtx.h)
   const float *tri;   // 9 floats per triangle (v0, e1, e2; device_common.h load_tri)
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;
@@ -71,15 +71,13 @@ struct DevScene {
   const float *texels;
   const float *tables;
   uint32_t n_tris, n_emitters;
-  uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane)
+  uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane: node groups, 8 B)
   uint32_t lds_entries;    // persistent kernels: stack entries kept in LDS
   uint32_t lds_top;        // persistent kernels: wide nodes [0, lds_top) read from a per-block LDS copy
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
-  int32_t *stack_ovf;      // persistent kernels: entries beyond lds_entries, [entry][thread]
+  uint2 *stack_ovf;        // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
-  uint32_t refill_lanes;   // persistent kernels: refill a wave once this many lanes are idle
-  uint32_t urefill;        // unified single-step traversal (trace_loop_u): the same, its own threshold
-  uint32_t speculate;      // persistent kernels: postpone one leaf per lane (not in STATS kernels)
+  uint32_t urefill;        // persistent kernels: refill a wave once this many lanes are idle
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
 };

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 4
+MTX_ABI_VERSION = 5
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -38,7 +38,9 @@ MTX_RENDER_NRC_CACHE = 4
 MTX_RESTIR_STAGE_B = 32
 
 MTX_ROUGH_TRANSMITTANCE_RES = 64
-MTX_BVH_MAX_LEAF = 8
+MTX_BVH_WIDTH = 8
+MTX_BVH_MAX_LEAF = 3
+MTX_BVH_NODE_WORDS = 20
 MTX_BVH_MAX_DEPTH = 40
 
 ERRORS = {-1: "MTX_E_ARG", -2: "MTX_E_HIP", -3: "MTX_E_NOSCENE", -4: "MTX_E_OOM", -5: "MTX_E_UNSUPPORTED"}
@@ -188,6 +190,8 @@ class Stats(C.Structure):
         ("cache_queries", C.c_uint64),
         ("cache_encode_ms", C.c_double),
         ("cache_mlp_ms", C.c_double),
+        ("streams", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:
@@ -259,7 +263,6 @@ EXPORTS = [
     "mtx_ctx_create",
     "mtx_ctx_destroy",
     "mtx_bvh_build",
-    "mtx_bvh_device_nodes",
     "mtx_roughplastic_tables",
     "mtx_scene_upload",
     "mtx_render",

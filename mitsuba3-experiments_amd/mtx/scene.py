@@ -257,7 +257,7 @@ class Scene:
     def _build_bvh(self, tri_vidx, tri_shape):
         from ._lib import check, lib
         n = len(tri_shape)
-        nodes = np.zeros((2 * n + 2) * 16, np.int32)
+        nodes = np.zeros((n + 1) * _abi.MTX_BVH_NODE_WORDS, np.int32)
         geom = np.zeros(12 * n, np.float32)
         perm = np.zeros(n, np.uint32)
         nn = C.c_uint32()
@@ -266,7 +266,7 @@ class Scene:
         check(lib().mtx_bvh_build(self.vpos.ctypes.data, len(self.vpos), tri_vidx.ctypes.data, n, nodes.ctypes.data,
                                   C.byref(nn), geom.ctypes.data, perm.ctypes.data, C.byref(depth)), "mtx_bvh_build")
         self.n_nodes = nn.value
-        self.nodes = np.ascontiguousarray(nodes[: 16 * nn.value])
+        self.nodes = np.ascontiguousarray(nodes[: _abi.MTX_BVH_NODE_WORDS * nn.value])
         self.tri_geom = geom
         self.tri_vidx = np.ascontiguousarray(tri_vidx.reshape(-1, 3)[perm].reshape(-1))
         self.tri_shape = np.ascontiguousarray(tri_shape[perm])

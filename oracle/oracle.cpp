@@ -79,11 +79,15 @@ struct Hit {
   uint32_t prim;
 };
 
-// Scalar traversal of the 4-wide BVH. Visit order (shared with the device
-// kernels through mtx_core/geometry.h wide_node_order): hit children by
-// ascending entry distance (near-ties by slot); the nearest is visited next,
-// the others are pushed farthest first. Closest-hit ties on t go to the smaller prim, so the
-// hit does not depend on the order; the visit counts do, and match the device.
+// Scalar traversal of the 8-wide compressed BVH (mtx.h), in the device
+// kernels' per-ray order (mtx_core/geometry.h cw_node_hits): a visited node
+// yields a node group (child_base, the hit inner children as mask bits in
+// octant order, imask) and a triangle group (tri_base, the hit leaves'
+// triangles as mask bits); the triangle group is tested first, one triangle
+// per step in ascending offset, then the next child of the node group (the
+// lowest bit) is visited with the rest of the group pushed; an empty group
+// pops the next one. Closest-hit ties on t go to the smaller prim, so the hit
+// does not depend on the order; the visit counts do, and match the device.
 // Diagnostic (tools/ only): visits per node index < g_hist_len are counted
 // into g_hist while orc_node_visit_hist runs (the top-of-tree share of node
 // fetches that an LDS-resident tree top would serve).
@@ -96,54 +100,59 @@ bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *
   TraceRay r = make_trace_ray(o, d, maxt);
   Hit h{maxt, 0.f, 0.f, 0xffffffffu};
   float tbest = maxt;
-  int32_t stack[3 * MTX_BVH_MAX_DEPTH + 2];
+  const uint32_t oct = ray_octant(r);
+  uint32_t stack[2 * (MTX_BVH_MAX_DEPTH + 2)];
   int sp = 0;
-  int32_t node = 0;
+  uint32_t gbase = 0, ghits = (1u << (24 + oct)) | 1u;  // the root: node 0 in slot 0
+  uint32_t tbase = 0, thits = 0;
   uint32_t nv = 0, tv = 0;
   bool hit = false;
   while (true) {
-    if (node >= 0) {
-      const int32_t *w = s.nodes + 16 * (size_t)node;
+    if (thits) {
+      const uint32_t prim = tbase + (uint32_t)ctz32(thits);
+      thits &= thits - 1u;
+      const float *g = s.tri_geom + 12 * (size_t)prim;
+      float t, u, v;
+      ++tv;
+      if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
+        if (ANY) {
+          hit = true;
+          break;
+        }
+        if (t < tbest || (t == tbest && prim < h.prim)) {
+          tbest = t;
+          h.t = t;
+          h.u = u;
+          h.v = v;
+          h.prim = prim;
+        }
+      }
+    } else if (ghits >> 24) {
+      const uint32_t p = (uint32_t)ctz32(ghits >> 24);
+      ghits &= ~(1u << (24 + p));
+      const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
+      if (ghits >> 24) {
+        stack[sp++] = gbase;
+        stack[sp++] = ghits;
+      }
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(s.nodes) + MTX_BVH_NODE_WORDS * (size_t)node;
       const float *f = reinterpret_cast<const float *>(w);
       ++nv;
-      if (g_hist && (uint32_t)node < g_hist_len) {
+      if (g_hist && node < g_hist_len) {
 #pragma omp atomic
         ++g_hist[node];
       }
-      uint32_t key[4];
-      const int n = wide_node_order(r, f[0], f[1], f[2], (uint32_t)w[3], (uint32_t)w[8], (uint32_t)w[9],
-                                    (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], tbest, key);
-      if (n > 0) {
-        for (int rr = n - 1; rr >= 1; --rr) stack[sp++] = wide_ref(key[rr], w[4], w[5], w[6], w[7]);
-        node = wide_ref(key[0], w[4], w[5], w[6], w[7]);
-        continue;
-      }
+      const uint32_t hm = cw_node_hits(r, oct, f[0], f[1], f[2], w[3], w[6], w[7], w + 8, tbest);
+      gbase = w[4];
+      ghits = (hm & 0xff000000u) | (w[3] >> 24);
+      tbase = w[5];
+      thits = hm & 0x00ffffffu;
+    } else if (sp > 0) {
+      ghits = stack[--sp];
+      gbase = stack[--sp];
     } else {
-      uint32_t first, count;
-      leaf_decode(node, &first, &count);
-      for (uint32_t k = 0; k < count; ++k) {
-        uint32_t prim = first + k;
-        const float *g = s.tri_geom + 12 * (size_t)prim;
-        float t, u, v;
-        ++tv;
-        if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
-          if (ANY) {
-            hit = true;
-            break;
-          }
-          if (t < tbest || (t == tbest && prim < h.prim)) {
-            tbest = t;
-            h.t = t;
-            h.u = u;
-            h.v = v;
-            h.prim = prim;
-          }
-        }
-      }
-      if (ANY && hit) break;
+      break;
     }
-    if (sp == 0) break;
-    node = stack[--sp];
   }
   if (nodes_visited) *nodes_visited = nv;
   if (tris_visited) *tris_visited = tv;

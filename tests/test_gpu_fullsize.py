@@ -8,8 +8,8 @@ branches (VERDICT r1 "next" #4).
 * The traversal stack's global spill area (csrc/device_common.h, pushes
   beyond the LDS entries): a fresh process with MTX_LDS_STACK=1 keeps one
   entry in LDS, so every deeper push and pop goes through global memory;
-  also the non-speculative and non-XCD-claiming traversal (MTX_SPECULATE=0,
-  MTX_XCD_CLAIM=0). The environment is read when the context is created, so
+  also without the LDS tree top (MTX_LDS_TOP=0) and the non-XCD-claiming
+  traversal (MTX_XCD_CLAIM=0). The environment is read when the context is created, so
   each variant runs in its own subprocess before any GPU call.
 * max_depth 65, the default of data/bedroom/scene.xml:6 (SURVEY §8d C2
   secondary configuration).
@@ -93,9 +93,9 @@ print("CHILD OK")
 """
 
 
-@pytest.mark.parametrize("env", [{"MTX_LDS_STACK": "1"}, {"MTX_LDS_STACK": "2", "MTX_SPECULATE": "0"},
+@pytest.mark.parametrize("env", [{"MTX_LDS_STACK": "1"}, {"MTX_LDS_STACK": "2", "MTX_LDS_TOP": "0"},
                                  {"MTX_XCD_CLAIM": "0", "MTX_TRACE_BATCH": "64"}],
-                         ids=["spill-all", "spill2-nospec", "noxcd-batch64"])
+                         ids=["spill-all", "spill2-notop", "noxcd-batch64"])
 def test_traversal_variants_bit_exact(env):
     """Traversal variants selected at context creation: bit-exact hits,
     visit counts and films on the 2 % scene and on the full-size scene."""

@@ -68,15 +68,36 @@ def _decode(org, e, q):
 
 
 def test_bvh_invariants(small_scene):
-    """4-wide quantised nodes (mtx.h): every triangle in exactly one leaf of
-    at most 8, children's decoded boxes contain their triangles / subtrees,
-    depth as reported."""
+    """8-wide compressed nodes (mtx.h): every triangle in exactly one leaf of
+    at most 3, leaves' triangles consecutive from tri_base in slot order,
+    inner children consecutive from child_base in slot order (breadth-first:
+    after their parent), meta bytes as documented, empty slots never hit
+    (q_lo 255 > q_hi 0), children's decoded boxes contain their triangles /
+    subtrees, depth as reported."""
     s = small_scene
     _check_bvh(s.nodes, s.tri_geom, s.n_tris, s.bvh_depth)
 
 
+def _node_children(u, i):
+    """[(slot, 'inner', node) | (slot, 'leaf', first, count)] of node i."""
+    imask, cb, tb = int(u[i, 3] >> 24), int(u[i, 4]), int(u[i, 5])
+    out, inner, off = [], 0, 0
+    for sl in range(8):
+        m = int((u[i, 6 + (sl >> 2)] >> (8 * (sl & 3))) & 255)
+        if (imask >> sl) & 1:
+            assert m == 0x20 | (24 + sl), (i, sl, m)
+            out.append((sl, "inner", cb + inner))
+            inner += 1
+        elif m:
+            cnt = {1: 1, 3: 2, 7: 3}[m >> 5]
+            assert (m & 31) == off and off + cnt <= 24, (i, sl, m, off)  # consecutive in slot order
+            out.append((sl, "leaf", tb + off, cnt))
+            off += cnt
+    return out
+
+
 def _check_bvh(nodes, tri_geom, n_tris, bvh_depth):
-    nodes = nodes.reshape(-1, 16)
+    nodes = nodes.reshape(-1, 20)
     f = nodes.view(np.float32)
     u = nodes.view(np.uint32)
     seen = np.zeros(n_tris, np.int32)
@@ -86,92 +107,47 @@ def _check_bvh(nodes, tri_geom, n_tris, bvh_depth):
     v2 = v0 + geom[:, 8:11]
     lo = np.minimum(np.minimum(v0, v1), v2)
     hi = np.maximum(np.maximum(v0, v1), v2)
-
-    def subtree_box(ref):
-        if ref < 0:
-            x = ~int(ref)
-            a, c = x >> 3, (x & 7) + 1
-            return lo[a:a + c].min(0), hi[a:a + c].max(0)
-        return boxes[ref]
-
-    boxes = {}
-    order = []
+    boxes, order, kids = {}, [], {}
     stack = [(0, 1)]
     max_depth = 0
     while stack:
         i, dep = stack.pop()
         order.append(i)
         max_depth = max(max_depth, dep)
-        nch = int(u[i, 3] >> 24)
-        assert 1 <= nch <= 4
-        for k in range(nch):
-            c = int(nodes[i, 4 + k])
-            if c >= 0:
-                stack.append((c, dep + 1))
+        kids[i] = _node_children(u, i)
+        assert kids[i]
+        for c in kids[i]:
+            if c[1] == "inner":
+                assert c[2] > i  # breadth-first: children after their parent
+                stack.append((c[2], dep + 1))
             else:
-                x = ~c
-                first, cnt = x >> 3, (x & 7) + 1
-                assert cnt <= 8
-                seen[first:first + cnt] += 1
+                seen[c[2]:c[2] + c[3]] += 1
     for i in reversed(order):  # children before parents
-        nch = int(u[i, 3] >> 24)
         e = [np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)) for a in range(3)]
+        assert all(-32 <= x <= 31 for x in e)
         blo = np.full(3, np.inf, np.float32)
         bhi = np.full(3, -np.inf, np.float32)
-        for k in range(nch):
-            clo, chi = subtree_box(int(nodes[i, 4 + k]))
+        used = {c[0] for c in kids[i]}
+        for sl in range(8):
+            qb = [(u[i, 8 + 4 * a + (sl >> 2)] >> (8 * (sl & 3))) & 255 for a in range(3)]
+            qt = [(u[i, 10 + 4 * a + (sl >> 2)] >> (8 * (sl & 3))) & 255 for a in range(3)]
+            if sl not in used:
+                assert qb == [255] * 3 and qt == [0] * 3
+        for c in kids[i]:
+            sl = c[0]
+            if c[1] == "inner":
+                clo, chi = boxes[c[2]]
+            else:
+                clo, chi = lo[c[2]:c[2] + c[3]].min(0), hi[c[2]:c[2] + c[3]].max(0)
             for a in range(3):
-                qlo = (u[i, 8 + 2 * a] >> (8 * k)) & 255
-                qhi = (u[i, 9 + 2 * a] >> (8 * k)) & 255
+                qlo = (u[i, 8 + 4 * a + (sl >> 2)] >> (8 * (sl & 3))) & 255
+                qhi = (u[i, 10 + 4 * a + (sl >> 2)] >> (8 * (sl & 3))) & 255
                 assert _decode(f[i, a], e[a], qlo) <= clo[a] and _decode(f[i, a], e[a], qhi) >= chi[a]
             blo, bhi = np.minimum(blo, clo), np.maximum(bhi, chi)
         boxes[i] = (blo, bhi)
-    assert (seen == 1).all() or ((seen >= 1).all() and n_tris == 1)
+    assert (seen == 1).all()
     assert max_depth <= 40 and max_depth == bvh_depth
-    _check_device_nodes(nodes, n_tris)
-
-
-def _check_device_nodes(nodes, n_tris):
-    """The builder's layout (mtx.h) and the 48-B device form decoded here in
-    numpy (bvh_build.cpp mtx_bvh_device_nodes; device_common.h wide_dref)
-    give every child reference of the 64-B node."""
-    import ctypes as C
-
-    from mtx import _lib
-
-    u = nodes.view(np.uint32)
-    for i in range(len(nodes)):
-        nch = int(u[i, 3] >> 24)
-        refs = [int(nodes[i, 4 + k]) for k in range(nch)]
-        n_in = sum(r >= 0 for r in refs)
-        assert all(r >= 0 for r in refs[:n_in]) and all(r < 0 for r in refs[n_in:])  # inner first
-        assert refs[:n_in] == list(range(refs[0], refs[0] + n_in)) if n_in else True
-        first = [(~r) >> 3 for r in refs[n_in:]]
-        cnt = [((~r) & 7) + 1 for r in refs[n_in:]]
-        assert all(first[j + 1] == first[j] + cnt[j] for j in range(len(first) - 1))
-        assert all(-32 <= np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)) <= 31 for a in range(3))
-    L = _lib.lib()
-    out = np.zeros((len(nodes), 12), np.int32)
-    assert L.mtx_bvh_device_nodes(np.ascontiguousarray(nodes).ctypes.data, len(nodes), n_tris, out.ctypes.data) == 0
-    w = out.view(np.uint32)
-    assert np.array_equal(out[:, 0:3], nodes[:, 0:3]) and np.array_equal(out[:, 6:12], nodes[:, 8:14])
-    ends = (w[:, 3] >> 20) | ((w[:, 4] >> 24) << 12) | ((w[:, 5] >> 24) << 20)
-    nb, tb = w[:, 4] & 0xFFFFFF, w[:, 5] & 0xFFFFFF
-    for i in range(len(nodes)):
-        nch = int((w[i, 3] >> 18) & 3) + 1
-        assert nch == int(u[i, 3] >> 24)
-        for a in range(3):
-            e6 = int((w[i, 3] >> (6 * a)) & 63)
-            assert (e6 - 64 if e6 >= 32 else e6) == int(np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)))
-        for k in range(nch):
-            e1 = int(ends[i] >> (6 * k)) & 63
-            e0 = int((int(ends[i]) << 6) >> (6 * k)) & 63
-            ref = int(nb[i]) + k if e1 == 0 else ~(((int(tb[i]) + e0) << 3) | (e1 - e0 - 1))
-            assert ref == int(nodes[i, 4 + k]), (i, k)
-    bad = nodes.copy()
-    bad[0, 4], bad[0, 5] = bad[0, 5], bad[0, 4]  # slot order broken
-    if int(u[0, 3] >> 24) >= 2 and bad[0, 4] != nodes[0, 4]:
-        assert L.mtx_bvh_device_nodes(bad.ctypes.data, len(bad), n_tris, out.ctypes.data) != 0
+    assert len(order) == len(nodes)
 
 
 def test_bvh_closest_hit_equals_brute_force(small_scene, oracle):
@@ -213,19 +189,19 @@ def _tiny_mesh(kind):
     return v, np.arange(3 * n, dtype=np.uint32).reshape(n, 3)
 
 
-@pytest.mark.parametrize("collapse", ["0", "1"])
+@pytest.mark.parametrize("cnode", ["1", "4"])
 @pytest.mark.parametrize("kind", ["one", "two", "nine", "identical", "planar", "random"])
-def test_bvh_build_small_and_degenerate_meshes(kind, collapse, monkeypatch):
-    """Greedy (MTX_BVH_COLLAPSE=0) and dynamic-programming collapses keep the
-    node invariants on tiny, coplanar and coincident-triangle meshes."""
+def test_bvh_build_small_and_degenerate_meshes(kind, cnode, monkeypatch):
+    """The 8-wide collapse keeps the node invariants on tiny, coplanar and
+    coincident-triangle meshes (two collapse node costs: other trees)."""
     import ctypes as C
 
     from mtx import _lib
 
-    monkeypatch.setenv("MTX_BVH_COLLAPSE", collapse)
+    monkeypatch.setenv("MTX_BVH_CNODE", cnode)
     v, idx = _tiny_mesh(kind)
     n = len(idx)
-    nodes = np.zeros((2 * n + 2) * 16, np.int32)
+    nodes = np.zeros((n + 1) * 20, np.int32)
     geom = np.zeros(12 * n, np.float32)
     perm = np.zeros(n, np.uint32)
     nn, dep = C.c_uint32(), C.c_uint32()
@@ -234,4 +210,4 @@ def test_bvh_build_small_and_degenerate_meshes(kind, collapse, monkeypatch):
                          C.byref(nn), geom.ctypes.data, perm.ctypes.data, C.byref(dep))
     assert rc == 0, L.mtx_last_error()
     assert sorted(perm.tolist()) == list(range(n))
-    _check_bvh(nodes[: 16 * nn.value], geom, n, dep.value)
+    _check_bvh(nodes[: 20 * nn.value], geom, n, dep.value)
