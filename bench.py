@@ -7,9 +7,11 @@ the job's work is the same at every N). Rank r of N traces the global sample
 range [r*256/N, (r+1)*256/N) of every pixel with global-lane seeding
 (path.py:156-161: lane = pixel*spp + sample), so the N=1 and N>1 films hold
 the same paths; the per-rank films are combined on rank 0 over RCCL by an
-all_to_all of film slices, a rank-order sum of each slice on its rank and a
-gather of the summed slices (deterministic, the same bits as gathering the
-films and summing them in rank order). Inputs (scene, BVH) are resident in
+all_to_all of film slices, a pairwise rank-tree sum of each slice on its rank
+and a gather of the summed slices. A film is the fixed binary tree of 8
+partial-slot films (32 samples each at spp 256), a rank at N = 2 / 4 / 8
+renders whole slots and the rank tree is the top of the same tree, so the
+combined film equals the N=1 film bit for bit. Inputs (scene, BVH) are resident in
 HBM before the timed region; the film stays in HBM and only the combine
 crosses GPUs. The timed region includes it.
 

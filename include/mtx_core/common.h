@@ -95,4 +95,24 @@ MTX_HD float luminance(V3 c) {
   return fmaf(c.z, 0.072169f, fmaf(c.y, 0.715160f, c.x * 0.212671f));
 }
 
+// ---- film partial slots (GPU-count-invariant films, DESIGN.md "Film") ----
+// A pixel's T = spp_total samples fall into 8 slots: slot k holds the global
+// sample indices [floor(k T / 8), floor((k + 1) T / 8)) (empty when T < 8
+// leaves it none). The film is the fixed binary tree of the 8 slot films, so
+// ranks that each render whole slots and are combined by the top of the same
+// tree give the one-device film bit for bit.
+struct V4 {
+  float x, y, z, w;
+};
+MTX_HD V4 add4(V4 a, V4 b) { return V4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w}; }
+MTX_HD uint32_t film_slot_end(uint32_t k, uint32_t T) { return (uint32_t)(((uint64_t)(k + 1) * T) >> 3); }
+MTX_HD uint32_t film_slot(uint32_t g, uint32_t T) {
+  uint32_t k = 0;
+  while (k < 7 && film_slot_end(k, T) <= g) ++k;
+  return k;
+}
+MTX_HD V4 film_tree8(const V4 s[8]) {
+  return add4(add4(add4(s[0], s[1]), add4(s[2], s[3])), add4(add4(s[4], s[5]), add4(s[6], s[7])));
+}
+
 }  // namespace mtx

@@ -1034,7 +1034,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     }
     mtxd::launch_restir_final(c->scene, b, p, r, st);
     mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, st);
-    mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, st);
+    mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, 1, st);
   }
   HIP_TRY(hipGetLastError());
   if (only_a) {
@@ -1098,7 +1098,10 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   if (two && (rc = ensure_wavefront2(c, cap, std::max<uint32_t>(a->max_depth, 1)))) return rc;
   if ((nrc_cache || nerad_render) && (rc = ensure_cache(c, cap))) return rc;
   if (two && nrc_cache && (rc = ensure_cache2(c, cap))) return rc;
-  if ((rc = dalloc(c->contrib, 9ull * 16 * band_px))) return rc;
+  // sample-sharded film renders: 8 partial slots (GPU-count-invariant films,
+  // DESIGN.md "Film"); PSSMLT splats and ReSTIR frames: one
+  const uint32_t film_slots = (mlt || a->integrator == MTX_INT_RESTIR_GI) ? 1u : 8u;
+  if ((rc = dalloc(c->contrib, 9ull * 16 * band_px * film_slots))) return rc;
   const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
   float4 *film_dev = (float4 *)film_rgbw;
   if (!film_on_device) {
@@ -1157,6 +1160,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.n_px = std::min(px_per_chunk, a->y1 * W - px0);
     p.band_y0 = a->y0;
     p.band_px = (a->y1 - a->y0) * W;
+    p.film_slots = film_slots;
     p.n_paths = p.n_px * a->spp;
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;
@@ -1198,7 +1202,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     HIP_TRY(hipEventRecord(c->w2.done, c->w2.stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->w2.done, 0));
   }
-  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, c->stream);
+  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, film_slots, c->stream);
   tm.end(3, e_all);
   HIP_TRY(hipGetLastError());
   if (!film_on_device)

@@ -1113,6 +1113,47 @@ __device__ __forceinline__ void film_accumulate(float4 acc[9], int x, int y, flo
   }
 }
 
+// Partial film slots (mtx_core/common.h film_slot): with p.film_slots == 8
+// a lane moves on to the next slot's contribution planes whenever its sample
+// index passes a slot end (the same for every lane of the launch: no
+// divergence) and writes all 8 slots (zeros for slots without samples);
+// otherwise one slot. contrib: [slot][9][band_px].
+struct FilmSlots {
+  uint32_t cur, end, T;
+  bool eight;
+  __device__ __forceinline__ void init(const ChunkParams &p) {
+    eight = p.film_slots == 8;
+    T = p.spp_total;
+    cur = 0;
+    end = eight ? film_slot_end(0, T) : 0xffffffffu;
+  }
+  __device__ __forceinline__ void flush(float4 acc[9], float4 *contrib, const ChunkParams &p, size_t o) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      contrib[((size_t)cur * 9 + k) * p.band_px + o] = acc[k];
+      acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    ++cur;
+    end = cur < 7 ? film_slot_end(cur, T) : 0xffffffffu;
+  }
+  // before accumulating global sample g
+  __device__ __forceinline__ void advance(uint32_t g, float4 acc[9], float4 *contrib, const ChunkParams &p, size_t o,
+                                          bool write) {
+    while (g >= end) {
+      if (write) {
+        flush(acc, contrib, p, o);
+      } else {
+        ++cur;
+        end = cur < 7 ? film_slot_end(cur, T) : 0xffffffffu;
+      }
+    }
+  }
+  __device__ __forceinline__ void finish(float4 acc[9], float4 *contrib, const ChunkParams &p, size_t o) {
+    const uint32_t n = eight ? 8u : 1u;
+    while (cur < n) flush(acc, contrib, p, o);
+  }
+};
+
 __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkParams p, float4 *contrib) {
   constexpr int S = kFilmStage;
   __shared__ float sv[5][64][S + 1];  // L.xyz, pos.xy
@@ -1120,6 +1161,10 @@ __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkPara
   const uint32_t pix = p.px0 + q;
   const int y = (int)(pix / p.width), x = (int)(pix - (uint32_t)y * p.width);
   const bool mask_valid = p.integrator == MTX_INT_PATH_MIS;
+  const bool live = q < p.n_px;
+  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: [slot][9][band_px]
+  FilmSlots fs;
+  fs.init(p);
   float4 acc[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1141,16 +1186,16 @@ __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkPara
       }
     }
     __syncthreads();
-    if (q < p.n_px)
-      for (uint32_t sm = 0; sm < ns; ++sm)
+    for (uint32_t sm = 0; sm < ns; ++sm) {
+      fs.advance(p.sample_offset + s0 + sm, acc, contrib, p, o, live);
+      if (live)
         film_accumulate(acc, x, y, make_float2(sv[3][lane][sm], sv[4][lane][sm]),
                         V3{sv[0][lane][sm], sv[1][lane][sm], sv[2][lane][sm]});
+    }
     __syncthreads();
   }
-  if (q >= p.n_px) return;
-  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: 9 planes of band_px
-#pragma unroll
-  for (int k = 0; k < 9; ++k) contrib[(size_t)k * p.band_px + o] = acc[k];
+  if (!live) return;
+  fs.finish(acc, contrib, p, o);
 }
 
 __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
@@ -1158,53 +1203,49 @@ __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
   if (q >= p.n_px) return;
   const uint32_t pix = p.px0 + q;
   const int y = (int)(pix / p.width), x = (int)(pix - (uint32_t)y * p.width);
+  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: [slot][9][band_px]
+  FilmSlots fs;
+  fs.init(p);
   float4 acc[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
+    fs.advance(p.sample_offset + sidx, acc, contrib, p, o, true);
     const uint32_t path = p.sample_major ? sidx * p.n_px + q : q * p.spp + sidx;
-    const float2 ps = b.pos[path];
-    const V3 L = final_L(b, p, path);
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      const float wy = fmaxf(0.f, 1.f - fabsf(ps.y - ((float)(y + dy - 1) + 0.5f)));
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const float wx = fmaxf(0.f, 1.f - fabsf(ps.x - ((float)(x + dx - 1) + 0.5f)));
-        const float w = wx * wy;
-        float4 &c = acc[dy * 3 + dx];
-        c.x = c.x + L.x * w;
-        c.y = c.y + L.y * w;
-        c.z = c.z + L.z * w;
-        c.w = c.w + w;
-      }
-    }
+    film_accumulate(acc, x, y, b.pos[path], final_L(b, p, path));
   }
-  const size_t o = (size_t)(pix - p.band_y0 * p.width);  // contrib: 9 planes of band_px
-#pragma unroll
-  for (int k = 0; k < 9; ++k) contrib[(size_t)k * p.band_px + o] = acc[k];
+  fs.finish(acc, contrib, p, o);
 }
 
-__global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, uint32_t y0, uint32_t y1) {
+// Stage 2: per film pixel and slot the 9 neighbours in (dy, dx) order, then
+// the slots' fixed binary tree (film_tree8) when nslots == 8.
+__global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, uint32_t y0, uint32_t y1,
+                              uint32_t nslots) {
   const uint32_t FW = W + 2, FH = (y1 - y0) + 2;
-  const size_t P = (size_t)(y1 - y0) * W;  // contrib: 9 planes of the band's pixels
+  const size_t P = (size_t)(y1 - y0) * W;  // contrib: [slot][9][band pixels]
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= FW * FH) return;
   const int px = (int)(q % FW) - 1, py = (int)(y0 + q / FW) - 1;
-  float r = 0.f, g = 0.f, bl = 0.f, w = 0.f;
+  V4 sl[8];
+  const uint32_t ns = nslots == 8 ? 8u : 1u;
+  for (uint32_t k = 0; k < ns; ++k) {
+    float r = 0.f, g = 0.f, bl = 0.f, w = 0.f;
 #pragma unroll
-  for (int dy = 0; dy < 3; ++dy)
+    for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
-      const int sxp = px - dx + 1, syp = py - dy + 1;
-      if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
-      const float4 c = contrib[(size_t)(dy * 3 + dx) * P + (size_t)(syp - (int)y0) * W + sxp];
-      r = r + c.x;
-      g = g + c.y;
-      bl = bl + c.z;
-      w = w + c.w;
-    }
-  film[q] = make_float4(r, g, bl, w);
+      for (int dx = 0; dx < 3; ++dx) {
+        const int sxp = px - dx + 1, syp = py - dy + 1;
+        if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
+        const float4 c = contrib[((size_t)k * 9 + (size_t)(dy * 3 + dx)) * P + (size_t)(syp - (int)y0) * W + sxp];
+        r = r + c.x;
+        g = g + c.y;
+        bl = bl + c.z;
+        w = w + c.w;
+      }
+    sl[k] = V4{r, g, bl, w};
+  }
+  const V4 f = ns == 8 ? film_tree8(sl) : sl[0];
+  film[q] = make_float4(f.x, f.y, f.z, f.w);
 }
 
 __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *valid_out) {
@@ -1506,9 +1547,9 @@ void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib
     hipLaunchKernelGGL(k_film_src_staged, dim3(blocks_for(p.n_px, 64)), dim3(64), 0, st, b, p, contrib);
 }
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
-                        hipStream_t st) {
+                        uint32_t nslots, hipStream_t st) {
   const uint64_t n = (uint64_t)(width + 2) * (y1 - y0 + 2);
-  hipLaunchKernelGGL(k_film_gather, dim3(blocks_for(n, 256)), dim3(256), 0, st, contrib, film, width, y0, y1);
+  hipLaunchKernelGGL(k_film_gather, dim3(blocks_for(n, 256)), dim3(256), 0, st, contrib, film, width, y0, y1, nslots);
 }
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st) {
   hipLaunchKernelGGL(k_collect, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, L_out, valid_out);

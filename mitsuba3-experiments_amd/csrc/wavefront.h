@@ -173,7 +173,8 @@ struct ChunkParams {
   uint32_t width, height;
   uint32_t px0, n_px;   // first film pixel (y*W+x) of the chunk and pixel count
   uint32_t band_y0;     // first row of the rendered band (film/contrib origin)
-  uint32_t band_px;     // pixels of the band (contrib: 9 planes of band_px float4)
+  uint32_t band_px;     // pixels of the band (contrib: film_slots x 9 planes of band_px float4)
+  uint32_t film_slots;  // 8: partial-slot film (mtx_core/common.h film_slot); 0 / 1: one slot
   uint32_t n_paths;
   float nrc_c;
   uint32_t stats;
@@ -200,7 +201,7 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
                   hipStream_t st);
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
-                        hipStream_t st);
+                        uint32_t nslots, hipStream_t st);
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);

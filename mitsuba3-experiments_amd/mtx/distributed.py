@@ -4,8 +4,9 @@ The reference has no distributed code; the path shards
 naturally (§8e):
   * sample shards (strong scaling, bench.py): rank r traces the global
     sample range [r*spp/N, (r+1)*spp/N) of every pixel of one fixed-spp
-    render; films are gathered to rank 0 and summed in rank order
-    (deterministic).
+    render; films are combined on rank 0 by a pairwise tree over the ranks
+    (deterministic; at N = 2, 4, 8 the top of the film's 8-slot tree, so the
+    combined film equals the one-GPU film bit for bit).
   * row bands (strong scaling): rank r traces film rows [y0_r, y1_r); each
     band carries its 1-row tent halo above and below, stitched on rank 0 by
     adding the overlapping halo rows in rank order.
@@ -71,11 +72,29 @@ def _comm(t, group=None):
     return t.cpu() if (t.is_cuda and _host_staged(group)) else t
 
 
+def _tree_sum(parts):
+    """Sum of `parts` (rank order) by adjacent pairs, level by level (an odd
+    last part moves up unchanged): for 2, 4 and 8 ranks the top of the film's
+    8-slot tree (mtx_core/common.h film_tree8), so sample-range shards of
+    whole slots combine to the one-device film bit for bit."""
+    import torch
+
+    level = list(parts)
+    if len(level) == 1:
+        return torch.zeros_like(level[0]) + level[0]
+    while len(level) > 1:
+        nxt = [level[i] + level[i + 1] for i in range(0, len(level) - 1, 2)]
+        if len(level) % 2:
+            nxt.append(level[-1])
+        level = nxt
+    return level[0]
+
+
 def gather_sum(film, group=None):
     """Sum of every rank's film in rank order, returned on rank 0 (None elsewhere).
     `film` is a torch tensor (device for nccl, cpu for gloo) or numpy array.
     One gather to rank 0 (point-to-point receives over xGMI with RCCL), then
-    a fixed rank-order sum: deterministic."""
+    a fixed pairwise tree over the ranks (_tree_sum): deterministic.""" 
     import torch
     import torch.distributed as dist
 
@@ -87,10 +106,7 @@ def gather_sum(film, group=None):
     dist.gather(c, parts, dst=0, group=group)
     if rank != 0:
         return None
-    total = torch.zeros_like(c)
-    for p in parts:
-        total.add_(p)
-    return total.to(t.device)
+    return _tree_sum(parts).to(t.device)
 
 
 _ALL_TO_ALL_BACKENDS = ("nccl", "gloo")  # backends with all_to_all_single (RCCL, gloo)
@@ -98,8 +114,8 @@ _ALL_TO_ALL_BACKENDS = ("nccl", "gloo")  # backends with all_to_all_single (RCCL
 
 def reduce_sum(film, group=None):
     """`gather_sum` with the sum spread over the ranks: an all_to_all hands
-    every rank one 1/N slice of every film, each rank sums its slice in rank
-    order, and rank 0 gathers the N summed slices (None on other ranks).
+    every rank one 1/N slice of every film, each rank sums its slice by the
+    same rank tree, and rank 0 gathers the N summed slices (None on other ranks).
     Bit-identical to `gather_sum` (the same additions, elementwise, in the
     same order); rank 0 receives (N-1)/N of one film instead of N-1 films
     and adds 1/N of them, and every xGMI link carries 2/N of a film."""
@@ -122,9 +138,7 @@ def reduce_sum(film, group=None):
     send = flat if chunk * world == n else torch.cat([flat, flat.new_zeros(chunk * world - n)])
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, group=group)
-    part = torch.zeros(chunk, dtype=c.dtype, device=c.device)
-    for r in range(world):
-        part.add_(recv[r * chunk:(r + 1) * chunk])
+    part = _tree_sum([recv[r * chunk:(r + 1) * chunk] for r in range(world)])
     parts = [torch.empty_like(part) for _ in range(world)] if rank == 0 else None
     dist.gather(part, parts, dst=0, group=group)
     if rank != 0:

@@ -93,10 +93,16 @@ def render_samples_nrc_cache(scene, args):
     return L, pos, q
 
 
-def film(width, y0, y1, spp, L, pos):
+def film(width, y0, y1, spp, L, pos, spp_total=None, sample_offset=0, nslots=8):
+    """The film of per-sample radiance in (pixel, sample) order: 8 partial
+    slots combined by a fixed tree (the mtx_render film, orc_film_slots), or
+    one slot (nslots=1: the PSSMLT / ReSTIR film order)."""
     f = np.zeros((y1 - y0 + 2, width + 2, 4), np.float32)
-    lib().orc_film(width, y0, y1, spp, np.ascontiguousarray(L).ctypes.data, np.ascontiguousarray(pos).ctypes.data,
-                   f.ctypes.data)
+    L_ = lib()
+    L_.orc_film_slots.argtypes = [C.c_uint32] * 7 + [C.c_void_p] * 3
+    L_.orc_film_slots(width, y0, y1, spp, spp if spp_total is None else spp_total, sample_offset, nslots,
+                      np.ascontiguousarray(L, np.float32).ctypes.data, np.ascontiguousarray(pos, np.float32).ctypes.data,
+                      f.ctypes.data)
     return f
 
 

@@ -684,16 +684,26 @@ int orc_render_samples(const mtx_scene_desc *d, const mtx_render_args *a, float 
 }
 
 // Film accumulation in the fixed order documented in DESIGN.md ("Film"):
-// stage 1 sums each source pixel's samples (s ascending) into its 3x3 tent
-// footprint; stage 2 gathers the 9 neighbours (dy, dx ascending).
-int orc_film(uint32_t W, uint32_t y0, uint32_t y1, uint32_t spp, const float *L, const float *pos, float *film) {
+// the samples of a pixel fall into `nslots` partial slots by their global
+// sample index g (film_slot: slot k holds g in [floor(k T / 8), floor((k+1)
+// T / 8)) of spp_total = T samples when nslots = 8; one slot otherwise);
+// per slot, stage 1 sums each source pixel's samples (g ascending) into its
+// 3x3 tent footprint and stage 2 gathers the 9 neighbours (dy, dx
+// ascending); the film is the fixed binary tree of the slot films
+// (mtx_core/common.h film_tree8). A sample-range shard of the same render
+// holds whole slots, so ranks combined by the same tree reproduce the
+// one-device film bit for bit (N = 1, 2, 4, 8).
+int orc_film_slots(uint32_t W, uint32_t y0, uint32_t y1, uint32_t spp, uint32_t spp_total, uint32_t sample_offset,
+                   uint32_t nslots, const float *L, const float *pos, float *film) {
   const uint32_t rows = y1 - y0;
-  std::vector<float> acc((size_t)rows * W * 36, 0.f);
+  const uint32_t NS = nslots == 8 ? 8u : 1u;
+  std::vector<float> acc((size_t)NS * rows * W * 36, 0.f);
 #pragma omp parallel for schedule(static)
   for (int64_t p = 0; p < (int64_t)rows * W; ++p) {
     int x = (int)(p % W), y = (int)(y0 + p / W);
-    float *a = &acc[36 * (size_t)p];
     for (uint32_t k = 0; k < spp; ++k) {
+      const uint32_t slot = NS == 8 ? film_slot(sample_offset + k, spp_total) : 0u;
+      float *a = &acc[36 * ((size_t)slot * rows * W + (size_t)p)];
       uint64_t o = (uint64_t)p * spp + k;
       float sx = pos[2 * o], sy = pos[2 * o + 1];
       float lr = L[3 * o], lg = L[3 * o + 1], lb = L[3 * o + 2];
@@ -715,23 +725,32 @@ int orc_film(uint32_t W, uint32_t y0, uint32_t y1, uint32_t spp, const float *L,
 #pragma omp parallel for schedule(static)
   for (int64_t q = 0; q < (int64_t)FW * FH; ++q) {
     int px = (int)(q % FW) - 1, py = (int)(y0 + q / FW) - 1;
-    float r = 0.f, g = 0.f, b = 0.f, w = 0.f;
-    for (int dy = 0; dy < 3; ++dy)
-      for (int dx = 0; dx < 3; ++dx) {
-        int sxp = px - dx + 1, syp = py - dy + 1;
-        if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
-        const float *c = &acc[36 * ((size_t)(syp - y0) * W + sxp) + 4 * (dy * 3 + dx)];
-        r = r + c[0];
-        g = g + c[1];
-        b = b + c[2];
-        w = w + c[3];
-      }
-    film[4 * q] = r;
-    film[4 * q + 1] = g;
-    film[4 * q + 2] = b;
-    film[4 * q + 3] = w;
+    V4 sl[8];
+    for (uint32_t k = 0; k < NS; ++k) {
+      float r = 0.f, g = 0.f, b = 0.f, w = 0.f;
+      for (int dy = 0; dy < 3; ++dy)
+        for (int dx = 0; dx < 3; ++dx) {
+          int sxp = px - dx + 1, syp = py - dy + 1;
+          if (sxp < 0 || sxp >= (int)W || syp < (int)y0 || syp >= (int)y1) continue;
+          const float *c = &acc[36 * ((size_t)k * rows * W + (size_t)(syp - y0) * W + sxp) + 4 * (dy * 3 + dx)];
+          r = r + c[0];
+          g = g + c[1];
+          b = b + c[2];
+          w = w + c[3];
+        }
+      sl[k] = V4{r, g, b, w};
+    }
+    const V4 f = NS == 8 ? film_tree8(sl) : sl[0];
+    film[4 * q] = f.x;
+    film[4 * q + 1] = f.y;
+    film[4 * q + 2] = f.z;
+    film[4 * q + 3] = f.w;
   }
   return 0;
+}
+
+int orc_film(uint32_t W, uint32_t y0, uint32_t y1, uint32_t spp, const float *L, const float *pos, float *film) {
+  return orc_film_slots(W, y0, y1, spp, spp, 0, 1, L, pos, film);
 }
 
 int orc_render(const mtx_scene_desc *d, const mtx_render_args *a, float *film) {
@@ -739,7 +758,7 @@ int orc_render(const mtx_scene_desc *d, const mtx_render_args *a, float *film) {
   const uint64_t ns = (uint64_t)(a->y1 - a->y0) * W * a->spp;
   std::vector<float> L(3 * ns), pos(2 * ns);
   orc_render_samples(d, a, L.data(), pos.data());
-  return orc_film(W, a->y0, a->y1, a->spp, L.data(), pos.data(), film);
+  return orc_film_slots(W, a->y0, a->y1, a->spp, a->spp_total, a->sample_offset, 8, L.data(), pos.data(), film);
 }
 
 

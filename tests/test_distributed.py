@@ -53,6 +53,27 @@ def _worker(rank, world, port, mode, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [4, 3])
+def test_sample_shards_combine_to_the_one_rank_film(tmp_path, oracle, world):
+    """GPU-count invariance: 4 ranks of 2 samples (2 whole
+    slots each) combine to the one-rank spp-8 film bit for bit; 3 ranks (the
+    shards split slots) equal it up to summation order (rtol 2e-6)."""
+    from mtx import load_dict, scene
+
+    out = os.path.join(tmp_path, "full.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), "samples", out), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    sc = scene.bedroom(width=48, height=27, scale=0.02, tex_res=32)
+    integ = load_dict({"type": "path_test"})
+    ref = oracle.render(sc, integ.render_args(sc, 4, 8, 0, sc.height, 8, 0))
+    if world == 4:
+        assert np.array_equal(got, ref)
+    else:
+        np.testing.assert_allclose(got, ref, rtol=2e-6, atol=1e-6)
+    assert ref[..., 3].sum() > 0
+
+
 @pytest.mark.parametrize("mode", ["samples", "rows", "chains"])
 def test_two_rank_combine(tmp_path, oracle, mode):
     from mtx import load_dict, scene
@@ -75,9 +96,12 @@ def test_two_rank_combine(tmp_path, oracle, mode):
         np.testing.assert_allclose(got, ref, rtol=2e-6, atol=1e-6)
         return
     if mode == "samples":
-        parts = [oracle.render(sc, integ.render_args(sc, 4, 4, 0, sc.height, 8, 4 * r)) for r in range(2)]
-        assert np.array_equal(got, parts[0] + parts[1])  # rank-order sum, bit-exact
+        # the film's 8 partial slots (one sample each at spp 8): each rank
+        # renders 4 whole slots and the rank sum is the top of the slot tree,
+        # so the combined film IS the one-rank film, bit for bit
         ref = oracle.render(sc, integ.render_args(sc, 4, 8, 0, sc.height, 8, 0))
+        assert np.array_equal(got, ref)
+        return
     else:
         ref = oracle.render(sc, integ.render_args(sc, 4, 4, 0, sc.height))
     np.testing.assert_allclose(got, ref, rtol=2e-6, atol=1e-6)
@@ -271,10 +295,10 @@ def _reduce_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_reduce_sum_matches_gather_sum(tmp_path, world):
-    """The sliced reduction (all_to_all + per-slice rank-order sum + gather)
-    is bit-identical to the gather-then-sum on rank 0, incl. films whose
+    """The sliced reduction (all_to_all + per-slice rank-tree sum + gather)
+    is bit-identical to the gather-then-tree-sum on rank 0, incl. films whose
     size is not a multiple of the world size."""
     out = os.path.join(tmp_path, "ok.npy")
     mp.start_processes(_reduce_worker, args=(world, _free_port(), out), nprocs=world, join=True, start_method="spawn")

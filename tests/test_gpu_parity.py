@@ -141,15 +141,19 @@ def test_two_stream_chunks_bit_exact(small_scene, oracle, name):
 
 
 def test_rank_shards_and_row_bands(small_scene, oracle):
-    """Sample-range shards (weak-scaling bench) and row bands (strong) combine
-    to the single-call film up to float summation order (rtol 2e-6)."""
+    """Sample-range shards of whole film slots (2 and 4 ranks at spp 8)
+    combine by the rank tree to the single-call film bit for bit (8-slot film,
+    mtx_core/common.h film_tree8); row bands up to float summation order of
+    the halo rows (rtol 2e-6)."""
     from mtx import load_dict
 
     integ = load_dict({"type": "path_test"})
     H, spp = small_scene.height, 4
     full = integ.render_film(small_scene, seed=9, spp=2 * spp, spp_total=2 * spp)
     parts = [integ.render_film(small_scene, seed=9, spp=spp, spp_total=2 * spp, sample_offset=r * spp) for r in range(2)]
-    np.testing.assert_allclose(parts[0] + parts[1], full, rtol=2e-6, atol=1e-6)
+    np.testing.assert_array_equal(parts[0] + parts[1], full)
+    q = [integ.render_film(small_scene, seed=9, spp=2, spp_total=8, sample_offset=2 * r) for r in range(4)]
+    np.testing.assert_array_equal((q[0] + q[1]) + (q[2] + q[3]), full)
     top = integ.render_film(small_scene, seed=9, spp=8, y0=0, y1=H // 2)
     bot = integ.render_film(small_scene, seed=9, spp=8, y0=H // 2, y1=H)
     stitched = np.zeros_like(full)
