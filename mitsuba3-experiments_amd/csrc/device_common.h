@@ -160,40 +160,48 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t *counte
 // LDS slots of one step are not overwritten while a slow wave still reads them.
 // The two counters are one 8-byte-aligned pair (c[0], c[1]): a single 64-bit
 // atomic reserves both (the low count never carries: it stays below 2^32).
+// Inside a block step's range of the second queue the entries with p1_hi
+// follow the others (NEE shadow rays: the rays of one emitter together, so
+// the any-hit waves that claim them walk one light's shadow frusta).
 template <int BLOCK>
-__device__ __forceinline__ void block_append2(bool p0, bool p1, uint32_t *c, uint32_t parity, uint32_t &s0,
-                                              uint32_t &s1) {
+__device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint32_t *c, uint32_t parity,
+                                              uint32_t &s0, uint32_t &s1) {
   constexpr int W = BLOCK / 64;
-  __shared__ uint32_t wcnt[2][2][W];
-  __shared__ uint32_t bbase[2][2];
+  __shared__ uint32_t wcnt[2][3][W];
+  __shared__ uint32_t bbase[2][3];
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+  const uint64_t m0 = __ballot(p0), ml = __ballot(p1 && !p1_hi), mh = __ballot(p1 && p1_hi);
   if (lane == 0) {
     wcnt[parity][0][wave] = (uint32_t)__popcll(m0);
-    wcnt[parity][1][wave] = (uint32_t)__popcll(m1);
+    wcnt[parity][1][wave] = (uint32_t)__popcll(ml);
+    wcnt[parity][2][wave] = (uint32_t)__popcll(mh);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t0 = 0, t1 = 0;
+    uint32_t t0 = 0, tl = 0, th = 0;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       t0 += wcnt[parity][0][w];
-      t1 += wcnt[parity][1][w];
+      tl += wcnt[parity][1][w];
+      th += wcnt[parity][2][w];
     }
     uint64_t base = 0;
-    if (t0 | t1)
-      base = atomicAdd(reinterpret_cast<unsigned long long *>(c), ((unsigned long long)t1 << 32) | t0);
+    if (t0 | tl | th)
+      base = atomicAdd(reinterpret_cast<unsigned long long *>(c), ((unsigned long long)(tl + th) << 32) | t0);
     bbase[parity][0] = (uint32_t)base;
     bbase[parity][1] = (uint32_t)(base >> 32);
+    bbase[parity][2] = (uint32_t)(base >> 32) + tl;
   }
   __syncthreads();
-  uint32_t o0 = bbase[parity][0], o1 = bbase[parity][1];
+  uint32_t o0 = bbase[parity][0], ol = bbase[parity][1], oh = bbase[parity][2];
   for (uint32_t w = 0; w < wave; ++w) {
     o0 += wcnt[parity][0][w];
-    o1 += wcnt[parity][1][w];
+    ol += wcnt[parity][1][w];
+    oh += wcnt[parity][2][w];
   }
   s0 = o0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-  s1 = o1 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+  s1 = p1_hi ? oh + __builtin_amdgcn_mbcnt_hi((uint32_t)(mh >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mh, 0u))
+             : ol + __builtin_amdgcn_mbcnt_hi((uint32_t)(ml >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ml, 0u));
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {

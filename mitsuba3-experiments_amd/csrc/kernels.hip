@@ -267,6 +267,7 @@ __device__ unsigned long long g_shade_stamps[kStampSegs + 2];
 struct ShadeIO {
   ShadowRec rec;
   bool emit;
+  bool em_hi;  // the shadow ray's emitter index is odd (block append: even emitters' rays first)
   bool query;  // NRC radiance-cache query at this hit (field.hip)
   float4 qp, qd, qt;
   float4 nro, nrd, nthr, nprev;  // the next ray and state: k_shade stores them at the path's append slot
@@ -298,6 +299,7 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   occ_noop = (fl & 14u) == 0u;
   io.emit = !(vis_noop && occ_noop);
   if (!io.emit) return;
+  io.em_hi = (ds.emitter & 1) != 0;
   const Ray sr = spawn_ray_to(si.p, si.n, ds.p);
   io.rec.o = make_float4(sr.o.x, sr.o.y, sr.o.z, sr.maxt);
   io.rec.d = make_float4(sr.d.x, sr.d.y, sr.d.z, 0.f);  // .w: the L index, set by k_shade after its append
@@ -960,6 +962,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     if (MTX_SHADE_PREFETCH && inext < count) path_n = ident ? inext : in_q[inext];
     ShadeIO io;
     io.emit = false;
+    io.em_hi = false;
     io.query = false;
 #if MTX_DIAG_STAMPS
     ++steps;
@@ -991,7 +994,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     stp = io.st;
 #endif
     uint32_t slot, sslot;
-    block_append2<kShadeBlock>(cont, io.emit, out_cnt, parity, slot, sslot);
+    block_append2<kShadeBlock>(cont, io.emit, io.emit && io.em_hi, out_cnt, parity, slot, sslot);
     if (cont) {
       out_q[slot] = path_c;
       b.ray_o[rp ^ 1u][slot] = io.nro;

@@ -201,7 +201,7 @@ def pssmlt(args, with_nee=False):
     cnt = cls({"iterations": min(it, 20)}).render_film(sc, seed=0, stats=True, counters=True, **shard)[1]
     chains = sc.width * sc.height * spp
     cpu = None
-    if rk.world == 1:
+    if rk.world == 1 and not args.no_cpu_baseline:
         # CPU: the oracle on whole film rows at 16 chains per pixel (the cost
         # per chain-iteration does not depend on the chain count), same
         # iterations, rows sized to the CPU budget
@@ -283,7 +283,7 @@ def restir(args):
     cnt = frame(W + args.frames, stats=True, counters=True)
     px = sc.width * sc.height
     cpu = None
-    if rk.world == 1:
+    if rk.world == 1 and not args.no_cpu_baseline:
         # CPU: the oracle's frame loop on the same 1920x1080 film (frame 0,
         # then as many frames as fit the CPU budget, at most 3)
         oracle.build()
@@ -342,7 +342,7 @@ def nrc(args):
     class A:  # cpu_baseline wants args.cpu_seconds only
         cpu_seconds = args.cpu_seconds
 
-    cpu = bench.cpu_baseline(sc, integ, A)
+    cpu = None if args.no_cpu_baseline else bench.cpu_baseline(sc, integ, A)
     _line("NRC Mpaths/sec on bedroom@1280x720 spp=4 (C5)", n / dt / 1e6, "Mpaths/s", reps, 1, dt * 1e3,
           {"workload": "nrc.py NRCIntegrator.sample: NEE+MIS segments, spread heuristic c=0.01, max_depth 10",
            "paths_per_step": n}, _trace_roofline(cnt, agg["trace_ms"] / reps, "step", args=args), cpu)
