@@ -97,9 +97,6 @@ MTX_HD V3 texture_eval(const BsdfData &d, int32_t tex, V2 uv) {
 
 MTX_HD V3 mat_color(const BsdfData &d, const mtx_material &m, V2 uv) {
   if (d.has_col) return d.col;
-#if defined(MTX_DEVICE_COMPILE) && defined(MTX_DIAG_NOTEX) && MTX_DIAG_NOTEX  // timing diagnostic only (wrong images)
-  return V3{m.rgb[0], m.rgb[1], m.rgb[2]};
-#endif
   if (m.tex >= 0) return texture_eval(d, m.tex, uv);
   return V3{m.rgb[0], m.rgb[1], m.rgb[2]};
 }
@@ -381,15 +378,7 @@ MTX_HD V3 twosided_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi
 }
 
 // BSDF::eval_pdf (value includes the cosine foreshortening, as upstream)
-// A/B knob (device only): MTX_BSDF_NOINLINE=1 keeps the two BSDF entry points
-// out of line (one copy of each material's code instead of one per call site).
-#if defined(MTX_DEVICE_COMPILE) && defined(MTX_BSDF_NOINLINE) && MTX_BSDF_NOINLINE
-#define MTX_BSDF_ENTRY __host__ __device__ __noinline__
-#else
-#define MTX_BSDF_ENTRY MTX_HD
-#endif
-
-MTX_BSDF_ENTRY void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
+MTX_HD void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, V3 wo, V3 *val, float *pdf) {
   twosided_eval_pdf(d, m, uv, wi, wo, val, pdf);
   if (m.flags & MTX_MF_MASK) {
     *val = *val * m.opacity;
@@ -398,7 +387,7 @@ MTX_BSDF_ENTRY void bsdf_eval_pdf(const BsdfData &d, const mtx_material &m, V2 u
 }
 
 // BSDF::sample -> (BSDFSample, weight = value/pdf)
-MTX_BSDF_ENTRY V3 bsdf_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
+MTX_HD V3 bsdf_sample(const BsdfData &d, const mtx_material &m, V2 uv, V3 wi, float u1, V2 u2, BSDFSample *bs) {
   // mask: nested lobe with probability `opacity`, else a Null pass-through.
   // The factors opacity / (1 - opacity) cancel in the weight and are not
   // included in bs.pdf (upstream mask.cpp).

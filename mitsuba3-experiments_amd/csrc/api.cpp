@@ -158,7 +158,6 @@ struct mtx_ctx {
   uint32_t xcd_claim = 1;
   uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
   DevBuf cq_keys, cq_perm, cq_ws;
-  uint32_t sample_major = 0;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
   double last_device_ms = 0.0;
@@ -211,7 +210,6 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS_MAX_LOG2")) c->streams_max_log2 = (uint32_t)std::max(16, std::min(31, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
-  if (const char *e = getenv("MTX_SAMPLE_MAJOR")) c->sample_major = atoi(e) != 0;
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
@@ -955,7 +953,6 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   p.band_px = (a->y1 - a->y0) * W;
   p.n_paths = nb;
   p.restir = 1;
-  p.sample_major = c->sample_major;
   p.stats = want_stats ? 1 : 0;
   if (want_stats) HIP_TRY(hipMemsetAsync(c->stats.p, 0, 64, c->stream));
   hipEvent_t e;
@@ -1164,8 +1161,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.n_paths = p.n_px * a->spp;
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;
-    p.sample_major = c->sample_major;
-    p.nrc_cache = nrc_cache ? 1u : 0u;
+      p.nrc_cache = nrc_cache ? 1u : 0u;
     // the film (and the cache apply) read an ending path's L only; PSSMLT's
     // chain kernels read its sampler state (mtx_sample_rays' k_collect and
     // ReSTIR's k_rs_collect build their own ChunkParams, which keep it)

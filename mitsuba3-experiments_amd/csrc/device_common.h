@@ -58,11 +58,7 @@ __device__ __forceinline__ SceneView make_view(const DevScene &s) {
 __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, float t, uint32_t prim, float u,
                                                              float v, V3 ray_d) {
   if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
-#ifdef MTX_DIAG_REC_MASK  // timing diagnostic only (wrong images): records of a few triangles
-  const float4 *r = s.shade_rec + 8 * (size_t)(prim & MTX_DIAG_REC_MASK);
-#else
   const float4 *r = s.shade_rec + 8 * (size_t)prim;
-#endif
   const float4 a = r[0], b = r[1], c = r[2];
   const uint32_t fl = __float_as_uint(c.w);
   const bool use_n = (fl & 1u) != 0, use_uv = (fl & 2u) != 0;

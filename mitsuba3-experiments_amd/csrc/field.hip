@@ -34,9 +34,6 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kFieldPad = 64;     // features per query (padded)
-#ifndef MTX_MLP_PREFETCH
-#define MTX_MLP_PREFETCH 0  // A/B: 1 = load the next tile's input at the top of the tile (180 VGPRs: slower)
-#endif
 constexpr float kLeakySlope = 0.01f;  // drjit.nn.LeakyReLU default
 
 // One thread per (query, level): the 8 corner gathers of a level are
@@ -133,9 +130,6 @@ __global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const u
   if (wave * 64 < n) load_in(wave, bin);
   for (uint32_t tile = wave; tile * 64 < n; tile += n_waves) {
     const uint32_t q0 = tile * 64;
-    half8 bnext[2][4];
-    // the next tile's features load while this tile's layers run
-    if (MTX_MLP_PREFETCH && (tile + n_waves) * 64 < n) load_in(tile + n_waves, bnext);
     f32x16 acc[2][2];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
@@ -193,14 +187,9 @@ __global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const u
         }
       }
     }
-    if (MTX_MLP_PREFETCH) {
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) bin[nt][ks] = bnext[nt][ks];
-    } else if ((tile + n_waves) * 64 < n) {
-      load_in(tile + n_waves, bin);
-    }
+    // (loading the next tile's features at the top of the tile instead took
+    // 180 VGPRs, 2 waves/SIMD: slower)
+    if ((tile + n_waves) * 64 < n) load_in(tile + n_waves, bin);
   }
 }
 

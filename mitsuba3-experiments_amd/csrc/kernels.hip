@@ -28,25 +28,18 @@
 
 using namespace mtx;
 
-// Tuning knob: minimum resident shade blocks per CU (caps VGPRs; 1 = none).
-#ifndef MTX_SHADE_PREFETCH
-#define MTX_SHADE_PREFETCH 1  // A/B: 0 = the next step's queue entry and hit load at the step's end
-#endif
-#ifndef MTX_SHADE_MIN_BLOCKS
-#define MTX_SHADE_MIN_BLOCKS 3
-#endif
+// Minimum resident shade blocks per CU (caps the shade kernels' VGPRs: 3
+// blocks of 256 threads = 3 waves/SIMD at <= 168 VGPRs).
+constexpr int kShadeMinBlocks = 3;
 
 namespace mtxd {
 
 // Closest-hit queries of bounce `bounce`: queue entries are path indices.
 // The hit record goes to the queue position k (not the path): the shade
 // kernel, which walks the same queue, then reads it coalesced and without
-// waiting for its queue entry (MTX_HIT_BY_PATH=1: the path-indexed form).
-#ifndef MTX_HIT_BY_PATH
-#define MTX_HIT_BY_PATH 0
-#endif
+// waiting for its queue entry.
 struct ClosestSrc {
-  using Payload = uint32_t;  // the queue position (the path with MTX_HIT_BY_PATH)
+  using Payload = uint32_t;  // the queue position
   WaveBuffers b;
   const uint32_t *queue;
   const float4 *ro, *rd;  // this bounce's ray planes, by queue position
@@ -54,7 +47,7 @@ struct ClosestSrc {
     const float4 o4 = ro[k], d4 = rd[k];
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
-    payload = MTX_HIT_BY_PATH ? queue[k] : k;
+    payload = k;
   }
   __device__ __forceinline__ void finish(uint32_t slot, bool, float t, uint32_t prim, float u, float v) const {
     b.hit[slot] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
@@ -62,19 +55,12 @@ struct ClosestSrc {
 };
 
 // 8 waves/SIMD for the trace kernels (their grid is sized for 8): left alone
-// the compiler takes 66 VGPRs for the any-hit kernel (7 waves); asked for 8 it
-// fits 55 without spills. Shadow 56.4 -> 55.6 ms per step (A/B, one box, 3
-// rounds). MTX_SHADOW_WAVES=0 builds the unconstrained form.
-#ifndef MTX_SHADOW_WAVES
-#define MTX_SHADOW_WAVES 8
-#endif
-#if MTX_SHADOW_WAVES
-#define MTX_SHADOW_ATTR __attribute__((amdgpu_waves_per_eu(MTX_SHADOW_WAVES)))
-#else
-#define MTX_SHADOW_ATTR
-#endif
+// the compiler took 66 VGPRs for the any-hit kernel (7 waves); asked for 8 it
+// fits without spills. Shadow 56.4 -> 55.6 ms per step (A/B, one box, 3
+// rounds, round 2).
+#define MTX_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 template <bool STATS>
-__global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
+__global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
@@ -97,18 +83,13 @@ __global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_closest(D
 // Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
 // contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
 // form).
-#ifndef MTX_SHADOW_CARRY
-#define MTX_SHADOW_CARRY 1  // A/B: 0 = the finish re-reads the record
-#endif
 struct ShadowSrc {
   // the lane carries its path and the record's contribution from the ray's
-  // start (MTX_SHADOW_CARRY), so the finish is one L load + store instead of
-  // a record load followed by the dependent L load
+  // start, so the finish is one L load + store instead of a record load
+  // followed by the dependent L load
   struct Payload {
     uint32_t k, li;  // record, L index of the target (plane * capacity + position)
-#if MTX_SHADOW_CARRY
     float4 t, x;
-#endif
   };
   WaveBuffers b;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, Payload &pl) const {
@@ -117,18 +98,11 @@ struct ShadowSrc {
     tmax = o4.w;
     pl.k = k;
     pl.li = __float_as_uint(d4.w);
-#if MTX_SHADOW_CARRY
     pl.t = b.shadow[k].t;
     pl.x = b.shadow[k].x;
-#endif
   }
   __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
-#if MTX_SHADOW_CARRY
     const float4 rt = pl.t, rx = pl.x;
-#else
-    const ShadowRec &rec = b.shadow[pl.k];
-    const float4 rt = rec.t, rx = rec.x;
-#endif
     const uint32_t li = pl.li;
     const uint32_t fl = __float_as_uint(rt.w);
     float4 L = b.L[0][li];
@@ -153,7 +127,7 @@ struct ShadowSrc {
 };
 
 template <bool STATS>
-__global__ __launch_bounds__(kTraceBlock) MTX_SHADOW_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
+__global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
   extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
   const ShadowSrc src{b};
   uint32_t nv = 0, tv = 0, nr = 0;
@@ -188,24 +162,16 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
   b.pos[i] = pos;
-  if (!p.ident0 || MTX_HIT_BY_PATH) b.queue[0][i] = i;
+  if (!p.ident0) b.queue[0][i] = i;
 }
 
 __global__ void k_raygen_camera(DevScene s, WaveBuffers b, ChunkParams p) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) b.counters[0] = p.n_paths;
   if (i >= p.n_paths) return;
-  // path order within the chunk (wavefront.h): pixel-major keeps the samples
-  // of one pixel in one wave (coherent traversal); sample-major puts
-  // consecutive pixels in a wave
-  uint32_t smp, px_local;
-  if (p.sample_major) {
-    smp = i / p.n_px;
-    px_local = i - smp * p.n_px;
-  } else {
-    px_local = i / p.spp;
-    smp = i - px_local * p.spp;
-  }
+  // path order within the chunk: pixel-major keeps the samples of one pixel
+  // in one wave (coherent traversal)
+  const uint32_t px_local = i / p.spp, smp = i - px_local * p.spp;
   const uint32_t pix = p.px0 + px_local;
   const uint32_t y = pix / p.width, x = pix - y * p.width;
   const uint32_t lane = pix * p.spp_total + p.sample_offset + smp;
@@ -307,20 +273,15 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
 }
 
-#ifndef MTX_EARLY_COLOR
-#define MTX_EARLY_COLOR 1  // A/B: 0 = each BSDF call looks the texture up itself
-#endif
 // BSDF data for one shading point: the textured colour of the diffuse and
 // roughplastic lobes fetched once (and early: its latency overlaps the work
 // before the first BSDF call), read by every BSDF call at this point.
 __device__ __forceinline__ BsdfData bsdf_at(const SceneView &sv, const mtx_material &mat, V2 uv) {
   BsdfData bd = sv.bsdf;
-#if MTX_EARLY_COLOR
   if (mat.tex >= 0 && (mat.type == MTX_MAT_DIFFUSE || mat.type == MTX_MAT_ROUGHPLASTIC)) {
     bd.col = texture_eval(sv.bsdf, mat.tex, uv);
     bd.has_col = true;
   }
-#endif
   return bd;
 }
 // path-mis: once a path ends, L.w (its prev_bsdf_pdf until then) holds
@@ -453,13 +414,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   }
 
   // ------------------------------ body ------------------------------------
-#if MTX_DIAG_DIFFUSE  // timing diagnostic only (wrong images): every material diffuse
-  mtx_material mat = sv.materials[si.material];
-  mat.type = MTX_MAT_DIFFUSE;
-  mat.flags = MTX_MF_TWOSIDED;
-#else
   const mtx_material mat = sv.materials[si.material];
-#endif
   // before the emitter sample; the NEE eval and the BSDF sample both read it
   const BsdfData bd = bsdf_at(sv, mat, si.uv);
 #if MTX_DIAG_STAMPS
@@ -915,16 +870,11 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   return false;
 }
 
-// blocks per CU the shade kernels are built for (their register budget)
-#ifndef MTX_PSP_BLOCKS
-#define MTX_PSP_BLOCKS 3  // PSSMLT with NEE (pssmltpath.py): A/B 2 = no spills at 2 waves/SIMD
-#endif
+// blocks per CU the shade kernels are built for (their register budget):
+// kShadeMinBlocks for every integrator (pssmltpath.py's shade at 2 blocks,
+// without its spills, measured slower: DESIGN.md §7)
 template <int INT>
-constexpr int shade_min_blocks() {
-  return INT == MTX_INT_PSSMLT_PATH ? MTX_PSP_BLOCKS : MTX_SHADE_MIN_BLOCKS;
-}
-template <int INT>
-__global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
+__global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
   const uint32_t count = b.counters[4 * bounce + 0];
   const uint32_t *in_q = b.queue[bounce & 1];
@@ -944,11 +894,11 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
   uint32_t path = 0;
   float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
   // an identity bounce-0 queue is not stored: position i is path i
-  const bool ident = bounce == 0 && p.ident0 && !MTX_HIT_BY_PATH;
+  const bool ident = bounce == 0 && p.ident0;
   if (blockIdx.x * kShadeBlock + threadIdx.x < count) {
     const uint32_t i0 = blockIdx.x * kShadeBlock + threadIdx.x;
     path = ident ? i0 : in_q[i0];
-    h = b.hit[MTX_HIT_BY_PATH ? path : i0];
+    h = b.hit[i0];
   }
 #if MTX_DIAG_STAMPS
   Stamps stp{};
@@ -959,7 +909,7 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
     const uint32_t i = base + threadIdx.x;
     const uint32_t inext = i + stride;
     uint32_t path_n = 0;
-    if (MTX_SHADE_PREFETCH && inext < count) path_n = ident ? inext : in_q[inext];
+    if (inext < count) path_n = ident ? inext : in_q[inext];
     ShadeIO io;
     io.emit = false;
     io.em_hi = false;
@@ -986,10 +936,8 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
         cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io);
     }
     const uint32_t path_c = path;
-    if (MTX_SHADE_PREFETCH) {
-      path = path_n;
-      if (inext < count) h = b.hit[MTX_HIT_BY_PATH ? path : inext];
-    }
+    path = path_n;
+    if (inext < count) h = b.hit[inext];
 #if MTX_DIAG_STAMPS
     stp = io.st;
 #endif
@@ -1029,10 +977,6 @@ __global__ __launch_bounds__(kShadeBlock, shade_min_blocks<INT>()) void k_shade(
           b.cq_t[q] = io.qt;
         }
       }
-    }
-    if (!MTX_SHADE_PREFETCH && inext < count) {
-      path = ident ? inext : in_q[inext];
-      h = b.hit[MTX_HIT_BY_PATH ? path : inext];
     }
 #if MTX_DIAG_STAMPS
     MTX_STAMP(stp, 7);
@@ -1094,10 +1038,7 @@ __device__ __forceinline__ V3 final_L(const WaveBuffers &b, const ChunkParams &p
 // Pixel-major chunks: a pixel's samples are contiguous, so one wave stages
 // 64 pixels x kFilmStage samples through LDS with coalesced loads, then each
 // lane accumulates its own pixel in sample order (same order as below).
-#ifndef MTX_FILM_STAGE
-#define MTX_FILM_STAGE 8  // A/B: 8 (11.5 KB of LDS per wave, twice the waves per CU) beats 16 by 0.8 ms and 4
-#endif
-constexpr int kFilmStage = MTX_FILM_STAGE;
+constexpr int kFilmStage = 8;  // 8 (11.5 KB of LDS per wave, twice the waves per CU) beat 16 by 0.8 ms, and 4
 
 __device__ __forceinline__ void film_accumulate(float4 acc[9], int x, int y, float2 ps, V3 L) {
 #pragma unroll
@@ -1214,7 +1155,7 @@ __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
   for (int k = 0; k < 9; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (uint32_t sidx = 0; sidx < p.spp; ++sidx) {
     fs.advance(p.sample_offset + sidx, acc, contrib, p, o, true);
-    const uint32_t path = p.sample_major ? sidx * p.n_px + q : q * p.spp + sidx;
+    const uint32_t path = q * p.spp + sidx;
     film_accumulate(acc, x, y, b.pos[path], final_L(b, p, path));
   }
   fs.finish(acc, contrib, p, o);
@@ -1353,7 +1294,7 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   const uint32_t fl = p.integrator == MTX_INT_PSSMLT_PATH ? (PF_PREV_DELTA << 16) : 0u;
   if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
-  if (!p.ident0 || MTX_HIT_BY_PATH) b.queue[0][i] = i;
+  if (!p.ident0) b.queue[0][i] = i;
 }
 
 // render_sample tail (:137-159): acceptance, cumulative weights, state swap.
@@ -1475,10 +1416,8 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
     case MTX_INT_SIMPLE:
       hipLaunchKernelGGL(k_shade<MTX_INT_SIMPLE>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
-    case MTX_INT_PSSMLT_PATH:  // the grid follows its own blocks per CU
-      hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>,
-                         dim3(std::max(1, grid * shade_min_blocks<MTX_INT_PSSMLT_PATH>() / MTX_SHADE_MIN_BLOCKS)),
-                         dim3(kShadeBlock), 0, st, s, b, p, bounce);
+    case MTX_INT_PSSMLT_PATH:
+      hipLaunchKernelGGL(k_shade<MTX_INT_PSSMLT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
       break;
     case MTX_INT_NERAD_RHS:
       hipLaunchKernelGGL(k_shade<MTX_INT_NERAD_RHS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
@@ -1544,7 +1483,7 @@ void launch_mlt_film(const WaveBuffers &b, const ChunkParams &p, float4 *contrib
   hipLaunchKernelGGL(k_mlt_film, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
 }
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st) {
-  if (p.sample_major || p.spp < 4)
+  if (p.spp < 4)
     hipLaunchKernelGGL(k_film_src, dim3(blocks_for(p.n_px, 128)), dim3(128), 0, st, b, p, contrib);
   else
     hipLaunchKernelGGL(k_film_src_staged, dim3(blocks_for(p.n_px, 64)), dim3(64), 0, st, b, p, contrib);

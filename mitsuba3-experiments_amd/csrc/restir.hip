@@ -92,11 +92,11 @@ __device__ __forceinline__ uint4 st_rng(const Pcg32 &g, uint32_t w) {
 __device__ __forceinline__ float4 f4(V3 v, float w) { return make_float4(v.x, v.y, v.z, w); }
 
 // band-local lane t = q * spp + s (pixel-major, the sampler lane order) ->
-// wavefront path index (see wavefront.h); global lane = r.lane0 + t
+// wavefront path index (the same: chunks are pixel-major); global lane =
+// r.lane0 + t
 __device__ __forceinline__ uint32_t path_of(uint32_t i, const ChunkParams &p) {
-  if (!p.sample_major) return i;
-  const uint32_t q = i / p.spp;
-  return (i - q * p.spp) * p.n_px + q;
+  (void)p;
+  return i;
 }
 
 }  // namespace

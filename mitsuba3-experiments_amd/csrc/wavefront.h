@@ -180,7 +180,6 @@ struct ChunkParams {
   uint32_t stats;
   uint32_t large_step;  // PSSMLT: i % 50 == 0 (pssmlt.py:209)
   uint32_t restir;      // ReSTIR GI secondary paths (path-mis loop, restirgi.py:459-588)
-  uint32_t sample_major;  // chunk path order: 1 = s * n_px + q, 0 = q * spp + s
   uint32_t nrc_cache;     // NRC: query the radiance field where the spread criterion stops
   uint32_t drop_end_misc; // film render: an ending path's sampler state is never read (its L is)
   uint32_t ident0;        // the bounce-0 queue is the identity (raygen): not stored, k_shade uses position = path
