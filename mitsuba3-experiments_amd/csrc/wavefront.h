@@ -77,7 +77,9 @@ struct DevScene {
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
   uint2 *stack_ovf;        // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
-  uint32_t urefill;        // persistent kernels: refill a wave once this many lanes are idle
+  uint32_t urefill;        // single-step loop: refill a wave once this many lanes are idle
+  uint32_t refill_lanes;   // while-while loop (any-hit): the same
+  uint32_t speculate;      // while-while loop: postpone one triangle group per lane (not in STATS kernels)
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
 };
