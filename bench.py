@@ -358,7 +358,13 @@ def main():
                                  "per step is `largest_kernel`",
                 "largest_kernel": largest,
             },
-            "kernels": dict(kernels, other_ms_per_step=round(agg["other_ms"] / K, 3)),
+            "kernels": dict(kernels, other_ms_per_step=round(agg["other_ms"] / K, 3),
+                            streams=int(cnt.get("streams", 1)),
+                            overlapped=bool(cnt.get("streams", 1) > 1),
+                            note=("per-kernel times are summed HIP-event intervals of launches that overlap on "
+                                  "two streams (this rank's render ran on two wavefronts): they do not add up "
+                                  "to ms_per_step" if cnt.get("streams", 1) > 1 else
+                                  "one stream: per-kernel times add up to the step with other_ms")),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -13,15 +13,15 @@ sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd"), os.path.join(ROO
 
 
 def node_levels(nodes, n_nodes):
-    w = nodes.reshape(-1, 16)
+    """Tree level of every 8-wide node (mtx.h: inner children are
+    child_base + rank among the inner slots, breadth-first)."""
+    w = nodes.reshape(-1, 20).view(np.uint32)
     lev = np.full(n_nodes, -1, np.int64)
     lev[0] = 0
     for i in range(n_nodes):  # breadth-first layout: parents precede children
-        nch = int(np.uint32(w[i, 3]) >> 24)
-        for k in range(nch):
-            c = int(w[i, 4 + k])
-            if c >= 0:
-                lev[c] = lev[i] + 1
+        n_inner = bin(int(w[i, 3] >> 24)).count("1")
+        for r in range(n_inner):
+            lev[int(w[i, 4]) + r] = lev[i] + 1
     return lev
 
 
