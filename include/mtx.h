@@ -334,6 +334,13 @@ int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolu
  * target is read-modify-write. */
 int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value);
+/* The stable group-by behind mtx_hashgrid_build / mtx_scatter_reduce_f32
+ * for caller keys (< n_keys): key_size, exclusive key_offset and order
+ * (element indices grouped by key, ascending inside a key). The Python
+ * scatter_reduce_with folds an arbitrary callable over it round by round,
+ * as reductions.py:21-54 does with one election per round. Host pointers. */
+int mtx_group_by_u32(mtx_ctx *ctx, const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size,
+                     uint32_t *key_offset, uint32_t *order);
 
 /* --------------------------- radiance field ----------------------- */
 /* nerad.py:54-106 Field (hash-grid + SH encoding, fp16 MLP with LeakyReLU,

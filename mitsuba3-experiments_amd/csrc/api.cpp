@@ -1665,6 +1665,43 @@ int mtx_hashgrid_build(mtx_ctx *c, const float *p, uint64_t n, uint32_t resoluti
   return MTX_OK;
 }
 
+int mtx_group_by_u32(mtx_ctx *c, const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size,
+                     uint32_t *key_offset, uint32_t *order) {
+  if (!c || !keys || !key_size || !key_offset || !order || n == 0 || n_keys == 0) {
+    mtx_set_error("mtx_group_by_u32: bad argument");
+    return MTX_E_ARG;
+  }
+  if (n >= (1ull << 31)) {
+    mtx_set_error("mtx_group_by_u32: n too large");
+    return MTX_E_ARG;
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (keys[i] >= n_keys) {
+      mtx_set_error("mtx_group_by_u32: keys[%llu] = %u out of range", (unsigned long long)i, keys[i]);
+      return MTX_E_ARG;
+    }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = dalloc(c->s1, 4 * n))) return rc;                // keys
+  if ((rc = dalloc(c->s2, 4 * (size_t)n_keys))) return rc;   // size
+  if ((rc = dalloc(c->s3, 4 * (size_t)n_keys))) return rc;   // offset
+  if ((rc = dalloc(c->s4, 4 * n))) return rc;                // order
+  if ((rc = dalloc(c->s5, mtxd::hashgrid_workspace_bytes(n, n_keys)))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->s1.p, keys, 4 * n, hipMemcpyHostToDevice, c->stream));
+  if ((rc = prim_timer_begin(c))) return rc;
+  rc = mtxd::group_by_u32((const uint32_t *)c->s1.p, n, n_keys, (uint32_t *)c->s2.p, (uint32_t *)c->s3.p,
+                          (uint32_t *)c->s4.p, c->s5.p, c->stream);
+  if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(key_size, c->s2.p, 4ull * n_keys, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(key_offset, c->s3.p, 4ull * n_keys, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(order, c->s4.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
 int mtx_scatter_reduce_f32(mtx_ctx *c, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value) {
   if (!c || !target || (n_value && (!value || !index)) || op < 0 || op > 3) {

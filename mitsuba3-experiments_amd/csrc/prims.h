@@ -20,6 +20,11 @@ size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells);
 int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,
                    uint32_t *cell_offset, uint32_t *sample_idx, void *ws, hipStream_t st);
 
+// Stable group-by of n keys < n_keys (hash-grid machinery; workspace:
+// hashgrid_workspace_bytes(n, n_keys)).
+int group_by_u32(const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size, uint32_t *key_offset,
+                 uint32_t *order, void *ws, hipStream_t st);
+
 // Stable sort permutation of n keys < 2^24 (hash-grid machinery).
 size_t sort24_workspace_bytes(uint64_t n);
 int sort24(const uint32_t *keys, uint64_t n, uint32_t *perm, void *ws, hipStream_t st);

@@ -1546,6 +1546,56 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
   return MTX_OK;
 }
 
+// Stable group-by of n keys < n_keys (the hash grid's machinery without the
+// hashing): key_size, exclusive key_offset and order (element indices grouped
+// by key, ascending index inside a key).
+int group_by_u32(const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size, uint32_t *key_offset,
+                 uint32_t *order, void *ws, hipStream_t st) {
+  if (int e = gb_attrs()) return e;
+  const GbPlan g = gb_plan(n, n_keys);
+  Carve cv{(char *)ws};
+  cv.take<float2>(1025);
+  if (g.msd) {
+    const uint32_t tiles = split_tiles<0>(n);
+    uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
+    uint32_t *out1 = cv.take<uint32_t>(n);
+    uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_keys + (1ull << g.s) - 1) >> g.s));
+    if (lds_lane_order(st))
+      hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n,
+                         g.s, g.top, tab, out1, slow);
+    else
+      hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n,
+                         g.s, g.top, tab, out1, slow);
+    return bk_launch<0>(out1, tab, tiles, g.s, g.top, n_keys, key_size, key_offset, order, nullptr, 0, slow, st);
+  }
+  const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
+  uint32_t *hist = cv.take<uint32_t>(hn), *hscan = cv.take<uint32_t>(hn);
+  void *scan_ws = cv.take<char>(scan_workspace_bytes(hn));
+  uint32_t *ka = cv.take<uint32_t>(n), *pa = cv.take<uint32_t>(n), *kb = cv.take<uint32_t>(n),
+           *pb = cv.take<uint32_t>(n);
+  const uint32_t *kin = keys, *pin = nullptr;
+  uint32_t *kbuf[2] = {ka, kb}, *pbuf[2] = {pa, pb};
+  int cur = 0, rc;
+  for (int shift = 0; shift < g.bits; shift += kMsMaxBits) {
+    const int bits = g.bits - shift < kMsMaxBits ? g.bits - shift : kMsMaxBits;
+    const bool last = shift + kMsMaxBits >= g.bits;
+    uint32_t *pout = last ? order : pbuf[cur];
+    if ((rc = ms_pass(kin, pin, n, shift, bits, g.tiles, hist, hscan, scan_ws, kbuf[cur], pout, nullptr, nullptr,
+                      st)))
+      return rc;
+    kin = kbuf[cur];
+    pin = pout;
+    cur ^= 1;
+  }
+  if ((uint64_t)n_keys > 4 * n)
+    hipLaunchKernelGGL(k_hash_offsets_search, dim3(nblk(n_keys, 256)), dim3(256), 0, st, kin, n, n_keys, key_offset,
+                       key_size);
+  else
+    hipLaunchKernelGGL(k_hash_ranges, dim3(nblk(n, kHashTile)), dim3(256), 0, st, kin, n, n_keys, key_offset,
+                       key_size);
+  return MTX_OK;
+}
+
 size_t sort24_workspace_bytes(uint64_t n) { return gb_bytes<0>(n, 1u << 24, gb_plan(n, 1u << 24)); }
 
 // Stable sort permutation of n keys < 2^24 (the hash grid's two levels

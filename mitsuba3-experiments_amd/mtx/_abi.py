@@ -275,6 +275,7 @@ EXPORTS = [
     "mtx_prefix_sum_f32_hs",
     "mtx_hashgrid_build",
     "mtx_scatter_reduce_f32",
+    "mtx_group_by_u32",
     "mtx_field_upload",
     "mtx_field_features",
     "mtx_field_mlp",

@@ -63,19 +63,60 @@ class HashGrid:
               "mtx_hashgrid_build")
 
 
+def group_by(keys, n_keys: int, device: int | None = None):
+    """The stable device group-by behind HashGrid and scatter_reduce_with:
+    (key_size, key_offset exclusive, order) with order[key_offset[k] + j] the
+    j-th element of key k in ascending element index (mtx_group_by_u32)."""
+    k = np.ascontiguousarray(keys, np.uint32)
+    n_keys = int(n_keys)
+    size = np.zeros(n_keys, np.uint32)
+    offset = np.zeros(n_keys, np.uint32)
+    order = np.zeros(len(k), np.uint32)
+    if len(k):
+        ctx = context(device)
+        check(lib().mtx_group_by_u32(ctx.handle, k.ctypes.data, len(k), n_keys, size.ctypes.data, offset.ctypes.data,
+                                     order.ctypes.data), "mtx_group_by_u32")
+    return size, offset, order
+
+
+def fold_rounds(func, target, value, size, offset, order):
+    """reductions.py:21-54's loop with a deterministic election: round r
+    applies `func(a, b)` once, vectorised, to every target that has more
+    than r values, with a = its current value and b = its r-th value in
+    ascending index (the reference elects an arbitrary one per round). Works
+    on numpy arrays; func sees arrays, as the reference's sees Dr.Jit ones."""
+    t = np.array(target, copy=True)
+    v = np.asarray(value)
+    size = np.asarray(size, np.int64)
+    offset = np.asarray(offset, np.int64)
+    order = np.asarray(order, np.int64)
+    rounds = int(size.max()) if len(size) else 0
+    for r in range(rounds):
+        sel = np.nonzero(size > r)[0]
+        res = np.asarray(func(t[sel], v[order[offset[sel] + r]]))
+        t[sel] = res
+    return t
+
+
 def scatter_reduce_with(op, target, value, index, device: int | None = None):
-    """reductions.py:12-54 for func in {ADD, MIN, MAX, MUL} (or 'add' / 'min' /
-    'max' / 'mul'). Returns the updated target; each target receives its
-    values in ascending index order. The reference accepts any callable
-    (`func(a, b)`, reductions.py:53); a device kernel cannot call Python, so
-    other callables raise TypeError (decided limitation)."""
+    """reductions.py:12-54. func in {'add', 'min', 'max', 'mul'} (or ADD, MIN,
+    MAX, MUL): one device pass, each target receiving its values in ascending
+    index order (f32). Any other callable `func(a, b)` (the reference accepts
+    any, :12, :53): the device groups the values by target (group_by) and the
+    callable is folded on the host round by round (fold_rounds), the
+    reference's structure with one deterministic election per round; target
+    and value may then have any numpy dtype func handles."""
     if isinstance(op, str):
         if op not in _OPS:
-            raise TypeError(f"scatter_reduce_with: unsupported func {op!r} (device ops: add, min, max, mul)")
+            raise TypeError(f"scatter_reduce_with: unknown func {op!r} (device ops: add, min, max, mul)")
         op = _OPS[op]
     elif callable(op):
-        raise TypeError("scatter_reduce_with: arbitrary Python callables cannot run on the device; "
-                        "use one of 'add', 'min', 'max', 'mul'")
+        idx = np.ascontiguousarray(index, np.uint32)
+        tgt = np.asarray(target)
+        if len(idx) and int(idx.max()) >= len(tgt):
+            raise ValueError("scatter_reduce_with: index out of range")
+        size, offset, order = group_by(idx, len(tgt), device)
+        return fold_rounds(op, tgt, value, size, offset, order)
     t = np.array(target, np.float32)
     v = np.ascontiguousarray(value, np.float32)
     i = np.ascontiguousarray(index, np.uint32)

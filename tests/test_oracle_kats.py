@@ -138,9 +138,17 @@ def test_multicore_primitive_baselines_equal_sequential(oracle):
         assert np.array_equal(oracle.scatter_reduce_mt(op, tgt, val, idx), oracle.scatter_reduce(op, tgt, val, idx))
 
 
-def test_scatter_reduce_mul_and_callable_rejected(oracle):
+def _np_group_by(idx, n_keys):
+    """numpy restatement of the device group-by (stable: ascending index)."""
+    order = np.argsort(idx, kind="stable").astype(np.uint32)
+    size = np.bincount(idx, minlength=n_keys).astype(np.uint32)
+    offset = (np.cumsum(size) - size).astype(np.uint32)
+    return size, offset, order
+
+
+def test_scatter_reduce_mul_and_unknown_op(oracle):
     """reductions.py:12 takes any func; the device op table adds mul
-    (sequential product per target) and rejects Python callables."""
+    (sequential product per target); an unknown op name raises."""
     from mtx import primitives
 
     rng = np.random.default_rng(3)
@@ -153,6 +161,28 @@ def test_scatter_reduce_mul_and_callable_rejected(oracle):
     assert np.array_equal(oracle.scatter_reduce(3, tgt, val, idx), ref)
     assert np.array_equal(oracle.scatter_reduce_mt(3, tgt, val, idx), ref)
     with pytest.raises(TypeError):
-        primitives.scatter_reduce_with(lambda a, b: a + b, tgt, val, idx)
-    with pytest.raises(TypeError):
         primitives.scatter_reduce_with("xor", tgt, val, idx)
+
+
+def test_scatter_reduce_callable_fold_rounds():
+    """A Python func (reductions.py:12, :53) is folded round by round over the
+    group-by (mtx.primitives.fold_rounds; the device provides the grouping,
+    here its numpy restatement): the KAT of reductions.py:57-63 (ten targets,
+    25 ones, index i % 10 -> 3 3 3 3 3 2 2 2 2 2) and, for a non-commutative
+    func and an integer dtype, the sequential loop in ascending index."""
+    from mtx import primitives
+
+    idx = (np.arange(25) % 10).astype(np.uint32)
+    t = primitives.fold_rounds(lambda a, b: a + b, np.zeros(10, np.float32), np.ones(25, np.float32),
+                               *_np_group_by(idx, 10))
+    assert np.array_equal(t, np.array([3] * 5 + [2] * 5, np.float32))
+    rng = np.random.default_rng(5)
+    idx = rng.integers(0, 33, 500).astype(np.uint32)
+    val = rng.integers(-9, 9, 500).astype(np.int64)
+    func = lambda a, b: 3 * a - b  # noqa: E731  (order-dependent)
+    tgt = rng.integers(-5, 5, 40).astype(np.int64)  # targets 33..39 receive nothing
+    ref = tgt.copy()
+    for i, v in zip(idx, val):
+        ref[i] = func(ref[i], v)
+    got = primitives.fold_rounds(func, tgt, val, *_np_group_by(idx, 40))
+    assert np.array_equal(got, ref) and got.dtype == np.int64

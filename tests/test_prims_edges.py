@@ -174,3 +174,39 @@ np.savez(sys.argv[2], cell=g.cell, size=g.cell_size, off=g.cell_offset, idx=g.sa
         outs.append(np.load(f))
     for k in ("cell", "size", "off", "idx", "t"):
         assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
+@pytest.mark.parametrize("n,n_keys", [(1, 1), (100003, 97), (1 << 20, 1 << 20), (200000, 1 << 26)])
+def test_group_by_matches_stable_sort(n, n_keys):
+    """mtx_group_by_u32 (the hash grid's stable group-by on caller keys; the
+    LSD multisplit path for n_keys >= 2^25): sizes, exclusive offsets and the
+    order equal numpy's stable argsort."""
+    from mtx import primitives
+
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, n_keys, n, dtype=np.uint64).astype(np.uint32)
+    size, offset, order = primitives.group_by(k, n_keys)
+    assert np.array_equal(order, np.argsort(k, kind="stable"))
+    ref = np.bincount(k, minlength=n_keys)
+    assert np.array_equal(size, ref) and np.array_equal(offset, np.cumsum(ref) - ref)
+
+
+def test_scatter_reduce_with_callable_on_device_grouping():
+    """reductions.py:12-54 with a Python func (here order-dependent, integer
+    dtype): the device groups by target, the func is folded round by round
+    (ascending index per target) -- equal to the sequential loop; the
+    reference's KAT (reductions.py:57-63)."""
+    from mtx import primitives
+
+    idx = (np.arange(25) % 10).astype(np.uint32)
+    t = primitives.scatter_reduce_with(lambda a, b: a + b, np.zeros(10, np.float32), np.ones(25, np.float32), idx)
+    assert np.array_equal(t, np.array([3] * 5 + [2] * 5, np.float32))
+    rng = np.random.default_rng(9)
+    idx = rng.integers(0, 1000, 50000).astype(np.uint32)
+    val = rng.integers(-9, 9, 50000).astype(np.int64)
+    tgt = rng.integers(-5, 5, 1200).astype(np.int64)
+    ref = tgt.copy()
+    for i, v in zip(idx, val):
+        ref[i] = (3 * ref[i] - v) % 1000003
+    got = primitives.scatter_reduce_with(lambda a, b: (3 * a - b) % 1000003, tgt, val, idx)
+    assert np.array_equal(got, ref)
