@@ -91,7 +91,7 @@ int upload(DevBuf &b, const T *src, size_t count, hipStream_t st) {
 struct Wave2 {
   hipStream_t stream = nullptr;
   hipEvent_t start = nullptr, done = nullptr;
-  DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, xheads, stack_ovf, clsq;
+  DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, xheads, stack_ovf;
   DevBuf cq_p, cq_d, cq_t, cq_count, f_feat, f_out;  // NRC radiance-cache queries of its chunks
   uint32_t capacity = 0;
 };
@@ -108,10 +108,6 @@ struct mtx_ctx {
   // scene
   DevBuf stack_ovf;  // traversal stack entries beyond the LDS part
   DevBuf shade_rec;  // per-triangle shading records
-  DevBuf tri_cls;    // per-triangle shading class (k_classify)
-  DevBuf clsq;       // queue positions by shading class (two planes of capacity)
-  uint32_t shade_split = 1;  // path / path-mis / nrc shade per material class (MTX_SHADE_SPLIT=0: one kernel)
-  int shade_light_grid = 0;
   // radiance field (mtx_field_upload)
   DevBuf field_table, field_frag, fq_p, fq_d, f_feat, f_out;
   DevBuf cq_p, cq_d, cq_t, cq_count;  // NRC cache queries of a chunk
@@ -159,8 +155,6 @@ struct mtx_ctx {
   uint32_t lds_top = MTX_LDS_TOP;  // wide nodes of the tree top kept in LDS per block (MTX_LDS_TOP env: A/B)
   uint32_t trace_batch = 128;  // queue entries per claim (256: +0.6 % closest, +1 % at spp 32; 64: +5 %)
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
-  uint32_t refill_lanes = 16;  // any-hit while-while loop
-  uint32_t speculate = 1;
   uint32_t xcd_claim = 1;
   uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
   DevBuf cq_keys, cq_perm, cq_ws;
@@ -212,17 +206,13 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   // grid is recomputed per scene: its LDS stack depends on the BVH depth).
   c->trace_grid = c->n_cu * 8;
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
-  c->shade_light_grid = c->n_cu * mtxd::shade_light_blocks_per_cu();
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS_MAX_LOG2")) c->streams_max_log2 = (uint32_t)std::max(16, std::min(31, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_REFILL_LANES")) c->refill_lanes = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_SPECULATE")) c->speculate = atoi(e) != 0;
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
-  if (const char *e = getenv("MTX_SHADE_SPLIT")) c->shade_split = atoi(e) != 0;
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
   *out = c;
   return MTX_OK;
@@ -238,7 +228,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters, &c->xheads, &c->rs_heads,  &c->stats,    &c->contrib, &c->film,
                     &c->mlt_cur, &c->mlt_L, &c->mlt_prop, &c->vpath, &c->vprop, &c->vpath_es, &c->vprop_es,
-                    &c->stack_ovf, &c->shade_rec, &c->tri_cls, &c->clsq, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
+                    &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_nbr, &c->rs_xs, &c->rs_ns,
                     &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5,
@@ -250,7 +240,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   for (DevBuf *b : bufs) dfree(*b);
   Wave2 &w = c->w2;
   for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.L, &w.prev, &w.misc, &w.pos, &w.hit, &w.q0, &w.q1, &w.shadow,
-                    &w.counters, &w.xheads, &w.stack_ovf, &w.clsq, &w.cq_p, &w.cq_d, &w.cq_t, &w.cq_count, &w.f_feat,
+                    &w.counters, &w.xheads, &w.stack_ovf, &w.cq_p, &w.cq_d, &w.cq_t, &w.cq_count, &w.f_feat,
                     &w.f_out})
     dfree(*b);
   if (w.start) hipEventDestroy(w.start);
@@ -405,15 +395,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     if ((rc = upload(c->shade_rec, rec.data(), rec.size(), st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));  // rec is freed at scope exit
   }
-  {
-    // shading class per triangle (k_classify): 0 light = a diffuse material
-    // (whatever its wrappers), 1 heavy = every other BSDF
-    std::vector<uint8_t> cls(d->n_tris);
-    for (uint32_t t = 0; t < d->n_tris; ++t)
-      cls[t] = d->materials[d->shapes[d->tri_shape[t]].material].type == MTX_MAT_DIFFUSE ? 0 : 1;
-    if ((rc = upload(c->tri_cls, cls.data(), cls.size(), st))) return rc;
-    HIP_TRY(hipStreamSynchronize(st));  // cls is freed at scope exit
-  }
   HIP_TRY(hipStreamSynchronize(st));
   mtxd::DevScene &s = c->scene;
   s.nodes = (const int4 *)c->nodes.p;
@@ -425,7 +406,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.vuv = (const float *)c->vuv.p;
   s.shapes = (const mtx_shape *)c->shapes.p;
   s.shade_rec = (const float4 *)c->shade_rec.p;
-  s.tri_cls = (const uint8_t *)c->tri_cls.p;
   s.materials = (const mtx_material *)c->materials.p;
   s.emitters = (const mtx_emitter *)c->emitters.p;
   s.textures = (const mtx_texture *)c->textures.p;
@@ -441,8 +421,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.lds_top = std::min<uint32_t>(d->n_nodes, c->lds_top);
   s.trace_batch = c->trace_batch;
   s.urefill = c->urefill;
-  s.refill_lanes = c->refill_lanes;
-  s.speculate = c->speculate;
   s.xcd_claim = c->xcd_claim;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
@@ -498,7 +476,6 @@ int ensure_wavefront(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     if ((rc = dalloc(c->q0, 4ull * cap))) return rc;
     if ((rc = dalloc(c->q1, 4ull * cap))) return rc;
     if ((rc = dalloc(c->shadow, sizeof(mtxd::ShadowRec) * (size_t)cap))) return rc;
-    if ((rc = dalloc(c->clsq, 8ull * cap))) return rc;
     c->capacity = cap;
   }
   if ((rc = dalloc(c->counters, 16ull * (max_depth + 2)))) return rc;
@@ -525,8 +502,6 @@ mtxd::WaveBuffers buffers(mtx_ctx *c) {
   b.queue[0] = (uint32_t *)c->q0.p;
   b.queue[1] = (uint32_t *)c->q1.p;
   b.shadow = (mtxd::ShadowRec *)c->shadow.p;
-  b.clsq[0] = (uint32_t *)c->clsq.p;
-  b.clsq[1] = b.clsq[0] + c->capacity;
   b.counters = (uint32_t *)c->counters.p;
   b.xheads = (uint32_t *)c->xheads.p;
   b.stats = (unsigned long long *)c->stats.p;
@@ -566,7 +541,6 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
     if ((rc = dalloc(w.q0, 4ull * cap))) return rc;
     if ((rc = dalloc(w.q1, 4ull * cap))) return rc;
     if ((rc = dalloc(w.shadow, sizeof(mtxd::ShadowRec) * (size_t)cap))) return rc;
-    if ((rc = dalloc(w.clsq, 8ull * cap))) return rc;
     w.capacity = cap;
   }
   if ((rc = dalloc(w.counters, 16ull * (max_depth + 2)))) return rc;
@@ -595,8 +569,6 @@ mtxd::WaveBuffers buffers2(mtx_ctx *c) {
   b.queue[0] = (uint32_t *)w.q0.p;
   b.queue[1] = (uint32_t *)w.q1.p;
   b.shadow = (mtxd::ShadowRec *)w.shadow.p;
-  b.clsq[0] = (uint32_t *)w.clsq.p;
-  b.clsq[1] = b.clsq[0] + w.capacity;
   b.counters = (uint32_t *)w.counters.p;
   b.xheads = (uint32_t *)w.xheads.p;
   b.capacity = w.capacity;
@@ -803,15 +775,7 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
       ++*n_trace;
     }
     e = tm.begin(2, st);
-    if (c->shade_split && mtxd::shade_split(p.integrator)) {
-      // per material class (kernels.hip k_classify): light hits with the
-      // diffuse-only shade at more waves, then the heavy ones
-      mtxd::launch_classify(s, b, bounce, c->shade_grid, st);
-      mtxd::launch_shade(s, b, p, bounce, c->shade_light_grid, st, 1);
-      mtxd::launch_shade(s, b, p, bounce, c->shade_grid, st, 2);
-    } else {
-      mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), st);
-    }
+    mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), st);
     tm.end(2, e, st);
     if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
         !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays

@@ -529,169 +529,6 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
   }
 }
 
-// ---------------------------------------------------------------------------
-// Persistent while-while traversal for any-hit rays (Aila & Laine 2009).
-//
-// A wave alternates a node phase -- lanes visit nodes until they hold a
-// triangle group -- and a triangle phase -- lanes test their groups. With
-// speculation (production kernels) a lane that receives a triangle group
-// while it has none postponed sets it aside and keeps descending, so the
-// triangle phase starts with more lanes busy; the wave leaves the node phase
-// once every traversing lane holds one. The any-hit result does not depend
-// on the order; the visit sequence does, so the STATS kernels (visit
-// counters, tests) do not speculate and follow the oracle's order.
-// ---------------------------------------------------------------------------
-template <bool ANY, bool STATS = false, class Src>
-__device__ __forceinline__ void trace_loop_ww(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
-                                              uint2 *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
-                                              uint32_t &nr, uint32_t *wave_iters = nullptr) {
-  const uint32_t lane = lane_id();
-  uint2 *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
-  const int lds_n = (int)s.lds_entries;
-  bool has = false, exhausted = false, hit = false, drained = false;
-  uint32_t res_lo = 0, res_hi = 0;
-  typename Src::Payload payload{};
-  uint32_t prim = 0xffffffffu;
-  TraceRay r;
-  float tbest = 0.f, bu = 0.f, bv = 0.f;
-  uint32_t oct = 0, gbase = 0, ghits = 0, tbase = 0, thits = 0, pbase = 0, phits = 0;
-  const int top_n = (int)s.lds_top;
-  int sp = 0;
-  const bool spec = !STATS && s.speculate;
-  const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
-  const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
-  if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + batch - 1) / batch) return;
-  uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
-  while (true) {
-    if (!exhausted) {
-      const uint64_t idle = __ballot(!has);
-      if ((uint32_t)__popcll(idle) >= s.refill_lanes || idle == ~0ull) {
-        const uint32_t n = (uint32_t)__popcll(idle);
-        const uint32_t left = res_hi - res_lo;
-        uint32_t base2 = 0, got2 = 0;
-        if (left < n && !drained)
-          drained = claim_rays(s, heads, count, batch, (uint32_t)(__ffsll((unsigned long long)idle) - 1), lane, seg,
-                               tries, base2, got2);
-        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-        uint32_t k = 0;
-        bool ok = false;
-        if (rk < left) {
-          k = res_lo + rk;
-          ok = true;
-        } else if (rk - left < got2) {
-          k = base2 + (rk - left);
-          ok = true;
-        }
-        if (n <= left) {
-          res_lo += n;
-        } else {
-          const uint32_t used2 = min(n - left, got2);
-          res_lo = base2 + used2;
-          res_hi = base2 + got2;
-        }
-        exhausted = drained && res_lo >= res_hi;
-        if (!has && ok) {
-          src.load(k, r, tbest, payload);
-          prim = 0xffffffffu;
-          bu = bv = 0.f;
-          hit = false;
-          oct = ray_octant(r);
-          gbase = 0;
-          ghits = (1u << (24 + oct)) | 1u;  // the root: node 0 in slot 0
-          tbase = thits = pbase = phits = 0;
-          sp = 0;
-          has = true;
-        }
-      }
-    }
-    if (__ballot(has) == 0) break;
-    // ---- node phase
-    while (true) {
-      const bool nodes_left = has && ((ghits >> 24) != 0 || sp > 0);
-      const bool want = nodes_left && thits == 0;
-      if (__ballot(want) == 0) break;
-      if (want) {
-        if (STATS) {
-          const uint64_t m = __ballot(true);
-          if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[0];
-        }
-        if ((ghits >> 24) == 0) {  // the next node group
-          --sp;
-          const uint2 g = stack_read(stk, ovf, sp, lds_n, s.ovf_threads);
-          gbase = g.x;
-          ghits = g.y;
-        }
-        const uint32_t p = (uint32_t)ctz32(ghits >> 24);
-        ghits &= ~(1u << (24 + p));
-        const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
-        if (ghits >> 24) {
-          const uint2 g = make_uint2(gbase, ghits);
-          if (sp < lds_n) {
-            stk[sp * kTraceBlock] = g;
-          } else {
-            ovf[(size_t)(sp - lds_n) * s.ovf_threads] = g;
-            asm volatile("" ::: "memory");  // keeps the two stores apart (no pointer select + flat store)
-          }
-          ++sp;
-        }
-        ++nv;
-        const CwVisit v = cw_visit(s, r, oct, node, tbest, top, top_n);
-        gbase = v.child_base;
-        ghits = (v.hits & 0xff000000u) | v.imask;
-        tbase = v.tri_base;
-        thits = v.hits & 0x00ffffffu;
-        if (spec && thits != 0 && phits == 0) {  // postpone it, keep descending
-          pbase = tbase;
-          phits = thits;
-          thits = 0;
-        }
-      }
-      // speculation: leave once every lane still descending holds a postponed group
-      if (spec && __ballot(has && thits == 0 && phits == 0 && ((ghits >> 24) != 0 || sp > 0)) == 0) break;
-    }
-    // ---- triangle phase: the postponed group, then the current one
-    while (true) {
-      const bool want = has && (phits | thits) != 0;
-      if (__ballot(want) == 0) break;
-      if (want) {
-        if (STATS) {
-          const uint64_t m = __ballot(true);
-          if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
-        }
-        uint32_t pr;
-        if (phits) {
-          pr = pbase + (uint32_t)ctz32(phits);
-          phits &= phits - 1u;
-        } else {
-          pr = tbase + (uint32_t)ctz32(thits);
-          thits &= thits - 1u;
-        }
-        const TriGeom g = load_tri(s, pr);
-        float t, u, v;
-        ++tv;
-        if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
-          if (ANY) {
-            hit = true;
-            thits = phits = ghits = 0;
-            sp = 0;
-          } else if (t < tbest || (t == tbest && pr < prim)) {
-            tbest = t;
-            prim = pr;
-            bu = u;
-            bv = v;
-          }
-        }
-      }
-    }
-    if (has && (ghits >> 24) == 0 && sp == 0) {
-      src.finish(payload, hit, tbest, prim, bu, bv);
-      has = false;
-      ++nr;
-    }
-  }
-}
-
 // stk: this thread's stack column (dynamic LDS + threadIdx.x). Every thread
 // of the block calls this (the LDS tree top is filled behind a barrier).
 template <bool ANY, bool STATS = false, class Src>
@@ -701,15 +538,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
   int4 *top = reinterpret_cast<int4 *>(stk - threadIdx.x + s.lds_entries * kTraceBlock);
   for (uint32_t i = threadIdx.x; i < 5 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
   __syncthreads();
-  // closest hit: the single-step loop; any-hit: while-while with
-  // speculation (MTX_ANYHIT_UNIFIED=1 builds the single-step loop for both)
-#ifndef MTX_ANYHIT_UNIFIED
-#define MTX_ANYHIT_UNIFIED 0
-#endif
-  if (ANY && !MTX_ANYHIT_UNIFIED)
-    trace_loop_ww<ANY, STATS>(s, src, count, heads, stk, top, nv, tv, nr, wave_iters);
-  else
-    trace_loop_u<ANY, STATS>(s, src, count, heads, stk, top, nv, tv, nr, wave_iters);
+  trace_loop_u<ANY, STATS>(s, src, count, heads, stk, top, nv, tv, nr, wave_iters);
 }
 
 }  // namespace mtxd

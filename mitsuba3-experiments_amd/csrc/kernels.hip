@@ -296,10 +296,7 @@ __device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, f
   (void)path;
   return lw != 0.f;
 }
-// CLS: 0 every hit; 1 light hits only (diffuse materials and misses: the
-// material type is the literal MTX_MAT_DIFFUSE, so every BSDF switch folds to
-// its diffuse case); 2 heavy hits (the other materials)
-template <int INT, int CLS = 0>
+template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                            const float4 h, ShadeIO &io) {
@@ -417,8 +414,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   }
 
   // ------------------------------ body ------------------------------------
-  mtx_material mat = sv.materials[si.material];
-  if constexpr (CLS == 1) mat.type = MTX_MAT_DIFFUSE;  // k_classify put only diffuse materials here
+  const mtx_material mat = sv.materials[si.material];
   // before the emitter sample; the NEE eval and the BSDF sample both read it
   const BsdfData bd = bsdf_at(sv, mat, si.uv);
 #if MTX_DIAG_STAMPS
@@ -874,54 +870,13 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
   return false;
 }
 
-// Shading classes (Laine, Karras & Aila 2013, "Megakernels considered
-// harmful": one kernel per material class, each with the registers its own
-// code needs). k_classify splits a bounce's queue positions by the hit's
-// class (tri_cls: diffuse material or miss -> light, else heavy) with one
-// block-level append per class per block step; k_shade<INT, 1> then shades
-// the light positions with every BSDF switch folded to the diffuse case (no
-// microfacet code: fewer VGPRs, more waves), k_shade<INT, 2> the heavy ones.
-// Both append to the bounce's next queue and shadow queue as one kernel
-// does. Positions keep their order inside a class, so the state reads at
-// them stay near coalesced.
-__global__ __launch_bounds__(kShadeBlock) void k_classify(DevScene s, WaveBuffers b, uint32_t bounce) {
-  const uint32_t count = b.counters[4 * bounce + 0];
-  uint32_t *cnt = &b.counters[4 * bounce + 2];
-  uint32_t parity = 0;
-  for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += gridDim.x * kShadeBlock, parity ^= 1u) {
-    const uint32_t k = base + threadIdx.x;
-    bool heavy = false;
-    if (k < count) {
-      const uint32_t prim = __float_as_uint(b.hit[k].y);
-      heavy = prim != 0xffffffffu && s.tri_cls[prim] != 0;
-    }
-    uint32_t sl, sh;
-    block_append2<kShadeBlock>(k < count && !heavy, heavy, false, cnt, parity, sl, sh);
-    if (k < count) {
-      if (heavy)
-        b.clsq[1][sh] = k;
-      else
-        b.clsq[0][sl] = k;
-    }
-  }
-}
-
 // blocks per CU the shade kernels are built for (their register budget):
 // kShadeMinBlocks for every integrator (pssmltpath.py's shade at 2 blocks,
-// without its spills, measured slower: DESIGN.md §7); the light-class shade 4
-constexpr int kShadeLightBlocks = 4;
-template <int INT, int CLS>
-constexpr int shade_blocks() {
-  return CLS == 1 ? kShadeLightBlocks : kShadeMinBlocks;
-}
-template <int INT, int CLS = 0>
-__global__ __launch_bounds__(kShadeBlock, (shade_blocks<INT, CLS>())) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
+// without its spills, measured slower: DESIGN.md §7)
+template <int INT>
+__global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene s, WaveBuffers b, ChunkParams p, uint32_t bounce) {
   const SceneView sv = make_view(s);
-  // CLS > 0: the class's queue positions (k_classify); position i of the
-  // loop below is then the class entry, pos(i) the bounce's queue position
-  const uint32_t count = CLS ? b.counters[4 * bounce + 1 + CLS] : b.counters[4 * bounce + 0];
-  const uint32_t *cls_q = CLS ? b.clsq[CLS - 1] : nullptr;
-  auto pos = [&](uint32_t i) -> uint32_t { return CLS ? cls_q[i] : i; };
+  const uint32_t count = b.counters[4 * bounce + 0];
   const uint32_t *in_q = b.queue[bounce & 1];
   uint32_t *out_q = b.queue[(bounce + 1) & 1];
   // [4(bounce+1)] next queue count, [4(bounce+1)+1] this bounce's shadow
@@ -940,11 +895,10 @@ __global__ __launch_bounds__(kShadeBlock, (shade_blocks<INT, CLS>())) void k_sha
   float4 h = make_float4(0.f, 0.f, 0.f, 0.f);
   // an identity bounce-0 queue is not stored: position i is path i
   const bool ident = bounce == 0 && p.ident0;
-  uint32_t k = 0;  // queue position of the current entry
   if (blockIdx.x * kShadeBlock + threadIdx.x < count) {
-    k = pos(blockIdx.x * kShadeBlock + threadIdx.x);
-    path = ident ? k : in_q[k];
-    h = b.hit[k];
+    const uint32_t i0 = blockIdx.x * kShadeBlock + threadIdx.x;
+    path = ident ? i0 : in_q[i0];
+    h = b.hit[i0];
   }
 #if MTX_DIAG_STAMPS
   Stamps stp{};
@@ -954,11 +908,8 @@ __global__ __launch_bounds__(kShadeBlock, (shade_blocks<INT, CLS>())) void k_sha
   for (uint32_t base = blockIdx.x * kShadeBlock; base < count; base += stride, parity ^= 1u) {
     const uint32_t i = base + threadIdx.x;
     const uint32_t inext = i + stride;
-    uint32_t path_n = 0, k_n = 0;
-    if (inext < count) {
-      k_n = pos(inext);
-      path_n = ident ? k_n : in_q[k_n];
-    }
+    uint32_t path_n = 0;
+    if (inext < count) path_n = ident ? inext : in_q[inext];
     ShadeIO io;
     io.emit = false;
     io.em_hi = false;
@@ -972,22 +923,21 @@ __global__ __launch_bounds__(kShadeBlock, (shade_blocks<INT, CLS>())) void k_sha
     const bool valid = i < count;
     if (valid) {
       if constexpr (INT == MTX_INT_PSSMLT_SIMPLE)
-        cont = shade_pssmlt(s, sv, b, p, bounce, path, k, h, io);
+        cont = shade_pssmlt(s, sv, b, p, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_SIMPLE)
-        cont = shade_simple(s, sv, b, p, bounce, path, k, h, io);
+        cont = shade_simple(s, sv, b, p, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_PSSMLT_PATH)
-        cont = shade_pssmlt_path(s, sv, b, p, bounce, path, k, h, io);
+        cont = shade_pssmlt_path(s, sv, b, p, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_NERAD_RHS)
-        cont = shade_nerad<false>(s, sv, b, bounce, path, k, h, io);
+        cont = shade_nerad<false>(s, sv, b, bounce, path, i, h, io);
       else if constexpr (INT == MTX_INT_NERAD)
-        cont = shade_nerad<true>(s, sv, b, bounce, path, k, h, io);
+        cont = shade_nerad<true>(s, sv, b, bounce, path, i, h, io);
       else
-        cont = shade_path<INT, CLS>(s, sv, b, p, bounce, path, k, h, io);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io);
     }
     const uint32_t path_c = path;
     path = path_n;
-    k = k_n;
-    if (inext < count) h = b.hit[k];
+    if (inext < count) h = b.hit[inext];
 #if MTX_DIAG_STAMPS
     stp = io.st;
 #endif
@@ -1451,30 +1401,8 @@ void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounc
   else
     hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
 }
-bool shade_split(uint32_t integrator) {
-  return integrator == MTX_INT_PATH_MIS || integrator == MTX_INT_PATH || integrator == MTX_INT_NRC;
-}
-void launch_classify(const DevScene &s, const WaveBuffers &b, uint32_t bounce, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_classify, dim3(grid), dim3(kShadeBlock), 0, st, s, b, bounce);
-}
-template <int CLS>
-static void launch_shade_cls(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce,
-                             int grid, hipStream_t st) {
-  switch (p.integrator) {
-    case MTX_INT_PATH:
-      hipLaunchKernelGGL((k_shade<MTX_INT_PATH, CLS>), dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
-      break;
-    case MTX_INT_NRC:
-      hipLaunchKernelGGL((k_shade<MTX_INT_NRC, CLS>), dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
-      break;
-    default:
-      hipLaunchKernelGGL((k_shade<MTX_INT_PATH_MIS, CLS>), dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
-  }
-}
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
-                  hipStream_t st, int cls) {
-  if (cls == 1) return launch_shade_cls<1>(s, b, p, bounce, grid, st);
-  if (cls == 2) return launch_shade_cls<2>(s, b, p, bounce, grid, st);
+                  hipStream_t st) {
   switch (p.integrator) {
     case MTX_INT_PATH:
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
@@ -1524,13 +1452,6 @@ int shade_stamps(unsigned long long *out) {
   (void)out;
   return -1;
 #endif
-}
-int shade_light_blocks_per_cu() {
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_shade<MTX_INT_PATH_MIS, 1>, kShadeBlock, 0) != hipSuccess ||
-      nb <= 0)
-    nb = 2;
-  return nb;
 }
 int shade_blocks_per_cu() {
   int nb = 0;

@@ -65,7 +65,6 @@ struct DevScene {
   const float *vuv;
   const mtx_shape *shapes;
   const float4 *shade_rec;  // 8 float4 per triangle (device_common.h compute_si_dev)
-  const uint8_t *tri_cls;   // shading class per triangle: 0 light (diffuse material), 1 heavy
   const mtx_material *materials;
   const mtx_emitter *emitters;
   const mtx_texture *textures;
@@ -78,9 +77,7 @@ struct DevScene {
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
   uint2 *stack_ovf;        // persistent kernels: entries beyond lds_entries, [entry][thread]
   uint32_t ovf_threads;    // threads of the persistent trace grid
-  uint32_t urefill;        // single-step loop: refill a wave once this many lanes are idle
-  uint32_t refill_lanes;   // while-while loop (any-hit): the same
-  uint32_t speculate;      // while-while loop: postpone one triangle group per lane (not in STATS kernels)
+  uint32_t urefill;        // persistent kernels: refill a wave once this many lanes are idle
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
 };
@@ -120,8 +117,7 @@ struct WaveBuffers {
   float4 *hit;
   uint32_t *queue[2];
   ShadowRec *shadow;
-  uint32_t *counters;   // per bounce b: [4b+0] rays of bounce b, [4b+1] shadow rays of bounce b-1 (one 8-B pair with the queue shade b-1 fills), [4b+2], [4b+3] queue positions of bounce b's light / heavy hits (k_classify)
-  uint32_t *clsq[2];    // queue positions of the bounce's hits by shading class (light: diffuse or miss; heavy: the rest)
+  uint32_t *counters;   // per bounce b: [4b+0] rays of bounce b, [4b+1] shadow rays of bounce b-1 (one 8-B pair with the queue shade b-1 fills), [4b+2], [4b+3] unused
   uint32_t *xheads;     // per bounce b: slot 2b closest-hit, 2b+1 shadow claim cursors (kXSlotWords each)
   unsigned long long *stats;  // nodes_c, tris_c, nodes_s, tris_s, rays_c, rays_s
   uint32_t capacity;
@@ -201,10 +197,7 @@ void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t boun
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st);
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
-                  hipStream_t st, int cls = 0);
-bool shade_split(uint32_t integrator);  // integrators whose shade runs per shading class
-int shade_light_blocks_per_cu();
-void launch_classify(const DevScene &s, const WaveBuffers &b, uint32_t bounce, int grid, hipStream_t st);
+                  hipStream_t st);
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
                         uint32_t nslots, hipStream_t st);
