@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MTX_ABI_VERSION 5
+#define MTX_ABI_VERSION 6
 
 enum {
   MTX_OK = 0,
@@ -108,13 +108,40 @@ typedef struct mtx_camera {
   uint32_t pad;
 } mtx_camera;
 
-/* BVH node (80 B, a compressed 8-wide node after Ylitie, Karras & Laine
- * 2017): up to 8 children with 8-bit quantised boxes, collapsed from a
- * binned-SAH BVH2 by dynamic programming over the 8-wide tree's SAH
- * (bvh_build.cpp). The children of a node sit in slots chosen so that
- * visiting slot s at position s ^ octant(ray) (octant bit a set when the
- * direction's component a is negative) is approximately front to back: no
- * per-visit sort. Breadth-first; a node's inner children are consecutive
+/* A scene carries two BVHs over the same triangles (round 4: each is the
+ * faster form for its query):
+ *
+ * Closest-hit BVH node (64 B, Scene.ray_intersect): up to 4 children with
+ * 8-bit quantised boxes, collapsed from a binned-SAH BVH2 by dynamic
+ * programming over the 4-wide tree's SAH (bvh_build.cpp); visited near child
+ * first (the traversal sorts the four entry distances). Breadth-first, the
+ * inner children of a node consecutive and first in slot order, then its
+ * leaves, whose triangle ranges are consecutive. Words:
+ *   f[0..2] = origin.xyz (fp32);  w[3] = bytes [ex, ey, ez, n_children],
+ *             e* int8 in [-32, 31]: axis scale 2^e
+ *   i[4..7] = child refs: >= 0 inner node index,
+ *             < 0 leaf: ~c = (first_tri << 3) | (count - 1)
+ *   w[8..13] = q_lo.x, q_hi.x, q_lo.y, q_hi.y, q_lo.z, q_hi.z: one byte per
+ *             child (child k in bits 8k..8k+7); bound = origin + q * 2^e in
+ *             fp32, conservative (contains the child's padded box)
+ *   w[14], w[15] = 0
+ * Its leaf order is THE triangle order of the scene (tri_geom, tri_vidx,
+ * tri_shape, hit records' prim). Triangles are 12 floats (48 B):
+ *   v0.xyz, 0, e1 = v1-v0 .xyz, 0, e2 = v2-v0 .xyz, 0 */
+#define MTX_BVH_WIDTH 4
+#define MTX_BVH_MAX_LEAF 8
+#define MTX_BVH_NODE_WORDS 16
+#define MTX_BVH_MAX_DEPTH 40
+
+/* Occlusion BVH node (80 B, Scene.ray_test: any hit; a compressed 8-wide
+ * node after Ylitie, Karras & Laine 2017), built over the closest-hit
+ * tree's triangle records (mtx_bvh_build_occlusion) with its own leaf order
+ * and its own copy of the records (occ_tri_geom): up to 8 children with
+ * 8-bit quantised boxes, collapsed from a binned-SAH BVH2 by dynamic
+ * programming over the 8-wide tree's SAH. The children sit in slots chosen
+ * so that visiting slot s at position s ^ octant(ray) (octant bit a set when
+ * the direction's component a is negative) is approximately front to back:
+ * no per-visit sort. Breadth-first; a node's inner children are consecutive
  * from child_base in slot order, its leaves' triangles consecutive from
  * tri_base in slot order. Words:
  *   f[0..2]  origin.xyz (fp32)
@@ -122,7 +149,7 @@ typedef struct mtx_camera {
  *            (axis scale 2^e); imask bit s set: slot s holds an inner node
  *   w[4]     child_base: node index of the first inner child; the inner
  *            child in slot s is child_base + popcount(imask & ((1 << s) - 1))
- *   w[5]     tri_base: first triangle (leaf order) of the node's leaves
+ *   w[5]     tri_base: first triangle (occlusion leaf order) of the leaves
  *   w[6..7]  meta, one byte per slot (slot s in byte s of the 8):
  *              0 = empty; inner: 0x20 | (24 + s);
  *              leaf of n = 1..3 triangles: ((1 << n) - 1) << 5 | offset,
@@ -130,18 +157,15 @@ typedef struct mtx_camera {
  *   w[8..19] q_lo.x, q_hi.x, q_lo.y, q_hi.y, q_lo.z, q_hi.z: 8 bytes each
  *            (two words, slot s in byte s); bound = origin + q * 2^e in
  *            fp32, conservative (contains the child's padded box); empty
- *            slots hold q_lo 255, q_hi 0
- * Triangles are stored in leaf order as 12 floats (48 B):
- *   v0.xyz, 0, e1 = v1-v0 .xyz, 0, e2 = v2-v0 .xyz, 0 */
-#define MTX_BVH_WIDTH 8
-#define MTX_BVH_MAX_LEAF 3
-#define MTX_BVH_NODE_WORDS 20
-#define MTX_BVH_MAX_DEPTH 40
+ *            slots hold q_lo 255, q_hi 0 */
+#define MTX_OCC_WIDTH 8
+#define MTX_OCC_MAX_LEAF 3
+#define MTX_OCC_NODE_WORDS 20
 
 typedef struct mtx_scene_desc {
   uint32_t n_tris, n_nodes, n_verts, n_shapes;
   uint32_t n_materials, n_emitters, n_textures, flags;
-  const int32_t *nodes;      /* MTX_BVH_NODE_WORDS (20) words per node */
+  const int32_t *nodes;      /* closest-hit BVH: MTX_BVH_NODE_WORDS (16) words per node */
   const float *tri_geom;     /* 12 floats per triangle (leaf order) */
   const uint32_t *tri_vidx;  /* 3 vertex indices per triangle (leaf order) */
   const uint32_t *tri_shape; /* shape index per triangle (leaf order) */
@@ -158,6 +182,12 @@ typedef struct mtx_scene_desc {
   uint32_t n_tables;         /* floats */
   uint32_t pad0;
   mtx_camera camera;
+  /* occlusion BVH (MTX_OCC_NODE_WORDS words per node) and its triangle
+   * records (12 floats each, its leaf order): both NULL = mtx_scene_upload
+   * builds them (mtx_bvh_build_occlusion over tri_geom) */
+  const int32_t *occ_nodes;
+  const float *occ_tri_geom;
+  uint32_t n_occ_nodes, pad1;
 } mtx_scene_desc;
 
 /* Integrators (the reference scripts whose sample() loop is replaced). */
@@ -246,13 +276,20 @@ void mtx_ctx_destroy(mtx_ctx *ctx);
 /* --------------------------- scene -------------------------------- */
 /* Host-only BVH build over an indexed triangle mesh (replaces the Embree /
  * OptiX acceleration-structure build behind mi.load_file, upstream): binned-
- * SAH BVH2, collapsed to the 8-wide node above.
+ * SAH BVH2, collapsed to the 4-wide closest-hit node above.
  * nodes_out: capacity (n_tris + 1) * MTX_BVH_NODE_WORDS words; tri_geom_out:
  * 12*n_tris floats; perm_out: n_tris (leaf order -> input triangle index);
- * depth_out: levels of the 8-wide tree (the traversal stack's bound). */
+ * depth_out: levels of the 4-wide tree (the traversal stack's bound). */
 int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t *tri_vidx, uint32_t n_tris,
                   int32_t *nodes_out, uint32_t *n_nodes_out, float *tri_geom_out, uint32_t *perm_out,
                   uint32_t *depth_out);
+/* Host-only occlusion BVH (8-wide node above) over n_tris triangle records
+ * (12 floats each, e.g. mtx_bvh_build's tri_geom_out). nodes_out: capacity
+ * (n_tris + 1) * MTX_OCC_NODE_WORDS words; tri_geom_out: the same records
+ * (bit-identical) in the occlusion tree's leaf order; perm_out (may be NULL):
+ * occlusion leaf order -> input record; depth_out: levels of the tree. */
+int mtx_bvh_build_occlusion(const float *tri_geom, uint32_t n_tris, int32_t *nodes_out, uint32_t *n_nodes_out,
+                            float *tri_geom_out, uint32_t *perm_out, uint32_t *depth_out);
 /* Host-only roughplastic precompute (upstream roughplastic constructor):
  * external transmittance table (64 floats) and internal reflectance. */
 int mtx_roughplastic_tables(uint32_t distribution, float alpha, float eta, float *table_out,

@@ -1,5 +1,6 @@
 // mtx_core/geometry.h — ray/box and ray/triangle tests on the BVH layout of
-// mtx.h (8-wide compressed nodes with 8-bit quantised child boxes). These replace the primitive tests inside Embree's rtcIntersect /
+// mtx.h (4-wide sorted nodes for closest hit, 8-wide compressed nodes for any
+// hit, both with 8-bit quantised child boxes). These replace the primitive tests inside Embree's rtcIntersect /
 // rtcOccluded and OptiX optixTrace behind Scene.ray_intersect / ray_test
 // (path-mis.py:69-71, restirgi.py:320,346). The triangle test is the
 // Moeller-Trumbore form of upstream Mesh::ray_intersect_triangle. Closest-hit
@@ -58,7 +59,7 @@ MTX_HD bool tri_intersect(const TraceRay &r, V3 p0, V3 e1, V3 e2, float tfar, fl
   return hit;
 }
 
-// ---- 8-wide compressed nodes (layout in mtx.h) ---------------------------
+// ---- quantised node frames (both node forms) ------------------------------
 // Child box bound = origin + q * 2^e, evaluated in fp32 exactly like this on
 // the host (builder) and the device, so the builder's conservative choice of
 // q holds for the traversal.
@@ -77,6 +78,101 @@ MTX_HD float wide_ldexp(float x, int e) {
 #endif
 }
 
+// ---- 4-wide sorted nodes (closest hit; layout MTX_BVH4 in mtx.h) --------
+// Slab tests of a node's children in the node's quantised frame: with
+// a = 2^e / d and b = (origin - o) / d per axis, a bound q is at
+// t = fma(q, a, b). Children hit within (0, tfar] get the sort key
+// (t bits with the 2 low bits cleared) | slot, misses 0x7f800000 | slot; the
+// four keys are sorted ascending (5 compare-exchanges), so the visit order is
+// by entry distance, near-ties by slot. Returns the number of hits.
+// qlx.. hold the four children's 8-bit bounds, child k in bits [8k, 8k+8).
+// wide_node_order_e takes the axis exponents and child count decoded (the
+// device's 48-B node keeps them in 6-bit fields, mtx_scene_upload).
+// wide_node_keys_e: the four keys in slot order (unsorted), for callers that
+// sort them together with the child references.
+MTX_HD int wide_node_keys_e(const TraceRay &r, float ox, float oy, float oz, int ex, int ey, int ez, int nch,
+                            uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
+                            float tfar, uint32_t key[4]) {
+  const float ax = wide_ldexp(r.idir.x, ex), bx = (ox - r.o.x) * r.idir.x;
+  const float ay = wide_ldexp(r.idir.y, ey), by = (oy - r.o.y) * r.idir.y;
+  const float az = wide_ldexp(r.idir.z, ez), bz = (oz - r.o.z) * r.idir.z;
+  // near / far bound of each axis from the direction's sign: fma(q, a, b)
+  // is monotonic in q, so this equals min / max of the two planes (NaN
+  // planes of a zero direction component are ignored either way)
+  int n = 0;  // children hit (hit keys sort below every miss key)
+  const bool nx_ = r.idir.x < 0.f, ny_ = r.idir.y < 0.f, nz_ = r.idir.z < 0.f;
+  const uint32_t qnx = nx_ ? qhx : qlx, qfx = nx_ ? qlx : qhx;
+  const uint32_t qny = ny_ ? qhy : qly, qfy = ny_ ? qly : qhy;
+  const uint32_t qnz = nz_ ? qhz : qlz, qfz = nz_ ? qlz : qhz;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int sh = 8 * k;
+#ifdef MTX_DEVICE_COMPILE
+    // the same six fmas, issued as three packed v_pk_fma_f32
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v tx = __builtin_elementwise_fma(f2v{(float)((qnx >> sh) & 255u), (float)((qfx >> sh) & 255u)},
+                                             f2v{ax, ax}, f2v{bx, bx});
+    const f2v ty = __builtin_elementwise_fma(f2v{(float)((qny >> sh) & 255u), (float)((qfy >> sh) & 255u)},
+                                             f2v{ay, ay}, f2v{by, by});
+    const f2v tz = __builtin_elementwise_fma(f2v{(float)((qnz >> sh) & 255u), (float)((qfz >> sh) & 255u)},
+                                             f2v{az, az}, f2v{bz, bz});
+    const float nx = tx.x, fx = tx.y, ny = ty.x, fy = ty.y, nz = tz.x, fz = tz.y;
+#else
+    const float nx = fmaf((float)((qnx >> sh) & 255u), ax, bx), fx = fmaf((float)((qfx >> sh) & 255u), ax, bx);
+    const float ny = fmaf((float)((qny >> sh) & 255u), ay, by), fy = fmaf((float)((qfy >> sh) & 255u), ay, by);
+    const float nz = fmaf((float)((qnz >> sh) & 255u), az, bz), fz = fmaf((float)((qfz >> sh) & 255u), az, bz);
+#endif
+    const float tmin = fmaxf(fmaxf(fmaxf(nx, ny), nz), 0.f);
+    const float tmax = fminf(fminf(fminf(fx, fy), fz), tfar);
+    const bool hit = k < nch && tmin <= tmax;
+    key[k] = hit ? ((f2u(tmin) & 0x7ffffffcu) | (uint32_t)k) : (0x7f800000u | (uint32_t)k);
+    n += hit ? 1 : 0;
+  }
+  return n;
+}
+
+MTX_HD int wide_node_order_e(const TraceRay &r, float ox, float oy, float oz, int ex, int ey, int ez, int nch,
+                             uint32_t qlx, uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz,
+                             float tfar, uint32_t key[4]) {
+  const int n = wide_node_keys_e(r, ox, oy, oz, ex, ey, ez, nch, qlx, qhx, qly, qhy, qlz, qhz, tfar, key);
+#define MTX_CAS(i, j)                                   \
+  {                                                     \
+    const uint32_t lo_ = key[i] < key[j] ? key[i] : key[j]; \
+    const uint32_t hi_ = key[i] < key[j] ? key[j] : key[i]; \
+    key[i] = lo_;                                       \
+    key[j] = hi_;                                       \
+  }
+  MTX_CAS(0, 1) MTX_CAS(2, 3) MTX_CAS(0, 2) MTX_CAS(1, 3) MTX_CAS(1, 2)
+#undef MTX_CAS
+  return n;
+}
+
+// The 64-B node form (mtx.h): int8 exponents in eb's bytes 0..2, the child
+// count in byte 3.
+MTX_HD int wide_node_order(const TraceRay &r, float ox, float oy, float oz, uint32_t eb, uint32_t qlx,
+                           uint32_t qhx, uint32_t qly, uint32_t qhy, uint32_t qlz, uint32_t qhz, float tfar,
+                           uint32_t key[4]) {
+  return wide_node_order_e(r, ox, oy, oz, (int)(int8_t)(uint8_t)(eb & 0xffu), (int)(int8_t)(uint8_t)((eb >> 8) & 0xffu),
+                           (int)(int8_t)(uint8_t)((eb >> 16) & 0xffu), (int)(eb >> 24), qlx, qhx, qly, qhy, qlz, qhz,
+                           tfar, key);
+}
+
+// Child reference of the slot encoded in a sort key.
+MTX_HD int32_t wide_ref(uint32_t key, int32_t r0, int32_t r1, int32_t r2, int32_t r3) {
+  // two bit selects (no branches on the device)
+  const bool b0 = (key & 1u) != 0u, b1 = (key & 2u) != 0u;
+  const int32_t lo = b0 ? r1 : r0, hi = b0 ? r3 : r2;
+  return b1 ? hi : lo;
+}
+
+MTX_HD void leaf_decode(int32_t c, uint32_t *first, uint32_t *count) {
+  uint32_t x = (uint32_t)(~c);
+  *first = x >> 3;
+  *count = (x & 7u) + 1u;
+}
+
+
+// ---- 8-wide compressed nodes (any hit; layout MTX_BVH8 in mtx.h) --------
 // Octant of a ray: bit a set when the direction's component a is negative
 // (the sign of the clamped reciprocal: -0 counts as negative). A node's slot s
 // is visited at position s ^ octant.

@@ -14,8 +14,10 @@ namespace mtx {
 
 // Pointers to the scene arrays (HBM on the device, host memory in the oracle).
 struct SceneView {
-  const int32_t *nodes;
-  const float *tri_geom;
+  const int32_t *nodes;         // closest-hit BVH (mtx.h, 16 words per node)
+  const float *tri_geom;        // its leaf-order triangle records (the scene's triangle order)
+  const int32_t *occ_nodes;     // occlusion BVH (mtx.h, 20 words per node)
+  const float *occ_tri_geom;    // its own leaf-order copy of the records
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;
   const float *vpos;

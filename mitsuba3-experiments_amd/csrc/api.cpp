@@ -130,7 +130,7 @@ struct mtx_ctx {
   bool has_nerad = false;
   uint32_t scene_n_shapes = 0;
   DevBuf nr_lhs, nr_qp, nr_qd, nr_Lrhs, nr_lanes;
-  DevBuf nodes, tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
+  DevBuf nodes, tri, occ_nodes, occ_tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
@@ -152,7 +152,9 @@ struct mtx_ctx {
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
-  uint32_t lds_top = MTX_LDS_TOP;  // wide nodes of the tree top kept in LDS per block (MTX_LDS_TOP env: A/B)
+  uint32_t lds_top = MTX_LDS_TOP;          // closest-hit tree nodes kept in LDS per block (MTX_LDS_TOP env: A/B)
+  uint32_t occ_lds_top = MTX_OCC_LDS_TOP;  // occlusion tree nodes kept in LDS per block (MTX_OCC_LDS_TOP)
+  uint32_t occ_lds_stack = mtxd::kOccLdsStack;
   uint32_t trace_batch = 128;  // queue entries per claim (256: +0.6 % closest, +1 % at spp 32; 64: +5 %)
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
   uint32_t xcd_claim = 1;
@@ -208,6 +210,9 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
+  if (const char *e = getenv("MTX_OCC_LDS_TOP")) c->occ_lds_top = (uint32_t)std::max(0, std::min(192, atoi(e)));
+  if (const char *e = getenv("MTX_OCC_LDS_STACK"))
+    c->occ_lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS_MAX_LOG2")) c->streams_max_log2 = (uint32_t)std::max(16, std::min(31, atoi(e)));
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
@@ -223,7 +228,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->w2.stream) hipStreamSynchronize(c->w2.stream);
-  DevBuf *bufs[] = {&c->nodes,  &c->tri,     &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
+  DevBuf *bufs[] = {&c->nodes,  &c->tri, &c->occ_nodes, &c->occ_tri, &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters, &c->xheads, &c->rs_heads,  &c->stats,    &c->contrib, &c->film,
@@ -264,12 +269,34 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     mtx_set_error("mtx_scene_upload: incomplete scene (need geometry, BVH, shapes, materials, >=1 emitter)");
     return MTX_E_ARG;
   }
-  // Validate the 8-wide nodes (mtx.h) on the host so that no kernel can
-  // read out of bounds, and find the tree depth (the traversal stack holds
-  // at most one node group per level); also rejects cycles.
-  uint32_t bvh_depth = 0;
+  // The occlusion BVH: given, or built here over the triangle records.
+  const bool occ_given = d->occ_nodes && d->occ_tri_geom && d->n_occ_nodes > 0;
+  if (!occ_given && (d->occ_nodes || d->occ_tri_geom)) {
+    mtx_set_error("mtx_scene_upload: occ_nodes and occ_tri_geom go together (both NULL: built here)");
+    return MTX_E_ARG;
+  }
+  std::vector<int32_t> occ_nodes_v;
+  std::vector<float> occ_geom_v;
+  const int32_t *occ_nodes = d->occ_nodes;
+  const float *occ_geom = d->occ_tri_geom;
+  uint32_t n_occ = d->n_occ_nodes;
+  int rc = 0;
+  if (!occ_given) {
+    occ_nodes_v.resize(((size_t)d->n_tris + 1) * MTX_OCC_NODE_WORDS);
+    occ_geom_v.resize(12 * (size_t)d->n_tris);
+    if ((rc = mtx_bvh_build_occlusion(d->tri_geom, d->n_tris, occ_nodes_v.data(), &n_occ, occ_geom_v.data(), nullptr,
+                                      nullptr)))
+      return rc;
+    occ_nodes = occ_nodes_v.data();
+    occ_geom = occ_geom_v.data();
+  }
+  // Validate both trees (mtx.h) on the host so that no kernel can read out
+  // of bounds, and find their depths (stack entries: a 4-wide level pushes
+  // at most 3 node references, an 8-wide level one node group); also
+  // rejects cycles.
+  uint32_t bvh_depth = 0, occ_depth = 0;
   {
-    std::vector<std::pair<uint32_t, uint32_t>> todo{{0u, 0u}};
+    std::vector<std::pair<int32_t, uint32_t>> todo{{0, 0u}};
     uint64_t visited = 0;
     while (!todo.empty()) {
       auto [nd, dep] = todo.back();
@@ -279,23 +306,58 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
         mtx_set_error("mtx_scene_upload: BVH is not a tree of depth <= %d", MTX_BVH_MAX_DEPTH);
         return MTX_E_ARG;
       }
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(d->nodes) + MTX_BVH_NODE_WORDS * (size_t)nd;
+      const int32_t *w = d->nodes + MTX_BVH_NODE_WORDS * (size_t)nd;
+      const uint32_t nch = (uint32_t)w[3] >> 24;
+      if (nch < 1 || nch > MTX_BVH_WIDTH) {
+        mtx_set_error("mtx_scene_upload: node %d has %u children", nd, nch);
+        return MTX_E_ARG;
+      }
+      for (uint32_t k = 0; k < nch; ++k) {
+        const int32_t ch = w[4 + k];
+        if (ch >= 0) {
+          if ((uint32_t)ch >= d->n_nodes) {
+            mtx_set_error("mtx_scene_upload: node %d child %d out of range", nd, ch);
+            return MTX_E_ARG;
+          }
+          todo.push_back({ch, dep + 1});
+        } else {
+          uint32_t x = (uint32_t)(~ch), first = x >> 3, cnt = (x & 7u) + 1;
+          if ((uint64_t)first + cnt > d->n_tris) {
+            mtx_set_error("mtx_scene_upload: leaf [%u,+%u) exceeds %u triangles", first, cnt, d->n_tris);
+            return MTX_E_ARG;
+          }
+        }
+      }
+    }
+  }
+  {
+    std::vector<std::pair<uint32_t, uint32_t>> todo{{0u, 0u}};
+    uint64_t visited = 0;
+    while (!todo.empty()) {
+      auto [nd, dep] = todo.back();
+      todo.pop_back();
+      occ_depth = std::max(occ_depth, dep + 1);
+      if (++visited > n_occ || dep >= MTX_BVH_MAX_DEPTH) {
+        mtx_set_error("mtx_scene_upload: occlusion BVH is not a tree of depth <= %d", MTX_BVH_MAX_DEPTH);
+        return MTX_E_ARG;
+      }
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(occ_nodes) + MTX_OCC_NODE_WORDS * (size_t)nd;
       const uint32_t imask = w[3] >> 24, child_base = w[4], tri_base = w[5];
       uint32_t inner = 0;
-      for (uint32_t sl = 0; sl < MTX_BVH_WIDTH; ++sl) {
+      for (uint32_t sl = 0; sl < MTX_OCC_WIDTH; ++sl) {
         const uint32_t m = (w[6 + (sl >> 2)] >> (8 * (sl & 3))) & 0xffu;
         const bool is_inner = (imask >> sl) & 1u;
         if (is_inner) {
           const uint32_t ch = child_base + inner++;
-          if (m != (0x20u | (24u + sl)) || ch >= d->n_nodes) {
-            mtx_set_error("mtx_scene_upload: node %u slot %u: bad inner child", nd, sl);
+          if (m != (0x20u | (24u + sl)) || ch >= n_occ) {
+            mtx_set_error("mtx_scene_upload: occlusion node %u slot %u: bad inner child", nd, sl);
             return MTX_E_ARG;
           }
           todo.push_back({ch, dep + 1});
         } else if (m != 0) {
           const uint32_t cb = m >> 5, off = m & 31u, cnt = cb == 1 ? 1u : cb == 3 ? 2u : cb == 7 ? 3u : 0u;
           if (cnt == 0 || off + cnt > 24 || (uint64_t)tri_base + off + cnt > d->n_tris) {
-            mtx_set_error("mtx_scene_upload: node %u slot %u: bad leaf", nd, sl);
+            mtx_set_error("mtx_scene_upload: occlusion node %u slot %u: bad leaf", nd, sl);
             return MTX_E_ARG;
           }
         }
@@ -338,17 +400,18 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     }
   }
   HIP_TRY(hipSetDevice(c->device));
-  int rc = 0;
   hipStream_t st = c->stream;
   if ((rc = upload(c->nodes, d->nodes, (size_t)MTX_BVH_NODE_WORDS * d->n_nodes, st))) return rc;
-  {
+  if ((rc = upload(c->occ_nodes, occ_nodes, (size_t)MTX_OCC_NODE_WORDS * n_occ, st))) return rc;
+  for (int tree = 0; tree < 2; ++tree) {
     // device triangles packed to 36 B (the ABI's 48-B records carry 3 pad
     // words): 3.6 instead of 2.7 triangles per 128-B line, same load count
+    const float *src = tree ? occ_geom : d->tri_geom;
     std::vector<float> g9(9ull * d->n_tris);
     for (size_t i = 0; i < d->n_tris; ++i)
       for (int k = 0; k < 3; ++k)
-        for (int j = 0; j < 3; ++j) g9[9 * i + 3 * k + j] = d->tri_geom[12 * i + 4 * k + j];
-    if ((rc = upload(c->tri, g9.data(), g9.size(), st))) return rc;
+        for (int j = 0; j < 3; ++j) g9[9 * i + 3 * k + j] = src[12 * i + 4 * k + j];
+    if ((rc = upload(tree ? c->occ_tri : c->tri, g9.data(), g9.size(), st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));  // g9 is freed at scope exit
   }
   if ((rc = upload(c->tri_vidx, d->tri_vidx, 3ull * d->n_tris, st))) return rc;
@@ -399,6 +462,8 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   mtxd::DevScene &s = c->scene;
   s.nodes = (const int4 *)c->nodes.p;
   s.tri = (const float *)c->tri.p;
+  s.occ_nodes = (const int4 *)c->occ_nodes.p;
+  s.occ_tri = (const float *)c->occ_tri.p;
   s.tri_vidx = (const uint32_t *)c->tri_vidx.p;
   s.tri_shape = (const uint32_t *)c->tri_shape.p;
   s.vpos = (const float *)c->vpos.p;
@@ -413,22 +478,23 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.tables = (const float *)c->tables.p;
   s.n_tris = d->n_tris;
   s.n_emitters = d->n_emitters;
-  s.stack_entries = bvh_depth + 1;
   s.camera = d->camera;
+  // LDS per trace block (8 blocks of 256 threads per CU fill the 160 KB):
+  // closest hit 16 x 4-B stack entries per lane + 64 nodes of 64 B,
+  // occlusion 8 x 8-B entries + 48 nodes of 80 B
+  s.stack_entries = 3 * bvh_depth + 1;
   s.lds_entries = std::min<uint32_t>(s.stack_entries, c->lds_stack);
-  // LDS copy of the tree top: with 8 stack entries (8 B) per lane and 8
-  // blocks of 256 threads per CU, 48 nodes (80 B) fill the 160 KB
   s.lds_top = std::min<uint32_t>(d->n_nodes, c->lds_top);
+  s.occ_stack_entries = occ_depth + 1;
+  s.occ_lds_entries = std::min<uint32_t>(s.occ_stack_entries, c->occ_lds_stack);
+  s.occ_lds_top = std::min<uint32_t>(n_occ, c->occ_lds_top);
   s.trace_batch = c->trace_batch;
   s.urefill = c->urefill;
   s.xcd_claim = c->xcd_claim;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
-  {
-    const size_t deep = s.stack_entries - s.lds_entries;
-    if ((rc = dalloc(c->stack_ovf, std::max<size_t>(8, deep * s.ovf_threads * sizeof(uint2))))) return rc;
-    s.stack_ovf = (uint2 *)c->stack_ovf.p;
-  }
+  if ((rc = dalloc(c->stack_ovf, mtxd::stack_ovf_bytes(s)))) return rc;
+  s.stack_ovf = c->stack_ovf.p;
   c->has_scene = true;
   return MTX_OK;
 }
@@ -546,8 +612,7 @@ int ensure_wavefront2(mtx_ctx *c, uint32_t cap, uint32_t max_depth) {
   if ((rc = dalloc(w.counters, 16ull * (max_depth + 2)))) return rc;
   if ((rc = dalloc(w.xheads, 8ull * mtxd::kXSlotWords * (max_depth + 2)))) return rc;
   const mtxd::DevScene &s = c->scene;
-  const size_t deep = s.stack_entries - s.lds_entries;
-  if ((rc = dalloc(w.stack_ovf, std::max<size_t>(8, deep * s.ovf_threads * sizeof(uint2))))) return rc;
+  if ((rc = dalloc(w.stack_ovf, mtxd::stack_ovf_bytes(s)))) return rc;
   return MTX_OK;
 }
 
@@ -971,7 +1036,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     if (two) {
       if ((rc = ensure_wavefront2(c, (a->y1 - ym) * W * spp, depth))) return rc;
       bw2 = buffers2(c);
-      s2.stack_ovf = (uint2 *)c->w2.stack_ovf.p;
+      s2.stack_ovf = c->w2.stack_ovf.p;
       HIP_TRY(hipEventRecord(c->w2.start, st));  // after the frame-0 clears
       HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
     }
@@ -1133,7 +1198,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     // the second stream starts after everything queued on the first
     b2 = buffers2(c);
     s2 = c->scene;
-    s2.stack_ovf = (uint2 *)c->w2.stack_ovf.p;
+    s2.stack_ovf = c->w2.stack_ovf.p;
     HIP_TRY(hipEventRecord(c->w2.start, c->stream));
     HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
   }

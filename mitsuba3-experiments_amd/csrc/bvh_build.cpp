@@ -1,18 +1,23 @@
 // bvh_build.cpp — host-side scene preprocessing for libmtx.
 //
-// * Binned-SAH BVH2 over an indexed triangle mesh (leaves of <= 3
-//   triangles), collapsed by SAH-optimal dynamic programming into 8-wide
-//   compressed nodes (80 B, layout in mtx.h: 8-bit quantised child boxes,
-//   children in octant-ordered slots, Ylitie, Karras & Laine 2017) with the
-//   triangles reordered into leaf order as {v0, e1, e2} records. Replaces
-//   the Embree / OptiX acceleration-structure build that mi.load_file
-//   performs upstream for Scene.ray_intersect (path-mis.py:69-71).
+// * The two BVHs of a scene (mtx.h), each a binned-SAH BVH2 collapsed by
+//   SAH-optimal dynamic programming (Ylitie, Karras & Laine 2017):
+//   - closest hit (mtx_bvh_build): BVH2 leaves of <= 8 triangles, 4-wide
+//     nodes (64 B, 8-bit quantised child boxes, sorted near-first by the
+//     traversal), laid out breadth-first with the triangles reordered into
+//     leaf order as {v0, e1, e2} records;
+//   - occlusion / any hit (mtx_bvh_build_occlusion): BVH2 leaves of <= 3
+//     triangles, compressed 8-wide nodes (80 B, children in octant-ordered
+//     slots, no per-visit sort) over the closest-hit tree's records.
+//   Replaces the Embree / OptiX acceleration-structure build that
+//   mi.load_file performs upstream for Scene.ray_intersect / ray_test
+//   (path-mis.py:69-71, restirgi.py:320,346).
 // * roughplastic precompute (upstream roughplastic constructor): the
 //   64-entry external transmittance table and the internal reflectance.
 //
 // BVH2 depth is capped at MTX_BVH_MAX_DEPTH inner levels (object-median
-// splits take over when the SAH would exceed it); the 8-wide tree is never
-// deeper, which bounds the device traversal's stack.
+// splits take over when the SAH would exceed it); the wide trees are never
+// deeper, which bounds the device traversal's stacks.
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -69,6 +74,7 @@ struct Builder {
   std::vector<uint32_t> order; // leaf order -> input tri
   float ct = kDefaultCt;
   int n_bins = 32;
+  uint32_t max_leaf2 = MTX_BVH_MAX_LEAF;  // BVH2 leaf size cap (the occlusion tree: MTX_OCC_MAX_LEAF)
   uint32_t max_depth_seen = 0;
 
   static int ceil_log2(uint32_t c) {
@@ -153,7 +159,7 @@ struct Builder {
           }
         }
       }
-      if (cnt <= MTX_BVH_MAX_LEAF && (best_axis < 0 || (float)cnt <= best_cost)) return 0;
+      if (cnt <= max_leaf2 && (best_axis < 0 || (float)cnt <= best_cost)) return 0;
       if (best_axis >= 0) {
         const float ext = cb.hi[best_axis] - cb.lo[best_axis];
         const float k = (float)nb / ext;
@@ -166,7 +172,7 @@ struct Builder {
         if (m > s && m < e) return m;
       }
     }
-    if (cnt <= MTX_BVH_MAX_LEAF) return 0;
+    if (cnt <= max_leaf2) return 0;
     // object median along the largest centroid extent (stable for ties)
     uint32_t m = s + cnt / 2;
     std::nth_element(idx.data() + s, idx.data() + m, idx.data() + e, [&](uint32_t x, uint32_t y) {
@@ -215,17 +221,20 @@ struct Builder {
     return (int32_t)node;
   }
 
-  // ---- collapse to 8-wide compressed nodes (layout in mtx.h) -------------
-  // SAH-optimal collapse (dynamic programming over the BVH2, Ylitie et al.
-  // 2017): cost[n][j] = least SAH cost of representing BVH2 subtree n as at
-  // most j children of a wide node (j = 1..8); a child is either a wide inner
-  // node (area * c_node + the best 8-way split of its subtree) or a leaf
-  // holding the whole subtree when it has <= MTX_BVH_MAX_LEAF triangles
-  // (area * c_tri * count; BVH2 subtrees are contiguous in leaf order).
-  static constexpr int kW = MTX_BVH_WIDTH;
-  float c_node = 1.0f, c_tri = 1.0f;
-  std::vector<float> dp_cost;      // (kW + 1) per BVH2 node (index j = 1..kW)
-  std::vector<uint8_t> dp_split;   // (kW + 1) per node: 0 = use j-1 slots, k = k slots left
+
+  // ---- SAH-optimal collapse (dynamic programming over the BVH2) ----------
+  // cost[n][j] = least SAH cost of representing BVH2 subtree n as at most j
+  // children of a wide node (j = 1..kw); a child is either a wide inner node
+  // (area * c_node + the best kw-way split of its subtree) or a leaf holding
+  // the whole subtree when it has <= max_leaf_w triangles (area * c_tri *
+  // count; BVH2 subtrees are contiguous in leaf order). Replaces the greedy
+  // largest-area opening (Ylitie et al. 2017, wide-BVH collapse).
+  static constexpr int kMaxW = 8;
+  int kw = MTX_BVH_WIDTH;                 // 4 (closest hit) or 8 (occlusion)
+  uint32_t max_leaf_w = MTX_BVH_MAX_LEAF;  // leaf size cap of the wide tree
+  float c_node = 1.0f, c_tri = 1.0f;      // tuned on the bedroom proxy (A/B: +1.8 % vs greedy, 4-wide)
+  std::vector<float> dp_cost;      // (kw + 1) per BVH2 node (index j = 1..kw)
+  std::vector<uint8_t> dp_split;   // (kw + 1) per node: 0 = use j-1 slots, k = k slots left
   std::vector<uint8_t> dp_leaf;    // 1: the subtree as one leaf (j = 1)
   std::vector<uint32_t> sub_first, sub_count;
   std::vector<Box> box2;           // padded box of each BVH2 node
@@ -243,21 +252,21 @@ struct Builder {
 
   void ref_info(int32_t ref, float area, float *cost, uint32_t *first, uint32_t *count) const {
     if (ref >= 0) {
-      for (int j = 1; j <= kW; ++j) cost[j] = dp_cost[(kW + 1) * (size_t)ref + j];
+      for (int j = 1; j <= kw; ++j) cost[j] = dp_cost[(kw + 1) * (size_t)ref + j];
       *first = sub_first[ref];
       *count = sub_count[ref];
     } else {
       const uint32_t code = ~(uint32_t)ref;
       *first = code >> 3;
       *count = (code & 7u) + 1u;
-      for (int j = 1; j <= kW; ++j) cost[j] = area * c_tri * (float)*count;
+      for (int j = 1; j <= kw; ++j) cost[j] = area * c_tri * (float)*count;
     }
   }
 
   void dp_prepare() {
     const size_t n2 = nodes.size() / 16;
-    dp_cost.assign((kW + 1) * n2, 0.f);
-    dp_split.assign((kW + 1) * n2, 0);
+    dp_cost.assign((kw + 1) * n2, 0.f);
+    dp_split.assign((kw + 1) * n2, 0);
     dp_leaf.assign(n2, 0);
     sub_first.assign(n2, 0);
     sub_count.assign(n2, 0);
@@ -271,15 +280,15 @@ struct Builder {
         if (r >= 0) box2[r] = child_box2((uint32_t)n, c);
       }
     for (size_t n = n2; n-- > 0;) {
-      float cl[kW + 1], cr[kW + 1];
+      float cl[kMaxW + 1], cr[kMaxW + 1];
       uint32_t fl, nl, fr, nr;
       ref_info(nodes[16 * n + 12], child_box2((uint32_t)n, 0).area(), cl, &fl, &nl);
       ref_info(nodes[16 * n + 13], child_box2((uint32_t)n, 1).area(), cr, &fr, &nr);
       sub_first[n] = std::min(fl, fr);
       sub_count[n] = nl + nr;
-      float dist[kW + 1];
-      uint8_t kbest[kW + 1] = {0};
-      for (int j = 2; j <= kW; ++j) {
+      float dist[kMaxW + 1];
+      uint8_t kbest[kMaxW + 1] = {0};
+      for (int j = 2; j <= kw; ++j) {
         dist[j] = INFINITY;
         for (int k = 1; k < j; ++k) {
           const float c = cl[k] + cr[j - k];
@@ -290,18 +299,18 @@ struct Builder {
         }
       }
       const float area = box2[n].area();
-      const float c_inner = area * c_node + dist[kW];
-      const float c_lf = sub_count[n] <= MTX_BVH_MAX_LEAF ? area * c_tri * (float)sub_count[n] : INFINITY;
-      float *Cn = &dp_cost[(kW + 1) * n];
+      const float c_inner = area * c_node + dist[kw];
+      const float c_lf = sub_count[n] <= max_leaf_w ? area * c_tri * (float)sub_count[n] : INFINITY;
+      float *Cn = &dp_cost[(kw + 1) * n];
       dp_leaf[n] = c_lf <= c_inner ? 1 : 0;
       Cn[1] = std::min(c_lf, c_inner);
-      for (int j = 2; j <= kW; ++j) {
+      for (int j = 2; j <= kw; ++j) {
         if (dist[j] < Cn[j - 1]) {
           Cn[j] = dist[j];
-          dp_split[(kW + 1) * n + j] = kbest[j];
+          dp_split[(kw + 1) * n + j] = kbest[j];
         } else {
           Cn[j] = Cn[j - 1];
-          dp_split[(kW + 1) * n + j] = 0;
+          dp_split[(kw + 1) * n + j] = 0;
         }
       }
     }
@@ -318,10 +327,10 @@ struct Builder {
       out.push_back({ref, box});
       return;
     }
-    int k = dp_split[(kW + 1) * (size_t)ref + j];
+    int k = dp_split[(kw + 1) * (size_t)ref + j];
     while (k == 0 && j > 1) {
       --j;
-      k = j > 1 ? dp_split[(kW + 1) * (size_t)ref + j] : 0;
+      k = j > 1 ? dp_split[(kw + 1) * (size_t)ref + j] : 0;
     }
     if (j == 1) {
       out.push_back({ref, box});
@@ -331,27 +340,167 @@ struct Builder {
     dp_expand(nodes[16 * (size_t)ref + 13], j - k, child_box2((uint32_t)ref, 1), out);
   }
 
+  // the wide children of BVH2 node n2 (a subtree that prefers one slot is
+  // still split at its root)
+  std::vector<Child> wide_children(uint32_t n2) const {
+    std::vector<Child> ch;
+    dp_expand((int32_t)n2, kw, box2[n2], ch);
+    if (ch.size() == 1) {
+      ch.clear();
+      dp_expand(nodes[16 * (size_t)n2 + 12], 1, child_box2(n2, 0), ch);
+      dp_expand(nodes[16 * (size_t)n2 + 13], 1, child_box2(n2, 1), ch);
+    }
+    return ch;
+  }
+
+  bool quant_ok = true;
+  static constexpr int kEMin = -32, kEMax = 31;
+  std::vector<int32_t> wnodes;  // the wide tree (16 or 20 words per node)
+  uint32_t wide_depth = 0;
+
+  // Quantisation of axis a of the children's boxes in the frame of their
+  // union: origin, exponent and the conservative 8-bit bounds of each child.
+  void quantise_axis(const std::vector<Child> &ch, const Box &u, int a, float *org_out, int *e_out,
+                     uint32_t *qlo_out, uint32_t *qhi_out) {
+    const float org = u.lo[a];
+    const double ext = (double)u.hi[a] - (double)org;
+    int e = kEMin;
+    if (ext > 0.0) {
+      int ee;
+      std::frexp(ext / 255.0, &ee);
+      e = std::max(kEMin, std::min(kEMax, ee));
+    }
+    while (e < kEMax && mtx::wide_decode(org, mtx::wide_scale((uint32_t)(e & 255)), 255u) < u.hi[a]) ++e;
+    const float sc = mtx::wide_scale((uint32_t)(e & 255));
+    const double dsc = std::ldexp(1.0, e);
+    for (size_t k = 0; k < ch.size(); ++k) {
+      double flo = std::floor(((double)ch[k].box.lo[a] - (double)org) / dsc);
+      double fhi = std::ceil(((double)ch[k].box.hi[a] - (double)org) / dsc);
+      uint32_t qlo = (uint32_t)std::max(0.0, std::min(255.0, flo));
+      uint32_t qhi = (uint32_t)std::max(0.0, std::min(255.0, fhi));
+      while (qlo > 0 && mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a]) --qlo;
+      while (qhi < 255 && mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a]) ++qhi;
+      if (mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a] || mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a])
+        quant_ok = false;
+      qlo_out[k] = qlo;
+      qhi_out[k] = qhi;
+    }
+    *org_out = org;
+    *e_out = e;
+  }
+
+  // ---- 4-wide closest-hit nodes (mtx.h) ----------------------------------
+  // Depth-first collapse into wnodes, then relayout4 reorders breadth-first.
+  int32_t collapse4(uint32_t node2, uint32_t depth) {
+    const std::vector<Child> ch = wide_children(node2);
+    const uint32_t w = (uint32_t)(wnodes.size() / 16);
+    wnodes.resize(wnodes.size() + 16, 0);
+    wide_depth = std::max(wide_depth, depth + 1);
+    int32_t refs[MTX_BVH_WIDTH] = {0, 0, 0, 0};
+    for (size_t k = 0; k < ch.size(); ++k) {
+      const int32_t r = ch[k].ref;
+      if (r < 0) {
+        refs[k] = r;
+      } else if (dp_leaf[r]) {  // the whole subtree as one leaf
+        refs[k] = ~(int32_t)((sub_first[r] << 3) | (sub_count[r] - 1u));
+      } else {
+        refs[k] = collapse4((uint32_t)r, depth + 1);
+      }
+    }
+    encode4(w, ch, refs);
+    return (int32_t)w;
+  }
+
+  void encode4(uint32_t w, const std::vector<Child> &ch, const int32_t *refs) {
+    Box u;
+    u.reset();
+    for (const Child &c : ch) u.grow(c.box);
+    int32_t *W = &wnodes[16 * (size_t)w];
+    uint32_t q[6] = {0, 0, 0, 0, 0, 0}, ebytes = 0;
+    for (int a = 0; a < 3; ++a) {
+      float org;
+      int e;
+      uint32_t qlo[kMaxW], qhi[kMaxW];
+      quantise_axis(ch, u, a, &org, &e, qlo, qhi);
+      for (size_t k = 0; k < ch.size(); ++k) {
+        q[2 * a] |= qlo[k] << (8 * k);
+        q[2 * a + 1] |= qhi[k] << (8 * k);
+      }
+      std::memcpy(&W[a], &org, 4);
+      ebytes |= (uint32_t)(e & 255) << (8 * a);
+    }
+    W[3] = (int32_t)(ebytes | ((uint32_t)ch.size() << 24));
+    for (int k = 0; k < MTX_BVH_WIDTH; ++k) W[4 + k] = refs[k];
+    for (int k = 0; k < 6; ++k) W[8 + k] = (int32_t)q[k];
+  }
+
+  // Breadth-first layout: the inner children of a node at consecutive
+  // indices (two 64-B siblings per 128-B line), a node's slots ordered inner
+  // children first (each group keeps its order), and the triangles
+  // re-ordered so that a node's leaf children are consecutive ranges in slot
+  // order.
+  void relayout4() {
+    std::vector<int32_t> out(16, 0);
+    std::vector<uint32_t> queue = {0}, tris;
+    tris.reserve(order.size());
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+      const int32_t *W = &wnodes[16 * (size_t)queue[qi]];
+      int slot[MTX_BVH_WIDTH], m = 0;
+      for (int k = 0; k < (int)((uint32_t)W[3] >> 24); ++k)
+        if (W[4 + k] >= 0) slot[m++] = k;
+      for (int k = 0; k < (int)((uint32_t)W[3] >> 24); ++k) {
+        bool dup = false;  // a one-triangle mesh's root holds its leaf twice
+        for (int j = 0; j < k; ++j) dup = dup || W[4 + j] == W[4 + k];
+        if (W[4 + k] < 0 && !dup) slot[m++] = k;
+      }
+      const int nch = m;
+      int32_t O[16] = {W[0], W[1], W[2], (int32_t)(((uint32_t)W[3] & 0xffffffu) | ((uint32_t)nch << 24)),
+                       0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      for (int a = 0; a < 6; ++a) {
+        uint32_t q = 0;
+        for (int j = 0; j < nch; ++j) q |= (((uint32_t)W[8 + a] >> (8 * slot[j])) & 255u) << (8 * j);
+        O[8 + a] = (int32_t)q;
+      }
+      for (int j = 0; j < nch; ++j) {
+        const int32_t r = W[4 + slot[j]];
+        if (r >= 0) {
+          O[4 + j] = (int32_t)queue.size();
+          queue.push_back((uint32_t)r);
+        } else {
+          const uint32_t code = ~(uint32_t)r, first = code >> 3, cnt = (code & 7u) + 1u;
+          O[4 + j] = ~(int32_t)(((uint32_t)tris.size() << 3) | (cnt - 1u));
+          for (uint32_t t = 0; t < cnt; ++t) tris.push_back(order[first + t]);
+        }
+      }
+      out.resize(16 * queue.size(), 0);
+      std::memcpy(&out[16 * qi], O, sizeof(O));
+    }
+    wnodes.swap(out);
+    order.swap(tris);
+  }
+
+  // ---- 8-wide occlusion nodes (mtx.h) ------------------------------------
   // Slot of each child: slot s is visited at position s ^ octant(ray), so
   // the child in slot s should lie towards the corner s of the node (axis a
   // on the + side when bit a of s is set). Greedy assignment (Ylitie et al.
   // 2017, section 3.2): repeatedly the unassigned (child, slot) pair with the
   // largest dot(centroid_child - centroid_node, corner_s); ties to the
   // smaller child, then the smaller slot.
-  static void assign_slots(const std::vector<Child> &ch, int slot_of[kW]) {
+  static void assign_slots(const std::vector<Child> &ch, int slot_of[kMaxW]) {
     Box u;
     u.reset();
     for (const Child &c : ch) u.grow(c.box);
-    double pc[3], cc[kW][3];
+    double pc[3], cc[kMaxW][3];
     for (int a = 0; a < 3; ++a) pc[a] = 0.5 * ((double)u.lo[a] + (double)u.hi[a]);
     for (size_t i = 0; i < ch.size(); ++i)
       for (int a = 0; a < 3; ++a) cc[i][a] = 0.5 * ((double)ch[i].box.lo[a] + (double)ch[i].box.hi[a]) - pc[a];
-    bool used_c[kW] = {false}, used_s[kW] = {false};
+    bool used_c[kMaxW] = {false}, used_s[kMaxW] = {false};
     for (size_t n = 0; n < ch.size(); ++n) {
       double best = -INFINITY;
       int bc = -1, bs = -1;
       for (size_t i = 0; i < ch.size(); ++i) {
         if (used_c[i]) continue;
-        for (int sl = 0; sl < kW; ++sl) {
+        for (int sl = 0; sl < kMaxW; ++sl) {
           if (used_s[sl]) continue;
           double v = 0.0;
           for (int a = 0; a < 3; ++a) v += ((sl >> a) & 1) ? cc[i][a] : -cc[i][a];
@@ -367,13 +516,8 @@ struct Builder {
     }
   }
 
-  bool quant_ok = true;
-  static constexpr int kEMin = -32, kEMax = 31;
-  std::vector<int32_t> wnodes;  // MTX_BVH_NODE_WORDS per wide node
-  uint32_t wide_depth = 0;
-
   // Quantised child boxes of node W in slots slot_of[k] (mtx.h layout).
-  void encode_boxes(int32_t *W, const std::vector<Child> &ch, const int *slot_of) {
+  void encode8(int32_t *W, const std::vector<Child> &ch, const int *slot_of) {
     Box u;
     u.reset();
     for (const Child &c : ch) u.grow(c.box);
@@ -384,30 +528,15 @@ struct Builder {
     }
     uint32_t ebytes = 0;
     for (int a = 0; a < 3; ++a) {
-      const float org = u.lo[a];
-      const double ext = (double)u.hi[a] - (double)org;
-      int e = kEMin;
-      if (ext > 0.0) {
-        int ee;
-        std::frexp(ext / 255.0, &ee);
-        e = std::max(kEMin, std::min(kEMax, ee));
-      }
-      while (e < kEMax && mtx::wide_decode(org, mtx::wide_scale((uint32_t)(e & 255)), 255u) < u.hi[a]) ++e;
-      const float sc = mtx::wide_scale((uint32_t)(e & 255));
-      const double dsc = std::ldexp(1.0, e);
+      float org;
+      int e;
+      uint32_t qlo[kMaxW], qhi[kMaxW];
+      quantise_axis(ch, u, a, &org, &e, qlo, qhi);
       for (size_t k = 0; k < ch.size(); ++k) {
-        double flo = std::floor(((double)ch[k].box.lo[a] - (double)org) / dsc);
-        double fhi = std::ceil(((double)ch[k].box.hi[a] - (double)org) / dsc);
-        uint32_t qlo = (uint32_t)std::max(0.0, std::min(255.0, flo));
-        uint32_t qhi = (uint32_t)std::max(0.0, std::min(255.0, fhi));
-        while (qlo > 0 && mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a]) --qlo;
-        while (qhi < 255 && mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a]) ++qhi;
-        if (mtx::wide_decode(org, sc, qlo) > ch[k].box.lo[a] || mtx::wide_decode(org, sc, qhi) < ch[k].box.hi[a])
-          quant_ok = false;
         const int sl = slot_of[k], wd = sl >> 2, sh = 8 * (sl & 3);
         uint32_t &lo = q[4 * a + wd], &hi = q[4 * a + 2 + wd];
-        lo = (lo & ~(255u << sh)) | (qlo << sh);
-        hi = (hi & ~(255u << sh)) | (qhi << sh);
+        lo = (lo & ~(255u << sh)) | (qlo[k] << sh);
+        hi = (hi & ~(255u << sh)) | (qhi[k] << sh);
       }
       std::memcpy(&W[a], &org, 4);
       ebytes |= (uint32_t)(e & 255) << (8 * a);
@@ -419,30 +548,24 @@ struct Builder {
   // Breadth-first wide tree: node i's inner children get consecutive
   // indices (slot order) when it is laid out, its leaves' triangles
   // consecutive slots of the new leaf order.
-  void collapse_wide() {
-    const int NW = MTX_BVH_NODE_WORDS;
+  void collapse8() {
+    const int NW = MTX_OCC_NODE_WORDS;
     std::vector<uint32_t> queue = {0}, level = {1}, tris;
     tris.reserve(order.size());
     wnodes.assign(NW, 0);
     for (size_t qi = 0; qi < queue.size(); ++qi) {
       const uint32_t n2 = queue[qi];
-      std::vector<Child> ch;
-      dp_expand((int32_t)n2, kW, box2[n2], ch);
-      if (ch.size() == 1) {  // a subtree that prefers one slot: still split the root in two
-        ch.clear();
-        dp_expand(nodes[16 * (size_t)n2 + 12], 1, child_box2(n2, 0), ch);
-        dp_expand(nodes[16 * (size_t)n2 + 13], 1, child_box2(n2, 1), ch);
-      }
+      std::vector<Child> ch = wide_children(n2);
       if (qi == 0 && n == 1) ch.resize(1);  // one triangle: the root's two BVH2 children are the same leaf
       wide_depth = std::max(wide_depth, level[qi]);
-      int slot_of[kW];
+      int slot_of[kMaxW];
       assign_slots(ch, slot_of);
-      int child_at[kW];
-      for (int sl = 0; sl < kW; ++sl) child_at[sl] = -1;
+      int child_at[kMaxW];
+      for (int sl = 0; sl < kMaxW; ++sl) child_at[sl] = -1;
       for (size_t k = 0; k < ch.size(); ++k) child_at[slot_of[k]] = (int)k;
       uint32_t imask = 0, meta[2] = {0, 0}, off = 0;
       const uint32_t child_base = (uint32_t)queue.size(), tri_base = (uint32_t)tris.size();
-      for (int sl = 0; sl < kW; ++sl) {
+      for (int sl = 0; sl < kMaxW; ++sl) {
         const int k = child_at[sl];
         if (k < 0) continue;
         const int32_t r = ch[k].ref;
@@ -477,7 +600,7 @@ struct Builder {
       W[5] = (int32_t)tri_base;
       W[6] = (int32_t)meta[0];
       W[7] = (int32_t)meta[1];
-      encode_boxes(W, ch, slot_of);
+      encode8(W, ch, slot_of);
     }
     order.swap(tris);
   }
@@ -521,6 +644,30 @@ struct Builder {
   }
 };
 
+
+
+// Build knobs (tuning experiments, tools/bvh_experiment.py): SAH traversal
+// cost relative to one triangle test, bins, and the collapse's node /
+// triangle costs.
+void apply_knobs(Builder &b) {
+  if (const char *e = getenv("MTX_BVH_CT")) b.ct = std::max(0.05f, (float)atof(e));
+  if (const char *e = getenv("MTX_BVH_BINS")) b.n_bins = std::max(2, std::min(kMaxBins, atoi(e)));
+  if (const char *e = getenv("MTX_BVH_CNODE")) b.c_node = (float)atof(e);
+  if (const char *e = getenv("MTX_BVH_CTRI")) b.c_tri = (float)atof(e);
+}
+
+int check_order(const Builder &b, uint32_t n_tris, const char *fn, const char *stage) {
+  if (b.order.size() != n_tris) {
+    mtx_set_error("%s: internal error (%zu triangles %s for %u)", fn, b.order.size(), stage, n_tris);
+    return MTX_E_ARG;
+  }
+  if (!b.quant_ok) {
+    mtx_set_error("%s: child box quantisation failed (non-finite or huge coordinates?)", fn);
+    return MTX_E_ARG;
+  }
+  return MTX_OK;
+}
+
 }  // namespace
 
 extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t *tri_vidx, uint32_t n_tris,
@@ -540,34 +687,23 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
       return MTX_E_ARG;
     }
   Builder b;
-  // build knobs (tuning experiments, tools/bvh_experiment.py): SAH traversal
-  // cost relative to one triangle test, bins, and the collapse's node /
-  // triangle costs
-  if (const char *e = getenv("MTX_BVH_CT")) b.ct = std::max(0.05f, (float)atof(e));
-  if (const char *e = getenv("MTX_BVH_BINS")) b.n_bins = std::max(2, std::min(kMaxBins, atoi(e)));
+  apply_knobs(b);
   b.vpos = vpos;
   b.vidx = tri_vidx;
   b.n = n_tris;
+  b.max_leaf2 = MTX_BVH_MAX_LEAF;
   b.run();
-  if (b.order.size() != n_tris) {
-    mtx_set_error("mtx_bvh_build: internal error (%zu leaf triangles for %u)", b.order.size(), n_tris);
-    return MTX_E_ARG;
-  }
-  if (const char *e = getenv("MTX_BVH_CNODE")) b.c_node = (float)atof(e);
-  if (const char *e = getenv("MTX_BVH_CTRI")) b.c_tri = (float)atof(e);
+  int rc;
+  if ((rc = check_order(b, n_tris, "mtx_bvh_build", "in BVH2 leaves"))) return rc;
+  b.kw = MTX_BVH_WIDTH;
+  b.max_leaf_w = MTX_BVH_MAX_LEAF;
   b.dp_prepare();
-  b.collapse_wide();
-  if (!b.quant_ok) {
-    mtx_set_error("mtx_bvh_build: child box quantisation failed (non-finite or huge coordinates?)");
-    return MTX_E_ARG;
-  }
-  if (b.order.size() != n_tris) {
-    mtx_set_error("mtx_bvh_build: internal error (%zu triangles after the collapse for %u)", b.order.size(), n_tris);
-    return MTX_E_ARG;
-  }
-  uint32_t n_nodes = (uint32_t)(b.wnodes.size() / MTX_BVH_NODE_WORDS);
+  b.wnodes.reserve(b.nodes.size() / 2 + 16);
+  b.collapse4(0, 0);
+  b.relayout4();
+  if ((rc = check_order(b, n_tris, "mtx_bvh_build", "after the collapse"))) return rc;
   std::memcpy(nodes_out, b.wnodes.data(), b.wnodes.size() * sizeof(int32_t));
-  *n_nodes_out = n_nodes;
+  *n_nodes_out = (uint32_t)(b.wnodes.size() / MTX_BVH_NODE_WORDS);
   for (uint32_t i = 0; i < n_tris; ++i) {
     uint32_t t = b.order[i];
     perm_out[i] = t;
@@ -578,6 +714,57 @@ extern "C" int mtx_bvh_build(const float *vpos, uint32_t n_verts, const uint32_t
     g[0] = p0[0]; g[1] = p0[1]; g[2] = p0[2]; g[3] = 0.f;
     g[4] = p1[0] - p0[0]; g[5] = p1[1] - p0[1]; g[6] = p1[2] - p0[2]; g[7] = 0.f;
     g[8] = p2[0] - p0[0]; g[9] = p2[1] - p0[1]; g[10] = p2[2] - p0[2]; g[11] = 0.f;
+  }
+  if (depth_out) *depth_out = b.wide_depth;
+  return MTX_OK;
+}
+
+// The occlusion tree is built over the triangle records themselves: vertices
+// v0, v0 + e1, v0 + e2 (fp32) give each triangle's box, and the output
+// records are the input records copied bit for bit, so an any-hit query
+// tests exactly the triangles a closest-hit query does (the rounding of
+// v0 + e1 is far inside the boxes' padding).
+extern "C" int mtx_bvh_build_occlusion(const float *tri_geom, uint32_t n_tris, int32_t *nodes_out,
+                                       uint32_t *n_nodes_out, float *tri_geom_out, uint32_t *perm_out,
+                                       uint32_t *depth_out) {
+  if (!tri_geom || !nodes_out || !n_nodes_out || !tri_geom_out || n_tris == 0) {
+    mtx_set_error("mtx_bvh_build_occlusion: null argument or empty mesh");
+    return MTX_E_ARG;
+  }
+  if (n_tris >= (1u << 28)) {
+    mtx_set_error("mtx_bvh_build_occlusion: %u triangles exceed the 2^28 leaf encoding", n_tris);
+    return MTX_E_ARG;
+  }
+  std::vector<float> pts(9 * (size_t)n_tris);
+  std::vector<uint32_t> vidx(3 * (size_t)n_tris);
+  for (size_t i = 0; i < n_tris; ++i) {
+    const float *g = &tri_geom[12 * i];
+    for (int a = 0; a < 3; ++a) {
+      pts[9 * i + a] = g[a];
+      pts[9 * i + 3 + a] = g[a] + g[4 + a];
+      pts[9 * i + 6 + a] = g[a] + g[8 + a];
+    }
+    for (int k = 0; k < 3; ++k) vidx[3 * i + k] = (uint32_t)(3 * i + k);
+  }
+  Builder b;
+  apply_knobs(b);
+  b.vpos = pts.data();
+  b.vidx = vidx.data();
+  b.n = n_tris;
+  b.max_leaf2 = MTX_OCC_MAX_LEAF;
+  b.run();
+  int rc;
+  if ((rc = check_order(b, n_tris, "mtx_bvh_build_occlusion", "in BVH2 leaves"))) return rc;
+  b.kw = MTX_OCC_WIDTH;
+  b.max_leaf_w = MTX_OCC_MAX_LEAF;
+  b.dp_prepare();
+  b.collapse8();
+  if ((rc = check_order(b, n_tris, "mtx_bvh_build_occlusion", "after the collapse"))) return rc;
+  std::memcpy(nodes_out, b.wnodes.data(), b.wnodes.size() * sizeof(int32_t));
+  *n_nodes_out = (uint32_t)(b.wnodes.size() / MTX_OCC_NODE_WORDS);
+  for (uint32_t i = 0; i < n_tris; ++i) {
+    if (perm_out) perm_out[i] = b.order[i];
+    std::memcpy(&tri_geom_out[12 * (size_t)i], &tri_geom[12 * (size_t)b.order[i]], 12 * sizeof(float));
   }
   if (depth_out) *depth_out = b.wide_depth;
   return MTX_OK;

@@ -1,6 +1,7 @@
 // device_common.h — device helpers shared by the gfx950 kernel files:
-// scene view, wave64 stream compaction, and the 8-wide BVH traversal whose
-// visit order and tie-breaking match oracle/oracle.cpp:trace_wide exactly.
+// scene view, wave64 stream compaction, and the two BVH traversals (4-wide
+// sorted closest hit, 8-wide compressed any hit) whose visit orders and
+// tie-breaking match oracle/oracle.cpp trace_closest / trace_any exactly.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -14,17 +15,22 @@ namespace mtxd {
 
 using namespace mtx;
 
-// Traversal stacks live in LDS, one column per lane ([entry][lane], 8-B node
-// groups); the number of entries is the uploaded BVH's depth + 1 (at most
-// MTX_BVH_MAX_DEPTH + 1), so shallow trees leave LDS for more waves per CU.
-inline size_t stack_bytes(const DevScene &s) { return (size_t)s.stack_entries * kTraceBlock * sizeof(uint2); }
-// The persistent kernels keep only the top s.lds_entries entries in LDS (so
+// Traversal stacks live in LDS, one column per lane ([entry][lane]): 4-B
+// node references (closest hit, 3 x depth + 1 entries) or 8-B node groups
+// (occlusion, depth + 1 entries). mtx_trace's kernel keeps the whole stack
+// of either tree in LDS.
+inline size_t stack_bytes(const DevScene &s) {
+  const size_t a = (size_t)s.stack_entries * sizeof(int32_t), b = (size_t)s.occ_stack_entries * sizeof(uint2);
+  return (a > b ? a : b) * kTraceBlock;
+}
+// The persistent kernels keep only the top lds_entries entries in LDS (so
 // LDS does not cap occupancy) and spill deeper entries to a per-thread global
 // area ([entry - lds_entries][thread], coalesced per depth), rarely touched.
-// Behind the stack columns each block holds an LDS copy of the first
-// s.lds_top wide nodes (the top of the breadth-first tree, 80 B each).
-inline size_t persistent_stack_bytes(const DevScene &s) {
-  return (size_t)s.lds_entries * kTraceBlock * sizeof(uint2) + (size_t)s.lds_top * 80;
+// Behind the stack columns each block holds an LDS copy of the first lds_top
+// nodes of its tree (the top of the breadth-first tree).
+inline size_t persistent_stack_bytes(const DevScene &s, bool occ) {
+  return occ ? (size_t)s.occ_lds_entries * kTraceBlock * sizeof(uint2) + (size_t)s.occ_lds_top * 80
+             : (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t) + (size_t)s.lds_top * 64;
 }
 constexpr int kShadeBlock = 256;
 
@@ -80,14 +86,14 @@ __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, 
                           __float_as_uint(a.w), (int32_t)__float_as_uint(b.w), use_n, n0, n1, n2, use_uv, t0, t1, t2);
 }
 
-// Triangle geometry of leaf-order triangle `prim`: 9 packed floats (36 B:
-// v0, e1 = v1 - v0, e2 = v2 - v0; mtx_scene_upload drops the ABI's pads),
-// three dwordx3 loads.
+// Triangle geometry of leaf-order triangle `prim` of a tree (DevScene::tri
+// or ::occ_tri): 9 packed floats (36 B: v0, e1 = v1 - v0, e2 = v2 - v0;
+// mtx_scene_upload drops the ABI's pads), three dwordx3 loads.
 struct TriGeom {
   V3 p0, e1, e2;
 };
-__device__ __forceinline__ TriGeom load_tri(const DevScene &s, uint32_t prim) {
-  const float *g = s.tri + 9 * (size_t)prim;
+__device__ __forceinline__ TriGeom load_tri(const float *tri, uint32_t prim) {
+  const float *g = tri + 9 * (size_t)prim;
   TriGeom t;
   t.p0 = V3{g[0], g[1], g[2]};
   t.e1 = V3{g[3], g[4], g[5]};
@@ -205,14 +211,128 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// ---------------------------------------------------------------------------
-// 8-wide compressed BVH (mtx.h): one node visit = five 16-B loads (from the
-// block's LDS copy of the tree top, or global memory) and
-// mtx_core/geometry.h cw_node_hits. A lane's traversal state is a node group
-// (child_base, hit inner children as bits 24..31 in octant order | imask) and
-// a triangle group (tri_base, hit leaves' triangles as bits 0..23); the stack
-// holds node groups, one 8-B entry per visited node at most.
-// ---------------------------------------------------------------------------
+
+// ===========================================================================
+// Closest hit: 4-wide BVH (mtx.h). One node visit = four 16-B loads (from
+// the block's LDS copy of the tree top, or global memory) and
+// mtx_core/geometry.h wide_node_keys_e; the child references ride along the
+// 5-exchange sorting network, so the visit order is by entry distance.
+// ===========================================================================
+__device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
+                                          int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
+  int4 a, rf, qa;
+  int2 qb;
+  if (node < top_n) {
+    // the LDS reads are inline asm: as plain loads the compiler merges the
+    // two branches into flat loads through a selected generic pointer, which
+    // take the vector-memory path for every lane
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    typedef int v2i __attribute__((ext_vector_type(2)));
+    v4i x0, x1, x2;
+    v2i x3;
+    const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 64u * (uint32_t)node;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:16\n\t"
+        "ds_read_b128 %2, %4 offset:32\n\t"
+        "ds_read_b64 %3, %4 offset:48\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+        : "v"(la));
+    a = make_int4(x0.x, x0.y, x0.z, x0.w);
+    rf = make_int4(x1.x, x1.y, x1.z, x1.w);
+    qa = make_int4(x2.x, x2.y, x2.z, x2.w);
+    qb = make_int2(x3.x, x3.y);
+  } else {
+    const int4 *np = s.nodes + 4 * node;
+    a = np[0];
+    rf = np[1];
+    qa = np[2];
+    qb = *reinterpret_cast<const int2 *>(np + 3);
+  }
+  uint32_t key[4];
+  const uint32_t eb = (uint32_t)a.w;
+  // the references ride along the compare-exchange network (one compare +
+  // four selects per exchange) instead of being picked by the sorted keys'
+  // slot bits afterwards: the keys are distinct (slot in the low bits), so
+  // the order and the references are those of wide_node_order + wide_ref
+  const int n = wide_node_keys_e(r, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z),
+                                 (int)(int8_t)(uint8_t)(eb & 0xffu), (int)(int8_t)(uint8_t)((eb >> 8) & 0xffu),
+                                 (int)(int8_t)(uint8_t)((eb >> 16) & 0xffu), (int)(eb >> 24), (uint32_t)qa.x,
+                                 (uint32_t)qa.y, (uint32_t)qa.z, (uint32_t)qa.w, (uint32_t)qb.x, (uint32_t)qb.y,
+                                 tbest, key);
+  c[0] = rf.x;
+  c[1] = rf.y;
+  c[2] = rf.z;
+  c[3] = rf.w;
+#define MTX_CAS2(i, j)                         \
+  {                                            \
+    const bool sw_ = key[j] < key[i];          \
+    const uint32_t ki_ = key[i], kj_ = key[j]; \
+    const int32_t ci_ = c[i], cj_ = c[j];      \
+    key[i] = sw_ ? kj_ : ki_;                  \
+    key[j] = sw_ ? ki_ : kj_;                  \
+    c[i] = sw_ ? cj_ : ci_;                    \
+    c[j] = sw_ ? ci_ : cj_;                    \
+  }
+  MTX_CAS2(0, 1) MTX_CAS2(2, 3) MTX_CAS2(0, 2) MTX_CAS2(1, 3) MTX_CAS2(1, 2)
+#undef MTX_CAS2
+  return n;
+}
+
+// Per-thread closest-hit traversal in the oracle's order (oracle/oracle.cpp
+// trace_closest) for mtx_trace: stk is this thread's LDS column.
+__device__ __forceinline__ void traverse_closest(const DevScene &s, int32_t *stk, const TraceRay &r, float &tbest,
+                                                 uint32_t &prim_best, float &bu, float &bv, uint32_t &nv,
+                                                 uint32_t &tv) {
+  int sp = 0;
+  int32_t node = 0;
+  while (true) {
+    if (node >= 0) {
+      int32_t cr[4];
+      ++nv;
+      const int n = wide_visit(s, r, node, tbest, cr);
+      if (n > 0) {
+#pragma unroll
+        for (int rr = 3; rr >= 1; --rr)
+          if (rr < n) {
+            stk[sp * kTraceBlock] = cr[rr];
+            ++sp;
+          }
+        node = cr[0];
+        continue;
+      }
+    } else {
+      uint32_t first, count;
+      leaf_decode(node, &first, &count);
+      for (uint32_t k = 0; k < count; ++k) {
+        const uint32_t prim = first + k;
+        const TriGeom g = load_tri(s.tri, prim);
+        float t, u, v;
+        ++tv;
+        if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v) &&
+            (t < tbest || (t == tbest && prim < prim_best))) {
+          tbest = t;
+          prim_best = prim;
+          bu = u;
+          bv = v;
+        }
+      }
+    }
+    if (sp == 0) break;
+    --sp;
+    node = stk[sp * kTraceBlock];
+  }
+}
+
+// ===========================================================================
+// Any hit: 8-wide compressed occlusion BVH (mtx.h). One node visit = five
+// 16-B loads and mtx_core/geometry.h cw_node_hits. A lane's traversal state
+// is a node group (child_base, hit inner children as bits 24..31 in octant
+// order | imask) and a triangle group (tri_base, hit leaves' triangles as
+// bits 0..23); the stack holds node groups, one 8-B entry per visited node
+// at most.
+// ===========================================================================
 struct CwVisit {
   uint32_t hits, child_base, tri_base, imask;
 };
@@ -221,9 +341,6 @@ __device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r
                                             float tbest, const int4 *top, int top_n) {
   int4 a, b, q0, q1, q2;
   if ((int)node < top_n) {
-    // the LDS reads are inline asm: as plain loads the compiler merges the
-    // two branches into flat loads through a selected generic pointer, which
-    // take the vector-memory path for every lane
     typedef int v4i __attribute__((ext_vector_type(4)));
     v4i x0, x1, x2, x3, x4;
     const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 80u * node;
@@ -242,7 +359,7 @@ __device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r
     q1 = make_int4(x3.x, x3.y, x3.z, x3.w);
     q2 = make_int4(x4.x, x4.y, x4.z, x4.w);
   } else {
-    const int4 *np = s.nodes + 5 * (size_t)node;
+    const int4 *np = s.occ_nodes + 5 * (size_t)node;
     a = np[0];
     b = np[1];
     q0 = np[2];
@@ -261,41 +378,28 @@ __device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r
   return v;
 }
 
-// Per-thread traversal in the oracle's order (oracle/oracle.cpp trace_wide)
-// for mtx_trace: stk is this thread's LDS column (s.stack_entries entries).
-template <bool ANY>
-__device__ __forceinline__ bool traverse(const DevScene &s, uint2 *stk, const TraceRay &r, float &tbest,
-                                         uint32_t &prim_best, float &bu, float &bv, uint32_t &nv, uint32_t &tv) {
+// Per-thread any-hit traversal in the oracle's order (oracle/oracle.cpp
+// trace_any) for mtx_trace: stk is this thread's LDS column.
+__device__ __forceinline__ bool traverse_occ(const DevScene &s, uint2 *stk, const TraceRay &r, float tmax,
+                                             uint32_t &nv, uint32_t &tv) {
   const uint32_t oct = ray_octant(r);
   int sp = 0;
   uint32_t gbase = 0, ghits = (1u << (24 + oct)) | 1u, tbase = 0, thits = 0;
-  bool hit_any = false;
   while (true) {
     if (thits) {
       const uint32_t prim = tbase + (uint32_t)ctz32(thits);
       thits &= thits - 1u;
-      const TriGeom g = load_tri(s, prim);
+      const TriGeom g = load_tri(s.occ_tri, prim);
       float t, u, v;
       ++tv;
-      if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
-        if (ANY) {
-          hit_any = true;
-          break;
-        }
-        if (t < tbest || (t == tbest && prim < prim_best)) {
-          tbest = t;
-          prim_best = prim;
-          bu = u;
-          bv = v;
-        }
-      }
+      if (tri_intersect(r, g.p0, g.e1, g.e2, tmax, &t, &u, &v)) return true;
     } else if (ghits >> 24) {
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
       ghits &= ~(1u << (24 + p));
       const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
       if (ghits >> 24) stk[(sp++) * kTraceBlock] = make_uint2(gbase, ghits);
       ++nv;
-      const CwVisit v = cw_visit(s, r, oct, node, tbest, nullptr, 0);
+      const CwVisit v = cw_visit(s, r, oct, node, tmax, nullptr, 0);
       gbase = v.child_base;
       ghits = (v.hits & 0xff000000u) | v.imask;
       tbase = v.tri_base;
@@ -305,25 +409,43 @@ __device__ __forceinline__ bool traverse(const DevScene &s, uint2 *stk, const Tr
       gbase = g.x;
       ghits = g.y;
     } else {
-      break;
+      return false;
     }
   }
-  return hit_any;
 }
 
-}  // namespace mtxd
-
-namespace mtxd {
+// ===========================================================================
+// Persistent single-step traversal loops (both trees).
+//
+// Every lane owns one ray at a time. Each iteration a lane with a ray does
+// one unit of work: one node visit, then (same iteration) one triangle test
+// if it holds triangles to test; nothing waits for the slowest lane of the
+// wave to reach a leaf. Finished lanes are refilled from a per-wave
+// reservoir of claimed queue indices once s.urefill lanes of the wave are
+// idle -- one device-scope atomic per claimed batch. Waves claim rays from
+// their own XCD's eighth of the queue first (that XCD's L2 then holds the
+// band's nodes). Each ray's visit sequence is the oracle's, with or without
+// STATS. Src provides: a Payload type (what a lane carries for its ray),
+// load(k, TraceRay&, float &tmax, Payload &) and finish(const Payload &, bool
+// any_hit, float t, uint32_t prim, float u, float v).
+// ===========================================================================
 
 // Stack entry e of a lane: LDS for e < lds_n, the global spill area above.
 // The LDS entry is read unconditionally (clamped) and the global one only on
 // the rare deep entries, so the common pop is a ds_read; a select between the
 // two pointers would compile to a flat load (vector-memory + LDS counters,
 // a texture-path slot per pop).
+__device__ __forceinline__ int32_t stack_read(const int32_t *stk, const int32_t *ovf, int e, int lds_n,
+                                              uint32_t ovf_threads) {
+  int32_t v = stk[min(e, lds_n - 1) * kTraceBlock];
+  asm volatile("" : "+v"(v));  // keeps the LDS read (no pointer select + flat load)
+  if (e >= lds_n) v = ovf[(size_t)(e - lds_n) * ovf_threads];
+  return v;
+}
 __device__ __forceinline__ uint2 stack_read(const uint2 *stk, const uint2 *ovf, int e, int lds_n,
                                             uint32_t ovf_threads) {
   uint2 v = stk[min(e, lds_n - 1) * kTraceBlock];
-  asm volatile("" : "+v"(v.x), "+v"(v.y));  // keeps the LDS read (no pointer select + flat load)
+  asm volatile("" : "+v"(v.x), "+v"(v.y));
   if (e >= lds_n) v = ovf[(size_t)(e - lds_n) * ovf_threads];
   return v;
 }
@@ -340,88 +462,60 @@ __device__ __forceinline__ uint32_t xseg_bound(uint32_t count, uint32_t k) {
   return (uint32_t)(((uint64_t)count * k) >> 3);
 }
 
-// Claim of the next queue entries for a wave (wave-uniform; the leader lane
-// does the atomic): [base2, base2 + got2) from the own XCD's segment first,
-// then the next segments; returns true once every segment is drained.
-// (Guided sizes -- each claim its fair share of what the segment has left,
-// read with an atomic load before the add -- measured much slower: closest
-// 61.3 -> 74.0 ms/step at spp 256, 9.45 -> 15.3 at spp 32)
-__device__ __forceinline__ bool claim_rays(const DevScene &s, uint32_t *heads, uint32_t count, uint32_t batch,
-                                           uint32_t leader, uint32_t lane, uint32_t &seg, uint32_t &tries,
-                                           uint32_t &base2, uint32_t &got2) {
-  while (true) {
-    const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
-    const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
-    uint32_t b = 0xffffffffu;
-    if (hi > lo) {
-      if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
-      b = __builtin_amdgcn_readlane(b, leader);
-    }
-    if (hi > lo && b < hi - lo) {
-      base2 = lo + b;
-      got2 = min(batch, hi - lo - b);
-      return false;
-    }
-    if (++tries >= kXcds) return true;
-    seg = (seg + 1) & (kXcds - 1u);
-  }
-}
+// A wave's reservoir of claimed queue indices. Claims take s.trace_batch
+// entries, cut down (to >= 64) when the queue is too short to give every
+// wave of the grid a batch: a small queue then still spreads over the chip
+// instead of running a few long per-lane chains; waves beyond the batches
+// exit at once (start() returns false). Claims come from the own XCD's
+// queue segment first, then the next segments. (Guided sizes -- each claim
+// its fair share of what the segment has left -- measured much slower:
+// closest 61.3 -> 74.0 ms/step at spp 256)
+struct RayReservoir {
+  uint32_t *heads;
+  uint32_t count, batch, seg, tries, res_lo, res_hi;
+  bool drained, exhausted;
 
-// ---------------------------------------------------------------------------
-// Persistent single-step traversal (closest hit and any-hit).
-//
-// Every lane owns one ray at a time. Each iteration a lane with a ray does
-// one unit of work: one node visit when its triangle group is empty, then
-// (same iteration) one triangle test when its triangle group is not; a lane
-// whose groups are both empty pops the next node group or finishes its ray.
-// Nothing waits for the slowest lane of the wave to reach a leaf. Finished
-// lanes are refilled from a per-wave reservoir of claimed queue indices once
-// s.urefill lanes of the wave are idle -- one device-scope atomic per
-// s.trace_batch rays. Waves claim rays from their own XCD's eighth of the
-// queue first (that XCD's L2 then holds the band's nodes). Each ray's visit
-// sequence is the oracle's (oracle/oracle.cpp trace_wide), with or without
-// STATS.
-// ---------------------------------------------------------------------------
-// heads: kXcds claim cursors (kXHeadStride words apart), zeroed before the
-// launch. Src provides: a Payload type (what a lane carries for its ray),
-// load(k, TraceRay&, float &tmax, Payload &) and finish(const Payload &, bool
-// any_hit, float t, uint32_t prim, float u, float v).
-template <bool ANY, bool STATS = false, class Src>
-__device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
-                                             uint2 *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
-                                             uint32_t &nr, uint32_t *wave_iters = nullptr) {
-  const uint32_t lane = lane_id();
-  uint2 *ovf = s.stack_ovf + blockIdx.x * kTraceBlock + threadIdx.x;
-  const int lds_n = (int)s.lds_entries;
-  bool has = false, exhausted = false, hit = false, drained = false;
-  uint32_t res_lo = 0, res_hi = 0;
-  typename Src::Payload payload{};
-  uint32_t prim = 0xffffffffu;
-  TraceRay r;
-  float tbest = 0.f, bu = 0.f, bv = 0.f;
-  uint32_t oct = 0, gbase = 0, ghits = 0, tbase = 0, thits = 0;
-  const int top_n = (int)s.lds_top;
-  int sp = 0;
-  // Claim size: s.trace_batch, cut down (to >= 64) when the queue is too
-  // short to give every wave of the grid a batch: a small queue then still
-  // spreads over the chip instead of running a few long per-lane chains.
-  // More waves than batches: the surplus exits at once (a near-empty queue
-  // would otherwise cost every wave of the grid its claim atomics).
-  const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
-  const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
-  if ((blockIdx.x * kTraceBlock + threadIdx.x) / 64u >= (count + batch - 1) / batch) return;
-  uint32_t seg = s.xcd_claim ? xcc_id() : 0u, tries = s.xcd_claim ? 0u : kXcds - 1u;
-  // claim one queue index for every lane in `want` from the wave's
-  // reservoir (topped up by claim_rays): k is this lane's, ok if it got one
-  auto take = [&](uint64_t want, uint32_t &k, bool &ok) {
+  __device__ __forceinline__ bool start(const DevScene &s, uint32_t *heads_, uint32_t count_) {
+    heads = heads_;
+    count = count_;
+    const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
+    batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
+    seg = s.xcd_claim ? xcc_id() : 0u;
+    tries = s.xcd_claim ? 0u : kXcds - 1u;
+    res_lo = res_hi = 0;
+    drained = exhausted = false;
+    return (blockIdx.x * kTraceBlock + threadIdx.x) / 64u < (count + batch - 1) / batch;
+  }
+
+  // [base2, base2 + got2) from the next non-empty segment (wave-uniform; the
+  // leader lane does the atomic); true once every segment is drained
+  __device__ __forceinline__ bool claim(const DevScene &s, uint32_t leader, uint32_t lane, uint32_t &base2,
+                                        uint32_t &got2) {
+    while (true) {
+      const uint32_t lo = s.xcd_claim ? xseg_bound(count, seg) : 0u;
+      const uint32_t hi = s.xcd_claim ? xseg_bound(count, seg + 1) : count;
+      uint32_t b = 0xffffffffu;
+      if (hi > lo) {
+        if (lane == leader) b = atomicAdd(heads + seg * kXHeadStride, batch);
+        b = __builtin_amdgcn_readlane(b, leader);
+      }
+      if (hi > lo && b < hi - lo) {
+        base2 = lo + b;
+        got2 = min(batch, hi - lo - b);
+        return false;
+      }
+      if (++tries >= kXcds) return true;
+      seg = (seg + 1) & (kXcds - 1u);
+    }
+  }
+
+  // one queue index for every lane in `want`: k is this lane's, ok if it got one
+  __device__ __forceinline__ void take(const DevScene &s, uint64_t want, uint32_t lane, uint32_t &k, bool &ok) {
     const uint32_t n = (uint32_t)__popcll(want);
     const uint32_t left = res_hi - res_lo;
     uint32_t base2 = 0, got2 = 0;
-    if (left < n && !drained)
-      drained = claim_rays(s, heads, count, batch, (uint32_t)(__ffsll((unsigned long long)want) - 1), lane, seg,
-                           tries, base2, got2);
-    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+    if (left < n && !drained) drained = claim(s, (uint32_t)(__ffsll((unsigned long long)want) - 1), lane, base2, got2);
+    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
     k = 0;
     ok = false;
     if (rk < left) {
@@ -439,18 +533,162 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
       res_hi = base2 + got2;
     }
     exhausted = drained && res_lo >= res_hi;
+  }
+};
+
+__device__ __forceinline__ void count_wave_iter(uint32_t lane, uint32_t *ctr) {
+  const uint64_t m = __ballot(true);
+  if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++*ctr;
+}
+
+// Closest hit on the 4-wide tree: a lane's work item is an inner node to
+// visit or a leaf's triangle range; a visit pushes the far hit children
+// (three unconditional LDS stores when they fit: dead entries above the new
+// top are harmless) and continues with the nearest.
+template <bool STATS, class Src>
+__device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
+                                                   int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
+                                                   uint32_t &nr, uint32_t *wave_iters) {
+  const uint32_t lane = lane_id();
+  int32_t *ovf = reinterpret_cast<int32_t *>(s.stack_ovf) + blockIdx.x * kTraceBlock + threadIdx.x;
+  const int lds_n = (int)s.lds_entries, top_n = (int)s.lds_top;
+  RayReservoir res;
+  if (!res.start(s, heads, count)) return;
+  bool has = false;
+  typename Src::Payload payload{};
+  uint32_t prim = 0xffffffffu;
+  TraceRay r;
+  float tbest = 0.f, bu = 0.f, bv = 0.f;
+  int32_t node = -1;              // >= 0: inner node to visit next
+  uint32_t tri = 0, tri_end = 0;  // triangles [tri, tri_end) of the current leaf
+  int sp = 0;
+  // next work item of a lane from its stack: an inner node, a leaf's
+  // triangle range, or nothing (the ray is finished)
+  auto pop_next = [&]() {
+    node = -1;
+    if (sp > 0) {
+      --sp;
+      const int32_t e = stack_read(stk, ovf, sp, lds_n, s.ovf_threads);
+      if (e >= 0) {
+        node = e;
+      } else {
+        uint32_t first, cnt;
+        leaf_decode(e, &first, &cnt);
+        tri = first;
+        tri_end = first + cnt;
+      }
+    }
   };
   while (true) {
-    if (!exhausted) {
+    if (!res.exhausted) {
       const uint64_t idle = __ballot(!has);
       if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
         uint32_t k;
         bool ok;
-        take(idle, k, ok);
+        res.take(s, idle, lane, k, ok);
         if (!has && ok) {
           src.load(k, r, tbest, payload);
           prim = 0xffffffffu;
           bu = bv = 0.f;
+          node = 0;
+          tri = tri_end = 0;
+          sp = 0;
+          has = true;
+        }
+      }
+    }
+    if (__ballot(has) == 0) break;
+    // ---- one inner-node visit
+    if (has && node >= 0) {
+      if (STATS) count_wave_iter(lane, &wave_iters[0]);
+      int32_t cr[4];
+      ++nv;
+      const int n = wide_visit(s, r, node, tbest, cr, top, top_n);
+      if (n > 0) {
+        const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
+        const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
+        if (sp + 3 <= lds_n) {
+          stk[sp * kTraceBlock] = e0;
+          stk[(sp + 1) * kTraceBlock] = e1;
+          stk[(sp + 2) * kTraceBlock] = c1;
+        } else {
+          const int32_t e[3] = {e0, e1, c1};
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            if (j < n - 1) {
+              const int q = sp + j;
+              if (q < lds_n)
+                stk[q * kTraceBlock] = e[j];
+              else
+                ovf[(size_t)(q - lds_n) * s.ovf_threads] = e[j];
+            }
+        }
+        sp += n - 1;
+        const int32_t c0 = cr[0];
+        if (c0 >= 0) {
+          node = c0;
+        } else {
+          uint32_t first, cnt;
+          leaf_decode(c0, &first, &cnt);
+          tri = first;
+          tri_end = first + cnt;
+          node = -1;
+        }
+      } else {
+        pop_next();
+      }
+    }
+    // ---- one triangle test
+    if (has && tri < tri_end) {
+      if (STATS) count_wave_iter(lane, &wave_iters[1]);
+      const uint32_t pr = tri;
+      const TriGeom g = load_tri(s.tri, pr);
+      float t, u, v;
+      ++tv;
+      ++tri;
+      if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v) && (t < tbest || (t == tbest && pr < prim))) {
+        tbest = t;
+        prim = pr;
+        bu = u;
+        bv = v;
+      }
+      if (tri >= tri_end) pop_next();
+    }
+    if (has && node < 0 && tri >= tri_end) {
+      src.finish(payload, prim != 0xffffffffu, tbest, prim, bu, bv);
+      has = false;
+      ++nr;
+    }
+  }
+}
+
+// Any hit on the 8-wide occlusion tree: a lane tests its triangle group
+// before the next child of its node group; an empty pair pops the next node
+// group. The first hit ends the ray.
+template <bool STATS, class Src>
+__device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
+                                               uint2 *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
+                                               uint32_t &nr, uint32_t *wave_iters) {
+  const uint32_t lane = lane_id();
+  uint2 *ovf = reinterpret_cast<uint2 *>(s.stack_ovf) + blockIdx.x * kTraceBlock + threadIdx.x;
+  const int lds_n = (int)s.occ_lds_entries, top_n = (int)s.occ_lds_top;
+  RayReservoir res;
+  if (!res.start(s, heads, count)) return;
+  bool has = false, hit = false;
+  typename Src::Payload payload{};
+  TraceRay r;
+  float tmax = 0.f;
+  uint32_t oct = 0, gbase = 0, ghits = 0, tbase = 0, thits = 0;
+  int sp = 0;
+  while (true) {
+    if (!res.exhausted) {
+      const uint64_t idle = __ballot(!has);
+      if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
+        uint32_t k;
+        bool ok;
+        res.take(s, idle, lane, k, ok);
+        if (!has && ok) {
+          src.load(k, r, tmax, payload);
           hit = false;
           oct = ray_octant(r);
           gbase = 0;
@@ -464,10 +702,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
     if (__ballot(has) == 0) break;
     // ---- one node visit: the nearest remaining child of the node group
     if (has && thits == 0 && (ghits >> 24) != 0) {
-      if (STATS) {
-        const uint64_t m = __ballot(true);
-        if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[0];
-      }
+      if (STATS) count_wave_iter(lane, &wave_iters[0]);
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
       ghits &= ~(1u << (24 + p));
       const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
@@ -482,7 +717,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         ++sp;
       }
       ++nv;
-      const CwVisit v = cw_visit(s, r, oct, node, tbest, top, top_n);
+      const CwVisit v = cw_visit(s, r, oct, node, tmax, top, top_n);
       gbase = v.child_base;
       ghits = (v.hits & 0xff000000u) | v.imask;
       tbase = v.tri_base;
@@ -490,27 +725,17 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
     }
     // ---- one triangle test of the triangle group
     if (has && thits != 0) {
-      if (STATS) {
-        const uint64_t m = __ballot(true);
-        if (lane == (uint32_t)(__ffsll((unsigned long long)m) - 1)) ++wave_iters[1];
-      }
+      if (STATS) count_wave_iter(lane, &wave_iters[1]);
       const uint32_t pr = tbase + (uint32_t)ctz32(thits);
       thits &= thits - 1u;
-      const TriGeom g = load_tri(s, pr);
+      const TriGeom g = load_tri(s.occ_tri, pr);
       float t, u, v;
       ++tv;
-      if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v)) {
-        if (ANY) {
-          hit = true;
-          thits = 0;
-          ghits = 0;
-          sp = 0;
-        } else if (t < tbest || (t == tbest && pr < prim)) {
-          tbest = t;
-          prim = pr;
-          bu = u;
-          bv = v;
-        }
+      if (tri_intersect(r, g.p0, g.e1, g.e2, tmax, &t, &u, &v)) {
+        hit = true;
+        thits = 0;
+        ghits = 0;
+        sp = 0;
       }
     }
     // ---- both groups empty: the next node group, or the ray is done
@@ -521,7 +746,7 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
         gbase = g.x;
         ghits = g.y;
       } else {
-        src.finish(payload, hit, tbest, prim, bu, bv);
+        src.finish(payload, hit, tmax, 0xffffffffu, 0.f, 0.f);
         has = false;
         ++nr;
       }
@@ -529,16 +754,28 @@ __device__ __forceinline__ void trace_loop_u(const DevScene &s, const Src &src, 
   }
 }
 
-// stk: this thread's stack column (dynamic LDS + threadIdx.x). Every thread
-// of the block calls this (the LDS tree top is filled behind a barrier).
+// The persistent traversal of a block: ANY = any hit on the occlusion tree,
+// else closest hit on the 4-wide tree. The block's dynamic LDS holds the
+// stack columns and then the tree top (persistent_stack_bytes), filled here
+// behind a barrier; every thread of the block calls this.
 template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
-                                           uint2 *stk, uint32_t &nv, uint32_t &tv, uint32_t &nr,
+                                           uint32_t &nv, uint32_t &tv, uint32_t &nr,
                                            uint32_t *wave_iters = nullptr) {
-  int4 *top = reinterpret_cast<int4 *>(stk - threadIdx.x + s.lds_entries * kTraceBlock);
-  for (uint32_t i = threadIdx.x; i < 5 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
-  __syncthreads();
-  trace_loop_u<ANY, STATS>(s, src, count, heads, stk, top, nv, tv, nr, wave_iters);
+  extern __shared__ int4 trace_lds[];
+  if (ANY) {
+    uint2 *cols = reinterpret_cast<uint2 *>(trace_lds);
+    int4 *top = reinterpret_cast<int4 *>(cols + s.occ_lds_entries * kTraceBlock);
+    for (uint32_t i = threadIdx.x; i < 5 * s.occ_lds_top; i += kTraceBlock) top[i] = s.occ_nodes[i];
+    __syncthreads();
+    trace_loop_occ<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+  } else {
+    int32_t *cols = reinterpret_cast<int32_t *>(trace_lds);
+    int4 *top = reinterpret_cast<int4 *>(cols + s.lds_entries * kTraceBlock);
+    for (uint32_t i = threadIdx.x; i < 4 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
+    __syncthreads();
+    trace_loop_closest<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+  }
 }
 
 }  // namespace mtxd

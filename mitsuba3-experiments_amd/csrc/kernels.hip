@@ -61,12 +61,12 @@ struct ClosestSrc {
 #define MTX_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
-  extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
+  // dynamic LDS: stack columns + tree top (device_common.h trace_loop)
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
-  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, stack + threadIdx.x, nv,
-                           tv, nr, wi);
+  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, nv, tv, nr,
+                           wi);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
     unsigned long long w0 = wave_sum_u64(wi[0]), w1 = wave_sum_u64(wi[1]);
@@ -128,10 +128,10 @@ struct ShadowSrc {
 
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
-  extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
+  // dynamic LDS: stack columns + tree top (device_common.h trace_loop)
   const ShadowSrc src{b};
   uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop<true>(s, src, b.counters[4 * (bounce + 1) + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, stack + threadIdx.x, nv, tv, nr);
+  trace_loop<true>(s, src, b.counters[4 * (bounce + 1) + 1], b.xheads + (2 * bounce + 1) * kXSlotWords, nv, tv, nr);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
     if ((threadIdx.x & 63) == 0 && n) {
@@ -1210,8 +1210,7 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
 // Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0).
 __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const float4 *rays, uint32_t n, int any_hit,
                                                            uint32_t *hits, uint32_t *visits) {
-  extern __shared__ uint2 stack[];  // s.stack_entries x kTraceBlock node groups (dynamic)
-  uint2 *stk = stack + threadIdx.x;
+  extern __shared__ int4 raw_lds[];  // one stack column per thread (device_common.h stack_bytes)
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float4 o4 = rays[2 * (size_t)i], d4 = rays[2 * (size_t)i + 1];
@@ -1219,9 +1218,9 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const flo
   float tbest = o4.w, bu = 0.f, bv = 0.f;
   uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
   if (any_hit) {
-    hits[i] = traverse<true>(s, stk, r, tbest, prim, bu, bv, nv, tv) ? 1u : 0u;
+    hits[i] = traverse_occ(s, reinterpret_cast<uint2 *>(raw_lds) + threadIdx.x, r, o4.w, nv, tv) ? 1u : 0u;
   } else {
-    traverse<false>(s, stk, r, tbest, prim, bu, bv, nv, tv);
+    traverse_closest(s, reinterpret_cast<int32_t *>(raw_lds) + threadIdx.x, r, tbest, prim, bu, bv, nv, tv);
     if (prim == 0xffffffffu) tbest = kInf;
     hits[4 * (size_t)i + 0] = __float_as_uint(tbest);
     hits[4 * (size_t)i + 1] = prim;
@@ -1390,16 +1389,16 @@ void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkPara
 void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                           hipStream_t st) {
   if (stats)
-    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, false), st, s, b, bounce);
   else
-    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, false), st, s, b, bounce);
 }
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st) {
   if (stats)
-    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_shadow<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, true), st, s, b, bounce);
   else
-    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, b, bounce);
+    hipLaunchKernelGGL(k_trace_shadow<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, true), st, s, b, bounce);
 }
 void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, uint32_t bounce, int grid,
                   hipStream_t st) {
@@ -1429,14 +1428,19 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
   }
 }
-// Resident blocks per CU of the persistent kernels (grid = n_cu x this).
+// Resident blocks per CU of the persistent kernels (grid = n_cu x this; the
+// fewer of the two trees' kernels).
 int trace_blocks_per_cu(const DevScene &s) {
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_trace_closest<false>, kTraceBlock, persistent_stack_bytes(s)) !=
-          hipSuccess ||
-      nb <= 0)
-    nb = 4;
-  return nb;
+  int nc = 0, na = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false>, kTraceBlock,
+                                                   persistent_stack_bytes(s, false)) != hipSuccess ||
+      nc <= 0)
+    nc = 4;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&na, k_trace_shadow<false>, kTraceBlock,
+                                                   persistent_stack_bytes(s, true)) != hipSuccess ||
+      na <= 0)
+    na = 4;
+  return nc < na ? nc : na;
 }
 // MTX_DIAG_STAMPS builds: read (and zero) the shade stamp sums; -1 otherwise.
 int shade_stamps(unsigned long long *out) {

@@ -416,10 +416,10 @@ struct TestSrc {
 };
 
 __global__ __launch_bounds__(kTraceBlock) void k_trace_test(DevScene s, RestirBuffers r, uint32_t occ_base) {
-  extern __shared__ uint2 stack[];  // s.lds_entries x kTraceBlock node groups + the tree top (dynamic)
+  // dynamic LDS: stack columns + tree top (device_common.h trace_loop)
   const TestSrc src{r, occ_base};
   uint32_t nv = 0, tv = 0, nr = 0;
-  trace_loop<true>(s, src, r.test_count[0], r.test_heads, stack + threadIdx.x, nv, tv, nr);
+  trace_loop<true>(s, src, r.test_count[0], r.test_heads, nv, tv, nr);
 }
 
 static inline unsigned rs_blocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -448,7 +448,7 @@ void launch_restir_final(const DevScene &s, const WaveBuffers &b, const ChunkPar
   hipLaunchKernelGGL(k_rs_final, dim3(rs_blocks(r.nb, 256)), dim3(256), 0, st, s, b, p, r);
 }
 void launch_trace_test(const DevScene &s, const RestirBuffers &r, uint32_t occ_base, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s), st, s, r, occ_base);
+  hipLaunchKernelGGL(k_trace_test, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, true), st, s, r, occ_base);
 }
 
 }  // namespace mtxd

@@ -41,9 +41,17 @@ enum : uint32_t {
 #define MTX_TRACE_BLOCK 256  // 8 blocks of 4 waves per CU: 20 KB of LDS each (stack + tree top)
 #endif
 constexpr int kTraceBlock = MTX_TRACE_BLOCK;  // threads per traversal block
-constexpr uint32_t kLdsStack = 8;    // default LDS part of the persistent traversal stack (8-B entries per lane)
+// LDS part of the persistent traversal stacks (per lane) and the tree tops
+// copied into LDS per trace block; both kernels' blocks take ~20 KB (8 per CU):
+// closest hit 16 x 4-B node refs + 64 x 64-B nodes, occlusion 8 x 8-B node
+// groups + 48 x 80-B nodes
+constexpr uint32_t kLdsStack = 16;
+constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_LDS_TOP
-#define MTX_LDS_TOP 48  // default wide nodes of the tree top copied into LDS per trace block (0 = none)
+#define MTX_LDS_TOP 64  // closest-hit tree nodes copied into LDS per trace block (0 = none)
+#endif
+#ifndef MTX_OCC_LDS_TOP
+#define MTX_OCC_LDS_TOP 48  // occlusion tree nodes copied into LDS per trace block (0 = none)
 #endif
 #ifndef MTX_STREAMS
 #define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)
@@ -56,8 +64,10 @@ constexpr uint32_t kXHeadStride = 32;
 constexpr uint32_t kXSlotWords = kXcds * kXHeadStride;
 
 struct DevScene {
-  const int4 *nodes;  // 5 x int4 per node: the 80-B ABI node (mtx.h)
-  const float *tri;   // 9 floats per triangle (v0, e1, e2; device_common.h load_tri)
+  const int4 *nodes;      // closest-hit BVH: 4 x int4 per node (the 64-B ABI node, mtx.h)
+  const float *tri;       // its leaf-order triangles, 9 floats each (v0, e1, e2; device_common.h load_tri)
+  const int4 *occ_nodes;  // occlusion BVH: 5 x int4 per node (the 80-B ABI node, mtx.h)
+  const float *occ_tri;   // its own leaf-order copy of the triangles (9 floats each)
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;
   const float *vpos;
@@ -71,16 +81,29 @@ struct DevScene {
   const float *texels;
   const float *tables;
   uint32_t n_tris, n_emitters;
-  uint32_t stack_entries;  // BVH depth + 1 (traversal stack entries per lane: node groups, 8 B)
+  uint32_t stack_entries;  // closest hit: 3 x depth + 1 stack entries per lane (4-B node refs)
   uint32_t lds_entries;    // persistent kernels: stack entries kept in LDS
-  uint32_t lds_top;        // persistent kernels: wide nodes [0, lds_top) read from a per-block LDS copy
+  uint32_t lds_top;        // persistent kernels: nodes [0, lds_top) read from a per-block LDS copy
+  uint32_t occ_stack_entries, occ_lds_entries, occ_lds_top;  // the same for the occlusion tree
+                                                             // (depth + 1 entries: 8-B node groups)
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
-  uint2 *stack_ovf;        // persistent kernels: entries beyond lds_entries, [entry][thread]
+  void *stack_ovf;         // persistent kernels: entries beyond the LDS part, [entry][thread]
+                           // (int32 node refs for closest hit, uint2 node groups for occlusion)
   uint32_t ovf_threads;    // threads of the persistent trace grid
   uint32_t urefill;        // persistent kernels: refill a wave once this many lanes are idle
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
 };
+
+// Global spill area of a wavefront's traversals (the deeper of the two
+// trees' needs; closest-hit and any-hit launches of one wavefront never
+// overlap).
+inline size_t stack_ovf_bytes(const DevScene &s) {
+  const size_t a = (size_t)(s.stack_entries - s.lds_entries) * sizeof(int32_t);
+  const size_t b = (size_t)(s.occ_stack_entries - s.occ_lds_entries) * sizeof(uint2);
+  const size_t n = (a > b ? a : b) * s.ovf_threads;
+  return n > 8 ? n : 8;
+}
 
 // Shadow-ray record (64 B): o.xyz maxt | d.xyz L index | T.xyz flags | X.xyz 0
 // (L index = plane * capacity + position of the path's L, WaveBuffers)

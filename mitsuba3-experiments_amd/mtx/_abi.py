@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 5
+MTX_ABI_VERSION = 6
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -38,10 +38,13 @@ MTX_RENDER_NRC_CACHE = 4
 MTX_RESTIR_STAGE_B = 32
 
 MTX_ROUGH_TRANSMITTANCE_RES = 64
-MTX_BVH_WIDTH = 8
-MTX_BVH_MAX_LEAF = 3
-MTX_BVH_NODE_WORDS = 20
+MTX_BVH_WIDTH = 4          # closest-hit BVH (mtx.h)
+MTX_BVH_MAX_LEAF = 8
+MTX_BVH_NODE_WORDS = 16
 MTX_BVH_MAX_DEPTH = 40
+MTX_OCC_WIDTH = 8          # occlusion (any-hit) BVH
+MTX_OCC_MAX_LEAF = 3
+MTX_OCC_NODE_WORDS = 20
 
 ERRORS = {-1: "MTX_E_ARG", -2: "MTX_E_HIP", -3: "MTX_E_NOSCENE", -4: "MTX_E_OOM", -5: "MTX_E_UNSUPPORTED"}
 
@@ -126,6 +129,10 @@ class SceneDesc(C.Structure):
         ("n_tables", C.c_uint32),
         ("pad0", C.c_uint32),
         ("camera", Camera),
+        ("occ_nodes", C.c_void_p),
+        ("occ_tri_geom", C.c_void_p),
+        ("n_occ_nodes", C.c_uint32),
+        ("pad1", C.c_uint32),
     ]
 
 
@@ -263,6 +270,7 @@ EXPORTS = [
     "mtx_ctx_create",
     "mtx_ctx_destroy",
     "mtx_bvh_build",
+    "mtx_bvh_build_occlusion",
     "mtx_roughplastic_tables",
     "mtx_scene_upload",
     "mtx_render",

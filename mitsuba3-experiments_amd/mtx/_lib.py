@@ -53,6 +53,7 @@ def lib() -> C.CDLL:
         "mtx_ctx_create": ([C.c_int, C.POINTER(vp)], C.c_int),
         "mtx_ctx_destroy": ([vp], None),
         "mtx_bvh_build": ([vp, u32, vp, u32, vp, C.POINTER(u32), vp, vp, C.POINTER(u32)], C.c_int),
+        "mtx_bvh_build_occlusion": ([vp, u32, vp, C.POINTER(u32), vp, vp, C.POINTER(u32)], C.c_int),
         "mtx_roughplastic_tables": ([u32, C.c_float, C.c_float, vp, C.POINTER(C.c_float)], C.c_int),
         "mtx_scene_upload": ([vp, C.POINTER(_abi.SceneDesc)], C.c_int),
         "mtx_render": ([vp, C.POINTER(_abi.RenderArgs), vp, C.c_int, C.POINTER(_abi.Stats)], C.c_int),

@@ -240,7 +240,8 @@ class Scene:
         s._build_bvh(tri_vidx, tri_shape)
         s.meta = {"scene": "bedroom-proxy" if not loaded else "xml", "proxy_version": proxy.PROXY_VERSION,
                   "scale": scale, "width": W, "height": H, "n_tris": int(s.n_tris), "budgets": budgets,
-                  "bvh_depth": s.bvh_depth, "n_nodes": int(s.n_nodes), "loaded_files": loaded}
+                  "bvh_depth": s.bvh_depth, "n_nodes": int(s.n_nodes), "occ_depth": s.occ_depth,
+                  "n_occ_nodes": int(s.n_occ_nodes), "loaded_files": loaded}
         return s
 
     @classmethod
@@ -273,6 +274,26 @@ class Scene:
         self.tri_perm = perm  # input triangle of each leaf-order triangle
         self.n_tris = n
         self.bvh_depth = depth.value
+        self._build_occlusion()
+
+    def _build_occlusion(self):
+        """The any-hit BVH (mtx.h occlusion node) over the closest-hit tree's
+        triangle records; occ_perm maps its leaf order to the scene's."""
+        from ._lib import check, lib
+        n = self.n_tris
+        nodes = np.zeros((n + 1) * _abi.MTX_OCC_NODE_WORDS, np.int32)
+        geom = np.zeros(12 * n, np.float32)
+        perm = np.zeros(n, np.uint32)
+        nn = C.c_uint32()
+        depth = C.c_uint32()
+        check(lib().mtx_bvh_build_occlusion(self.tri_geom.ctypes.data, n, nodes.ctypes.data, C.byref(nn),
+                                            geom.ctypes.data, perm.ctypes.data, C.byref(depth)),
+              "mtx_bvh_build_occlusion")
+        self.n_occ_nodes = nn.value
+        self.occ_nodes = np.ascontiguousarray(nodes[: _abi.MTX_OCC_NODE_WORDS * nn.value])
+        self.occ_tri_geom = geom
+        self.occ_perm = perm
+        self.occ_depth = depth.value
 
     # ------------------------------------------------------------- export --
     @property
@@ -320,10 +341,14 @@ class Scene:
         d.tables = self.tables.ctypes.data
         d.n_tables = self.n_tables
         d.camera = self.camera
+        d.occ_nodes = self.occ_nodes.ctypes.data
+        d.occ_tri_geom = self.occ_tri_geom.ctypes.data
+        d.n_occ_nodes = self.n_occ_nodes
         return d
 
     def save(self, path: str):
         np.savez(path, vpos=self.vpos, vnormal=self.vnormal, vuv=self.vuv, nodes=self.nodes, tri_geom=self.tri_geom,
+                 occ_nodes=self.occ_nodes, occ_tri_geom=self.occ_tri_geom, occ_perm=self.occ_perm,
                  tri_vidx=self.tri_vidx, tri_shape=self.tri_shape, texels=self.texels, tables=self.tables,
                  shapes=np.frombuffer(bytes(self.shapes), np.uint8),
                  materials=np.frombuffer(bytes(self.materials), np.uint8),
@@ -331,14 +356,15 @@ class Scene:
                  textures=np.frombuffer(bytes(self.textures), np.uint8),
                  camera=np.frombuffer(bytes(self.camera), np.uint8),
                  meta=np.frombuffer(json.dumps(self.meta).encode(), np.uint8),
-                 counts=np.array([self.n_tris, self.n_nodes, self.n_textures, self.n_tables, self.bvh_depth],
-                                 np.int64))
+                 counts=np.array([self.n_tris, self.n_nodes, self.n_textures, self.n_tables, self.bvh_depth,
+                                  self.n_occ_nodes, self.occ_depth], np.int64))
 
     @classmethod
     def load(cls, path: str) -> "Scene":
         z = np.load(path, allow_pickle=False)
         s = cls()
-        for k in ("vpos", "vnormal", "vuv", "nodes", "tri_geom", "tri_vidx", "tri_shape", "texels", "tables"):
+        for k in ("vpos", "vnormal", "vuv", "nodes", "tri_geom", "tri_vidx", "tri_shape", "texels", "tables",
+                  "occ_nodes", "occ_tri_geom", "occ_perm"):
             setattr(s, k, np.ascontiguousarray(z[k]))
 
         def arr(T, raw):
@@ -352,7 +378,8 @@ class Scene:
         s.textures = arr(_abi.Texture, z["textures"])
         s.camera = _abi.Camera.from_buffer_copy(z["camera"].tobytes())
         s.meta = json.loads(z["meta"].tobytes().decode())
-        s.n_tris, s.n_nodes, s.n_textures, s.n_tables, s.bvh_depth = (int(x) for x in z["counts"])
+        (s.n_tris, s.n_nodes, s.n_textures, s.n_tables, s.bvh_depth, s.n_occ_nodes,
+         s.occ_depth) = (int(x) for x in z["counts"])
         return s
 
 

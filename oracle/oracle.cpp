@@ -57,6 +57,12 @@ SceneView make_view(const mtx_scene_desc *d) {
   SceneView s;
   s.nodes = d->nodes;
   s.tri_geom = d->tri_geom;
+  if (!d->occ_nodes || !d->occ_tri_geom) {
+    std::fprintf(stderr, "oracle: the scene desc needs its occlusion BVH (occ_nodes, occ_tri_geom)\n");
+    std::abort();
+  }
+  s.occ_nodes = d->occ_nodes;
+  s.occ_tri_geom = d->occ_tri_geom;
   s.tri_vidx = d->tri_vidx;
   s.tri_shape = d->tri_shape;
   s.vpos = d->vpos;
@@ -79,27 +85,83 @@ struct Hit {
   uint32_t prim;
 };
 
-// Scalar traversal of the 8-wide compressed BVH (mtx.h), in the device
-// kernels' per-ray order (mtx_core/geometry.h cw_node_hits): a visited node
-// yields a node group (child_base, the hit inner children as mask bits in
-// octant order, imask) and a triangle group (tri_base, the hit leaves'
-// triangles as mask bits); the triangle group is tested first, one triangle
-// per step in ascending offset, then the next child of the node group (the
-// lowest bit) is visited with the rest of the group pushed; an empty group
-// pops the next one. Closest-hit ties on t go to the smaller prim, so the hit
-// does not depend on the order; the visit counts do, and match the device.
 // Diagnostic (tools/ only): visits per node index < g_hist_len are counted
 // into g_hist while orc_node_visit_hist runs (the top-of-tree share of node
 // fetches that an LDS-resident tree top would serve).
 static uint64_t *g_hist = nullptr;
 static uint32_t g_hist_len = 0;
 
-template <bool ANY>
-bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *nodes_visited,
-                uint32_t *tris_visited) {
+// Scalar closest-hit traversal of the 4-wide BVH (mtx.h) in the device
+// kernels' per-ray order: a node's hit children sorted by entry distance
+// (mtx_core/geometry.h wide_node_order), the nearest visited next and the
+// others pushed far-to-near; a leaf's triangles in index order. Ties on t
+// go to the smaller prim, so the hit does not depend on the order; the
+// visit counts do, and match the device (device_common.h trace_loop_closest).
+Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
   TraceRay r = make_trace_ray(o, d, maxt);
   Hit h{maxt, 0.f, 0.f, 0xffffffffu};
   float tbest = maxt;
+  int32_t stack[3 * MTX_BVH_MAX_DEPTH + 2];
+  int sp = 0;
+  int32_t node = 0;
+  uint32_t nv = 0, tv = 0;
+  while (true) {
+    if (node >= 0) {
+      const int32_t *w = s.nodes + MTX_BVH_NODE_WORDS * (size_t)node;
+      const float *f = reinterpret_cast<const float *>(w);
+      ++nv;
+      if (g_hist && (uint32_t)node < g_hist_len) {
+#pragma omp atomic
+        ++g_hist[node];
+      }
+      uint32_t key[4];
+      const int n = wide_node_order(r, f[0], f[1], f[2], (uint32_t)w[3], (uint32_t)w[8], (uint32_t)w[9],
+                                    (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], tbest, key);
+      if (n > 0) {
+        for (int rr = n - 1; rr >= 1; --rr) stack[sp++] = wide_ref(key[rr], w[4], w[5], w[6], w[7]);
+        node = wide_ref(key[0], w[4], w[5], w[6], w[7]);
+        continue;
+      }
+    } else {
+      uint32_t first, count;
+      leaf_decode(node, &first, &count);
+      for (uint32_t k = 0; k < count; ++k) {
+        uint32_t prim = first + k;
+        const float *g = s.tri_geom + 12 * (size_t)prim;
+        float t, u, v;
+        ++tv;
+        if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
+          if (t < tbest || (t == tbest && prim < h.prim)) {
+            tbest = t;
+            h.t = t;
+            h.u = u;
+            h.v = v;
+            h.prim = prim;
+          }
+        }
+      }
+    }
+    if (sp == 0) break;
+    node = stack[--sp];
+  }
+  if (nodes_visited) *nodes_visited = nv;
+  if (tris_visited) *tris_visited = tv;
+  if (h.prim == 0xffffffffu) h.t = kInf;
+  return h;
+}
+
+// Scalar any-hit traversal of the 8-wide occlusion BVH (mtx.h) in the device
+// kernels' per-ray order (mtx_core/geometry.h cw_node_hits): a visited node
+// yields a node group (child_base, the hit inner children as mask bits in
+// octant order, imask) and a triangle group (tri_base, the hit leaves'
+// triangles as mask bits); the triangle group is tested first, one triangle
+// per step in ascending offset, then the next child of the node group (the
+// lowest bit) is visited with the rest of the group pushed; an empty group
+// pops the next one. The answer (any triangle hit in (0, maxt]) does not
+// depend on the tree; the visit counts do, and match the device
+// (device_common.h trace_loop_occ).
+bool trace_any(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
+  TraceRay r = make_trace_ray(o, d, maxt);
   const uint32_t oct = ray_octant(r);
   uint32_t stack[2 * (MTX_BVH_MAX_DEPTH + 2)];
   int sp = 0;
@@ -111,21 +173,12 @@ bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *
     if (thits) {
       const uint32_t prim = tbase + (uint32_t)ctz32(thits);
       thits &= thits - 1u;
-      const float *g = s.tri_geom + 12 * (size_t)prim;
+      const float *g = s.occ_tri_geom + 12 * (size_t)prim;
       float t, u, v;
       ++tv;
-      if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
-        if (ANY) {
-          hit = true;
-          break;
-        }
-        if (t < tbest || (t == tbest && prim < h.prim)) {
-          tbest = t;
-          h.t = t;
-          h.u = u;
-          h.v = v;
-          h.prim = prim;
-        }
+      if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, maxt, &t, &u, &v)) {
+        hit = true;
+        break;
       }
     } else if (ghits >> 24) {
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
@@ -135,14 +188,14 @@ bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *
         stack[sp++] = gbase;
         stack[sp++] = ghits;
       }
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(s.nodes) + MTX_BVH_NODE_WORDS * (size_t)node;
+      const uint32_t *w = reinterpret_cast<const uint32_t *>(s.occ_nodes) + MTX_OCC_NODE_WORDS * (size_t)node;
       const float *f = reinterpret_cast<const float *>(w);
       ++nv;
       if (g_hist && node < g_hist_len) {
 #pragma omp atomic
         ++g_hist[node];
       }
-      const uint32_t hm = cw_node_hits(r, oct, f[0], f[1], f[2], w[3], w[6], w[7], w + 8, tbest);
+      const uint32_t hm = cw_node_hits(r, oct, f[0], f[1], f[2], w[3], w[6], w[7], w + 8, maxt);
       gbase = w[4];
       ghits = (hm & 0xff000000u) | (w[3] >> 24);
       tbase = w[5];
@@ -156,19 +209,7 @@ bool trace_wide(const SceneView &s, V3 o, V3 d, float maxt, Hit *out, uint32_t *
   }
   if (nodes_visited) *nodes_visited = nv;
   if (tris_visited) *tris_visited = tv;
-  if (h.prim == 0xffffffffu) h.t = kInf;
-  if (out) *out = h;
-  return ANY ? hit : h.prim != 0xffffffffu;
-}
-
-Hit trace_closest(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
-  Hit h;
-  trace_wide<false>(s, o, d, maxt, &h, nodes_visited, tris_visited);
-  return h;
-}
-
-bool trace_any(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
-  return trace_wide<true>(s, o, d, maxt, nullptr, nodes_visited, tris_visited);
+  return hit;
 }
 
 Hit brute_closest(const SceneView &s, V3 o, V3 d, float maxt) {

@@ -5,7 +5,8 @@ in the reference tree, so these vectors pin the oracle
 against drift; their contents are data (inputs and outputs), nothing from
 the reference's sources. Vectors:
   rng_seed0 / rng_seed7   first 64 draws of sampler lanes 0..1023
-  trace_rays / trace_hits 4096 rays on the 2 %-budget bedroom proxy
+  trace_rays / trace_hits 4096 rays on the 2 %-budget bedroom proxy (closest hit)
+  any_rays / any_hits     the same rays, every other one with maxt in [0.05, 2) (any hit)
   film_<integrator>       64x36, spp 16, seed 0 films (path_test, mypath, nrc, integrator = simple.py)
   film_pssmlt_simple      32x18, spp 2, seed 2, 60 Metropolis iterations
   film_pssmlt             the same for pssmltpath.py (NEE + MIS proposals)
@@ -45,7 +46,8 @@ def restir_frames(s, frames=3):
 
 def scene_digest(s):
     h = hashlib.sha256()
-    for a in (s.vpos, s.vnormal, s.vuv, s.nodes, s.tri_geom, s.tri_vidx, s.tri_shape, s.texels, s.tables):
+    for a in (s.vpos, s.vnormal, s.vuv, s.nodes, s.tri_geom, s.tri_vidx, s.tri_shape, s.texels, s.tables,
+              s.occ_nodes, s.occ_tri_geom):
         h.update(np.ascontiguousarray(a).tobytes())
     for a in (s.shapes, s.materials, s.emitters, s.textures, s.camera):
         h.update(bytes(a))
@@ -62,6 +64,12 @@ def golden_rays(s, n=4096, seed=123):
     return rays
 
 
+def any_rays(rays, seed=321):
+    r = rays.copy()
+    r[::2, 3] = np.random.default_rng(seed).uniform(0.05, 2.0, len(r[::2])).astype(np.float32)
+    return r
+
+
 def compute():
     s = scene.bedroom(width=64, height=36, scale=0.02, tex_res=64)
     out = {"scene_sha": np.frombuffer(scene_digest(s).encode(), np.uint8)}
@@ -70,6 +78,8 @@ def compute():
     rays = golden_rays(s)
     out["trace_rays"] = rays
     out["trace_hits"] = oracle.trace(s, rays)[0]
+    out["any_rays"] = any_rays(rays)
+    out["any_hits"] = oracle.trace(s, out["any_rays"], any_hit=True)[0]
     for name in INTEGRATORS:
         integ = load_dict({"type": name})
         out[f"film_{name}"] = oracle.render(s, integ.render_args(s, 0, 16))

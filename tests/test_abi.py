@@ -26,7 +26,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 5
+    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 6
 
 
 def test_struct_sizes_match_header():
@@ -69,6 +69,9 @@ def test_bvh_build_rejects_bad_input():
     rc = L.mtx_bvh_build(v.ctypes.data, 3, idx.ctypes.data, 1, nodes.ctypes.data, C.byref(nn), geom.ctypes.data,
                          perm.ctypes.data, C.byref(dep))
     assert rc == -1 and b"out of range" in L.mtx_last_error()
+    rc = L.mtx_bvh_build_occlusion(geom.ctypes.data, 0, nodes.ctypes.data, C.byref(nn), geom.ctypes.data, None,
+                                   C.byref(dep))
+    assert rc == -1 and b"empty" in L.mtx_last_error()
 
 
 def test_roughplastic_tables():

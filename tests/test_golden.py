@@ -30,6 +30,7 @@ def test_golden_rng(golden, oracle):
 
 def test_golden_trace(golden, oracle, small_scene):
     assert np.array_equal(oracle.trace(small_scene, golden["trace_rays"])[0], golden["trace_hits"])
+    assert np.array_equal(oracle.trace(small_scene, golden["any_rays"], any_hit=True)[0], golden["any_hits"])
 
 
 @pytest.mark.parametrize("name", ["path_test", "mypath", "nrc", "integrator"])
@@ -62,6 +63,9 @@ def test_golden_independent_of_bvh_collapse(golden, oracle, small_scene, monkeyp
     same = sc.tri_perm[h[~miss, 1]] == small_scene.tri_perm[g[~miss, 1]]
     assert same.mean() > 0.995
     assert np.array_equal(h[~miss][same][:, 2:], g[~miss][same][:, 2:])
+    # any hit: a different occlusion tree, the same answers
+    assert not np.array_equal(sc.occ_perm, small_scene.occ_perm)
+    assert np.array_equal(oracle.trace(sc, golden["any_rays"], any_hit=True)[0], golden["any_hits"])
     # the others are exact-t ties: rays through a shared edge, or onto
     # coplanar overlapping surfaces of two shapes (the floor and the carpet
     # at y = 0): the hit point (same t) lies in both triangles' planes

@@ -5,10 +5,11 @@ branches (VERDICT r1 "next" #4).
   visit counts of 2^16 rays, and the path_test film (path-mis.py:24-155) at
   spp 2, bit-exact against the oracle (the oracle traces the same 1.84 M
   paths on the host cores in about a second).
-* The traversal stack's global spill area (csrc/device_common.h, pushes
-  beyond the LDS entries): a fresh process with MTX_LDS_STACK=1 keeps one
-  entry in LDS, so every deeper push and pop goes through global memory;
-  also without the LDS tree top (MTX_LDS_TOP=0) and the non-XCD-claiming
+* The traversal stacks' global spill area (csrc/device_common.h, pushes
+  beyond the LDS entries): a fresh process with MTX_LDS_STACK=1 and
+  MTX_OCC_LDS_STACK=1 keeps one entry of either tree's stack in LDS, so every
+  deeper push and pop goes through global memory; also without the LDS tree
+  tops (MTX_LDS_TOP=0, MTX_OCC_LDS_TOP=0) and the non-XCD-claiming
   traversal (MTX_XCD_CLAIM=0). The environment is read when the context is created, so
   each variant runs in its own subprocess before any GPU call.
 * max_depth 65, the default of data/bedroom/scene.xml:6 (SURVEY §8d C2
@@ -93,7 +94,9 @@ print("CHILD OK")
 """
 
 
-@pytest.mark.parametrize("env", [{"MTX_LDS_STACK": "1"}, {"MTX_LDS_STACK": "2", "MTX_LDS_TOP": "0"},
+@pytest.mark.parametrize("env", [{"MTX_LDS_STACK": "1", "MTX_OCC_LDS_STACK": "1"},
+                                 {"MTX_LDS_STACK": "2", "MTX_LDS_TOP": "0", "MTX_OCC_LDS_STACK": "2",
+                                  "MTX_OCC_LDS_TOP": "0"},
                                  {"MTX_XCD_CLAIM": "0", "MTX_TRACE_BATCH": "64"}],
                          ids=["spill-all", "spill2-notop", "noxcd-batch64"])
 def test_traversal_variants_bit_exact(env):

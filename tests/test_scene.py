@@ -68,18 +68,95 @@ def _decode(org, e, q):
 
 
 def test_bvh_invariants(small_scene):
-    """8-wide compressed nodes (mtx.h): every triangle in exactly one leaf of
-    at most 3, leaves' triangles consecutive from tri_base in slot order,
-    inner children consecutive from child_base in slot order (breadth-first:
-    after their parent), meta bytes as documented, empty slots never hit
-    (q_lo 255 > q_hi 0), children's decoded boxes contain their triangles /
+    """Closest-hit tree, 4-wide quantised nodes (mtx.h): every triangle in
+    exactly one leaf of at most 8, a node's inner children first in slot order
+    and at consecutive indices after it (breadth-first), its leaves' triangle
+    ranges consecutive, children's decoded boxes contain their triangles /
     subtrees, depth as reported."""
     s = small_scene
-    _check_bvh(s.nodes, s.tri_geom, s.n_tris, s.bvh_depth)
+    _check_bvh4(s.nodes, s.tri_geom, s.n_tris, s.bvh_depth)
+
+
+def test_occlusion_bvh_invariants(small_scene):
+    """Occlusion tree, 8-wide compressed nodes (mtx.h): every triangle in
+    exactly one leaf of at most 3, leaves' triangles consecutive from tri_base
+    in slot order, inner children consecutive from child_base in slot order
+    (breadth-first: after their parent), meta bytes as documented, empty slots
+    never hit (q_lo 255 > q_hi 0), children's decoded boxes contain their
+    triangles / subtrees, depth as reported; its records are the scene's
+    records bit for bit, permuted."""
+    s = small_scene
+    _check_occ(s.occ_nodes, s.occ_tri_geom, s.n_tris, s.occ_depth)
+    assert sorted(s.occ_perm.tolist()) == list(range(s.n_tris))
+    assert np.array_equal(s.occ_tri_geom.reshape(-1, 12).view(np.uint32),
+                          s.tri_geom.reshape(-1, 12)[s.occ_perm].view(np.uint32))
+
+
+def _tri_boxes(tri_geom):
+    geom = tri_geom.reshape(-1, 12)
+    v0 = geom[:, 0:3]
+    v1 = v0 + geom[:, 4:7]
+    v2 = v0 + geom[:, 8:11]
+    return np.minimum(np.minimum(v0, v1), v2), np.maximum(np.maximum(v0, v1), v2)
+
+
+def _check_bvh4(nodes, tri_geom, n_tris, bvh_depth):
+    nodes = nodes.reshape(-1, 16)
+    f = nodes.view(np.float32)
+    u = nodes.view(np.uint32)
+    seen = np.zeros(n_tris, np.int32)
+    lo, hi = _tri_boxes(tri_geom)
+
+    def subtree_box(ref):
+        if ref < 0:
+            x = ~int(ref)
+            a, c = x >> 3, (x & 7) + 1
+            return lo[a:a + c].min(0), hi[a:a + c].max(0)
+        return boxes[ref]
+
+    boxes, order = {}, []
+    stack = [(0, 1)]
+    max_depth = 0
+    while stack:
+        i, dep = stack.pop()
+        order.append(i)
+        max_depth = max(max_depth, dep)
+        nch = int(u[i, 3] >> 24)
+        assert 1 <= nch <= 4
+        refs = [int(nodes[i, 4 + k]) for k in range(nch)]
+        n_in = sum(r >= 0 for r in refs)
+        assert all(r >= 0 for r in refs[:n_in])  # inner children first
+        assert refs[:n_in] == list(range(refs[0], refs[0] + n_in)) if n_in else True
+        assert all(r > i for r in refs[:n_in])  # breadth-first: children after their parent
+        firsts = [(~r) >> 3 for r in refs[n_in:]]
+        cnts = [((~r) & 7) + 1 for r in refs[n_in:]]
+        assert all(firsts[j + 1] == firsts[j] + cnts[j] for j in range(len(firsts) - 1))
+        for r in refs[:n_in]:
+            stack.append((r, dep + 1))
+        for a, c in zip(firsts, cnts):
+            assert c <= 8
+            seen[a:a + c] += 1
+    for i in reversed(order):  # children before parents
+        nch = int(u[i, 3] >> 24)
+        e = [np.int8(np.uint8((u[i, 3] >> (8 * a)) & 255)) for a in range(3)]
+        assert all(-32 <= x <= 31 for x in e)
+        blo = np.full(3, np.inf, np.float32)
+        bhi = np.full(3, -np.inf, np.float32)
+        for k in range(nch):
+            clo, chi = subtree_box(int(nodes[i, 4 + k]))
+            for a in range(3):
+                qlo = (u[i, 8 + 2 * a] >> (8 * k)) & 255
+                qhi = (u[i, 9 + 2 * a] >> (8 * k)) & 255
+                assert _decode(f[i, a], e[a], qlo) <= clo[a] and _decode(f[i, a], e[a], qhi) >= chi[a]
+            blo, bhi = np.minimum(blo, clo), np.maximum(bhi, chi)
+        boxes[i] = (blo, bhi)
+    assert (seen == 1).all()
+    assert max_depth <= 40 and max_depth == bvh_depth
+    assert len(order) == len(nodes)
 
 
 def _node_children(u, i):
-    """[(slot, 'inner', node) | (slot, 'leaf', first, count)] of node i."""
+    """[(slot, 'inner', node) | (slot, 'leaf', first, count)] of occlusion node i."""
     imask, cb, tb = int(u[i, 3] >> 24), int(u[i, 4]), int(u[i, 5])
     out, inner, off = [], 0, 0
     for sl in range(8):
@@ -96,17 +173,12 @@ def _node_children(u, i):
     return out
 
 
-def _check_bvh(nodes, tri_geom, n_tris, bvh_depth):
+def _check_occ(nodes, tri_geom, n_tris, depth):
     nodes = nodes.reshape(-1, 20)
     f = nodes.view(np.float32)
     u = nodes.view(np.uint32)
     seen = np.zeros(n_tris, np.int32)
-    geom = tri_geom.reshape(-1, 12)
-    v0 = geom[:, 0:3]
-    v1 = v0 + geom[:, 4:7]
-    v2 = v0 + geom[:, 8:11]
-    lo = np.minimum(np.minimum(v0, v1), v2)
-    hi = np.maximum(np.maximum(v0, v1), v2)
+    lo, hi = _tri_boxes(tri_geom)
     boxes, order, kids = {}, [], {}
     stack = [(0, 1)]
     max_depth = 0
@@ -146,21 +218,37 @@ def _check_bvh(nodes, tri_geom, n_tris, bvh_depth):
             blo, bhi = np.minimum(blo, clo), np.maximum(bhi, chi)
         boxes[i] = (blo, bhi)
     assert (seen == 1).all()
-    assert max_depth <= 40 and max_depth == bvh_depth
+    assert max_depth <= 40 and max_depth == depth
     assert len(order) == len(nodes)
 
 
-def test_bvh_closest_hit_equals_brute_force(small_scene, oracle):
-    rng = np.random.default_rng(11)
-    n = 6000
+def _random_rays(n, seed):
+    rng = np.random.default_rng(seed)
     rays = np.zeros((n, 8), np.float32)
     rays[:, 0:3] = rng.uniform([-3.0, 0.05, -1.2], [3.8, 2.6, 3.6], (n, 3))
     d = rng.normal(size=(n, 3))
     rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
     rays[:, 3] = 3e38
+    return rays, rng
+
+
+def test_bvh_closest_hit_equals_brute_force(small_scene, oracle):
+    rays, _ = _random_rays(6000, 11)
     h, _ = oracle.trace(small_scene, rays)
     b, _ = oracle.trace(small_scene, rays, brute=True)
     assert np.array_equal(h, b)
+
+
+def test_occlusion_any_hit_equals_brute_force(small_scene, oracle):
+    """The occlusion tree answers ray_test exactly as a brute-force closest
+    hit does: occluded iff some triangle lies in (0, maxt] (finite and
+    unbounded maxt)."""
+    rays, rng = _random_rays(6000, 12)
+    rays[::2, 3] = rng.uniform(0.05, 2.0, 3000).astype(np.float32)
+    a, _ = oracle.trace(small_scene, rays, any_hit=True)
+    b, _ = oracle.trace(small_scene, rays, brute=True)
+    assert 0 < a.sum() < len(a)
+    assert np.array_equal(a.astype(bool), b.reshape(-1, 4)[:, 1] != 0xFFFFFFFF)
 
 
 def test_scene_save_load_roundtrip(small_scene, tmp_path):
@@ -170,6 +258,8 @@ def test_scene_save_load_roundtrip(small_scene, tmp_path):
     small_scene.save(p)
     t = scene.Scene.load(p)
     assert np.array_equal(t.nodes, small_scene.nodes) and bytes(t.materials) == bytes(small_scene.materials)
+    assert np.array_equal(t.occ_nodes, small_scene.occ_nodes) and t.occ_depth == small_scene.occ_depth
+    assert np.array_equal(t.occ_tri_geom, small_scene.occ_tri_geom)
     assert bytes(t.camera) == bytes(small_scene.camera)
     assert json.dumps(t.meta, sort_keys=True) == json.dumps(small_scene.meta, sort_keys=True)
 
@@ -192,8 +282,9 @@ def _tiny_mesh(kind):
 @pytest.mark.parametrize("cnode", ["1", "4"])
 @pytest.mark.parametrize("kind", ["one", "two", "nine", "identical", "planar", "random"])
 def test_bvh_build_small_and_degenerate_meshes(kind, cnode, monkeypatch):
-    """The 8-wide collapse keeps the node invariants on tiny, coplanar and
-    coincident-triangle meshes (two collapse node costs: other trees)."""
+    """Both collapses (4-wide closest hit, 8-wide occlusion) keep the node
+    invariants on tiny, coplanar and coincident-triangle meshes (two collapse
+    node costs: other trees)."""
     import ctypes as C
 
     from mtx import _lib
@@ -201,7 +292,7 @@ def test_bvh_build_small_and_degenerate_meshes(kind, cnode, monkeypatch):
     monkeypatch.setenv("MTX_BVH_CNODE", cnode)
     v, idx = _tiny_mesh(kind)
     n = len(idx)
-    nodes = np.zeros((n + 1) * 20, np.int32)
+    nodes = np.zeros((n + 1) * 16, np.int32)
     geom = np.zeros(12 * n, np.float32)
     perm = np.zeros(n, np.uint32)
     nn, dep = C.c_uint32(), C.c_uint32()
@@ -210,4 +301,13 @@ def test_bvh_build_small_and_degenerate_meshes(kind, cnode, monkeypatch):
                          C.byref(nn), geom.ctypes.data, perm.ctypes.data, C.byref(dep))
     assert rc == 0, L.mtx_last_error()
     assert sorted(perm.tolist()) == list(range(n))
-    _check_bvh(nodes[: 20 * nn.value], geom, n, dep.value)
+    _check_bvh4(nodes[: 16 * nn.value], geom, n, dep.value)
+    onodes = np.zeros((n + 1) * 20, np.int32)
+    ogeom = np.zeros(12 * n, np.float32)
+    operm = np.zeros(n, np.uint32)
+    rc = L.mtx_bvh_build_occlusion(geom.ctypes.data, n, onodes.ctypes.data, C.byref(nn), ogeom.ctypes.data,
+                                   operm.ctypes.data, C.byref(dep))
+    assert rc == 0, L.mtx_last_error()
+    assert sorted(operm.tolist()) == list(range(n))
+    assert np.array_equal(ogeom.reshape(-1, 12), geom.reshape(-1, 12)[operm])
+    _check_occ(onodes[: 20 * nn.value], ogeom, n, dep.value)

@@ -1,7 +1,7 @@
 """Share of BVH node visits that land in the top levels of the tree (oracle
 traversal, CPU): camera rays, diffuse secondary rays from their hits and
-shadow rays to the emitters, as in tools/bvh_experiment.py. Sizes an
-LDS-resident tree top for the traversal kernels."""
+shadow rays to the emitters (occlusion tree), as in tools/bvh_experiment.py.
+Sizes the LDS-resident tree tops of the traversal kernels."""
 import os
 import sys
 
@@ -13,12 +13,25 @@ sys.path[:0] = [os.path.join(ROOT, "mitsuba3-experiments_amd"), os.path.join(ROO
 
 
 def node_levels(nodes, n_nodes):
-    """Tree level of every 8-wide node (mtx.h: inner children are
+    """Tree level of every 4-wide closest-hit node (mtx.h: child refs >= 0
+    are inner nodes, breadth-first)."""
+    w = nodes.reshape(-1, 16)
+    lev = np.full(n_nodes, -1, np.int64)
+    lev[0] = 0
+    for i in range(n_nodes):  # breadth-first layout: parents precede children
+        for k in range(int(w[i, 3].view(np.uint32) >> 24)):
+            if w[i, 4 + k] >= 0:
+                lev[int(w[i, 4 + k])] = lev[i] + 1
+    return lev
+
+
+def occ_node_levels(nodes, n_nodes):
+    """Tree level of every 8-wide occlusion node (mtx.h: inner children are
     child_base + rank among the inner slots, breadth-first)."""
     w = nodes.reshape(-1, 20).view(np.uint32)
     lev = np.full(n_nodes, -1, np.int64)
     lev[0] = 0
-    for i in range(n_nodes):  # breadth-first layout: parents precede children
+    for i in range(n_nodes):
         n_inner = bin(int(w[i, 3] >> 24)).count("1")
         for r in range(n_inner):
             lev[int(w[i, 4]) + r] = lev[i] + 1
@@ -31,6 +44,7 @@ def main(n=200_000):
 
     sc = scene.bedroom(cache_dir=os.path.join(ROOT, ".cache"))
     lev = node_levels(np.asarray(sc.nodes), int(sc.n_nodes))
+    olev = occ_node_levels(np.asarray(sc.occ_nodes), int(sc.n_occ_nodes))
     H = 4096
     rng = np.random.default_rng(0)
     cam = sc.camera
@@ -68,10 +82,11 @@ def main(n=200_000):
     dist = np.linalg.norm(sd, axis=1)
     r3 = np.zeros((len(p), 8), np.float32)
     r3[:, 0:3], r3[:, 4:7], r3[:, 3] = p, sd / dist[:, None], dist * 0.999
-    print(f"nodes {sc.n_nodes}, nodes per level (top 6):",
-          [int((lev == k).sum()) for k in range(6)], "first index of level:",
-          [int(np.argmax(lev == k)) for k in range(6)])
+    for nm, lv in (("closest-hit", lev), ("occlusion", olev)):
+        print(f"{nm} nodes {len(lv)}, nodes per level (top 6):", [int((lv == k).sum()) for k in range(6)],
+              "first index of level:", [int(np.argmax(lv == k)) for k in range(6)])
     for name, rr, anyh in (("primary", rays, False), ("secondary", r2, False), ("shadow", r3, True)):
+        lev = olev if anyh else lev
         _, vv = oracle.trace(sc, rr, any_hit=anyh)
         tot = float(vv[:, 0].sum())
         hist = oracle.node_visit_hist(sc, rr, H, any_hit=anyh).astype(np.float64)
