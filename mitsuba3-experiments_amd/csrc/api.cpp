@@ -815,40 +815,57 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
   }
 }
 
+// One bounce of a chunk: closest hit, shade, NEE shadow rays.
+void launch_bounce(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
+                   uint64_t *n_trace, uint64_t *n_shadow, const mtxd::DevScene &s, hipStream_t st, uint32_t bounce) {
+  // nerad RHS lanes start at their surface point (no bounce-0 trace) and
+  // trace NEE rays at that point only
+  const bool nerad = p.integrator == MTX_INT_NERAD_RHS, nerad_render = p.integrator == MTX_INT_NERAD;
+  hipEvent_t e;
+  // past its second vertex the nerad RHS chain only continues through
+  // delta surfaces (next_smooth_si): a small queue, traced and shaded by
+  // an eighth of the persistent grid (dispatching the full grid of
+  // immediately-exiting blocks costs more than the work)
+  const int div = (nerad && bounce >= 2) ? 8 : 1;
+  if (!(nerad && bounce == 0)) {
+    e = tm.begin(0, st);
+    mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), st);
+    tm.end(0, e, st);
+    ++*n_trace;
+  }
+  e = tm.begin(2, st);
+  mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), st);
+  tm.end(2, e, st);
+  if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
+      !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays
+    e = tm.begin(1, st);
+    mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, st);
+    tm.end(1, e, st);
+    ++*n_shadow;
+  }
+}
+
+// Bounces of a chunk's loop (an NRC cache query needs one more trace + shade
+// after the last segment).
+uint32_t bounce_iters(const mtxd::ChunkParams &p) {
+  return std::max<uint32_t>(p.max_depth, 1) + (p.nrc_cache ? 1u : 0u);
+}
+
+// Paths a depth limit left queued keep their result in a queue plane.
+void finish_bounces(const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, hipStream_t st) {
+  if (p.integrator != MTX_INT_NERAD_RHS && p.integrator != MTX_INT_NERAD)
+    mtxd::launch_flush_tail(b, bounce_iters(p), b.capacity, p.integrator, st);
+}
+
 // Runs one chunk's bounce loop (rays already generated, counters[0] set).
 void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
                  uint64_t *n_trace, uint64_t *n_shadow, const mtxd::DevScene *scene = nullptr,
                  hipStream_t stream = nullptr) {
   const mtxd::DevScene &s = scene ? *scene : c->scene;
   hipStream_t st = stream ? stream : c->stream;
-  // an NRC cache query needs one more trace + shade after the last segment
-  const uint32_t depth_iters = std::max<uint32_t>(p.max_depth, 1) + (p.nrc_cache ? 1u : 0u);
-  // nerad RHS lanes start at their surface point (no bounce-0 trace) and
-  // trace NEE rays at that point only
-  const bool nerad = p.integrator == MTX_INT_NERAD_RHS, nerad_render = p.integrator == MTX_INT_NERAD;
+  const uint32_t depth_iters = bounce_iters(p);
   for (uint32_t bounce = 0; bounce < depth_iters; ++bounce) {
-    hipEvent_t e;
-    // past its second vertex the nerad RHS chain only continues through
-    // delta surfaces (next_smooth_si): a small queue, traced and shaded by
-    // an eighth of the persistent grid (dispatching the full grid of
-    // immediately-exiting blocks costs more than the work)
-    const int div = (nerad && bounce >= 2) ? 8 : 1;
-    if (!(nerad && bounce == 0)) {
-      e = tm.begin(0, st);
-      mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), st);
-      tm.end(0, e, st);
-      ++*n_trace;
-    }
-    e = tm.begin(2, st);
-    mtxd::launch_shade(s, b, p, bounce, std::max(1, c->shade_grid / div), st);
-    tm.end(2, e, st);
-    if (p.integrator != MTX_INT_PSSMLT_SIMPLE && p.integrator != MTX_INT_SIMPLE && !nerad_render &&
-        !(nerad && bounce > 0)) {  // PSSMLT, simple and the nerad render trace no NEE rays
-      e = tm.begin(1, st);
-      mtxd::launch_trace_shadow(s, b, bounce, p.stats, c->trace_grid, st);
-      tm.end(1, e, st);
-      ++*n_shadow;
-    }
+    launch_bounce(c, b, p, tm, n_trace, n_shadow, s, st, bounce);
     // Deep paths (max_depth 65, scene.xml:6): stop launching once the queue
     // has drained (checked every 8 bounces).
     if (depth_iters > 16 && (bounce & 7) == 7 && bounce + 1 < depth_iters) {
@@ -858,8 +875,7 @@ void run_bounces(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams
       if (cnt == 0) return;
     }
   }
-  // paths a depth limit left queued keep their result in a queue plane
-  if (!nerad && !nerad_render) mtxd::launch_flush_tail(b, depth_iters, b.capacity, p.integrator, st);
+  finish_bounces(b, p, st);
 }
 
 int fill_stats(mtx_ctx *c, mtx_stats *stats, bool want_stats, Timer &tm, uint64_t n_trace, uint64_t n_shadow,
@@ -1040,34 +1056,47 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
       HIP_TRY(hipEventRecord(c->w2.start, st));  // after the frame-0 clears
       HIP_TRY(hipStreamWaitEvent(c->w2.stream, c->w2.start, 0));
     }
-    for (int h = 0; h < (two ? 2 : 1); ++h) {
+    // The halves' launches are enqueued interleaved, step by step (prologue,
+    // each bounce, epilogue), so the second stream starts at once instead of
+    // after the host has queued all of the first half's launches.
+    const int halves = two ? 2 : 1;
+    hipStream_t sh[2] = {st, c->w2.stream};
+    const mtxd::DevScene *sc[2] = {&c->scene, &s2};
+    mtxd::WaveBuffers bh[2], b1[2];
+    mtxd::ChunkParams ph[2];
+    mtxd::RestirBuffers rh[2];
+    for (int h = 0; h < halves; ++h) {
       const uint32_t ya = h ? ym : a->y0, yb = h ? a->y1 : ym;
-      hipStream_t sh = h ? c->w2.stream : st;
-      const mtxd::DevScene &sc = h ? s2 : c->scene;
-      mtxd::WaveBuffers bh = h ? bw2 : b;
-      bh.rs_xs = b.rs_xs + (size_t)(ya - a->y0) * W * spp;  // path-indexed within the half
-      bh.rs_ns = b.rs_ns + (size_t)(ya - a->y0) * W * spp;
-      mtxd::ChunkParams ph = p;
-      ph.px0 = ya * W;
-      ph.n_px = (yb - ya) * W;
-      ph.n_paths = ph.n_px * spp;
-      mtxd::RestirBuffers rh = r;
-      rh.lane0 = ya * W * spp;
-      rh.nb = ph.n_paths;
+      bh[h] = h ? bw2 : b;
+      bh[h].rs_xs = b.rs_xs + (size_t)(ya - a->y0) * W * spp;  // path-indexed within the half
+      bh[h].rs_ns = b.rs_ns + (size_t)(ya - a->y0) * W * spp;
+      ph[h] = p;
+      ph[h].px0 = ya * W;
+      ph[h].n_px = (yb - ya) * W;
+      ph[h].n_paths = ph[h].n_px * spp;
+      rh[h] = r;
+      rh[h].lane0 = ya * W * spp;
+      rh[h].nb = ph[h].n_paths;
       // sample_initial: primary rays and their closest hits
-      HIP_TRY(reset_counters(bh, depth, sh));
-      mtxd::launch_raygen_camera(sc, bh, ph, sh);
-      e = tm.begin(0, sh);
-      mtxd::launch_trace_closest(sc, bh, 0, ph.stats, c->trace_grid, sh);
-      tm.end(0, e, sh);
+      HIP_TRY(reset_counters(bh[h], depth, sh[h]));
+      mtxd::launch_raygen_camera(*sc[h], bh[h], ph[h], sh[h]);
+      e = tm.begin(0, sh[h]);
+      mtxd::launch_trace_closest(*sc[h], bh[h], 0, ph[h].stats, c->trace_grid, sh[h]);
+      tm.end(0, e, sh[h]);
       ++*n_trace;
-      HIP_TRY(reset_counters(bh, depth, sh));
-      mtxd::launch_restir_begin(sc, bh, ph, rh, sh);
-      mtxd::WaveBuffers b1 = bh;  // k_rs_begin left the secondary rays in the parity-1 planes
-      b1.ray_par = 1;
-      run_bounces(c, b1, ph, tm, n_trace, n_shadow, &sc, sh);  // sample_ray (path-mis loop)
-      mtxd::launch_restir_collect(bh, ph, rh, sh);
-      mtxd::launch_restir_temporal(rh, ph, sh);
+      HIP_TRY(reset_counters(bh[h], depth, sh[h]));
+      mtxd::launch_restir_begin(*sc[h], bh[h], ph[h], rh[h], sh[h]);
+      b1[h] = bh[h];  // k_rs_begin left the secondary rays in the parity-1 planes
+      b1[h].ray_par = 1;
+    }
+    // sample_ray (the path-mis loop)
+    const uint32_t iters = bounce_iters(p);
+    for (uint32_t bounce = 0; bounce < iters; ++bounce)
+      for (int h = 0; h < halves; ++h) launch_bounce(c, b1[h], ph[h], tm, n_trace, n_shadow, *sc[h], sh[h], bounce);
+    for (int h = 0; h < halves; ++h) {
+      finish_bounces(b1[h], ph[h], sh[h]);
+      mtxd::launch_restir_collect(bh[h], ph[h], rh[h], sh[h]);
+      mtxd::launch_restir_temporal(rh[h], ph[h], sh[h]);
     }
     if (two) {  // stage B reads every lane of the band
       HIP_TRY(hipEventRecord(c->w2.done, c->w2.stream));
@@ -1178,9 +1207,12 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     uint64_t n_trace = 0, n_shadow = 0;
     if ((rc = render_restir(c, a, film_dev, tm, &n_trace, &n_shadow, want_stats))) return rc;
     tm.end(3, e_all);
-    if (!film_on_device)
+    // stage A writes no film: no copy, and no wait unless stats were asked
+    // for (the caller's stage B follows on the same stream)
+    const bool stage_a = (a->restir_flags & MTX_RESTIR_STAGE_A) != 0;
+    if (!film_on_device && !stage_a)
       HIP_TRY(hipMemcpyAsync(film_rgbw, film_dev, film_floats * 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!stage_a || stats) HIP_TRY(hipStreamSynchronize(c->stream));
     return fill_stats(c, stats, want_stats, tm, n_trace, n_shadow, (uint64_t)W * H * a->spp);
   }
   if (mlt) {

@@ -81,6 +81,32 @@ def test_trace_closest_and_any_hit_bit_exact(small_scene, oracle):
     assert np.array_equal(g_vis2, c_vis2)
 
 
+def test_upload_builds_the_occlusion_tree_when_absent(small_scene, oracle):
+    """A scene desc without the occlusion BVH (occ_nodes = NULL, the C ABI's
+    drop-in case): mtx_scene_upload builds it from tri_geom with the same
+    builder, so any-hit answers and visit counts equal the oracle's on the
+    Python-built tree."""
+    import copy
+
+    sc = copy.copy(small_scene)
+    full = sc.desc
+
+    def desc():
+        d = full()
+        d.occ_nodes, d.occ_tri_geom, d.n_occ_nodes = None, None, 0
+        return d
+
+    sc.desc = desc
+    o, d = _camera_rays(small_scene, 2048, seed=4)
+    rays = np.zeros((len(o), 8), np.float32)
+    rays[:, 0:3], rays[:, 4:7] = o, d
+    rays[:, 3] = np.float32(3.0e38)
+    rays[1::3, 3] = np.float32(0.7)
+    g_any, g_vis = _trace_gpu(sc, rays, True)
+    c_any, c_vis = oracle.trace(small_scene, rays, True)
+    assert np.array_equal(g_any, c_any) and np.array_equal(g_vis, c_vis)
+
+
 @pytest.mark.parametrize("name", INTEGRATORS)
 def test_sample_rays_bit_exact(small_scene, oracle, name):
     from mtx import IndependentSampler, load_dict
