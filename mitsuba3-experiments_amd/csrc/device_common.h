@@ -32,7 +32,6 @@ inline size_t persistent_stack_bytes(const DevScene &s, bool occ) {
   return occ ? (size_t)s.occ_lds_entries * kTraceBlock * sizeof(uint2) + (size_t)s.occ_lds_top * 80
              : (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t) + (size_t)s.lds_top * 64;
 }
-constexpr int kShadeBlock = 256;
 
 __device__ __forceinline__ SceneView make_view(const DevScene &s) {
   SceneView v;
@@ -296,6 +295,12 @@ __device__ __forceinline__ void traverse_closest(const DevScene &s, int32_t *stk
 #pragma unroll
         for (int rr = 3; rr >= 1; --rr)
           if (rr < n) {
+#ifdef MTX_MEGA_CHECK
+            if (sp >= (int)s.stack_entries) {
+              printf("closest stack overflow sp %d\n", sp);
+              return;
+            }
+#endif
             stk[sp * kTraceBlock] = cr[rr];
             ++sp;
           }
@@ -305,6 +310,12 @@ __device__ __forceinline__ void traverse_closest(const DevScene &s, int32_t *stk
     } else {
       uint32_t first, count;
       leaf_decode(node, &first, &count);
+#ifdef MTX_MEGA_CHECK
+      if (first + count > s.n_tris) {
+        printf("closest leaf %u+%u\n", first, count);
+        return;
+      }
+#endif
       for (uint32_t k = 0; k < count; ++k) {
         const uint32_t prim = first + k;
         const TriGeom g = load_tri(s.tri, prim);
@@ -397,6 +408,12 @@ __device__ __forceinline__ bool traverse_occ(const DevScene &s, uint2 *stk, cons
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
       ghits &= ~(1u << (24 + p));
       const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
+#ifdef MTX_MEGA_CHECK
+      if (sp >= (int)s.occ_stack_entries) {
+        printf("occ stack overflow sp %d\n", sp);
+        return false;
+      }
+#endif
       if (ghits >> 24) stk[(sp++) * kTraceBlock] = make_uint2(gbase, ghits);
       ++nv;
       const CwVisit v = cw_visit(s, r, oct, node, tmax, nullptr, 0);

@@ -80,6 +80,29 @@ __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_closest(De
   }
 }
 
+// A shadow record's contribution to its path's L (T, X and flags of
+// make_shadow): fma(T, X, L) or L + X when the ray is unoccluded, the
+// flagged channels NaN when it is occluded.
+__device__ __forceinline__ void apply_shadow(float4 &L, float4 rt, float4 rx, bool occluded) {
+  const uint32_t fl = __float_as_uint(rt.w);
+  if (!occluded) {
+    if (fl & 1u) {
+      L.x = fmaf(rt.x, rx.x, L.x);
+      L.y = fmaf(rt.y, rx.y, L.y);
+      L.z = fmaf(rt.z, rx.z, L.z);
+    } else {
+      L.x = L.x + rx.x;
+      L.y = L.y + rx.y;
+      L.z = L.z + rx.z;
+    }
+  } else {
+    const float qnan = __uint_as_float(0x7fc00000u);
+    if (fl & 2u) L.x = qnan;
+    if (fl & 4u) L.y = qnan;
+    if (fl & 8u) L.z = qnan;
+  }
+}
+
 // Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
 // contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
 // form).
@@ -102,27 +125,9 @@ struct ShadowSrc {
     pl.x = b.shadow[k].x;
   }
   __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
-    const float4 rt = pl.t, rx = pl.x;
-    const uint32_t li = pl.li;
-    const uint32_t fl = __float_as_uint(rt.w);
-    float4 L = b.L[0][li];
-    if (!occluded) {
-      if (fl & 1u) {
-        L.x = fmaf(rt.x, rx.x, L.x);
-        L.y = fmaf(rt.y, rx.y, L.y);
-        L.z = fmaf(rt.z, rx.z, L.z);
-      } else {
-        L.x = L.x + rx.x;
-        L.y = L.y + rx.y;
-        L.z = L.z + rx.z;
-      }
-    } else {
-      const float qnan = __uint_as_float(0x7fc00000u);
-      if (fl & 2u) L.x = qnan;
-      if (fl & 4u) L.y = qnan;
-      if (fl & 8u) L.z = qnan;
-    }
-    b.L[0][li] = L;
+    float4 L = b.L[0][pl.li];
+    apply_shadow(L, pl.t, pl.x, occluded);
+    b.L[0][pl.li] = L;
   }
 };
 
@@ -1009,6 +1014,81 @@ __global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator
   }
 }
 
+// Path megakernel for short wavefronts (ReSTIR GI's secondary paths of a
+// row band): each thread takes one queued path and runs all of its bounces
+// -- closest hit (traverse_closest), shade_path, the NEE shadow ray
+// (traverse_occ) applied to its L at once -- with its state kept at its own
+// queue position (no compaction). A short queue leaves most lanes of the
+// wavefront kernels idle and each launch waits for its slowest ray, once per
+// bounce and kernel; here a path waits only on its own chain. Same operations
+// per path as the wavefront kernels (same hits: the closest hit does not
+// depend on the visit order; same shading code), so the same bits. The block's
+// dynamic LDS holds one traversal stack column per thread (stack_bytes).
+template <int INT>
+__global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_path_mega(DevScene s, WaveBuffers b, ChunkParams p) {
+  static_assert(INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH, "megakernel: path / path-mis only");
+  extern __shared__ int4 mega_lds[];
+  const SceneView sv = make_view(s);
+  const uint32_t count = b.counters[0];
+  const uint32_t iters = p.max_depth > 1u ? p.max_depth : 1u;
+  int32_t *stk = reinterpret_cast<int32_t *>(mega_lds) + threadIdx.x;
+  uint2 *ostk = reinterpret_cast<uint2 *>(mega_lds) + threadIdx.x;
+#ifdef MTX_MEGA_CHECK
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    printf("mega: count %u cap %u iters %u stack %u occ %u grid %u\n", count, b.capacity, iters, s.stack_entries,
+           s.occ_stack_entries, gridDim.x);
+  if (count > b.capacity) return;
+#endif
+  for (uint32_t qi = blockIdx.x * kShadeBlock + threadIdx.x; qi < count; qi += gridDim.x * kShadeBlock) {
+    const uint32_t path = p.ident0 ? qi : b.queue[0][qi];
+#ifdef MTX_MEGA_CHECK
+    if (path >= b.capacity) {
+      printf("mega: path %u at %u\n", path, qi);
+      return;
+    }
+#endif
+    bool cont = true;
+    for (uint32_t bounce = 0; bounce < iters && cont; ++bounce) {
+      const uint32_t rp = (bounce + b.ray_par) & 1u;
+      const float4 o4 = b.ray_o[rp][qi], d4 = b.ray_d[rp][qi];
+      const TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+      float tbest = o4.w, bu = 0.f, bv = 0.f;
+      uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
+      traverse_closest(s, stk, r, tbest, prim, bu, bv, nv, tv);
+      const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
+      ShadeIO io;
+      io.emit = false;
+      io.em_hi = false;
+      io.query = false;
+      cont = shade_path<INT>(s, sv, b, p, bounce, path, qi, h, io);
+      if (io.emit) {
+        const float4 so = io.rec.o, sd = io.rec.d;
+        const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
+        apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+      }
+      if (cont) {
+        b.ray_o[rp ^ 1u][qi] = io.nro;
+        b.ray_d[rp ^ 1u][qi] = io.nrd;
+        b.thr[rp ^ 1u][qi] = io.nthr;
+        b.prev[rp ^ 1u][qi] = io.nprev;
+        b.L[rp ^ 1u][qi] = io.nL;
+        b.misc[rp ^ 1u][qi] = io.nmisc;
+      } else {
+        b.L[kFinal][path] = io.nL;
+        if (!p.drop_end_misc) b.misc[kFinal][path] = io.nmisc;
+      }
+    }
+    if (cont) {  // still queued after the last bounce: k_flush_tail's move
+      const uint32_t rp = (iters + b.ray_par) & 1u;
+      float4 L = b.L[rp][qi];
+      const uint4 m = b.misc[rp][qi];
+      if (INT == MTX_INT_PATH_MIS) L.w = end_w(m.w >> 16, L.w);
+      b.L[kFinal][path] = L;
+      b.misc[kFinal][path] = m;
+    }
+  }
+}
+
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a
 // plain sum: L = L + T * out, as the oracle-side composition in the tests).
 __global__ void k_cache_apply(WaveBuffers b, const float *out, const uint32_t *perm) {
@@ -1468,6 +1548,22 @@ void launch_cache_apply(const WaveBuffers &b, const float *out, uint32_t capacit
                         const uint32_t *perm) {
   const unsigned blocks = (unsigned)std::min<uint64_t>((capacity + 255) / 256, 16384);
   hipLaunchKernelGGL(k_cache_apply, dim3(std::max(1u, blocks)), dim3(256), 0, st, b, out, perm);
+}
+// Resident blocks per CU of the path megakernel (its LDS stacks and the shade
+// register budget).
+int mega_blocks_per_cu(const DevScene &s) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_path_mega<MTX_INT_PATH_MIS>, kShadeBlock, stack_bytes(s)) !=
+          hipSuccess ||
+      nb <= 0)
+    nb = 1;
+  return nb;
+}
+void launch_path_mega(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, int grid, hipStream_t st) {
+  if (p.integrator == MTX_INT_PATH)
+    hipLaunchKernelGGL(k_path_mega<MTX_INT_PATH>, dim3(grid), dim3(kShadeBlock), stack_bytes(s), st, s, b, p);
+  else
+    hipLaunchKernelGGL(k_path_mega<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), stack_bytes(s), st, s, b, p);
 }
 void launch_flush_tail(const WaveBuffers &b, uint32_t bounce, uint32_t capacity, uint32_t integrator,
                        hipStream_t st) {

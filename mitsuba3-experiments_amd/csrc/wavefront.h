@@ -41,6 +41,7 @@ enum : uint32_t {
 #define MTX_TRACE_BLOCK 256  // 8 blocks of 4 waves per CU: 20 KB of LDS each (stack + tree top)
 #endif
 constexpr int kTraceBlock = MTX_TRACE_BLOCK;  // threads per traversal block
+constexpr int kShadeBlock = 256;             // threads per shade / path-megakernel block
 // LDS part of the persistent traversal stacks (per lane) and the tree tops
 // copied into LDS per trace block; both kernels' blocks take ~20 KB (8 per CU):
 // closest hit 16 x 4-B node refs + 64 x 64-B nodes, occlusion 8 x 8-B node
@@ -211,6 +212,9 @@ struct ChunkParams {
 // -------- launch wrappers (kernels.hip) --------
 int trace_blocks_per_cu(const DevScene &s);
 int shade_blocks_per_cu();
+int mega_blocks_per_cu(const DevScene &s);
+// all bounces of a short path-mis / path wavefront in one kernel (k_path_mega)
+void launch_path_mega(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, int grid, hipStream_t st);
 int shade_stamps(unsigned long long *out);  // diagnostic builds (MTX_DIAG_STAMPS)
 void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
