@@ -17,8 +17,7 @@
 // path's next state at its append slot). L and misc have a third, per-path
 // plane that an ending path's state lands in (film, chain and ReSTIR
 // kernels). pos is per path, hit per queue position. Paths of a chunk are
-// pixel-major by default: path = q * spp + s for sample s of the chunk's
-// pixel q (sample-major q + s * n_px with MTX_SAMPLE_MAJOR=1).
+// pixel-major: path = q * spp + s for sample s of the chunk's pixel q.
 // Queues are u32 path indices compacted per 256-thread block (ballot + mbcnt
 // + LDS, one atomic per block step); shadow rays are 64-byte records.
 #pragma once

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Interleaved A/B of MTX_* environment settings (incl. MTX_LIB_VARIANT) on one
+# Interleaved A/B of MTX_* environment settings on one
 # box: one compact line per run. Usage: tools/env_ab.sh TAG ROUNDS "BENCH ARGS" "VAR=a" "VAR=b VAR2=c" ...
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
