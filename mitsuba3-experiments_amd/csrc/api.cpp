@@ -159,9 +159,9 @@ struct mtx_ctx {
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
   uint32_t xcd_claim = 1;
   // path megakernel for wavefronts of at most this many paths (ReSTIR
-  // stage A halves; MTX_MEGA_PATHS, 0 = off; 0xffffffff = the resident lanes
-  // of the megakernel's grid). Off until it is fault-free on the device.
-  uint32_t mega_paths = 0;
+  // stage A halves; MTX_MEGA_PATHS, 0 = off; default 0xffffffff = the
+  // resident lanes of the megakernel's grid)
+  uint32_t mega_paths = 0xffffffffu;
   int mega_grid = 0;
   uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
   DevBuf cq_keys, cq_perm, cq_ws;
@@ -223,7 +223,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
-  if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)std::max(0, atoi(e));
+  if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)strtoul(e, nullptr, 0);
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
   *out = c;
   return MTX_OK;
@@ -822,18 +822,6 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
   }
 }
 
-#ifdef MTX_MEGA_CHECK
-#define MTX_DBG_SYNC(tag)                                                                      \
-  do {                                                                                         \
-    hipError_t e_ = hipDeviceSynchronize();                                                    \
-    fprintf(stderr, "sync %s: %s\n", tag, hipGetErrorString(e_));                             \
-  } while (0)
-#else
-#define MTX_DBG_SYNC(tag) \
-  do {                    \
-  } while (0)
-#endif
-
 // One bounce of a chunk: closest hit, shade, NEE shadow rays.
 void launch_bounce(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkParams &p, Timer &tm,
                    uint64_t *n_trace, uint64_t *n_shadow, const mtxd::DevScene &s, hipStream_t st, uint32_t bounce) {
@@ -1107,7 +1095,6 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
       mtxd::launch_restir_begin(*sc[h], bh[h], ph[h], rh[h], sh[h]);
       b1[h] = bh[h];  // k_rs_begin left the secondary rays in the parity-1 planes
       b1[h].ray_par = 1;
-      MTX_DBG_SYNC("prologue");
     }
     // sample_ray (the path-mis loop): a half of at most c->mega_paths paths
     // runs all its bounces in the path megakernel (no counters: STATS
@@ -1123,7 +1110,6 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
                              std::max(1, std::min<int>(c->mega_grid, (ph[h].n_paths + mtxd::kShadeBlock - 1) /
                                                                          mtxd::kShadeBlock)),
                              sh[h]);
-      MTX_DBG_SYNC("mega");
       tm.end(0, e, sh[h]);
       ++*n_trace;
     }
@@ -1134,9 +1120,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     for (int h = 0; h < halves; ++h) {
       if (!mega[h]) finish_bounces(b1[h], ph[h], sh[h]);
       mtxd::launch_restir_collect(bh[h], ph[h], rh[h], sh[h]);
-      MTX_DBG_SYNC("collect");
       mtxd::launch_restir_temporal(rh[h], ph[h], sh[h]);
-      MTX_DBG_SYNC("temporal");
     }
     if (two) {  // stage B reads every lane of the band
       HIP_TRY(hipEventRecord(c->w2.done, c->w2.stream));

@@ -15,13 +15,15 @@ namespace mtxd {
 
 using namespace mtx;
 
-// Traversal stacks live in LDS, one column per lane ([entry][lane]): 4-B
-// node references (closest hit, 3 x depth + 1 entries) or 8-B node groups
-// (occlusion, depth + 1 entries). mtx_trace's kernel keeps the whole stack
-// of either tree in LDS.
+// Traversal stacks live in LDS, one column of 4-B words per lane
+// ([word][lane]): node references (closest hit, 3 x depth + 1 words) or node
+// groups (occlusion, depth + 1 entries of two words). mtx_trace's kernel and
+// the path megakernel keep the whole stack of either tree in LDS; a thread
+// may run both traversals on its one column (the path megakernel does), and
+// no thread's words overlap another's.
 inline size_t stack_bytes(const DevScene &s) {
-  const size_t a = (size_t)s.stack_entries * sizeof(int32_t), b = (size_t)s.occ_stack_entries * sizeof(uint2);
-  return (a > b ? a : b) * kTraceBlock;
+  const size_t a = s.stack_entries, b = 2 * (size_t)s.occ_stack_entries;
+  return (a > b ? a : b) * sizeof(uint32_t) * kTraceBlock;
 }
 // The persistent kernels keep only the top lds_entries entries in LDS (so
 // LDS does not cap occupancy) and spill deeper entries to a per-thread global
@@ -295,12 +297,6 @@ __device__ __forceinline__ void traverse_closest(const DevScene &s, int32_t *stk
 #pragma unroll
         for (int rr = 3; rr >= 1; --rr)
           if (rr < n) {
-#ifdef MTX_MEGA_CHECK
-            if (sp >= (int)s.stack_entries) {
-              printf("closest stack overflow sp %d\n", sp);
-              return;
-            }
-#endif
             stk[sp * kTraceBlock] = cr[rr];
             ++sp;
           }
@@ -310,12 +306,6 @@ __device__ __forceinline__ void traverse_closest(const DevScene &s, int32_t *stk
     } else {
       uint32_t first, count;
       leaf_decode(node, &first, &count);
-#ifdef MTX_MEGA_CHECK
-      if (first + count > s.n_tris) {
-        printf("closest leaf %u+%u\n", first, count);
-        return;
-      }
-#endif
       for (uint32_t k = 0; k < count; ++k) {
         const uint32_t prim = first + k;
         const TriGeom g = load_tri(s.tri, prim);
@@ -390,8 +380,9 @@ __device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r
 }
 
 // Per-thread any-hit traversal in the oracle's order (oracle/oracle.cpp
-// trace_any) for mtx_trace: stk is this thread's LDS column.
-__device__ __forceinline__ bool traverse_occ(const DevScene &s, uint2 *stk, const TraceRay &r, float tmax,
+// trace_any) for mtx_trace and the path megakernel: stk is this thread's LDS
+// column of words; node group e takes words 2e (base) and 2e + 1 (bits).
+__device__ __forceinline__ bool traverse_occ(const DevScene &s, uint32_t *stk, const TraceRay &r, float tmax,
                                              uint32_t &nv, uint32_t &tv) {
   const uint32_t oct = ray_octant(r);
   int sp = 0;
@@ -408,13 +399,11 @@ __device__ __forceinline__ bool traverse_occ(const DevScene &s, uint2 *stk, cons
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
       ghits &= ~(1u << (24 + p));
       const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
-#ifdef MTX_MEGA_CHECK
-      if (sp >= (int)s.occ_stack_entries) {
-        printf("occ stack overflow sp %d\n", sp);
-        return false;
+      if (ghits >> 24) {
+        stk[(2 * sp) * kTraceBlock] = gbase;
+        stk[(2 * sp + 1) * kTraceBlock] = ghits;
+        ++sp;
       }
-#endif
-      if (ghits >> 24) stk[(sp++) * kTraceBlock] = make_uint2(gbase, ghits);
       ++nv;
       const CwVisit v = cw_visit(s, r, oct, node, tmax, nullptr, 0);
       gbase = v.child_base;
@@ -422,9 +411,9 @@ __device__ __forceinline__ bool traverse_occ(const DevScene &s, uint2 *stk, cons
       tbase = v.tri_base;
       thits = v.hits & 0x00ffffffu;
     } else if (sp > 0) {
-      const uint2 g = stk[(--sp) * kTraceBlock];
-      gbase = g.x;
-      ghits = g.y;
+      --sp;
+      gbase = stk[(2 * sp) * kTraceBlock];
+      ghits = stk[(2 * sp + 1) * kTraceBlock];
     } else {
       return false;
     }

@@ -1032,21 +1032,9 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_path_mega(DevS
   const uint32_t count = b.counters[0];
   const uint32_t iters = p.max_depth > 1u ? p.max_depth : 1u;
   int32_t *stk = reinterpret_cast<int32_t *>(mega_lds) + threadIdx.x;
-  uint2 *ostk = reinterpret_cast<uint2 *>(mega_lds) + threadIdx.x;
-#ifdef MTX_MEGA_CHECK
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    printf("mega: count %u cap %u iters %u stack %u occ %u grid %u\n", count, b.capacity, iters, s.stack_entries,
-           s.occ_stack_entries, gridDim.x);
-  if (count > b.capacity) return;
-#endif
+  uint32_t *ostk = reinterpret_cast<uint32_t *>(mega_lds) + threadIdx.x;  // the same column
   for (uint32_t qi = blockIdx.x * kShadeBlock + threadIdx.x; qi < count; qi += gridDim.x * kShadeBlock) {
     const uint32_t path = p.ident0 ? qi : b.queue[0][qi];
-#ifdef MTX_MEGA_CHECK
-    if (path >= b.capacity) {
-      printf("mega: path %u at %u\n", path, qi);
-      return;
-    }
-#endif
     bool cont = true;
     for (uint32_t bounce = 0; bounce < iters && cont; ++bounce) {
       const uint32_t rp = (bounce + b.ray_par) & 1u;
@@ -1298,7 +1286,7 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const flo
   float tbest = o4.w, bu = 0.f, bv = 0.f;
   uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
   if (any_hit) {
-    hits[i] = traverse_occ(s, reinterpret_cast<uint2 *>(raw_lds) + threadIdx.x, r, o4.w, nv, tv) ? 1u : 0u;
+    hits[i] = traverse_occ(s, reinterpret_cast<uint32_t *>(raw_lds) + threadIdx.x, r, o4.w, nv, tv) ? 1u : 0u;
   } else {
     traverse_closest(s, reinterpret_cast<int32_t *>(raw_lds) + threadIdx.x, r, tbest, prim, bu, bv, nv, tv);
     if (prim == 0xffffffffu) tbest = kInf;
