@@ -1050,8 +1050,16 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // rows split into two halves traced on two wavefronts / streams: one
     // half's kernels fill the tails of the other's short (~2 M-ray)
     // persistent launches. Same lanes, same draws: bit-identical.
+    // A band of at most mega_max paths (default: twice the megakernel's
+    // resident lanes) runs its secondary paths in the path megakernel on one
+    // wavefront instead: one launch of at most the resident blocks, whose
+    // waves claim the queued paths 64 at a time (two concurrent
+    // megakernels, one per half, only queue behind each other).
     const uint32_t rows = a->y1 - a->y0;
-    const bool two = c->streams > 1 && rows >= 2 && nb >= (1u << 16);
+    const uint32_t mega_max =
+        c->mega_paths == 0xffffffffu ? 2u * (uint32_t)c->mega_grid * mtxd::kShadeBlock : c->mega_paths;
+    const bool mega_all = !p.stats && nb <= mega_max;
+    const bool two = !mega_all && c->streams > 1 && rows >= 2 && nb >= (1u << 16);
     if (two) tm.streams = 2;
     const uint32_t ym = two ? a->y0 + rows / 2 : a->y1;
     mtxd::DevScene s2 = c->scene;
@@ -1100,10 +1108,8 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // runs all its bounces in the path megakernel (no counters: STATS
     // renders keep the wavefront kernels)
     bool mega[2] = {false, false};
-    const uint32_t mega_max =
-        c->mega_paths == 0xffffffffu ? (uint32_t)c->mega_grid * mtxd::kShadeBlock : c->mega_paths;
     for (int h = 0; h < halves; ++h) {
-      mega[h] = !ph[h].stats && ph[h].n_paths <= mega_max;
+      mega[h] = mega_all;
       if (!mega[h]) continue;
       e = tm.begin(0, sh[h]);
       mtxd::launch_path_mega(*sc[h], b1[h], ph[h],

@@ -1024,8 +1024,11 @@ __global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator
 // per path as the wavefront kernels (same hits: the closest hit does not
 // depend on the visit order; same shading code), so the same bits. The block's
 // dynamic LDS holds one traversal stack column per thread (stack_bytes).
+#ifndef MTX_MEGA_MIN_BLOCKS
+#define MTX_MEGA_MIN_BLOCKS kShadeMinBlocks  // A/B: 4 = <= 128 VGPRs (spills), every band path resident at once
+#endif
 template <int INT>
-__global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_path_mega(DevScene s, WaveBuffers b, ChunkParams p) {
+__global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_path_mega(DevScene s, WaveBuffers b, ChunkParams p) {
   static_assert(INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH, "megakernel: path / path-mis only");
   extern __shared__ int4 mega_lds[];
   const SceneView sv = make_view(s);
@@ -1033,46 +1036,57 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_path_mega(DevS
   const uint32_t iters = p.max_depth > 1u ? p.max_depth : 1u;
   int32_t *stk = reinterpret_cast<int32_t *>(mega_lds) + threadIdx.x;
   uint32_t *ostk = reinterpret_cast<uint32_t *>(mega_lds) + threadIdx.x;  // the same column
-  for (uint32_t qi = blockIdx.x * kShadeBlock + threadIdx.x; qi < count; qi += gridDim.x * kShadeBlock) {
-    const uint32_t path = p.ident0 ? qi : b.queue[0][qi];
-    bool cont = true;
-    for (uint32_t bounce = 0; bounce < iters && cont; ++bounce) {
-      const uint32_t rp = (bounce + b.ray_par) & 1u;
-      const float4 o4 = b.ray_o[rp][qi], d4 = b.ray_d[rp][qi];
-      const TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
-      float tbest = o4.w, bu = 0.f, bv = 0.f;
-      uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
-      traverse_closest(s, stk, r, tbest, prim, bu, bv, nv, tv);
-      const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
-      ShadeIO io;
-      io.emit = false;
-      io.em_hi = false;
-      io.query = false;
-      cont = shade_path<INT>(s, sv, b, p, bounce, path, qi, h, io);
-      if (io.emit) {
-        const float4 so = io.rec.o, sd = io.rec.d;
-        const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
-        apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+  // waves claim 64 queue positions at a time (counters[2], zeroed with the
+  // bounce counters): a wave that finishes its paths early takes the next
+  // batch while slow ones still run
+  const uint32_t lane = threadIdx.x & 63u;
+  while (true) {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&b.counters[2], 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= count) break;
+    const uint32_t qi = base + lane;
+    if (qi < count) {  // reconverges before the next claim
+      const uint32_t path = p.ident0 ? qi : b.queue[0][qi];
+      bool cont = true;
+      for (uint32_t bounce = 0; bounce < iters && cont; ++bounce) {
+        const uint32_t rp = (bounce + b.ray_par) & 1u;
+        const float4 o4 = b.ray_o[rp][qi], d4 = b.ray_d[rp][qi];
+        const TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+        float tbest = o4.w, bu = 0.f, bv = 0.f;
+        uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
+        traverse_closest(s, stk, r, tbest, prim, bu, bv, nv, tv);
+        const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
+        ShadeIO io;
+        io.emit = false;
+        io.em_hi = false;
+        io.query = false;
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, qi, h, io);
+        if (io.emit) {
+          const float4 so = io.rec.o, sd = io.rec.d;
+          const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
+          apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+        }
+        if (cont) {
+          b.ray_o[rp ^ 1u][qi] = io.nro;
+          b.ray_d[rp ^ 1u][qi] = io.nrd;
+          b.thr[rp ^ 1u][qi] = io.nthr;
+          b.prev[rp ^ 1u][qi] = io.nprev;
+          b.L[rp ^ 1u][qi] = io.nL;
+          b.misc[rp ^ 1u][qi] = io.nmisc;
+        } else {
+          b.L[kFinal][path] = io.nL;
+          if (!p.drop_end_misc) b.misc[kFinal][path] = io.nmisc;
+        }
       }
-      if (cont) {
-        b.ray_o[rp ^ 1u][qi] = io.nro;
-        b.ray_d[rp ^ 1u][qi] = io.nrd;
-        b.thr[rp ^ 1u][qi] = io.nthr;
-        b.prev[rp ^ 1u][qi] = io.nprev;
-        b.L[rp ^ 1u][qi] = io.nL;
-        b.misc[rp ^ 1u][qi] = io.nmisc;
-      } else {
-        b.L[kFinal][path] = io.nL;
-        if (!p.drop_end_misc) b.misc[kFinal][path] = io.nmisc;
+      if (cont) {  // still queued after the last bounce: k_flush_tail's move
+        const uint32_t rp = (iters + b.ray_par) & 1u;
+        float4 L = b.L[rp][qi];
+        const uint4 m = b.misc[rp][qi];
+        if (INT == MTX_INT_PATH_MIS) L.w = end_w(m.w >> 16, L.w);
+        b.L[kFinal][path] = L;
+        b.misc[kFinal][path] = m;
       }
-    }
-    if (cont) {  // still queued after the last bounce: k_flush_tail's move
-      const uint32_t rp = (iters + b.ray_par) & 1u;
-      float4 L = b.L[rp][qi];
-      const uint4 m = b.misc[rp][qi];
-      if (INT == MTX_INT_PATH_MIS) L.w = end_w(m.w >> 16, L.w);
-      b.L[kFinal][path] = L;
-      b.misc[kFinal][path] = m;
     }
   }
 }
