@@ -92,3 +92,45 @@ def test_pssmlt_band_256_chains_60_iterations_bit_exact(full_scene, oracle, name
         c = oracle.pssmlt_render(full_scene, integ.render_args(full_scene, 5, 128, y0, y1, spp, 128), it)
         np.testing.assert_array_equal(parts[1], c)
         np.testing.assert_allclose(parts[0] + parts[1], film, rtol=5e-5, atol=1e-6)
+
+
+_MEGA_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [{pkg!r}, {orc!r}, {tests!r}]
+import binding as oracle
+from mtx import load_dict, scene
+from test_gpu_fullsize_integrators import RESTIR_C4
+oracle.build()
+sc = scene.bedroom().with_film(1920, 1080)
+integ = load_dict({{"type": "restirgi", **RESTIR_C4}})
+ci = load_dict({{"type": "restirgi", **RESTIR_C4}})
+orc = oracle.RestirOracle(sc)
+for fr in range(2):
+    ci.n = fr
+    ref = orc.frame(sc, ci.render_args(sc, fr, 1))
+    film = integ.render_film(sc, seed=fr, spp=1)
+    assert np.array_equal(film, ref), ("frame", fr)
+assert np.array_equal(integ.state("sample"), orc.cur)
+assert np.array_equal(integ.state("temporal"), orc.tres)
+print("CHILD OK")
+"""
+
+
+def test_restir_1080p_path_megakernel_bit_exact():
+    """The path megakernel (csrc/kernels.hip k_path_mega: every bounce of a
+    secondary path in one thread, waves claiming 64 paths at a time) forced
+    on for the whole 1080p frame (MTX_MEGA_PATHS above its 2.07 M paths;
+    by default it runs only short bands): films, samples and temporal
+    reservoirs bit-exact against the oracle over two frames. The
+    environment is read at context creation, hence the subprocess."""
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    code = _MEGA_CHILD.format(pkg=os.path.join(ROOT, "mitsuba3-experiments_amd"), orc=os.path.join(ROOT, "oracle"),
+                              tests=os.path.join(ROOT, "tests"))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MTX_MEGA_PATHS="4000000"),
+                       capture_output=True, text=True, timeout=280, cwd=ROOT)
+    assert r.returncode == 0 and "CHILD OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
