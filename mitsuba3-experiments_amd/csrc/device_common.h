@@ -769,6 +769,13 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
                                            uint32_t &nv, uint32_t &tv, uint32_t &nr,
                                            uint32_t *wave_iters = nullptr) {
   extern __shared__ int4 trace_lds[];
+  // a block none of whose waves gets a claim batch (a short queue:
+  // RayReservoir::start) exits before it fills its tree top
+  {
+    const uint32_t n_grid_waves = gridDim.x * (kTraceBlock / 64u);
+    const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
+    if (blockIdx.x * (kTraceBlock / 64u) >= (count + batch - 1) / batch) return;
+  }
   if (ANY) {
     uint2 *cols = reinterpret_cast<uint2 *>(trace_lds);
     int4 *top = reinterpret_cast<int4 *>(cols + s.occ_lds_entries * kTraceBlock);
