@@ -157,6 +157,7 @@ struct mtx_ctx {
   uint32_t occ_lds_stack = mtxd::kOccLdsStack;
   uint32_t trace_batch = 128;  // queue entries per claim (256: +0.6 % closest, +1 % at spp 32; 64: +5 %)
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
+  uint32_t occ_urefill = 24;  // any hit on the 8-wide tree (MTX_OCC_UREFILL)
   uint32_t xcd_claim = 1;
   // path megakernel for wavefronts of at most this many paths (ReSTIR
   // stage A halves; MTX_MEGA_PATHS, 0 = off; default 0xffffffff = the
@@ -222,6 +223,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
+  if (const char *e = getenv("MTX_OCC_UREFILL")) c->occ_urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)strtoul(e, nullptr, 0);
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
@@ -496,6 +498,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.occ_lds_top = std::min<uint32_t>(n_occ, c->occ_lds_top);
   s.trace_batch = c->trace_batch;
   s.urefill = c->urefill;
+  s.occ_urefill = c->occ_urefill;
   s.xcd_claim = c->xcd_claim;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
   c->mega_grid = c->n_cu * mtxd::mega_blocks_per_cu(s);

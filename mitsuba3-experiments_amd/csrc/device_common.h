@@ -689,7 +689,7 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
   while (true) {
     if (!res.exhausted) {
       const uint64_t idle = __ballot(!has);
-      if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
+      if ((uint32_t)__popcll(idle) >= s.occ_urefill || idle == ~0ull) {
         uint32_t k;
         bool ok;
         res.take(s, idle, lane, k, ok);

@@ -91,6 +91,7 @@ struct DevScene {
                            // (int32 node refs for closest hit, uint2 node groups for occlusion)
   uint32_t ovf_threads;    // threads of the persistent trace grid
   uint32_t urefill;        // persistent kernels: refill a wave once this many lanes are idle
+  uint32_t occ_urefill;    // the same for the any-hit kernels
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
 };
