@@ -157,7 +157,7 @@ struct mtx_ctx {
   uint32_t occ_lds_stack = mtxd::kOccLdsStack;
   uint32_t trace_batch = 128;  // queue entries per claim (256: +0.6 % closest, +1 % at spp 32; 64: +5 %)
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
-  uint32_t occ_urefill = 24;  // any hit on the 8-wide tree (MTX_OCC_UREFILL)
+  uint32_t occ_urefill = 12;  // any hit on the 8-wide tree (MTX_OCC_UREFILL; 8-16 alike, 24: shadow +1 ms, 32/40: +2/+3 ms)
   uint32_t xcd_claim = 1;
   // path megakernel for wavefronts of at most this many paths (ReSTIR
   // stage A halves; MTX_MEGA_PATHS, 0 = off; default 0xffffffff = the
