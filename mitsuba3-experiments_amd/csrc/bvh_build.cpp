@@ -748,6 +748,12 @@ extern "C" int mtx_bvh_build_occlusion(const float *tri_geom, uint32_t n_tris, i
   }
   Builder b;
   apply_knobs(b);
+  // the occlusion tree's own costs (tuning experiments): an any-hit ray
+  // stops at its first hit, so the SAH's weights need not be the closest
+  // hit's
+  if (const char *e = getenv("MTX_OCC_CT")) b.ct = std::max(0.05f, (float)atof(e));
+  if (const char *e = getenv("MTX_OCC_CNODE")) b.c_node = (float)atof(e);
+  if (const char *e = getenv("MTX_OCC_CTRI")) b.c_tri = (float)atof(e);
   b.vpos = pts.data();
   b.vidx = vidx.data();
   b.n = n_tris;
