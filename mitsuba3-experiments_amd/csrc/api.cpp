@@ -415,7 +415,9 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     // device triangles packed to 36 B (the ABI's 48-B records carry 3 pad
     // words): 3.6 instead of 2.7 triangles per 128-B line, same load count
     const float *src = tree ? occ_geom : d->tri_geom;
-    std::vector<float> g9(9ull * d->n_tris);
+    // (+4 floats: the merged-load traversal reads a triangle's last word with
+    // a 16-B load, 12 B past the last record)
+    std::vector<float> g9(9ull * d->n_tris + 4, 0.f);
     for (size_t i = 0; i < d->n_tris; ++i)
       for (int k = 0; k < 3; ++k)
         for (int j = 0; j < 3; ++j) g9[9 * i + 3 * k + j] = src[12 * i + 4 * k + j];
@@ -1054,10 +1056,10 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // half's kernels fill the tails of the other's short (~2 M-ray)
     // persistent launches. Same lanes, same draws: bit-identical.
     // A band of at most mega_max paths (default: twice the megakernel's
-    // resident lanes) runs its secondary paths in the path megakernel on one
-    // wavefront instead: one launch of at most the resident blocks, whose
-    // waves claim the queued paths 64 at a time (two concurrent
-    // megakernels, one per half, only queue behind each other).
+    // resident lanes, 2 x mega_grid x kShadeBlock) runs all of its secondary
+    // paths in the path megakernel on ONE wavefront instead (the band is not
+    // split into halves then): one launch of at most the resident blocks,
+    // whose waves claim the queued paths 64 at a time.
     const uint32_t rows = a->y1 - a->y0;
     const uint32_t mega_max =
         c->mega_paths == 0xffffffffu ? 2u * (uint32_t)c->mega_grid * mtxd::kShadeBlock : c->mega_paths;
@@ -1107,8 +1109,8 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
       b1[h] = bh[h];  // k_rs_begin left the secondary rays in the parity-1 planes
       b1[h].ray_par = 1;
     }
-    // sample_ray (the path-mis loop): a half of at most c->mega_paths paths
-    // runs all its bounces in the path megakernel (no counters: STATS
+    // sample_ray (the path-mis loop): with mega_all (halves == 1) the whole
+    // band runs all its bounces in the path megakernel (no counters: STATS
     // renders keep the wavefront kernels)
     bool mega[2] = {false, false};
     for (int h = 0; h < halves; ++h) {

@@ -21,6 +21,8 @@ using namespace mtx;
 // the path megakernel keep the whole stack of either tree in LDS; a thread
 // may run both traversals on its one column (the path megakernel does), and
 // no thread's words overlap another's.
+// (stride kTraceBlock: every kernel that calls traverse_closest / traverse_occ
+// runs blocks of kTraceBlock threads; k_path_mega asserts it.)
 inline size_t stack_bytes(const DevScene &s) {
   const size_t a = s.stack_entries, b = 2 * (size_t)s.occ_stack_entries;
   return (a > b ? a : b) * sizeof(uint32_t) * kTraceBlock;
@@ -219,38 +221,35 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 // mtx_core/geometry.h wide_node_keys_e; the child references ride along the
 // 5-exchange sorting network, so the visit order is by entry distance.
 // ===========================================================================
-__device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
-                                          int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
-  int4 a, rf, qa;
-  int2 qb;
-  if (node < top_n) {
-    // the LDS reads are inline asm: as plain loads the compiler merges the
-    // two branches into flat loads through a selected generic pointer, which
-    // take the vector-memory path for every lane
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    typedef int v2i __attribute__((ext_vector_type(2)));
-    v4i x0, x1, x2;
-    v2i x3;
-    const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 64u * (uint32_t)node;
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:16\n\t"
-        "ds_read_b128 %2, %4 offset:32\n\t"
-        "ds_read_b64 %3, %4 offset:48\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-        : "v"(la));
-    a = make_int4(x0.x, x0.y, x0.z, x0.w);
-    rf = make_int4(x1.x, x1.y, x1.z, x1.w);
-    qa = make_int4(x2.x, x2.y, x2.z, x2.w);
-    qb = make_int2(x3.x, x3.y);
-  } else {
-    const int4 *np = s.nodes + 4 * node;
-    a = np[0];
-    rf = np[1];
-    qa = np[2];
-    qb = *reinterpret_cast<const int2 *>(np + 3);
-  }
+// The 64-B node of the block's LDS tree-top copy (inline asm: as plain loads
+// the compiler merges an LDS branch and a global branch into flat loads
+// through a selected generic pointer, which take the vector-memory path for
+// every lane).
+__device__ __forceinline__ void lds_node64(const int4 *top, int32_t node, int4 &a, int4 &rf, int4 &qa, int2 &qb) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  v4i x0, x1, x2;
+  v2i x3;
+  const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 64u * (uint32_t)node;
+  asm volatile(
+      "ds_read_b128 %0, %4\n\t"
+      "ds_read_b128 %1, %4 offset:16\n\t"
+      "ds_read_b128 %2, %4 offset:32\n\t"
+      "ds_read_b64 %3, %4 offset:48\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+      : "v"(la));
+  a = make_int4(x0.x, x0.y, x0.z, x0.w);
+  rf = make_int4(x1.x, x1.y, x1.z, x1.w);
+  qa = make_int4(x2.x, x2.y, x2.z, x2.w);
+  qb = make_int2(x3.x, x3.y);
+}
+
+// Slab tests of a 4-wide node's children (words a, rf, qa, qb of mtx.h) and
+// the near-first order: returns the number of hit children, c[] the child
+// references sorted by entry distance.
+__device__ __forceinline__ int wide_visit_regs(const TraceRay &r, int4 a, int4 rf, int4 qa, int2 qb, float tbest,
+                                               int32_t c[4]) {
   uint32_t key[4];
   const uint32_t eb = (uint32_t)a.w;
   // the references ride along the compare-exchange network (one compare +
@@ -279,6 +278,30 @@ __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, 
   MTX_CAS2(0, 1) MTX_CAS2(2, 3) MTX_CAS2(0, 2) MTX_CAS2(1, 3) MTX_CAS2(1, 2)
 #undef MTX_CAS2
   return n;
+}
+
+__device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
+                                          int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
+  int4 a, rf, qa;
+  int2 qb;
+  if (node < top_n) {
+    lds_node64(top, node, a, rf, qa, qb);
+  } else {
+    const int4 *np = s.nodes + 4 * node;
+    a = np[0];
+    rf = np[1];
+    qa = np[2];
+    qb = *reinterpret_cast<const int2 *>(np + 3);
+  }
+  return wide_visit_regs(r, a, rf, qa, qb, tbest, c);
+}
+
+// A 16-B load from a 4-B aligned address (the 36-B packed triangles; global
+// memory needs dword alignment only).
+typedef int v4i_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ int4 ld16(const void *p) {
+  const v4i_a4 v = *reinterpret_cast<const v4i_a4 *>(p);
+  return make_int4(v.x, v.y, v.z, v.w);
 }
 
 // Per-thread closest-hit traversal in the oracle's order (oracle/oracle.cpp
@@ -338,35 +361,29 @@ struct CwVisit {
   uint32_t hits, child_base, tri_base, imask;
 };
 
-__device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r, uint32_t oct, uint32_t node,
-                                            float tbest, const int4 *top, int top_n) {
-  int4 a, b, q0, q1, q2;
-  if ((int)node < top_n) {
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    v4i x0, x1, x2, x3, x4;
-    const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 80u * node;
-    asm volatile(
-        "ds_read_b128 %0, %5\n\t"
-        "ds_read_b128 %1, %5 offset:16\n\t"
-        "ds_read_b128 %2, %5 offset:32\n\t"
-        "ds_read_b128 %3, %5 offset:48\n\t"
-        "ds_read_b128 %4, %5 offset:64\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(x4)
-        : "v"(la));
-    a = make_int4(x0.x, x0.y, x0.z, x0.w);
-    b = make_int4(x1.x, x1.y, x1.z, x1.w);
-    q0 = make_int4(x2.x, x2.y, x2.z, x2.w);
-    q1 = make_int4(x3.x, x3.y, x3.z, x3.w);
-    q2 = make_int4(x4.x, x4.y, x4.z, x4.w);
-  } else {
-    const int4 *np = s.occ_nodes + 5 * (size_t)node;
-    a = np[0];
-    b = np[1];
-    q0 = np[2];
-    q1 = np[3];
-    q2 = np[4];
-  }
+__device__ __forceinline__ void lds_node80(const int4 *top, uint32_t node, int4 &a, int4 &b, int4 &q0, int4 &q1,
+                                           int4 &q2) {
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  v4i x0, x1, x2, x3, x4;
+  const uint32_t la = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 80u * node;
+  asm volatile(
+      "ds_read_b128 %0, %5\n\t"
+      "ds_read_b128 %1, %5 offset:16\n\t"
+      "ds_read_b128 %2, %5 offset:32\n\t"
+      "ds_read_b128 %3, %5 offset:48\n\t"
+      "ds_read_b128 %4, %5 offset:64\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3), "=&v"(x4)
+      : "v"(la));
+  a = make_int4(x0.x, x0.y, x0.z, x0.w);
+  b = make_int4(x1.x, x1.y, x1.z, x1.w);
+  q0 = make_int4(x2.x, x2.y, x2.z, x2.w);
+  q1 = make_int4(x3.x, x3.y, x3.z, x3.w);
+  q2 = make_int4(x4.x, x4.y, x4.z, x4.w);
+}
+
+__device__ __forceinline__ CwVisit cw_visit_regs(const TraceRay &r, uint32_t oct, int4 a, int4 b, int4 q0, int4 q1,
+                                                 int4 q2, float tbest) {
   const uint32_t q[12] = {(uint32_t)q0.x, (uint32_t)q0.y, (uint32_t)q0.z, (uint32_t)q0.w,
                           (uint32_t)q1.x, (uint32_t)q1.y, (uint32_t)q1.z, (uint32_t)q1.w,
                           (uint32_t)q2.x, (uint32_t)q2.y, (uint32_t)q2.z, (uint32_t)q2.w};
@@ -377,6 +394,22 @@ __device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r
   v.tri_base = (uint32_t)b.y;
   v.imask = (uint32_t)a.w >> 24;
   return v;
+}
+
+__device__ __forceinline__ CwVisit cw_visit(const DevScene &s, const TraceRay &r, uint32_t oct, uint32_t node,
+                                            float tbest, const int4 *top, int top_n) {
+  int4 a, b, q0, q1, q2;
+  if ((int)node < top_n) {
+    lds_node80(top, node, a, b, q0, q1, q2);
+  } else {
+    const int4 *np = s.occ_nodes + 5 * (size_t)node;
+    a = np[0];
+    b = np[1];
+    q0 = np[2];
+    q1 = np[3];
+    q2 = np[4];
+  }
+  return cw_visit_regs(r, oct, a, b, q0, q1, q2, tbest);
 }
 
 // Per-thread any-hit traversal in the oracle's order (oracle/oracle.cpp
@@ -551,7 +584,16 @@ __device__ __forceinline__ void count_wave_iter(uint32_t lane, uint32_t *ctr) {
 // visit or a leaf's triangle range; a visit pushes the far hit children
 // (three unconditional LDS stores when they fit: dead entries above the new
 // top are harmless) and continues with the nearest.
-template <bool STATS, class Src>
+//
+// MERGE: a lane does ONE work item per iteration -- a node visit or one
+// triangle test -- and the node lanes and the triangle lanes of a wave fetch
+// their data with the same load instructions (node: 16 + 16 + 16 + 8 B,
+// triangle: 16 + 16 + 16 B of its 36-B record, the last load reading 12 B
+// of the next record). The vector-memory address path costs per wave
+// instruction (and per distinct line), not per active lane, so an
+// iteration issues 4 load instructions instead of 4 + 3. Same visit order,
+// same counts.
+template <bool STATS, bool MERGE, class Src>
 __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                                    int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
                                                    uint32_t &nr, uint32_t *wave_iters) {
@@ -605,11 +647,27 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
     }
     if (__ballot(has) == 0) break;
     // ---- one inner-node visit
-    if (has && node >= 0) {
+    const bool dn = has && node >= 0;
+    const bool dt = MERGE && has && node < 0 && tri < tri_end;
+    int4 x0 = make_int4(0, 0, 0, 0), x1 = x0, x2 = x0;
+    int2 x3 = make_int2(0, 0);
+    if (MERGE) {
+      const bool in_lds = dn && node < top_n;
+      if (in_lds) lds_node64(top, node, x0, x1, x2, x3);
+      if ((dn && !in_lds) || dt) {
+        const char *gp = dn ? reinterpret_cast<const char *>(s.nodes + 4 * node)
+                            : reinterpret_cast<const char *>(s.tri + 9 * (size_t)tri);
+        x0 = ld16(gp);
+        x1 = ld16(gp + 16);
+        x2 = ld16(gp + 32);
+        if (dn) x3 = *reinterpret_cast<const int2 *>(gp + 48);
+      }
+    }
+    if (dn) {
       if (STATS) count_wave_iter(lane, &wave_iters[0]);
       int32_t cr[4];
       ++nv;
-      const int n = wide_visit(s, r, node, tbest, cr, top, top_n);
+      const int n = MERGE ? wide_visit_regs(r, x0, x1, x2, x3, tbest, cr) : wide_visit(s, r, node, tbest, cr, top, top_n);
       if (n > 0) {
         const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
         const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
@@ -644,11 +702,18 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
         pop_next();
       }
     }
-    // ---- one triangle test
-    if (has && tri < tri_end) {
+    // ---- one triangle test (MERGE: only a lane that did no node visit)
+    if (MERGE ? dt : (has && tri < tri_end)) {
       if (STATS) count_wave_iter(lane, &wave_iters[1]);
       const uint32_t pr = tri;
-      const TriGeom g = load_tri(s.tri, pr);
+      TriGeom g;
+      if (MERGE) {
+        g.p0 = V3{__int_as_float(x0.x), __int_as_float(x0.y), __int_as_float(x0.z)};
+        g.e1 = V3{__int_as_float(x0.w), __int_as_float(x1.x), __int_as_float(x1.y)};
+        g.e2 = V3{__int_as_float(x1.z), __int_as_float(x1.w), __int_as_float(x2.x)};
+      } else {
+        g = load_tri(s.tri, pr);
+      }
       float t, u, v;
       ++tv;
       ++tri;
@@ -671,7 +736,10 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
 // Any hit on the 8-wide occlusion tree: a lane tests its triangle group
 // before the next child of its node group; an empty pair pops the next node
 // group. The first hit ends the ray.
-template <bool STATS, class Src>
+// MERGE: one work item per lane and iteration (a node visit, or one triangle
+// test of the triangle group), node and triangle fetches sharing the load
+// instructions (node 5 x 16 B, triangle 3 x 16 B), as for closest hit.
+template <bool STATS, bool MERGE, class Src>
 __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                                uint2 *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
                                                uint32_t &nr, uint32_t *wave_iters) {
@@ -707,11 +775,31 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
     }
     if (__ballot(has) == 0) break;
     // ---- one node visit: the nearest remaining child of the node group
-    if (has && thits == 0 && (ghits >> 24) != 0) {
+    const bool dn = has && thits == 0 && (ghits >> 24) != 0;
+    const bool dt = MERGE && has && thits != 0;
+    uint32_t node = 0;
+    int4 x0 = make_int4(0, 0, 0, 0), x1 = x0, x2 = x0, x3 = x0, x4 = x0;
+    if (MERGE) {
+      if (dn) node = cw_inner_child(gbase, ghits & 0xffu, oct, (uint32_t)ctz32(ghits >> 24));
+      const bool in_lds = dn && (int)node < top_n;
+      if (in_lds) lds_node80(top, node, x0, x1, x2, x3, x4);
+      if ((dn && !in_lds) || dt) {
+        const char *gp = dn ? reinterpret_cast<const char *>(s.occ_nodes + 5 * (size_t)node)
+                            : reinterpret_cast<const char *>(s.occ_tri + 9 * (size_t)(tbase + (uint32_t)ctz32(thits)));
+        x0 = ld16(gp);
+        x1 = ld16(gp + 16);
+        x2 = ld16(gp + 32);
+        if (dn) {
+          x3 = ld16(gp + 48);
+          x4 = ld16(gp + 64);
+        }
+      }
+    }
+    if (dn) {
       if (STATS) count_wave_iter(lane, &wave_iters[0]);
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
       ghits &= ~(1u << (24 + p));
-      const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
+      if (!MERGE) node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
       if (ghits >> 24) {
         const uint2 g = make_uint2(gbase, ghits);
         if (sp < lds_n) {
@@ -723,18 +811,26 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
         ++sp;
       }
       ++nv;
-      const CwVisit v = cw_visit(s, r, oct, node, tmax, top, top_n);
+      const CwVisit v = MERGE ? cw_visit_regs(r, oct, x0, x1, x2, x3, x4, tmax) : cw_visit(s, r, oct, node, tmax, top, top_n);
       gbase = v.child_base;
       ghits = (v.hits & 0xff000000u) | v.imask;
       tbase = v.tri_base;
       thits = v.hits & 0x00ffffffu;
     }
-    // ---- one triangle test of the triangle group
-    if (has && thits != 0) {
+    // ---- one triangle test of the triangle group (MERGE: only a lane that
+    // did no node visit)
+    if (MERGE ? dt : (has && thits != 0)) {
       if (STATS) count_wave_iter(lane, &wave_iters[1]);
       const uint32_t pr = tbase + (uint32_t)ctz32(thits);
       thits &= thits - 1u;
-      const TriGeom g = load_tri(s.occ_tri, pr);
+      TriGeom g;
+      if (MERGE) {
+        g.p0 = V3{__int_as_float(x0.x), __int_as_float(x0.y), __int_as_float(x0.z)};
+        g.e1 = V3{__int_as_float(x0.w), __int_as_float(x1.x), __int_as_float(x1.y)};
+        g.e2 = V3{__int_as_float(x1.z), __int_as_float(x1.w), __int_as_float(x2.x)};
+      } else {
+        g = load_tri(s.occ_tri, pr);
+      }
       float t, u, v;
       ++tv;
       if (tri_intersect(r, g.p0, g.e1, g.e2, tmax, &t, &u, &v)) {
@@ -781,13 +877,19 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     int4 *top = reinterpret_cast<int4 *>(cols + s.occ_lds_entries * kTraceBlock);
     for (uint32_t i = threadIdx.x; i < 5 * s.occ_lds_top; i += kTraceBlock) top[i] = s.occ_nodes[i];
     __syncthreads();
-    trace_loop_occ<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+    if constexpr ((MTX_TRAV_MERGE & 2) != 0)
+      trace_loop_occ<STATS, true>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+    else
+      trace_loop_occ<STATS, false>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
   } else {
     int32_t *cols = reinterpret_cast<int32_t *>(trace_lds);
     int4 *top = reinterpret_cast<int4 *>(cols + s.lds_entries * kTraceBlock);
     for (uint32_t i = threadIdx.x; i < 4 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
     __syncthreads();
-    trace_loop_closest<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+    if constexpr ((MTX_TRAV_MERGE & 1) != 0)
+      trace_loop_closest<STATS, true>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+    else
+      trace_loop_closest<STATS, false>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
   }
 }
 

@@ -1008,7 +1008,10 @@ __global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator
     const uint32_t path = q[k];
     float4 L = b.L[rp][k];
     const uint4 m = b.misc[rp][k];
-    if (integrator == MTX_INT_PATH_MIS) L.w = end_w(m.w >> 16, L.w);
+    // decided by the shade variant: ReSTIR GI's secondary paths are shaded by
+    // the path-mis kernel (launch_shade), so their final L.w is valid_ray too,
+    // the bits k_path_mega<PATH_MIS> stores for the same path
+    if (integrator == MTX_INT_PATH_MIS || integrator == MTX_INT_RESTIR_GI) L.w = end_w(m.w >> 16, L.w);
     b.L[kFinal][path] = L;
     b.misc[kFinal][path] = m;
   }
@@ -1027,6 +1030,10 @@ __global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator
 #ifndef MTX_MEGA_MIN_BLOCKS
 #define MTX_MEGA_MIN_BLOCKS kShadeMinBlocks  // A/B: 4 = <= 128 VGPRs (spills), every band path resident at once
 #endif
+// The traversals index their LDS stack columns with the stride kTraceBlock and
+// stack_bytes() sizes the allocation with it: a megakernel block of another
+// width would let threads share stack words.
+static_assert(kShadeBlock == kTraceBlock, "k_path_mega: stack column stride must equal the block width");
 template <int INT>
 __global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_path_mega(DevScene s, WaveBuffers b, ChunkParams p) {
   static_assert(INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH, "megakernel: path / path-mis only");

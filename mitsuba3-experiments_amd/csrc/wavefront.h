@@ -53,6 +53,9 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_OCC_LDS_TOP
 #define MTX_OCC_LDS_TOP 48  // occlusion tree nodes copied into LDS per trace block (0 = none)
 #endif
+#ifndef MTX_TRAV_MERGE
+#define MTX_TRAV_MERGE 0  // bit 0 / 1: closest-hit / any-hit loop with shared node + triangle loads (device_common.h)
+#endif
 #ifndef MTX_STREAMS
 #define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)
 #endif

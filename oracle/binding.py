@@ -326,6 +326,29 @@ def probe(scene, op, inputs):
     return out
 
 
+def si_probe(items):
+    """orc_si_probe: si_from_vertices item by item; items is (n, 40) float32
+    (layout in oracle.cpp), returns (n, 24): p, n, s, t, ns, uv(+0), wi."""
+    x = np.ascontiguousarray(items, np.float32)
+    assert x.ndim == 2 and x.shape[1] == 40
+    out = np.zeros((len(x), 24), np.float32)
+    L = lib()
+    L.orc_si_probe.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p]
+    assert L.orc_si_probe(len(x), x.ctypes.data, out.ctypes.data) == 0
+    return out
+
+
+def tex_probe(scene, tex, uv):
+    """orc_tex_probe: bilinear repeat-wrapped lookups of one scene texture."""
+    uv = np.ascontiguousarray(uv, np.float32)
+    out = np.zeros((len(uv), 3), np.float32)
+    d = scene.desc()
+    L = lib()
+    L.orc_tex_probe.argtypes = [C.POINTER(_abi.SceneDesc), C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p]
+    assert L.orc_tex_probe(C.byref(d), tex, len(uv), uv.ctypes.data, out.ctypes.data) == 0
+    return out
+
+
 # ---- multi-core CPU baselines (bench.py cpu_baseline legs; equal results) --
 def prefix_sum_u32_mt(x, inclusive=True):
     x = np.ascontiguousarray(x, np.uint32)

@@ -1473,6 +1473,46 @@ int orc_probe(const mtx_scene_desc *d, int op, uint64_t n, const float *in, floa
   return 0;
 }
 
+// Surface interaction from explicit vertex data (mtx_core/interaction.h
+// si_from_vertices, the arithmetic compute_si and the device's shading
+// records share) for the float64 pins of tests/test_shared_pins.py.
+// 40 floats in per item: t u v | ray_d[3] | p0 p1 p2 [9] | use_n | n0 n1 n2 [9] |
+// use_uv | uv0 uv1 uv2 [6] | pad. 24 floats out: p[3] n[3] s[3] t[3] ns[3] uv[2] wi[3] pad.
+int orc_si_probe(uint64_t n, const float *in, float *out) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const float *a = in + 40 * i;
+    float *o = out + 24 * i;
+    auto v3 = [&](int k) { return V3{a[k], a[k + 1], a[k + 2]}; };
+    const SurfaceInteraction si =
+        si_from_vertices(a[0], 0u, a[1], a[2], v3(3), v3(6), v3(9), v3(12), 0u, -1, a[15] != 0.f, v3(16), v3(19),
+                         v3(22), a[25] != 0.f, V2{a[26], a[27]}, V2{a[28], a[29]}, V2{a[30], a[31]});
+    const V3 q[6] = {si.p, si.n, si.sh.s, si.sh.t, si.sh.n, V3{si.uv.x, si.uv.y, 0.f}};
+    for (int k = 0; k < 6; ++k) {
+      o[3 * k] = q[k].x;
+      o[3 * k + 1] = q[k].y;
+      o[3 * k + 2] = q[k].z;
+    }
+    o[17] = si.wi.x;
+    o[18] = si.wi.y;
+    o[19] = si.wi.z;
+  }
+  return 0;
+}
+
+// Bitmap lookups (mtx_core/bsdf.h texture_eval) of texture `tex` of a scene
+// at n uv pairs; 3 floats out per item.
+int orc_tex_probe(const mtx_scene_desc *d, uint32_t tex, uint64_t n, const float *uv, float *out) {
+  SceneView s = make_view(d);
+  if (tex >= d->n_textures) return -1;
+  for (uint64_t i = 0; i < n; ++i) {
+    const V3 c = texture_eval(s.bsdf, (int32_t)tex, V2{uv[2 * i], uv[2 * i + 1]});
+    out[3 * i] = c.x;
+    out[3 * i + 1] = c.y;
+    out[3 * i + 2] = c.z;
+  }
+  return 0;
+}
+
 // Warps used by the integrators (upstream mitsuba/core/warp.h).
 // op: 0 cosine hemisphere (3), 1 uniform disk concentric (2), 2 uniform
 // disk (2), 3 std normal (2), 4 uniform hemisphere (3)
