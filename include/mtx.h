@@ -188,6 +188,15 @@ typedef struct mtx_scene_desc {
   const int32_t *occ_nodes;
   const float *occ_tri_geom;
   uint32_t n_occ_nodes, pad1;
+  /* scene triangle (closest-hit leaf order) of each occlusion leaf-order
+   * triangle (mtx_bvh_build_occlusion's perm). Given with occ_nodes /
+   * occ_tri_geom: mtx_scene_upload checks occ_tri_geom[i] ==
+   * tri_geom[occ_perm[i]] for every i and that it is a permutation; NULL
+   * with given trees: derived at upload by matching the records, and the
+   * trees rejected (MTX_E_ARG) unless occ_tri_geom is a permutation of
+   * tri_geom. The 8-wide closest-hit traversal reports scene triangles
+   * through it. */
+  const uint32_t *occ_perm;
 } mtx_scene_desc;
 
 /* Integrators (the reference scripts whose sample() loop is replaced). */
@@ -346,8 +355,10 @@ int mtx_sample_rays(mtx_ctx *ctx, const mtx_render_args *args, uint64_t n, const
 
 /* Raw closest-hit / any-hit traversal (Scene.ray_intersect / ray_test,
  * path-mis.py:69-71, restirgi.py:320). rays: 8n floats (o.xyz, tmax, d.xyz,
- * 0); hits: 4n words (t, prim, u, v) for closest-hit, or n words (1 =
- * occluded) for any-hit. visits (optional, 2n u32): node and triangle visits. */
+ * 0); any_hit: 0 closest hit (4-wide tree), 1 any hit, 2 closest hit on the
+ * 8-wide tree (near-first sorted children, the same answer); hits: 4n words
+ * (t, prim, u, v) for closest hit, or n words (1 = occluded) for any hit.
+ * visits (optional, 2n u32): node and triangle visits. */
 int mtx_trace(mtx_ctx *ctx, uint64_t n, const float *rays, int any_hit, uint32_t *hits,
               uint32_t *visits);
 
@@ -366,9 +377,10 @@ int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolu
 /* reductions.py:12-54 scatter_reduce_with for func in {ADD=0, MIN=1, MAX=2,
  * MUL=3}: target[index[i]] = func(target[index[i]], value[i]), each target's
  * values applied in ascending i order (deterministic; the reference's order
- * is race-defined). The reference takes any Python callable (:12, :53); a
- * device kernel cannot run one, so the op table is fixed.
- * target is read-modify-write. */
+ * is race-defined). The reference takes any Python callable (:12, :53): the
+ * Python layer folds such a callable over mtx_group_by_u32 /
+ * mtx_group_by_u32_dev's groups, round by round (on the device with torch
+ * tensors). target is read-modify-write. */
 int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value);
 /* The stable group-by behind mtx_hashgrid_build / mtx_scatter_reduce_f32
@@ -378,6 +390,13 @@ int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_targe
  * as reductions.py:21-54 does with one election per round. Host pointers. */
 int mtx_group_by_u32(mtx_ctx *ctx, const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size,
                      uint32_t *key_offset, uint32_t *order);
+/* mtx_group_by_u32 on DEVICE pointers of the context's device (keys: n u32,
+ * key_size / key_offset: n_keys u32, order: n u32), for callers whose data
+ * stays in HBM (mtx.primitives.scatter_reduce_with with torch tensors). The
+ * keys are range-checked on the device first (MTX_E_ARG if one is >= n_keys);
+ * returns after the results are complete. */
+int mtx_group_by_u32_dev(mtx_ctx *ctx, const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size,
+                         uint32_t *key_offset, uint32_t *order);
 
 /* --------------------------- radiance field ----------------------- */
 /* nerad.py:54-106 Field (hash-grid + SH encoding, fp16 MLP with LeakyReLU,

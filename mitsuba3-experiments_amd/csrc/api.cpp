@@ -130,7 +130,7 @@ struct mtx_ctx {
   bool has_nerad = false;
   uint32_t scene_n_shapes = 0;
   DevBuf nr_lhs, nr_qp, nr_qd, nr_Lrhs, nr_lanes;
-  DevBuf nodes, tri, occ_nodes, occ_tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
+  DevBuf nodes, tri, occ_nodes, occ_tri, occ_prim, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
@@ -147,7 +147,7 @@ struct mtx_ctx {
   // film
   DevBuf contrib, film;
   // scratch for sample_rays / trace / primitives
-  DevBuf s0, s1, s2, s3, s4, s5;
+  DevBuf s0, s1, s2, s3, s4, s5, s6;
   int trace_grid = 0, shade_grid = 0;
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
@@ -159,6 +159,8 @@ struct mtx_ctx {
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
   uint32_t occ_urefill = 12;  // any hit on the 8-wide tree (MTX_OCC_UREFILL; 8-16 alike, 24: shadow +1 ms, 32/40: +2/+3 ms)
   uint32_t xcd_claim = 1;
+  // closest hit of the wavefront kernels on the 8-wide tree (MTX_CLOSEST_CW=1)
+  uint32_t closest_cw = MTX_CLOSEST_CW;
   // path megakernel for wavefronts of at most this many paths (ReSTIR
   // stage A halves; MTX_MEGA_PATHS, 0 = off; default 0xffffffff = the
   // resident lanes of the megakernel's grid)
@@ -223,6 +225,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
+  if (const char *e = getenv("MTX_CLOSEST_CW")) c->closest_cw = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_OCC_UREFILL")) c->occ_urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)strtoul(e, nullptr, 0);
@@ -236,7 +239,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->w2.stream) hipStreamSynchronize(c->w2.stream);
-  DevBuf *bufs[] = {&c->nodes,  &c->tri, &c->occ_nodes, &c->occ_tri, &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
+  DevBuf *bufs[] = {&c->nodes,  &c->tri, &c->occ_nodes, &c->occ_tri, &c->occ_prim, &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters, &c->xheads, &c->rs_heads,  &c->stats,    &c->contrib, &c->film,
@@ -244,7 +247,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
                     &c->stack_ovf, &c->shade_rec, &c->field_table, &c->field_frag, &c->fq_p, &c->fq_d,
                     &c->f_feat, &c->f_out, &c->cq_p, &c->cq_d, &c->cq_t, &c->cq_count, &c->rs_samp[0], &c->rs_samp[1], &c->rs_tres, &c->rs_sres, &c->rs_radius, &c->rs_hit,
                     &c->rs_dir, &c->rs_emit, &c->rs_rng, &c->rs_rays, &c->rs_count, &c->rs_occ, &c->rs_qM, &c->rs_nbr, &c->rs_xs, &c->rs_ns,
-                    &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5,
+                    &c->s0,     &c->s1,      &c->s2,       &c->s3,        &c->s4,       &c->s5, &c->s6,
                     &c->cq_keys, &c->cq_perm, &c->cq_ws,
                     &c->field_w16, &c->tr_p, &c->tr_m, &c->tr_v, &c->tr_g, &c->tr_wpart, &c->tr_loss, &c->tr_out,
                     &c->tr_dfeat, &c->tr_feat, &c->tr_flag, &c->tr_target, &c->nr_shape_pmf, &c->nr_shape_cdf,
@@ -267,6 +270,63 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   delete c;
 }
 
+// Caller-supplied occlusion trees: their triangle records must be the
+// scene's (a stale pair would answer shadow rays against other geometry).
+// With d->occ_perm the claimed correspondence is checked record by record
+// and as a permutation; without it the records of both arrays are sorted
+// and matched. perm[i] = scene triangle of occlusion triangle i.
+static int occ_match(const mtx_scene_desc *d, std::vector<uint32_t> &perm) {
+  const uint32_t n = d->n_tris;
+  auto rec = [](const float *g, uint32_t i, int w) {
+    uint32_t x;
+    memcpy(&x, g + 12 * (size_t)i + 4 * (w / 3) + (w % 3), 4);
+    return x;
+  };
+  auto same = [&](uint32_t i, uint32_t j) {
+    for (int w = 0; w < 9; ++w)
+      if (rec(d->occ_tri_geom, i, w) != rec(d->tri_geom, j, w)) return false;
+    return true;
+  };
+  perm.assign(n, 0u);
+  if (d->occ_perm) {
+    std::vector<uint8_t> seen(n, 0);
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t j = d->occ_perm[i];
+      if (j >= n || seen[j] || !same(i, j)) {
+        mtx_set_error("mtx_scene_upload: occ_perm[%u] = %u does not map occlusion triangle %u to an unused scene "
+                      "triangle with the same record",
+                      i, j, i);
+        return MTX_E_ARG;
+      }
+      seen[j] = 1;
+      perm[i] = j;
+    }
+    return MTX_OK;
+  }
+  std::vector<uint32_t> a(n), b(n);
+  for (uint32_t i = 0; i < n; ++i) a[i] = b[i] = i;
+  auto less = [&](const float *g) {
+    return [&, g](uint32_t x, uint32_t y) {
+      for (int w = 0; w < 9; ++w) {
+        const uint32_t u = rec(g, x, w), v = rec(g, y, w);
+        if (u != v) return u < v;
+      }
+      return x < y;
+    };
+  };
+  std::sort(a.begin(), a.end(), less(d->occ_tri_geom));
+  std::sort(b.begin(), b.end(), less(d->tri_geom));
+  for (uint32_t k = 0; k < n; ++k) {
+    if (!same(a[k], b[k])) {
+      mtx_set_error("mtx_scene_upload: occ_tri_geom is not a permutation of tri_geom (occ_nodes / occ_tri_geom "
+                    "must come from mtx_bvh_build_occlusion over this tri_geom)");
+      return MTX_E_ARG;
+    }
+    perm[a[k]] = b[k];
+  }
+  return MTX_OK;
+}
+
 int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   if (!c || !d) {
     mtx_set_error("mtx_scene_upload: null argument");
@@ -285,18 +345,26 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   }
   std::vector<int32_t> occ_nodes_v;
   std::vector<float> occ_geom_v;
+  std::vector<uint32_t> occ_perm_v;
   const int32_t *occ_nodes = d->occ_nodes;
   const float *occ_geom = d->occ_tri_geom;
+  const uint32_t *occ_perm = d->occ_perm;
   uint32_t n_occ = d->n_occ_nodes;
   int rc = 0;
   if (!occ_given) {
     occ_nodes_v.resize(((size_t)d->n_tris + 1) * MTX_OCC_NODE_WORDS);
     occ_geom_v.resize(12 * (size_t)d->n_tris);
-    if ((rc = mtx_bvh_build_occlusion(d->tri_geom, d->n_tris, occ_nodes_v.data(), &n_occ, occ_geom_v.data(), nullptr,
-                                      nullptr)))
+    occ_perm_v.resize(d->n_tris);
+    if ((rc = mtx_bvh_build_occlusion(d->tri_geom, d->n_tris, occ_nodes_v.data(), &n_occ, occ_geom_v.data(),
+                                      occ_perm_v.data(), nullptr)))
       return rc;
     occ_nodes = occ_nodes_v.data();
     occ_geom = occ_geom_v.data();
+    occ_perm = occ_perm_v.data();
+  } else if ((rc = occ_match(d, occ_perm_v))) {
+    return rc;
+  } else {
+    occ_perm = occ_perm_v.data();
   }
   // Validate both trees (mtx.h) on the host so that no kernel can read out
   // of bounds, and find their depths (stack entries: a 4-wide level pushes
@@ -424,6 +492,8 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     if ((rc = upload(tree ? c->occ_tri : c->tri, g9.data(), g9.size(), st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));  // g9 is freed at scope exit
   }
+  if ((rc = upload(c->occ_prim, occ_perm, (size_t)d->n_tris, st))) return rc;
+  HIP_TRY(hipStreamSynchronize(st));  // occ_perm_v is freed at scope exit
   if ((rc = upload(c->tri_vidx, d->tri_vidx, 3ull * d->n_tris, st))) return rc;
   if ((rc = upload(c->tri_shape, d->tri_shape, (size_t)d->n_tris, st))) return rc;
   if ((rc = upload(c->vpos, d->vpos, 3ull * d->n_verts, st))) return rc;
@@ -474,6 +544,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.tri = (const float *)c->tri.p;
   s.occ_nodes = (const int4 *)c->occ_nodes.p;
   s.occ_tri = (const float *)c->occ_tri.p;
+  s.occ_prim = (const uint32_t *)c->occ_prim.p;
   s.tri_vidx = (const uint32_t *)c->tri_vidx.p;
   s.tri_shape = (const uint32_t *)c->tri_shape.p;
   s.vpos = (const float *)c->vpos.p;
@@ -498,6 +569,8 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.occ_stack_entries = occ_depth + 1;
   s.occ_lds_entries = std::min<uint32_t>(s.occ_stack_entries, c->occ_lds_stack);
   s.occ_lds_top = std::min<uint32_t>(n_occ, c->occ_lds_top);
+  s.cw_stack_entries = 7 * occ_depth + 1;
+  s.closest_cw = c->closest_cw;
   s.trace_batch = c->trace_batch;
   s.urefill = c->urefill;
   s.occ_urefill = c->occ_urefill;
@@ -1493,6 +1566,10 @@ int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *
     mtx_set_error("no scene uploaded");
     return MTX_E_NOSCENE;
   }
+  if (any_hit < 0 || any_hit > 2) {
+    mtx_set_error("mtx_trace: mode %d (0 closest hit, 1 any hit, 2 closest hit on the 8-wide tree)", any_hit);
+    return MTX_E_ARG;
+  }
   if (n == 0) return MTX_OK;
   if (n >= (1ull << 31)) {
     mtx_set_error("mtx_trace: too many rays");
@@ -1500,7 +1577,7 @@ int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *
   }
   HIP_TRY(hipSetDevice(c->device));
   int rc;
-  const size_t hit_words = any_hit ? n : 4 * n;
+  const size_t hit_words = any_hit == 1 ? n : 4 * n;
   if ((rc = dalloc(c->s0, 32ull * n))) return rc;
   if ((rc = dalloc(c->s1, 4ull * hit_words))) return rc;
   if (visits && (rc = dalloc(c->s2, 8ull * n))) return rc;
@@ -1793,6 +1870,41 @@ int mtx_group_by_u32(mtx_ctx *c, const uint32_t *keys, uint64_t n, uint32_t n_ke
   HIP_TRY(hipMemcpyAsync(key_size, c->s2.p, 4ull * n_keys, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(key_offset, c->s3.p, 4ull * n_keys, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(order, c->s4.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
+int mtx_group_by_u32_dev(mtx_ctx *c, const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size,
+                         uint32_t *key_offset, uint32_t *order) {
+  if (!c || !keys || !key_size || !key_offset || !order || n == 0 || n_keys == 0) {
+    mtx_set_error("mtx_group_by_u32_dev: bad argument");
+    return MTX_E_ARG;
+  }
+  if (n >= (1ull << 31)) {
+    mtx_set_error("mtx_group_by_u32_dev: n too large");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = dalloc(c->s5, mtxd::hashgrid_workspace_bytes(n, n_keys)))) return rc;
+  if ((rc = dalloc(c->s6, 64))) return rc;
+  // the keys are device data: range-checked on the device before any
+  // kernel indexes with them
+  HIP_TRY(hipMemsetAsync(c->s6.p, 0, 4, c->stream));
+  mtxd::keys_in_range(keys, n, n_keys, (uint32_t *)c->s6.p, c->stream);
+  uint32_t bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, c->s6.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (bad) {
+    mtx_set_error("mtx_group_by_u32_dev: a key is >= n_keys (%u)", n_keys);
+    return MTX_E_ARG;
+  }
+  if ((rc = prim_timer_begin(c))) return rc;
+  rc = mtxd::group_by_u32(keys, n, n_keys, key_size, key_offset, order, c->s5.p, c->stream);
+  if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   prim_timer_read(c);
   return MTX_OK;

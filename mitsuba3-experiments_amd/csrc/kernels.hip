@@ -59,13 +59,14 @@ struct ClosestSrc {
 // fits without spills. Shadow 56.4 -> 55.6 ms per step (A/B, one box, 3
 // rounds, round 2).
 #define MTX_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
-template <bool STATS>
+// CW: on the 8-wide tree (trace_loop_closest_cw), else the 4-wide tree.
+template <bool STATS, bool CW>
 __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   // dynamic LDS: stack columns + tree top (device_common.h trace_loop)
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
-  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, nv, tv, nr,
+  trace_loop<false, STATS, CW>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, nv, tv, nr,
                            wi);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
@@ -1296,20 +1297,25 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
   valid_out[i] = v;
 }
 
-// Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0).
-__global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const float4 *rays, uint32_t n, int any_hit,
-                                                           uint32_t *hits, uint32_t *visits) {
-  extern __shared__ int4 raw_lds[];  // one stack column per thread (device_common.h stack_bytes)
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0). mode 0
+// closest hit (4-wide tree), 1 any hit, 2 closest hit on the 8-wide tree
+// (its stack spills to the wavefront's global area: the grid is at most the
+// persistent trace grid, grid-stride over the rays).
+__device__ __forceinline__ void trace_raw_one(const DevScene &s, const float4 *rays, uint32_t i, int any_hit,
+                                              uint32_t *hits, uint32_t *visits, int4 *raw_lds) {
   const float4 o4 = rays[2 * (size_t)i], d4 = rays[2 * (size_t)i + 1];
   TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
   float tbest = o4.w, bu = 0.f, bv = 0.f;
   uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
-  if (any_hit) {
+  if (any_hit == 1) {
     hits[i] = traverse_occ(s, reinterpret_cast<uint32_t *>(raw_lds) + threadIdx.x, r, o4.w, nv, tv) ? 1u : 0u;
   } else {
-    traverse_closest(s, reinterpret_cast<int32_t *>(raw_lds) + threadIdx.x, r, tbest, prim, bu, bv, nv, tv);
+    if (any_hit == 2)
+      traverse_closest_cw(s, reinterpret_cast<uint2 *>(raw_lds) + threadIdx.x,
+                          reinterpret_cast<uint2 *>(s.stack_ovf) + blockIdx.x * kTraceBlock + threadIdx.x, r, tbest,
+                          prim, bu, bv, nv, tv);
+    else
+      traverse_closest(s, reinterpret_cast<int32_t *>(raw_lds) + threadIdx.x, r, tbest, prim, bu, bv, nv, tv);
     if (prim == 0xffffffffu) tbest = kInf;
     hits[4 * (size_t)i + 0] = __float_as_uint(tbest);
     hits[4 * (size_t)i + 1] = prim;
@@ -1320,6 +1326,13 @@ __global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const flo
     visits[2 * (size_t)i] = nv;
     visits[2 * (size_t)i + 1] = tv;
   }
+}
+
+__global__ __launch_bounds__(kTraceBlock) void k_trace_raw(DevScene s, const float4 *rays, uint32_t n, int any_hit,
+                                                           uint32_t *hits, uint32_t *visits) {
+  extern __shared__ int4 raw_lds[];  // one stack column per thread (device_common.h stack_bytes)
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    trace_raw_one(s, rays, i, any_hit, hits, visits, raw_lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1477,10 +1490,18 @@ void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkPara
 }
 void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                           hipStream_t st) {
-  if (stats)
-    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, false), st, s, b, bounce);
-  else
-    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), persistent_stack_bytes(s, false), st, s, b, bounce);
+  const size_t lds = persistent_stack_bytes(s, s.closest_cw != 0);
+  if (s.closest_cw) {
+    if (stats)
+      hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
+    else
+      hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
+  } else {
+    if (stats)
+      hipLaunchKernelGGL((k_trace_closest<true, false>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
+    else
+      hipLaunchKernelGGL((k_trace_closest<false, false>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
+  }
 }
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st) {
@@ -1521,8 +1542,10 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
 // fewer of the two trees' kernels).
 int trace_blocks_per_cu(const DevScene &s) {
   int nc = 0, na = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false>, kTraceBlock,
-                                                   persistent_stack_bytes(s, false)) != hipSuccess ||
+  if (s.closest_cw ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false, true>, kTraceBlock,
+                                                                 persistent_stack_bytes(s, true)) != hipSuccess
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false, false>, kTraceBlock,
+                                                                 persistent_stack_bytes(s, false)) != hipSuccess ||
       nc <= 0)
     nc = 4;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&na, k_trace_shadow<false>, kTraceBlock,
@@ -1607,7 +1630,9 @@ void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, ui
 }
 void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any_hit, uint32_t *hits,
                       uint32_t *visits, hipStream_t st) {
-  hipLaunchKernelGGL(k_trace_raw, dim3(blocks_for(n, kTraceBlock)), dim3(kTraceBlock), stack_bytes(s), st, s, rays, n, any_hit,
+  // at most the persistent grid's threads: mode 2 indexes the spill area by thread
+  const unsigned grid = std::min<unsigned>(blocks_for(n, kTraceBlock), s.ovf_threads / kTraceBlock);
+  hipLaunchKernelGGL(k_trace_raw, dim3(std::max(1u, grid)), dim3(kTraceBlock), stack_bytes(s), st, s, rays, n, any_hit,
                      hits, visits);
 }
 

@@ -25,6 +25,9 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
 int group_by_u32(const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *key_size, uint32_t *key_offset,
                  uint32_t *order, void *ws, hipStream_t st);
 
+// *bad (device word, zeroed by the caller) becomes non-zero if a key >= n_keys.
+int keys_in_range(const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *bad, hipStream_t st);
+
 // Stable sort permutation of n keys < 2^24 (hash-grid machinery).
 size_t sort24_workspace_bytes(uint64_t n);
 int sort24(const uint32_t *keys, uint64_t n, uint32_t *perm, void *ws, hipStream_t st);

@@ -1546,6 +1546,23 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
   return MTX_OK;
 }
 
+// Device-side key check of mtx_group_by_u32_dev: *bad becomes non-zero when
+// any key is >= n_keys (one ballot per wave, one store by the wave's first
+// lane; no kernel reads a key out of range afterwards).
+__global__ __launch_bounds__(256) void k_keys_in_range(const uint32_t *__restrict__ keys, uint64_t n, uint32_t n_keys,
+                                                       uint32_t *bad) {
+  bool any = false;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256ull)
+    any = any || keys[i] >= n_keys;
+  if (__ballot(any) != 0 && (threadIdx.x & 63u) == 0) *bad = 1u;
+}
+int keys_in_range(const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *bad, hipStream_t st) {
+  const uint64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_keys_in_range, dim3((unsigned)(blocks < 4096 ? (blocks ? blocks : 1) : 4096)), dim3(256), 0, st,
+                     keys, n, n_keys, bad);
+  return MTX_OK;
+}
+
 // Stable group-by of n keys < n_keys (the hash grid's machinery without the
 // hashing): key_size, exclusive key_offset and order (element indices grouped
 // by key, ascending index inside a key).

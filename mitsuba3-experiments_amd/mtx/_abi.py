@@ -133,6 +133,7 @@ class SceneDesc(C.Structure):
         ("occ_tri_geom", C.c_void_p),
         ("n_occ_nodes", C.c_uint32),
         ("pad1", C.c_uint32),
+        ("occ_perm", C.c_void_p),
     ]
 
 
@@ -284,6 +285,7 @@ EXPORTS = [
     "mtx_hashgrid_build",
     "mtx_scatter_reduce_f32",
     "mtx_group_by_u32",
+    "mtx_group_by_u32_dev",
     "mtx_field_upload",
     "mtx_field_features",
     "mtx_field_mlp",

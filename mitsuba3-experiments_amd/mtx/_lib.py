@@ -72,6 +72,7 @@ def lib() -> C.CDLL:
         "mtx_hashgrid_build": ([vp, vp, u64, u32, u32, vp, vp, vp, vp], C.c_int),
         "mtx_scatter_reduce_f32": ([vp, C.c_int, vp, u64, vp, vp, u64], C.c_int),
         "mtx_group_by_u32": ([vp, vp, u64, u32, vp, vp, vp], C.c_int),
+        "mtx_group_by_u32_dev": ([vp, vp, u64, u32, vp, vp, vp], C.c_int),
         "mtx_field_train_init": ([vp, C.POINTER(_abi.FieldOpt)], C.c_int),
         "mtx_field_grad": ([vp, u64, vp, vp, vp, C.c_float, vp, C.POINTER(C.c_double), vp, vp], C.c_int),
         "mtx_field_train_step": ([vp, u64, vp, vp, vp, C.POINTER(_abi.TrainStats)], C.c_int),

@@ -84,7 +84,9 @@ def fold_rounds(func, target, value, size, offset, order):
     applies `func(a, b)` once, vectorised, to every target that has more
     than r values, with a = its current value and b = its r-th value in
     ascending index (the reference elects an arbitrary one per round). Works
-    on numpy arrays; func sees arrays, as the reference's sees Dr.Jit ones."""
+    on numpy arrays; func sees arrays, as the reference's sees Dr.Jit ones.
+    Host cost: one vectorised numpy round per value of the largest group (a
+    skewed index costs that many rounds, as the reference's loop does)."""
     t = np.array(target, copy=True)
     v = np.asarray(value)
     size = np.asarray(size, np.int64)
@@ -98,25 +100,104 @@ def fold_rounds(func, target, value, size, offset, order):
     return t
 
 
+def _torch_cuda(x) -> bool:
+    import sys
+
+    torch = sys.modules.get("torch")
+    return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
+
+
+def group_by_device(keys, n_keys: int):
+    """group_by on a torch tensor in HBM (mtx_group_by_u32_dev): returns
+    (key_size, key_offset, order) as int32 tensors on the keys' device, with
+    no host copy of the data (keys < 2^31)."""
+    import torch
+
+    k = keys.to(torch.int32).contiguous()
+    dev = k.device
+    n_keys = int(n_keys)
+    size = torch.empty(n_keys, dtype=torch.int32, device=dev)
+    offset = torch.empty(n_keys, dtype=torch.int32, device=dev)
+    order = torch.empty(len(k), dtype=torch.int32, device=dev)
+    if len(k):
+        ctx = context(dev.index if dev.index is not None else torch.cuda.current_device())
+        torch.cuda.synchronize(dev)  # libmtx runs on its own stream: the keys must be complete
+        check(lib().mtx_group_by_u32_dev(ctx.handle, k.data_ptr(), len(k), n_keys, size.data_ptr(),
+                                         offset.data_ptr(), order.data_ptr()), "mtx_group_by_u32_dev")
+    else:
+        size.zero_()
+        offset.zero_()
+    return size, offset, order
+
+
+def fold_rounds_device(func, target, value, size, offset, order):
+    """fold_rounds with torch tensors on the device: func(a, b) runs on HBM
+    arrays (torch ops) as the reference's runs inside its Dr.Jit loop
+    (reductions.py:23-54). Targets are ordered by their value count, largest
+    first, so round r updates the first cnt[r] of them; the only host reads
+    are the round count and the per-round counts (one small copy)."""
+    import torch
+
+    t = target.clone()
+    sz = size.to(torch.int64)
+    rounds = int(sz.max().item()) if len(sz) else 0
+    if rounds == 0:
+        return t
+    _, tid = torch.sort(sz, descending=True, stable=True)
+    hist = torch.bincount(sz, minlength=rounds + 1)
+    at_least = hist.flip(0).cumsum(0).flip(0)  # at_least[k] = #targets with >= k values
+    cnt = at_least[1:rounds + 1].cpu().tolist()
+    off = offset.to(torch.int64)[tid]
+    ordr = order.to(torch.int64)
+    for r in range(rounds):
+        m = int(cnt[r])
+        sel = tid[:m]
+        t[sel] = func(t[sel], value[ordr[off[:m] + r]])
+    return t
+
+
 def scatter_reduce_with(op, target, value, index, device: int | None = None):
     """reductions.py:12-54. func in {'add', 'min', 'max', 'mul'} (or ADD, MIN,
     MAX, MUL): one device pass, each target receiving its values in ascending
     index order (f32). Any other callable `func(a, b)` (the reference accepts
     any, :12, :53): the device groups the values by target (group_by) and the
-    callable is folded on the host round by round (fold_rounds), the
-    reference's structure with one deterministic election per round; target
-    and value may then have any numpy dtype func handles."""
+    callable is folded round by round, the reference's structure with one
+    deterministic election per round -- on the device when target / value /
+    index are torch tensors in HBM (group_by_device + fold_rounds_device:
+    func sees device tensors, nothing goes through the host), else on the host
+    over numpy arrays of any dtype func handles."""
+    if len(value) != len(index):
+        raise ValueError(f"scatter_reduce_with: {len(value)} values for {len(index)} indices")
+    on_device = any(_torch_cuda(x) for x in (target, value, index))
     if isinstance(op, str):
         if op not in _OPS:
             raise TypeError(f"scatter_reduce_with: unknown func {op!r} (device ops: add, min, max, mul)")
         op = _OPS[op]
     elif callable(op):
+        if on_device:
+            import torch
+
+            dev = next(x.device for x in (target, value, index) if _torch_cuda(x))
+            tgt = torch.as_tensor(target, device=dev)
+            val = torch.as_tensor(value, device=dev)
+            idx = torch.as_tensor(index, device=dev).to(torch.int64)
+            if len(idx) and (int(idx.min().item()) < 0 or int(idx.max().item()) >= len(tgt)):
+                raise ValueError("scatter_reduce_with: index out of range")
+            size, offset, order = group_by_device(idx, len(tgt))
+            return fold_rounds_device(op, tgt, val, size, offset, order)
         idx = np.ascontiguousarray(index, np.uint32)
         tgt = np.asarray(target)
         if len(idx) and int(idx.max()) >= len(tgt):
             raise ValueError("scatter_reduce_with: index out of range")
         size, offset, order = group_by(idx, len(tgt), device)
         return fold_rounds(op, tgt, value, size, offset, order)
+    if on_device:
+        # the fixed ops take host pointers (mtx_scatter_reduce_f32): one copy each way
+        import torch
+
+        dev = next(x.device for x in (target, value, index) if _torch_cuda(x))
+        host = [x.cpu().numpy() if _torch_cuda(x) else x for x in (target, value, index)]
+        return torch.as_tensor(scatter_reduce_with(op, *host, device=dev.index), device=dev)
     t = np.array(target, np.float32)
     v = np.ascontiguousarray(value, np.float32)
     i = np.ascontiguousarray(index, np.uint32)

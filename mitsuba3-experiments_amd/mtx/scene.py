@@ -344,6 +344,8 @@ class Scene:
         d.occ_nodes = self.occ_nodes.ctypes.data
         d.occ_tri_geom = self.occ_tri_geom.ctypes.data
         d.n_occ_nodes = self.n_occ_nodes
+        self.occ_perm = np.ascontiguousarray(self.occ_perm, np.uint32)
+        d.occ_perm = self.occ_perm.ctypes.data
         return d
 
     def save(self, path: str):

@@ -52,7 +52,7 @@ def _trace_gpu(scene, rays, any_hit):
     ctx = _ctx()
     integrators._bind_scene(ctx, scene)
     n = len(rays)
-    hits = np.zeros(n if any_hit else 4 * n, np.uint32)
+    hits = np.zeros(n if int(any_hit) == 1 else 4 * n, np.uint32)  # any_hit 2: closest hit, 8-wide tree
     visits = np.zeros(2 * n, np.uint32)
     r = np.ascontiguousarray(rays, np.float32)
     check(lib().mtx_trace(ctx.handle, n, r.ctypes.data, int(any_hit), hits.ctypes.data, visits.ctypes.data),
