@@ -91,7 +91,7 @@ int upload(DevBuf &b, const T *src, size_t count, hipStream_t st) {
 struct Wave2 {
   hipStream_t stream = nullptr;
   hipEvent_t start = nullptr, done = nullptr;
-  DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, xheads, stack_ovf;
+  DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, xheads, stack_ovf, cq_perm, cq_cursor;
   DevBuf cq_p, cq_d, cq_t, cq_count, f_feat, f_out;  // NRC radiance-cache queries of its chunks
   uint32_t capacity = 0;
 };
@@ -166,7 +166,9 @@ struct mtx_ctx {
   // resident lanes of the megakernel's grid)
   uint32_t mega_paths = 0xffffffffu;
   int mega_grid = 0;
-  uint32_t cache_sort = 0;  // MTX_CACHE_SORT=1: NRC cache queries encoded in Morton order (measured slower)
+  // NRC cache query order: MTX_CACHE_SORT=1 Morton-sorted (host sync; measured slower), 2 grouped
+  // by region on the device with one eighth of the rows per XCD (field.hip)
+  uint32_t cache_sort = MTX_CACHE_SORT;
   DevBuf cq_keys, cq_perm, cq_ws;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -229,7 +231,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_OCC_UREFILL")) c->occ_urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)strtoul(e, nullptr, 0);
-  if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = atoi(e) != 0;
+  if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = (uint32_t)std::max(0, std::min(2, atoi(e)));
   *out = c;
   return MTX_OK;
 }
@@ -257,7 +259,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   Wave2 &w = c->w2;
   for (DevBuf *b : {&w.ray_o, &w.ray_d, &w.thr, &w.L, &w.prev, &w.misc, &w.pos, &w.hit, &w.q0, &w.q1, &w.shadow,
                     &w.counters, &w.xheads, &w.stack_ovf, &w.cq_p, &w.cq_d, &w.cq_t, &w.cq_count, &w.f_feat,
-                    &w.f_out})
+                    &w.f_out, &w.cq_perm, &w.cq_cursor})
     dfree(*b);
   if (w.start) hipEventDestroy(w.start);
   if (w.done) hipEventDestroy(w.done);
@@ -483,9 +485,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     // device triangles packed to 36 B (the ABI's 48-B records carry 3 pad
     // words): 3.6 instead of 2.7 triangles per 128-B line, same load count
     const float *src = tree ? occ_geom : d->tri_geom;
-    // (+4 floats: the merged-load traversal reads a triangle's last word with
-    // a 16-B load, 12 B past the last record)
-    std::vector<float> g9(9ull * d->n_tris + 4, 0.f);
+    std::vector<float> g9(9ull * d->n_tris);
     for (size_t i = 0; i < d->n_tris; ++i)
       for (int k = 0; k < 3; ++k)
         for (int j = 0; j < 3; ++j) g9[9 * i + 3 * k + j] = src[12 * i + 4 * k + j];
@@ -856,12 +856,23 @@ struct Timer {
 // `stream` with the feature / output buffers of the chunk's wavefront: the
 // context's by default, the second wavefront's in a two-stream render).
 void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false,
-               hipStream_t stream = nullptr, DevBuf *feat = nullptr, DevBuf *out = nullptr) {
+               hipStream_t stream = nullptr, DevBuf *feat = nullptr, DevBuf *out = nullptr, DevBuf *perm_buf = nullptr,
+               DevBuf *cursor_buf = nullptr) {
   hipStream_t st = stream ? stream : c->stream;
   DevBuf &f_feat = feat ? *feat : c->f_feat, &f_out = out ? *out : c->f_out;
   const uint32_t *perm = nullptr;
+  int xcd_split = 0;
   hipEvent_t e = tm.begin(4, st);
-  if (c->cache_sort && !nerad_render && st == c->stream) {
+  if (c->cache_sort == 2 && !nerad_render) {
+    // region-grouped rows, the blocks of each XCD on one eighth of them
+    // (field.hip k_field_encode xcd_split): device-only, no host round trip
+    DevBuf &pb = perm_buf ? *perm_buf : c->cq_perm, &cb = cursor_buf ? *cursor_buf : c->cq_keys;
+    if (!dalloc(pb, 4ull * cap) && !dalloc(cb, 4ull * 512)) {
+      mtxd::field_bucket_queries(c->field, b.cq_p, b.cq_count, cap, (uint32_t *)cb.p, (uint32_t *)pb.p, c->n_cu, st);
+      perm = (const uint32_t *)pb.p;
+      xcd_split = 1;
+    }
+  } else if (c->cache_sort && !nerad_render && st == c->stream) {
     // encode the queries in Morton order (a stable sort of 24-bit cell codes
     // with the hash-grid group-by): the hash-grid corner gathers of
     // neighbouring rows then share table lines. The MLP row order follows;
@@ -877,7 +888,7 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
         perm = (const uint32_t *)c->cq_perm.p;
     }
   }
-  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm);
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split);
   tm.end(4, e, st);
   e = tm.begin(5, st);
   mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden, (float *)f_out.p,
@@ -1284,7 +1295,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   const uint64_t n_paths_all = (uint64_t)band_px * a->spp;
   // (NRC + cache: each wavefront has its own query / feature buffers, so one
   // chunk's cache pass overlaps the other's bounces; not with the Morton sort)
-  const bool two = c->streams > 1 && !mlt && !(nrc_cache && c->cache_sort) && !nerad_render &&
+  const bool two = c->streams > 1 && !mlt && !(nrc_cache && c->cache_sort == 1) && !nerad_render &&
                    a->integrator != MTX_INT_RESTIR_GI && n_paths_all >= (1u << 16) &&
                    n_paths_all <= (1ull << c->streams_max_log2);
   // the default chunk is sized for every wavefront the render allocates
@@ -1392,7 +1403,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     run_bounces(c, bc, p, tm, &n_trace, &n_shadow, &sc, st);
     if (nrc_cache) {
       if (second)
-        run_cache(c, bc, p.n_paths, tm, false, st, &c->w2.f_feat, &c->w2.f_out);
+        run_cache(c, bc, p.n_paths, tm, false, st, &c->w2.f_feat, &c->w2.f_out, &c->w2.cq_perm, &c->w2.cq_cursor);
       else
         run_cache(c, b, p.n_paths, tm);
     }

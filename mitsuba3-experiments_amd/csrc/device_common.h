@@ -251,7 +251,7 @@ __device__ __forceinline__ void lds_node64(const int4 *top, int32_t node, int4 &
 // the near-first order: returns the number of hit children, c[] the child
 // references sorted by entry distance.
 __device__ __forceinline__ int wide_visit_regs(const TraceRay &r, int4 a, int4 rf, int4 qa, int2 qb, float tbest,
-                                               int32_t c[4]) {
+                                               int32_t c[4], uint32_t *key_out = nullptr) {
   uint32_t key[4];
   const uint32_t eb = (uint32_t)a.w;
   // the references ride along the compare-exchange network (one compare +
@@ -279,11 +279,16 @@ __device__ __forceinline__ int wide_visit_regs(const TraceRay &r, int4 a, int4 r
   }
   MTX_CAS2(0, 1) MTX_CAS2(2, 3) MTX_CAS2(0, 2) MTX_CAS2(1, 3) MTX_CAS2(1, 2)
 #undef MTX_CAS2
+  if (key_out) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) key_out[k] = key[k];
+  }
   return n;
 }
 
 __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, int32_t node, float tbest,
-                                          int32_t c[4], const int4 *top = nullptr, int top_n = 0) {
+                                          int32_t c[4], const int4 *top = nullptr, int top_n = 0,
+                                          uint32_t *key_out = nullptr) {
   int4 a, rf, qa;
   int2 qb;
   if (node < top_n) {
@@ -295,15 +300,7 @@ __device__ __forceinline__ int wide_visit(const DevScene &s, const TraceRay &r, 
     qa = np[2];
     qb = *reinterpret_cast<const int2 *>(np + 3);
   }
-  return wide_visit_regs(r, a, rf, qa, qb, tbest, c);
-}
-
-// A 16-B load from a 4-B aligned address (the 36-B packed triangles; global
-// memory needs dword alignment only).
-typedef int v4i_a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ int4 ld16(const void *p) {
-  const v4i_a4 v = *reinterpret_cast<const v4i_a4 *>(p);
-  return make_int4(v.x, v.y, v.z, v.w);
+  return wide_visit_regs(r, a, rf, qa, qb, tbest, c, key_out);
 }
 
 // Per-thread closest-hit traversal in the oracle's order (oracle/oracle.cpp
@@ -586,16 +583,7 @@ __device__ __forceinline__ void count_wave_iter(uint32_t lane, uint32_t *ctr) {
 // visit or a leaf's triangle range; a visit pushes the far hit children
 // (three unconditional LDS stores when they fit: dead entries above the new
 // top are harmless) and continues with the nearest.
-//
-// MERGE: a lane does ONE work item per iteration -- a node visit or one
-// triangle test -- and the node lanes and the triangle lanes of a wave fetch
-// their data with the same load instructions (node: 16 + 16 + 16 + 8 B,
-// triangle: 16 + 16 + 16 B of its 36-B record, the last load reading 12 B
-// of the next record). The vector-memory address path costs per wave
-// instruction (and per distinct line), not per active lane, so an
-// iteration issues 4 load instructions instead of 4 + 3. Same visit order,
-// same counts.
-template <bool STATS, bool MERGE, class Src>
+template <bool STATS, class Src>
 __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                                    int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
                                                    uint32_t &nr, uint32_t *wave_iters) {
@@ -649,27 +637,11 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
     }
     if (__ballot(has) == 0) break;
     // ---- one inner-node visit
-    const bool dn = has && node >= 0;
-    const bool dt = MERGE && has && node < 0 && tri < tri_end;
-    int4 x0 = make_int4(0, 0, 0, 0), x1 = x0, x2 = x0;
-    int2 x3 = make_int2(0, 0);
-    if (MERGE) {
-      const bool in_lds = dn && node < top_n;
-      if (in_lds) lds_node64(top, node, x0, x1, x2, x3);
-      if ((dn && !in_lds) || dt) {
-        const char *gp = dn ? reinterpret_cast<const char *>(s.nodes + 4 * node)
-                            : reinterpret_cast<const char *>(s.tri + 9 * (size_t)tri);
-        x0 = ld16(gp);
-        x1 = ld16(gp + 16);
-        x2 = ld16(gp + 32);
-        if (dn) x3 = *reinterpret_cast<const int2 *>(gp + 48);
-      }
-    }
-    if (dn) {
+    if (has && node >= 0) {
       if (STATS) count_wave_iter(lane, &wave_iters[0]);
       int32_t cr[4];
       ++nv;
-      const int n = MERGE ? wide_visit_regs(r, x0, x1, x2, x3, tbest, cr) : wide_visit(s, r, node, tbest, cr, top, top_n);
+      const int n = wide_visit(s, r, node, tbest, cr, top, top_n);
       if (n > 0) {
         const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
         const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
@@ -704,18 +676,11 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
         pop_next();
       }
     }
-    // ---- one triangle test (MERGE: only a lane that did no node visit)
-    if (MERGE ? dt : (has && tri < tri_end)) {
+    // ---- one triangle test
+    if (has && tri < tri_end) {
       if (STATS) count_wave_iter(lane, &wave_iters[1]);
       const uint32_t pr = tri;
-      TriGeom g;
-      if (MERGE) {
-        g.p0 = V3{__int_as_float(x0.x), __int_as_float(x0.y), __int_as_float(x0.z)};
-        g.e1 = V3{__int_as_float(x0.w), __int_as_float(x1.x), __int_as_float(x1.y)};
-        g.e2 = V3{__int_as_float(x1.z), __int_as_float(x1.w), __int_as_float(x2.x)};
-      } else {
-        g = load_tri(s.tri, pr);
-      }
+      const TriGeom g = load_tri(s.tri, pr);
       float t, u, v;
       ++tv;
       ++tri;
@@ -738,10 +703,7 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
 // Any hit on the 8-wide occlusion tree: a lane tests its triangle group
 // before the next child of its node group; an empty pair pops the next node
 // group. The first hit ends the ray.
-// MERGE: one work item per lane and iteration (a node visit, or one triangle
-// test of the triangle group), node and triangle fetches sharing the load
-// instructions (node 5 x 16 B, triangle 3 x 16 B), as for closest hit.
-template <bool STATS, bool MERGE, class Src>
+template <bool STATS, class Src>
 __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                                uint2 *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
                                                uint32_t &nr, uint32_t *wave_iters) {
@@ -777,31 +739,11 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
     }
     if (__ballot(has) == 0) break;
     // ---- one node visit: the nearest remaining child of the node group
-    const bool dn = has && thits == 0 && (ghits >> 24) != 0;
-    const bool dt = MERGE && has && thits != 0;
-    uint32_t node = 0;
-    int4 x0 = make_int4(0, 0, 0, 0), x1 = x0, x2 = x0, x3 = x0, x4 = x0;
-    if (MERGE) {
-      if (dn) node = cw_inner_child(gbase, ghits & 0xffu, oct, (uint32_t)ctz32(ghits >> 24));
-      const bool in_lds = dn && (int)node < top_n;
-      if (in_lds) lds_node80(top, node, x0, x1, x2, x3, x4);
-      if ((dn && !in_lds) || dt) {
-        const char *gp = dn ? reinterpret_cast<const char *>(s.occ_nodes + 5 * (size_t)node)
-                            : reinterpret_cast<const char *>(s.occ_tri + 9 * (size_t)(tbase + (uint32_t)ctz32(thits)));
-        x0 = ld16(gp);
-        x1 = ld16(gp + 16);
-        x2 = ld16(gp + 32);
-        if (dn) {
-          x3 = ld16(gp + 48);
-          x4 = ld16(gp + 64);
-        }
-      }
-    }
-    if (dn) {
+    if (has && thits == 0 && (ghits >> 24) != 0) {
       if (STATS) count_wave_iter(lane, &wave_iters[0]);
       const uint32_t p = (uint32_t)ctz32(ghits >> 24);
       ghits &= ~(1u << (24 + p));
-      if (!MERGE) node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
+      const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
       if (ghits >> 24) {
         const uint2 g = make_uint2(gbase, ghits);
         if (sp < lds_n) {
@@ -813,26 +755,18 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
         ++sp;
       }
       ++nv;
-      const CwVisit v = MERGE ? cw_visit_regs(r, oct, x0, x1, x2, x3, x4, tmax) : cw_visit(s, r, oct, node, tmax, top, top_n);
+      const CwVisit v = cw_visit(s, r, oct, node, tmax, top, top_n);
       gbase = v.child_base;
       ghits = (v.hits & 0xff000000u) | v.imask;
       tbase = v.tri_base;
       thits = v.hits & 0x00ffffffu;
     }
-    // ---- one triangle test of the triangle group (MERGE: only a lane that
-    // did no node visit)
-    if (MERGE ? dt : (has && thits != 0)) {
+    // ---- one triangle test of the triangle group
+    if (has && thits != 0) {
       if (STATS) count_wave_iter(lane, &wave_iters[1]);
       const uint32_t pr = tbase + (uint32_t)ctz32(thits);
       thits &= thits - 1u;
-      TriGeom g;
-      if (MERGE) {
-        g.p0 = V3{__int_as_float(x0.x), __int_as_float(x0.y), __int_as_float(x0.z)};
-        g.e1 = V3{__int_as_float(x0.w), __int_as_float(x1.x), __int_as_float(x1.y)};
-        g.e2 = V3{__int_as_float(x1.z), __int_as_float(x1.w), __int_as_float(x2.x)};
-      } else {
-        g = load_tri(s.occ_tri, pr);
-      }
+      const TriGeom g = load_tri(s.occ_tri, pr);
       float t, u, v;
       ++tv;
       if (tri_intersect(r, g.p0, g.e1, g.e2, tmax, &t, &u, &v)) {
@@ -1086,19 +1020,14 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     __syncthreads();
     if constexpr (CW && !ANY)
       trace_loop_closest_cw<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
-    else if constexpr ((MTX_TRAV_MERGE & 2) != 0)
-      trace_loop_occ<STATS, true>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
     else
-      trace_loop_occ<STATS, false>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+      trace_loop_occ<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
   } else {
     int32_t *cols = reinterpret_cast<int32_t *>(trace_lds);
     int4 *top = reinterpret_cast<int4 *>(cols + s.lds_entries * kTraceBlock);
     for (uint32_t i = threadIdx.x; i < 4 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
     __syncthreads();
-    if constexpr ((MTX_TRAV_MERGE & 1) != 0)
-      trace_loop_closest<STATS, true>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
-    else
-      trace_loop_closest<STATS, false>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+    trace_loop_closest<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
   }
 }
 

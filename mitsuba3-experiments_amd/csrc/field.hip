@@ -42,17 +42,31 @@ constexpr float kLeakySlope = 0.01f;  // drjit.nn.LeakyReLU default
 // and written out as 16-B stores (one 128-B row = 8 lanes).
 constexpr uint32_t kEncodeBlock = 256;
 
+// xcd_split (rows grouped by region, k_cache_bucket_*): the blocks that
+// share an XCD (equal blockIdx % 8 under the observed round-robin placement,
+// MI355X_MICROARCH.md "Workgroup dispatch") take one contiguous eighth of the
+// rows, i.e. one eighth of the space, so each XCD's 4 MiB L2 holds the table
+// entries of its own region instead of all of them. Speed only: any
+// placement gives the same rows.
 __global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, const float4 *qp, const float4 *qd,
                                                                const uint32_t *count, uint32_t n_max,
-                                                               uint16_t *feat, const uint32_t *perm) {
+                                                               uint16_t *feat, const uint32_t *perm, int xcd_split) {
   extern __shared__ uint4 rows[];  // 256 / n_levels rows of 128 B
   const uint32_t n = count ? min(*count, n_max) : n_max;
   const uint32_t L = e.n_levels, qpb = kEncodeBlock / L;
   uint16_t *row_h = reinterpret_cast<uint16_t *>(rows);
   const uint32_t ql = threadIdx.x / L, l = threadIdx.x - ql * L;
-  for (uint32_t q0 = blockIdx.x * qpb; q0 < n; q0 += gridDim.x * qpb) {
+  uint32_t lo = 0, hi = n, first = blockIdx.x, stride = gridDim.x;
+  if (xcd_split) {
+    const uint32_t g = blockIdx.x & 7u;
+    lo = (uint32_t)(((uint64_t)n * g) >> 3);
+    hi = (uint32_t)(((uint64_t)n * (g + 1)) >> 3);
+    first = blockIdx.x >> 3;
+    stride = gridDim.x >> 3;
+  }
+  for (uint32_t q0 = lo + first * qpb; q0 < hi; q0 += stride * qpb) {
     const uint32_t q = q0 + ql;
-    if (ql < qpb && q < n) {
+    if (ql < qpb && q < hi) {
       const uint32_t qs = perm ? perm[q] : q;  // Morton-ordered rows: neighbouring threads share table lines
       const float4 p = qp[qs];
       const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
@@ -64,7 +78,7 @@ __global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, 
       }
     }
     __syncthreads();
-    const uint32_t nq = min(qpb, n - q0);
+    const uint32_t nq = min(qpb, hi - q0);
     for (uint32_t c = threadIdx.x; c < nq * (kFieldPad / 8); c += kEncodeBlock)
       reinterpret_cast<uint4 *>(feat + (size_t)kFieldPad * q0)[c] = rows[c];
     __syncthreads();
@@ -238,16 +252,105 @@ void field_morton_keys(const FieldEncoding &e, const float4 *qp, uint32_t n, uin
   if (n) hipLaunchKernelGGL(k_morton_keys, dim3((n + 255) / 256), dim3(256), 0, st, e, qp, n, keys);
 }
 
+// ---- region bucketing of the cache queries (no host round trip) -------
+// Bucket = 3-bit-per-axis Morton cell of the query in the field's box (512
+// regions); rows are grouped by bucket (order inside a bucket arbitrary: a
+// row's features and MLP column depend on its query only, and each path has
+// at most one query, so the film is unchanged).
+constexpr uint32_t kCacheBuckets = 512;
+constexpr uint32_t kBucketTile = 4096;  // queries per block of the scatter
+
+__device__ __forceinline__ uint32_t cache_bucket(const FieldEncoding &e, float4 p) {
+  const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
+  auto c = [](float v) { return (uint32_t)fminf(fmaxf(v * 8.f, 0.f), 7.f); };
+  const uint32_t x = c(pn.x), y = c(pn.y), z = c(pn.z);
+  uint32_t m = 0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b) m |= (((x >> b) & 1u) << (3 * b)) | (((y >> b) & 1u) << (3 * b + 1)) | (((z >> b) & 1u) << (3 * b + 2));
+  return m;
+}
+
+// counts per bucket (cursor[0..511], zeroed by the caller)
+__global__ __launch_bounds__(256) void k_cache_bucket_count(FieldEncoding e, const float4 *qp, const uint32_t *count,
+                                                            uint32_t n_max, uint32_t *cursor) {
+  __shared__ uint32_t h[kCacheBuckets];
+  for (uint32_t i = threadIdx.x; i < kCacheBuckets; i += 256) h[i] = 0;
+  __syncthreads();
+  const uint32_t n = min(*count, n_max);
+  for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < n; q += gridDim.x * 256) atomicAdd(&h[cache_bucket(e, qp[q])], 1u);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < kCacheBuckets; i += 256)
+    if (h[i]) atomicAdd(&cursor[i], h[i]);
+}
+
+// counts -> exclusive offsets, in place (one block of 512 threads)
+__global__ __launch_bounds__(kCacheBuckets) void k_cache_bucket_scan(uint32_t *cursor) {
+  __shared__ uint32_t v[kCacheBuckets];
+  const uint32_t i = threadIdx.x;
+  const uint32_t x = cursor[i];
+  v[i] = x;
+  __syncthreads();
+  for (uint32_t off = 1; off < kCacheBuckets; off <<= 1) {
+    const uint32_t y = i >= off ? v[i - off] : 0u;
+    __syncthreads();
+    v[i] += y;
+    __syncthreads();
+  }
+  cursor[i] = v[i] - x;
+}
+
+// perm[row] = query: per block tile, LDS counts, one reservation per
+// (block, bucket), LDS cursors for the positions
+__global__ __launch_bounds__(256) void k_cache_bucket_scatter(FieldEncoding e, const float4 *qp, const uint32_t *count,
+                                                              uint32_t n_max, uint32_t *cursor, uint32_t *perm) {
+  __shared__ uint32_t h[kCacheBuckets];
+  constexpr uint32_t kPer = kBucketTile / 256;
+  const uint32_t n = min(*count, n_max);
+  for (uint32_t t0 = blockIdx.x * kBucketTile; t0 < n; t0 += gridDim.x * kBucketTile) {
+    for (uint32_t i = threadIdx.x; i < kCacheBuckets; i += 256) h[i] = 0;
+    __syncthreads();
+    uint32_t bk[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t q = t0 + k * 256 + threadIdx.x;
+      bk[k] = q < n ? cache_bucket(e, qp[q]) : 0xffffffffu;
+      if (q < n) atomicAdd(&h[bk[k]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kCacheBuckets; i += 256)
+      if (h[i]) h[i] = atomicAdd(&cursor[i], h[i]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k)
+      if (bk[k] != 0xffffffffu) perm[atomicAdd(&h[bk[k]], 1u)] = t0 + k * 256 + threadIdx.x;
+    __syncthreads();
+  }
+}
+
+void field_bucket_queries(const FieldEncoding &e, const float4 *qp, const uint32_t *count, uint32_t n_max,
+                          uint32_t *cursor, uint32_t *perm, int n_cu, hipStream_t st) {
+  if (n_max == 0) return;
+  hipMemsetAsync(cursor, 0, 4 * kCacheBuckets, st);
+  const unsigned g1 = (unsigned)std::min<uint64_t>((n_max + 255) / 256, (uint64_t)n_cu * 4);
+  hipLaunchKernelGGL(k_cache_bucket_count, dim3(std::max(1u, g1)), dim3(256), 0, st, e, qp, count, n_max, cursor);
+  hipLaunchKernelGGL(k_cache_bucket_scan, dim3(1), dim3(kCacheBuckets), 0, st, cursor);
+  const unsigned g2 = (unsigned)std::min<uint64_t>((n_max + kBucketTile - 1) / kBucketTile, (uint64_t)n_cu * 4);
+  hipLaunchKernelGGL(k_cache_bucket_scatter, dim3(std::max(1u, g2)), dim3(256), 0, st, e, qp, count, n_max, cursor,
+                     perm);
+}
+
 int field_encode(const FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count, uint32_t n_max,
-                 uint16_t *feat, hipStream_t st, const uint32_t *perm) {
+                 uint16_t *feat, hipStream_t st, const uint32_t *perm, int xcd_split) {
   if (n_max == 0) return MTX_OK;
   if (e.n_levels == 0 || e.n_levels > kEncodeBlock) {
     mtx_set_error("field_encode: unsupported n_levels %u", e.n_levels);
     return MTX_E_ARG;
   }
   const uint32_t qpb = kEncodeBlock / e.n_levels;
-  const unsigned blocks = (unsigned)std::min<uint64_t>((n_max + qpb - 1) / qpb, 256ull * 64);
-  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(kEncodeBlock), (size_t)qpb * kFieldPad * 2, st, e, qp, qd, count, n_max, feat, perm);
+  unsigned blocks = (unsigned)std::min<uint64_t>((n_max + qpb - 1) / qpb, 256ull * 64);
+  if (xcd_split) blocks = (blocks + 7u) & ~7u;  // whole groups of 8
+  hipLaunchKernelGGL(k_field_encode, dim3(blocks), dim3(kEncodeBlock), (size_t)qpb * kFieldPad * 2, st, e, qp, qd,
+                     count, n_max, feat, perm, xcd_split);
   return MTX_OK;
 }
 

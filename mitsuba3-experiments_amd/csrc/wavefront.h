@@ -53,11 +53,11 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_OCC_LDS_TOP
 #define MTX_OCC_LDS_TOP 48  // occlusion tree nodes copied into LDS per trace block (0 = none)
 #endif
-#ifndef MTX_TRAV_MERGE
-#define MTX_TRAV_MERGE 0  // bit 0 / 1: closest-hit / any-hit loop with shared node + triangle loads (device_common.h)
-#endif
 #ifndef MTX_CLOSEST_CW
 #define MTX_CLOSEST_CW 0  // closest hit on the 8-wide tree (device_common.h trace_loop_closest_cw)
+#endif
+#ifndef MTX_CACHE_SORT
+#define MTX_CACHE_SORT 0  // NRC cache query order (api.cpp run_cache): 0 as appended, 1 Morton sort, 2 region x XCD
 #endif
 #ifndef MTX_STREAMS
 #define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)

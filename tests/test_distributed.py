@@ -53,10 +53,12 @@ def _worker(rank, world, port, mode, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [4, 3])
+@pytest.mark.parametrize("world", [8, 4, 3])
 def test_sample_shards_combine_to_the_one_rank_film(tmp_path, oracle, world):
-    """GPU-count invariance: 4 ranks of 2 samples (2 whole
-    slots each) combine to the one-rank spp-8 film bit for bit; 3 ranks (the
+    """GPU-count invariance: 8 ranks of 1 sample (one film
+    slot per rank, the 8-GPU node) and 4 ranks of 2 samples (2 whole slots
+    each) combine to the one-rank spp-8 film bit for bit (lane seeding
+    path.py:156-161: a sample's lane is the same at every N); 3 ranks (the
     shards split slots) equal it up to summation order (rtol 2e-6)."""
     from mtx import load_dict, scene
 
@@ -67,7 +69,7 @@ def test_sample_shards_combine_to_the_one_rank_film(tmp_path, oracle, world):
     sc = scene.bedroom(width=48, height=27, scale=0.02, tex_res=32)
     integ = load_dict({"type": "path_test"})
     ref = oracle.render(sc, integ.render_args(sc, 4, 8, 0, sc.height, 8, 0))
-    if world == 4:
+    if world in (4, 8):
         assert np.array_equal(got, ref)
     else:
         np.testing.assert_allclose(got, ref, rtol=2e-6, atol=1e-6)

@@ -167,9 +167,10 @@ def test_nrc_cache_two_streams_bit_exact(small_scene, oracle, chunk):
 @pytest.mark.gpu
 def test_nrc_cache_morton_order_unchanged(tmp_path):
     """MTX_CACHE_SORT=1 encodes the cache queries in Morton order (sorted with
-    the hash-grid group-by; measured slower, so off by default); queue order
-    otherwise. Both films are identical (each query's features and MLP column
-    are its own)."""
+    the hash-grid group-by; measured slower); 2 groups them by region on the
+    device, one eighth of the rows per XCD (also on the second wavefront of a
+    two-stream render: chunk_paths); queue order otherwise. All films are
+    identical (each query's features and MLP column are its own)."""
     import os
     import subprocess
     import sys
@@ -182,12 +183,14 @@ from mtx import load_dict, scene
 from mtx.field import Field
 sc = scene.bedroom(width=64, height=36, scale=0.02, tex_res=64)
 integ = load_dict({"type": "nrc", "field": Field(sc, seed=5, table_scale=1.0)})
-np.save(sys.argv[2], integ.render_film(sc, seed=7, spp=4))
+kw = {"chunk_paths": int(sys.argv[3])} if int(sys.argv[3]) else {}
+np.save(sys.argv[2], integ.render_film(sc, seed=7, spp=4, **kw))
 '''
     films = []
-    for flag in ("1", "0"):
-        f = tmp_path / f"f{flag}.npy"
-        subprocess.run([sys.executable, "-c", code, os.path.join(root, "mitsuba3-experiments_amd"), str(f)],
+    for flag, chunk in (("1", 0), ("0", 0), ("2", 0), ("2", 5000), ("0", 5000)):
+        f = tmp_path / f"f{flag}_{chunk}.npy"
+        subprocess.run([sys.executable, "-c", code, os.path.join(root, "mitsuba3-experiments_amd"), str(f), str(chunk)],
                        check=True, env=dict(os.environ, MTX_CACHE_SORT=flag), timeout=300)
         films.append(np.load(f))
-    np.testing.assert_array_equal(films[0], films[1])
+    for f in films[1:]:
+        np.testing.assert_array_equal(films[0], f)

@@ -210,3 +210,41 @@ def test_scatter_reduce_with_callable_on_device_grouping():
         ref[i] = (3 * ref[i] - v) % 1000003
     got = primitives.scatter_reduce_with(lambda a, b: (3 * a - b) % 1000003, tgt, val, idx)
     assert np.array_equal(got, ref)
+
+
+def test_scatter_reduce_with_callable_in_hbm():
+    """reductions.py:12-54 with a Python func on torch tensors in HBM: the
+    grouping is mtx_group_by_u32_dev (device pointers, no host copy of the
+    data) and func runs on device tensors round by round, as the reference's
+    runs inside its Dr.Jit loop -- equal to the sequential loop, the KAT
+    (reductions.py:57-63), a skewed index, and out-of-range keys rejected."""
+    import torch
+
+    from mtx import primitives
+
+    dev = torch.device("cuda", 0)
+    idx = torch.arange(25, device=dev) % 10
+    t = primitives.scatter_reduce_with(lambda a, b: a + b, torch.zeros(10, device=dev), torch.ones(25, device=dev),
+                                       idx)
+    assert t.is_cuda and torch.equal(t.cpu(), torch.tensor([3.0] * 5 + [2.0] * 5))
+    rng = np.random.default_rng(11)
+    for n_t, skew in ((1200, False), (300, True)):
+        idx_np = rng.integers(0, n_t, 60000).astype(np.int64)
+        if skew:
+            idx_np[: 20000] = 7  # one target takes a third of the values
+        val_np = rng.integers(-9, 9, 60000).astype(np.int64)
+        tgt_np = rng.integers(-5, 5, n_t).astype(np.int64)
+        ref = tgt_np.copy()
+        for i, v in zip(idx_np, val_np):
+            ref[i] = (3 * ref[i] - v) % 1000003
+        got = primitives.scatter_reduce_with(lambda a, b: (3 * a - b) % 1000003, torch.as_tensor(tgt_np, device=dev),
+                                             torch.as_tensor(val_np, device=dev), torch.as_tensor(idx_np, device=dev))
+        assert got.is_cuda and np.array_equal(got.cpu().numpy(), ref)
+    # the device group-by itself equals numpy's stable argsort
+    k = torch.as_tensor(rng.integers(0, 5000, 1 << 20), device=dev)
+    size, offset, order = primitives.group_by_device(k, 5000)
+    kn = k.cpu().numpy()
+    assert np.array_equal(order.cpu().numpy(), np.argsort(kn, kind="stable"))
+    assert np.array_equal(size.cpu().numpy(), np.bincount(kn, minlength=5000))
+    with pytest.raises(Exception):
+        primitives.group_by_device(torch.tensor([1, 2, 5000], device=dev), 5000)

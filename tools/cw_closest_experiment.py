@@ -72,6 +72,9 @@ def main(n=100_000):
             ms = v[:, 0] >> 16
             line[f"cw8_mode{mode}"] = [float((v[:, 0] & 0xffff).mean()), float(v[:, 1].mean()),
                                        int(np.percentile(ms, 50)), int(np.percentile(ms, 99)), int(ms.max())]
+        hp, vp = oracle.trace(sc, rays, 2)  # the production 8-wide traversal (trace_closest_cw)
+        assert np.array_equal(hp, h4)
+        line["cw8_production"] = [float(vp[:, 0].mean()), float(vp[:, 1].mean())]
         t = np.zeros(len(rays), np.float32)
         v = np.zeros((len(rays), 2), np.uint32)
         rr = np.ascontiguousarray(rays)
