@@ -1035,6 +1035,15 @@ __global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator
 // stack_bytes() sizes the allocation with it: a megakernel block of another
 // width would let threads share stack words.
 static_assert(kShadeBlock == kTraceBlock, "k_path_mega: stack column stride must equal the block width");
+// Round 5: lanes, not waves, take paths. Each iteration a lane runs ONE
+// bounce of its path; a lane whose path has ended takes the next queued path
+// as soon as kMegaRefill lanes of its wave are idle (one claim atomic per
+// refill for all of them, consecutive queue positions), so a wave no longer
+// waits for the longest of its 64 paths before any lane starts another (the
+// round-4 form claimed 64 paths per wave and ran them to completion).
+#ifndef MTX_MEGA_REFILL
+#define MTX_MEGA_REFILL 16  // idle lanes of a wave that trigger a claim (64: the round-4 whole-wave batches)
+#endif
 template <int INT>
 __global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_path_mega(DevScene s, WaveBuffers b, ChunkParams p) {
   static_assert(INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH, "megakernel: path / path-mis only");
@@ -1044,56 +1053,65 @@ __global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_path_mega(
   const uint32_t iters = p.max_depth > 1u ? p.max_depth : 1u;
   int32_t *stk = reinterpret_cast<int32_t *>(mega_lds) + threadIdx.x;
   uint32_t *ostk = reinterpret_cast<uint32_t *>(mega_lds) + threadIdx.x;  // the same column
-  // waves claim 64 queue positions at a time (counters[2], zeroed with the
-  // bounce counters): a wave that finishes its paths early takes the next
-  // batch while slow ones still run
   const uint32_t lane = threadIdx.x & 63u;
+  bool has = false, drained = false;
+  uint32_t qi = 0, path = 0, bounce = 0;
   while (true) {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&b.counters[2], 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base >= count) break;
-    const uint32_t qi = base + lane;
-    if (qi < count) {  // reconverges before the next claim
-      const uint32_t path = p.ident0 ? qi : b.queue[0][qi];
-      bool cont = true;
-      for (uint32_t bounce = 0; bounce < iters && cont; ++bounce) {
-        const uint32_t rp = (bounce + b.ray_par) & 1u;
-        const float4 o4 = b.ray_o[rp][qi], d4 = b.ray_d[rp][qi];
-        const TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
-        float tbest = o4.w, bu = 0.f, bv = 0.f;
-        uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
-        traverse_closest(s, stk, r, tbest, prim, bu, bv, nv, tv);
-        const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
-        ShadeIO io;
-        io.emit = false;
-        io.em_hi = false;
-        io.query = false;
-        cont = shade_path<INT>(s, sv, b, p, bounce, path, qi, h, io);
-        if (io.emit) {
-          const float4 so = io.rec.o, sd = io.rec.d;
-          const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
-          apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
-        }
-        if (cont) {
-          b.ray_o[rp ^ 1u][qi] = io.nro;
-          b.ray_d[rp ^ 1u][qi] = io.nrd;
-          b.thr[rp ^ 1u][qi] = io.nthr;
-          b.prev[rp ^ 1u][qi] = io.nprev;
-          b.L[rp ^ 1u][qi] = io.nL;
-          b.misc[rp ^ 1u][qi] = io.nmisc;
-        } else {
-          b.L[kFinal][path] = io.nL;
-          if (!p.drop_end_misc) b.misc[kFinal][path] = io.nmisc;
+    // ---- refill: the idle lanes of the wave claim consecutive queue positions
+    if (!drained) {
+      const uint64_t idle = __ballot(!has);
+      const uint32_t n_idle = (uint32_t)__popcll(idle);
+      if (n_idle >= MTX_MEGA_REFILL || idle == ~0ull) {
+        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&b.counters[2], n_idle);
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (base + n_idle >= count) drained = true;
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        if (!has && base + rk < count) {
+          has = true;
+          qi = base + rk;
+          path = p.ident0 ? qi : b.queue[0][qi];
+          bounce = 0;
         }
       }
-      if (cont) {  // still queued after the last bounce: k_flush_tail's move
-        const uint32_t rp = (iters + b.ray_par) & 1u;
-        float4 L = b.L[rp][qi];
-        const uint4 m = b.misc[rp][qi];
-        if (INT == MTX_INT_PATH_MIS) L.w = end_w(m.w >> 16, L.w);
+    }
+    if (__ballot(has) == 0) break;
+    if (has) {
+      // ---- one bounce of the lane's path
+      const uint32_t rp = (bounce + b.ray_par) & 1u;
+      const float4 o4 = b.ray_o[rp][qi], d4 = b.ray_d[rp][qi];
+      const TraceRay r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+      float tbest = o4.w, bu = 0.f, bv = 0.f;
+      uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
+      traverse_closest(s, stk, r, tbest, prim, bu, bv, nv, tv);
+      const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
+      ShadeIO io;
+      io.emit = false;
+      io.em_hi = false;
+      io.query = false;
+      const bool cont = shade_path<INT>(s, sv, b, p, bounce, path, qi, h, io);
+      if (io.emit) {
+        const float4 so = io.rec.o, sd = io.rec.d;
+        const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
+        apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+      }
+      ++bounce;
+      if (cont && bounce < iters) {
+        b.ray_o[rp ^ 1u][qi] = io.nro;
+        b.ray_d[rp ^ 1u][qi] = io.nrd;
+        b.thr[rp ^ 1u][qi] = io.nthr;
+        b.prev[rp ^ 1u][qi] = io.nprev;
+        b.L[rp ^ 1u][qi] = io.nL;
+        b.misc[rp ^ 1u][qi] = io.nmisc;
+      } else {
+        // ended, or still queued after the last bounce (k_flush_tail's move:
+        // a path-mis path's final L.w holds valid_ray)
+        float4 L = io.nL;
+        if (cont && INT == MTX_INT_PATH_MIS) L.w = end_w(io.nmisc.w >> 16, L.w);
         b.L[kFinal][path] = L;
-        b.misc[kFinal][path] = m;
+        if (!p.drop_end_misc || cont) b.misc[kFinal][path] = io.nmisc;
+        has = false;
       }
     }
   }
