@@ -166,9 +166,15 @@ struct mtx_ctx {
   // resident lanes of the megakernel's grid)
   uint32_t mega_paths = 0xffffffffu;
   int mega_grid = 0;
+  // such a band's whole stage A (raygen .. collect) in one per-lane launch
+  // (kernels.hip k_rs_stage_a; MTX_RS_FUSED=0: raygen, trace, k_rs_begin, the
+  // megakernel and k_rs_collect as separate launches)
+  uint32_t rs_fused = 1;
   // NRC cache query order: MTX_CACHE_SORT=1 Morton-sorted (host sync; measured slower), 2 grouped
   // by region on the device with one eighth of the rows per XCD (field.hip)
   uint32_t cache_sort = MTX_CACHE_SORT;
+  // NRC cache encoder: level-major lanes (field.hip k_field_encode_lm; MTX_ENCODE_LM=0: query-major)
+  uint32_t encode_lm = MTX_ENCODE_LM;
   DevBuf cq_keys, cq_perm, cq_ws;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -230,7 +236,9 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_CLOSEST_CW")) c->closest_cw = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_OCC_UREFILL")) c->occ_urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
+  if (const char *e = getenv("MTX_RS_FUSED")) c->rs_fused = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)strtoul(e, nullptr, 0);
+  if (const char *e = getenv("MTX_ENCODE_LM")) c->encode_lm = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = (uint32_t)std::max(0, std::min(2, atoi(e)));
   *out = c;
   return MTX_OK;
@@ -867,7 +875,7 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
     // region-grouped rows, the blocks of each XCD on one eighth of them
     // (field.hip k_field_encode xcd_split): device-only, no host round trip
     DevBuf &pb = perm_buf ? *perm_buf : c->cq_perm, &cb = cursor_buf ? *cursor_buf : c->cq_keys;
-    if (!dalloc(pb, 4ull * cap) && !dalloc(cb, 4ull * 512)) {
+    if (!dalloc(pb, 4ull * cap) && !dalloc(cb, 4ull * 32768)) {
       mtxd::field_bucket_queries(c->field, b.cq_p, b.cq_count, cap, (uint32_t *)cb.p, (uint32_t *)pb.p, c->n_cu, st);
       perm = (const uint32_t *)pb.p;
       xcd_split = 1;
@@ -888,7 +896,8 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
         perm = (const uint32_t *)c->cq_perm.p;
     }
   }
-  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split);
+  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split,
+                     (int)c->encode_lm);
   tm.end(4, e, st);
   e = tm.begin(5, st);
   mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden, (float *)f_out.p,
@@ -1165,11 +1174,24 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // after the host has queued all of the first half's launches.
     const int halves = two ? 2 : 1;
     hipStream_t sh[2] = {st, c->w2.stream};
+    if (mega_all && c->rs_fused) {
+      // the whole stage A up to k_rs_collect in one per-lane launch
+      // (kernels.hip k_rs_stage_a), then the temporal pass
+      HIP_TRY(reset_counters(b, depth, st));
+      e = tm.begin(0, st);
+      mtxd::launch_rs_stage_a(c->scene, b, p, r,
+                              std::max(1, std::min<int>(c->mega_grid, (nb + mtxd::kShadeBlock - 1) / mtxd::kShadeBlock)),
+                              st);
+      tm.end(0, e, st);
+      ++*n_trace;
+      mtxd::launch_restir_temporal(r, p, st);
+    }
+    const bool fused = mega_all && c->rs_fused;
     const mtxd::DevScene *sc[2] = {&c->scene, &s2};
     mtxd::WaveBuffers bh[2], b1[2];
     mtxd::ChunkParams ph[2];
     mtxd::RestirBuffers rh[2];
-    for (int h = 0; h < halves; ++h) {
+    for (int h = 0; h < (fused ? 0 : halves); ++h) {
       const uint32_t ya = h ? ym : a->y0, yb = h ? a->y1 : ym;
       bh[h] = h ? bw2 : b;
       bh[h].rs_xs = b.rs_xs + (size_t)(ya - a->y0) * W * spp;  // path-indexed within the half
@@ -1197,7 +1219,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     // band runs all its bounces in the path megakernel (no counters: STATS
     // renders keep the wavefront kernels)
     bool mega[2] = {false, false};
-    for (int h = 0; h < halves; ++h) {
+    for (int h = 0; h < (fused ? 0 : halves); ++h) {
       mega[h] = mega_all;
       if (!mega[h]) continue;
       e = tm.begin(0, sh[h]);
@@ -1208,11 +1230,11 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
       tm.end(0, e, sh[h]);
       ++*n_trace;
     }
-    const uint32_t iters = bounce_iters(p);
+    const uint32_t iters = fused ? 0u : bounce_iters(p);
     for (uint32_t bounce = 0; bounce < iters; ++bounce)
       for (int h = 0; h < halves; ++h)
         if (!mega[h]) launch_bounce(c, b1[h], ph[h], tm, n_trace, n_shadow, *sc[h], sh[h], bounce);
-    for (int h = 0; h < halves; ++h) {
+    for (int h = 0; h < (fused ? 0 : halves); ++h) {
       if (!mega[h]) finish_bounces(b1[h], ph[h], sh[h]);
       mtxd::launch_restir_collect(bh[h], ph[h], rh[h], sh[h]);
       mtxd::launch_restir_temporal(rh[h], ph[h], sh[h]);

@@ -85,6 +85,58 @@ __global__ __launch_bounds__(kEncodeBlock) void k_field_encode(FieldEncoding e, 
   }
 }
 
+// Level-major encoder (round 5): a block takes 64 queries; 64 threads first
+// compute each query's p_norm (once, not once per level) and its direct
+// features (p_norm, wi, SH, padding), then the block's 256 threads walk the
+// 64 x n_levels (query, level) items with the query fastest, so the 64 lanes
+// of a wave gather from ONE level's table at 64 queries: with the rows
+// grouped by region (MTX_CACHE_SORT=2) the coarse levels' corners of nearby
+// queries share lines (the TA prices a gather by the distinct lines it
+// touches), where the query-major mapping above spreads a wave over 16
+// tables. Same arithmetic per feature: the same rows.
+constexpr uint32_t kEncQ = 64;
+__global__ __launch_bounds__(256) void k_field_encode_lm(FieldEncoding e, const float4 *qp, const float4 *qd,
+                                                         const uint32_t *count, uint32_t n_max, uint16_t *feat,
+                                                         const uint32_t *perm, int xcd_split) {
+  __shared__ uint4 rows[kEncQ * kFieldPad / 8];
+  __shared__ float4 pn_s[kEncQ];
+  uint16_t *row_h = reinterpret_cast<uint16_t *>(rows);
+  const uint32_t n = count ? min(*count, n_max) : n_max;
+  const uint32_t L = e.n_levels, F = e.n_features;
+  uint32_t lo = 0, hi = n, first = blockIdx.x, stride = gridDim.x;
+  if (xcd_split) {
+    const uint32_t g = blockIdx.x & 7u;
+    lo = (uint32_t)(((uint64_t)n * g) >> 3);
+    hi = (uint32_t)(((uint64_t)n * (g + 1)) >> 3);
+    first = blockIdx.x >> 3;
+    stride = gridDim.x >> 3;
+  }
+  for (uint32_t q0 = lo + first * kEncQ; q0 < hi; q0 += stride * kEncQ) {
+    const uint32_t nq = min(kEncQ, hi - q0);
+    if (threadIdx.x < nq) {
+      const uint32_t qs = perm ? perm[q0 + threadIdx.x] : q0 + threadIdx.x;
+      const float4 p = qp[qs], d = qd[qs];
+      const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
+      pn_s[threadIdx.x] = make_float4(pn.x, pn.y, pn.z, 0.f);
+      field_features_direct(e, pn, V3{d.x, d.y, d.z}, row_h + (size_t)kFieldPad * threadIdx.x, kFieldPad);
+    }
+    __syncthreads();
+    const uint32_t items = kEncQ * L;
+#pragma unroll 4
+    for (uint32_t it = threadIdx.x; it < items; it += 256) {
+      const uint32_t q = it & (kEncQ - 1u), l = it / kEncQ;
+      if (q < nq) {
+        const float4 pn = pn_s[q];
+        field_hashgrid_level(e, V3{pn.x, pn.y, pn.z}, l, row_h + (size_t)kFieldPad * q + 3 + F * l);
+      }
+    }
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < nq * (kFieldPad / 8); c += 256)
+      reinterpret_cast<uint4 *>(feat + (size_t)kFieldPad * q0)[c] = rows[c];
+    __syncthreads();
+  }
+}
+
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 
 // Accumulator -> next layer's B operand: round to fp16, then LeakyReLU in
@@ -257,16 +309,21 @@ void field_morton_keys(const FieldEncoding &e, const float4 *qp, uint32_t n, uin
 // regions); rows are grouped by bucket (order inside a bucket arbitrary: a
 // row's features and MLP column depend on its query only, and each path has
 // at most one query, so the film is unchanged).
-constexpr uint32_t kCacheBuckets = 512;
+#ifndef MTX_CACHE_AXIS_BITS
+#define MTX_CACHE_AXIS_BITS 3  // Morton bits per axis of the cache-query regions (3: 512 regions)
+#endif
+constexpr uint32_t kCacheAxisBits = MTX_CACHE_AXIS_BITS;
+constexpr uint32_t kCacheBuckets = 1u << (3 * kCacheAxisBits);
 constexpr uint32_t kBucketTile = 4096;  // queries per block of the scatter
 
 __device__ __forceinline__ uint32_t cache_bucket(const FieldEncoding &e, float4 p) {
   const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
-  auto c = [](float v) { return (uint32_t)fminf(fmaxf(v * 8.f, 0.f), 7.f); };
+  constexpr float kCells = (float)(1u << kCacheAxisBits);
+  auto c = [](float v) { return (uint32_t)fminf(fmaxf(v * kCells, 0.f), kCells - 1.f); };
   const uint32_t x = c(pn.x), y = c(pn.y), z = c(pn.z);
   uint32_t m = 0;
 #pragma unroll
-  for (int b = 0; b < 3; ++b) m |= (((x >> b) & 1u) << (3 * b)) | (((y >> b) & 1u) << (3 * b + 1)) | (((z >> b) & 1u) << (3 * b + 2));
+  for (int b = 0; b < (int)kCacheAxisBits; ++b) m |= (((x >> b) & 1u) << (3 * b)) | (((y >> b) & 1u) << (3 * b + 1)) | (((z >> b) & 1u) << (3 * b + 2));
   return m;
 }
 
@@ -283,20 +340,34 @@ __global__ __launch_bounds__(256) void k_cache_bucket_count(FieldEncoding e, con
     if (h[i]) atomicAdd(&cursor[i], h[i]);
 }
 
-// counts -> exclusive offsets, in place (one block of 512 threads)
-__global__ __launch_bounds__(kCacheBuckets) void k_cache_bucket_scan(uint32_t *cursor) {
-  __shared__ uint32_t v[kCacheBuckets];
+// counts -> exclusive offsets, in place (one block of 512 threads, each
+// owning kCacheBuckets / 512 consecutive counts)
+constexpr uint32_t kScanPer = kCacheBuckets >= 512 ? kCacheBuckets / 512 : 1;
+__global__ __launch_bounds__(512) void k_cache_bucket_scan(uint32_t *cursor) {
+  __shared__ uint32_t v[512];
   const uint32_t i = threadIdx.x;
-  const uint32_t x = cursor[i];
-  v[i] = x;
+  uint32_t x[kScanPer], sum = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    const uint32_t j = i * kScanPer + k;
+    x[k] = j < kCacheBuckets ? cursor[j] : 0u;
+    sum += x[k];
+  }
+  v[i] = sum;
   __syncthreads();
-  for (uint32_t off = 1; off < kCacheBuckets; off <<= 1) {
+  for (uint32_t off = 1; off < 512; off <<= 1) {
     const uint32_t y = i >= off ? v[i - off] : 0u;
     __syncthreads();
     v[i] += y;
     __syncthreads();
   }
-  cursor[i] = v[i] - x;
+  uint32_t run = v[i] - sum;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanPer; ++k) {
+    const uint32_t j = i * kScanPer + k;
+    if (j < kCacheBuckets) cursor[j] = run;
+    run += x[k];
+  }
 }
 
 // perm[row] = query: per block tile, LDS counts, one reservation per
@@ -333,15 +404,22 @@ void field_bucket_queries(const FieldEncoding &e, const float4 *qp, const uint32
   hipMemsetAsync(cursor, 0, 4 * kCacheBuckets, st);
   const unsigned g1 = (unsigned)std::min<uint64_t>((n_max + 255) / 256, (uint64_t)n_cu * 4);
   hipLaunchKernelGGL(k_cache_bucket_count, dim3(std::max(1u, g1)), dim3(256), 0, st, e, qp, count, n_max, cursor);
-  hipLaunchKernelGGL(k_cache_bucket_scan, dim3(1), dim3(kCacheBuckets), 0, st, cursor);
+  hipLaunchKernelGGL(k_cache_bucket_scan, dim3(1), dim3(512), 0, st, cursor);
   const unsigned g2 = (unsigned)std::min<uint64_t>((n_max + kBucketTile - 1) / kBucketTile, (uint64_t)n_cu * 4);
   hipLaunchKernelGGL(k_cache_bucket_scatter, dim3(std::max(1u, g2)), dim3(256), 0, st, e, qp, count, n_max, cursor,
                      perm);
 }
 
 int field_encode(const FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count, uint32_t n_max,
-                 uint16_t *feat, hipStream_t st, const uint32_t *perm, int xcd_split) {
+                 uint16_t *feat, hipStream_t st, const uint32_t *perm, int xcd_split, int level_major) {
   if (n_max == 0) return MTX_OK;
+  if (level_major && e.n_levels >= 1 && e.n_levels <= kFieldMaxLevels) {
+    unsigned blocks = (unsigned)std::min<uint64_t>((n_max + kEncQ - 1) / kEncQ, 256ull * 32);
+    if (xcd_split) blocks = (blocks + 7u) & ~7u;
+    hipLaunchKernelGGL(k_field_encode_lm, dim3(blocks), dim3(256), 0, st, e, qp, qd, count, n_max, feat, perm,
+                       xcd_split);
+    return MTX_OK;
+  }
   if (e.n_levels == 0 || e.n_levels > kEncodeBlock) {
     mtx_set_error("field_encode: unsupported n_levels %u", e.n_levels);
     return MTX_E_ARG;

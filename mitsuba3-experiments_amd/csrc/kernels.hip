@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "restir_dev.h"
 
 using namespace mtx;
 
@@ -1115,6 +1116,161 @@ __global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_path_mega(
       }
     }
   }
+}
+
+// ReSTIR GI stage A of a short band in ONE launch (round 5): a lane takes a
+// pixel sample t of the band and runs restirgi.py's sample_initial for it --
+// the camera ray (k_raygen_camera), the primary closest hit, k_rs_begin's
+// emittance and BSDF / hemisphere sample (:419-448), then the secondary
+// path's bounces (the path megakernel's body, :459-588) and k_rs_collect's
+// L_o / sampler store -- with its path state at its own position t, then
+// takes the next sample (lanes refill as in k_path_mega). The same per-lane
+// operations as the five launches it replaces (hits do not depend on the
+// traversal order), so the same reservoirs and films; k_rs_temporal follows
+// as its own launch (it reads other pixels' samples).
+__global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_rs_stage_a(DevScene s, WaveBuffers b,
+                                                                                  ChunkParams p, RestirBuffers r) {
+  extern __shared__ int4 mega_lds[];
+  const SceneView sv = make_view(s);
+  const uint32_t count = r.nb;
+  const uint32_t iters = p.max_depth > 1u ? p.max_depth : 1u;
+  int32_t *stk = reinterpret_cast<int32_t *>(mega_lds) + threadIdx.x;
+  uint32_t *ostk = reinterpret_cast<uint32_t *>(mega_lds) + threadIdx.x;
+  // b.ray_par == 1 (launch_rs_stage_a): the secondary loop's bounce-0 rays are parity 1
+  const uint32_t lane = threadIdx.x & 63u;
+  const size_t n = r.n;
+  bool has = false, drained = false, started = false;
+  uint32_t t = 0, bounce = 0;
+  while (true) {
+    if (!drained) {
+      const uint64_t idle = __ballot(!has);
+      const uint32_t n_idle = (uint32_t)__popcll(idle);
+      if (n_idle >= MTX_MEGA_REFILL || idle == ~0ull) {
+        const uint32_t leader = (uint32_t)(__ffsll((unsigned long long)idle) - 1);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&b.counters[2], n_idle);
+        base = __builtin_amdgcn_readlane(base, leader);
+        if (base + n_idle >= count) drained = true;
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+        if (!has && base + rk < count) {
+          has = true;
+          started = false;
+          t = base + rk;
+        }
+      }
+    }
+    if (__ballot(has) == 0) break;
+    if (has) {
+      const uint32_t i = r.lane0 + t;
+      float4 o4, d4;
+      Pcg32 rng;
+      if (!started) {
+        // the camera ray of sample t (k_raygen_camera; init_path's sampler state)
+        const uint32_t px_local = t / p.spp, smp = t - px_local * p.spp;
+        const uint32_t pix = p.px0 + px_local;
+        const uint32_t y = pix / p.width, x = pix - y * p.width;
+        rng = sampler_lane(p.seed, pix * p.spp_total + p.sample_offset + smp);
+        const V2 u = rng.next_2d();  // film jitter (path.py:45)
+        const Ray ray = camera_ray(s.camera, V2{((float)x + u.x) / (float)p.width, ((float)y + u.y) / (float)p.height});
+        o4 = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);
+        d4 = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
+      } else {
+        const uint32_t rp = (bounce + 1u) & 1u;
+        o4 = b.ray_o[rp][t];
+        d4 = b.ray_d[rp][t];
+      }
+      const TraceRay tr = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
+      float tbest = o4.w, bu = 0.f, bv = 0.f;
+      uint32_t prim = 0xffffffffu, nv = 0, tv = 0;
+      traverse_closest(s, stk, tr, tbest, prim, bu, bv, nv, tv);
+      const float4 h = make_float4(prim == 0xffffffffu ? kInf : tbest, __uint_as_float(prim), bu, bv);
+      float4 Lf;
+      uint4 mf;
+      bool done = false;
+      if (!started) {
+        // k_rs_begin (:419-448)
+        r.prim_hit[i] = h;
+        r.prim_dir[i] = d4;
+        const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, V3{d4.x, d4.y, d4.z});
+        r.emit[i] = f4(emitter_eval(sv, si.emitter, si.wi), 0.f);
+        V3 wo;
+        float pdf;
+        if (r.flags & MTX_RESTIR_BSDF_SAMPLING) {
+          const float s1 = rng.next_1d();
+          const V2 s2 = rng.next_2d();
+          BSDFSample bs;
+          bs.wo = v3s(0.f);
+          bs.pdf = 0.f;
+          if (si.valid) bsdf_sample(sv.bsdf, sv.materials[si.material], si.uv, si.wi, s1, s2, &bs);
+          wo = bs.wo;
+          pdf = bs.pdf;
+        } else {
+          wo = square_to_uniform_hemisphere(rng.next_2d());
+          pdf = square_to_uniform_hemisphere_pdf(wo);
+        }
+        r.cur[i] = si.valid ? f4(si.p, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r.cur[n + i] = si.valid ? f4(si.n, pdf) : make_float4(0.f, 0.f, 0.f, pdf);
+        if (si.valid) {
+          const Ray nr = spawn_ray(si.p, si.n, to_world(si.sh, wo));
+          b.ray_o[1][t] = make_float4(nr.o.x, nr.o.y, nr.o.z, nr.maxt);
+          b.ray_d[1][t] = make_float4(nr.d.x, nr.d.y, nr.d.z, 0.f);
+          b.misc[1][t] = st_rng(rng, PF_PREV_DELTA << 16);  // depth 0, prev_bsdf_delta
+          started = true;
+          bounce = 0;
+        } else {
+          rng.advance(6);
+          Lf = make_float4(0.f, 0.f, 0.f, 1.f);
+          mf = st_rng(rng, 0u);
+          b.rs_xs[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+          b.rs_ns[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+          done = true;
+        }
+      } else {
+        // one bounce of the secondary path (k_path_mega's body)
+        const uint32_t rp = (bounce + 1u) & 1u;
+        ShadeIO io;
+        io.emit = false;
+        io.em_hi = false;
+        io.query = false;
+        const bool cont = shade_path<MTX_INT_PATH_MIS>(s, sv, b, p, bounce, t, t, h, io);
+        if (io.emit) {
+          const float4 so = io.rec.o, sd = io.rec.d;
+          const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
+          apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+        }
+        ++bounce;
+        if (cont && bounce < iters) {
+          b.ray_o[rp ^ 1u][t] = io.nro;
+          b.ray_d[rp ^ 1u][t] = io.nrd;
+          b.thr[rp ^ 1u][t] = io.nthr;
+          b.prev[rp ^ 1u][t] = io.nprev;
+          b.L[rp ^ 1u][t] = io.nL;
+          b.misc[rp ^ 1u][t] = io.nmisc;
+        } else {
+          Lf = io.nL;
+          if (cont) Lf.w = end_w(io.nmisc.w >> 16, Lf.w);
+          mf = io.nmisc;
+          done = true;
+        }
+      }
+      if (done) {
+        // k_rs_collect: L_o = select(valid_ray, result, 0) (:588), x_s / n_s of
+        // the first secondary hit (written by the bounce-0 shade), sampler state
+        const bool valid_ray = ((mf.w >> 16) & PF_VALID_RAY) != 0;
+        r.cur[2 * n + i] = b.rs_xs[t];
+        r.cur[3 * n + i] = b.rs_ns[t];
+        r.cur[4 * n + i] = valid_ray ? make_float4(Lf.x, Lf.y, Lf.z, 0.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r.rng[i] = mf;
+        has = false;
+      }
+    }
+  }
+}
+void launch_rs_stage_a(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
+                       int grid, hipStream_t st) {
+  WaveBuffers b1 = b;
+  b1.ray_par = 1;
+  hipLaunchKernelGGL(k_rs_stage_a, dim3(grid), dim3(kShadeBlock), stack_bytes(s), st, s, b1, p, r);
 }
 
 // L += T * Field(query) for the NRC cache queries of a chunk (nrc.py L is a

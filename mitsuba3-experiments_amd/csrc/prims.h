@@ -42,9 +42,10 @@ void field_prepack(const uint16_t *weights, uint32_t n_in, uint32_t n_hidden, ui
 // perm (optional): row i encodes query perm[i]; xcd_split: the blocks of one
 // XCD take one contiguous eighth of the rows (rows grouped by region)
 int field_encode(const mtx::FieldEncoding &e, const float4 *qp, const float4 *qd, const uint32_t *count,
-                 uint32_t n_max, uint16_t *feat, hipStream_t st, const uint32_t *perm = nullptr, int xcd_split = 0);
+                 uint32_t n_max, uint16_t *feat, hipStream_t st, const uint32_t *perm = nullptr, int xcd_split = 0,
+                 int level_major = 0);
 // Groups the cache queries by region (512 Morton cells of the field's box)
-// on the device: perm[row] = query; cursor: 512-word workspace. No host sync.
+// on the device: perm[row] = query; cursor: a 32768-word workspace. No host sync.
 void field_bucket_queries(const mtx::FieldEncoding &e, const float4 *qp, const uint32_t *count, uint32_t n_max,
                           uint32_t *cursor, uint32_t *perm, int n_cu, hipStream_t st);
 // 24-bit Morton codes (8 bits per axis of the field's bounding box) of n queries

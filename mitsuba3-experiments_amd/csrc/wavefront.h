@@ -57,7 +57,10 @@ constexpr uint32_t kOccLdsStack = 8;
 #define MTX_CLOSEST_CW 0  // closest hit on the 8-wide tree (device_common.h trace_loop_closest_cw)
 #endif
 #ifndef MTX_CACHE_SORT
-#define MTX_CACHE_SORT 0  // NRC cache query order (api.cpp run_cache): 0 as appended, 1 Morton sort, 2 region x XCD
+#define MTX_CACHE_SORT 2  // NRC cache query order (api.cpp run_cache): 0 as appended, 1 Morton sort, 2 region x XCD
+#endif
+#ifndef MTX_ENCODE_LM
+#define MTX_ENCODE_LM 1  // NRC cache encoder with level-major lanes (field.hip k_field_encode_lm)
 #endif
 #ifndef MTX_STREAMS
 #define MTX_STREAMS 2  // mtx_render: chunks alternate between two wavefronts on two streams (1 = one)
@@ -227,6 +230,9 @@ int shade_blocks_per_cu();
 int mega_blocks_per_cu(const DevScene &s);
 // all bounces of a short path-mis / path wavefront in one kernel (k_path_mega)
 void launch_path_mega(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, int grid, hipStream_t st);
+// ReSTIR GI stage A of a short band (raygen .. collect) in one per-lane launch (kernels.hip)
+void launch_rs_stage_a(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const RestirBuffers &r,
+                       int grid, hipStream_t st);
 int shade_stamps(unsigned long long *out);  // diagnostic builds (MTX_DIAG_STAMPS)
 void launch_raygen_camera(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, const float *rays,
