@@ -175,6 +175,8 @@ struct mtx_ctx {
   uint32_t cache_sort = MTX_CACHE_SORT;
   // NRC cache encoder: level-major lanes (field.hip k_field_encode_lm; MTX_ENCODE_LM=0: query-major)
   uint32_t encode_lm = MTX_ENCODE_LM;
+  // NRC cache: encode + MLP + apply in one launch (field.hip k_field_cache_fused; MTX_CACHE_FUSED=0: three)
+  uint32_t cache_fused = 1;
   DevBuf cq_keys, cq_perm, cq_ws;
   std::vector<hipEvent_t> events;
   hipEvent_t prim_ev[2] = {nullptr, nullptr};
@@ -238,6 +240,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_RS_FUSED")) c->rs_fused = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_MEGA_PATHS")) c->mega_paths = (uint32_t)strtoul(e, nullptr, 0);
+  if (const char *e = getenv("MTX_CACHE_FUSED")) c->cache_fused = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_ENCODE_LM")) c->encode_lm = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_CACHE_SORT")) c->cache_sort = (uint32_t)std::max(0, std::min(2, atoi(e)));
   *out = c;
@@ -896,17 +899,25 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
         perm = (const uint32_t *)c->cq_perm.p;
     }
   }
-  mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split,
-                     (int)c->encode_lm);
-  tm.end(4, e, st);
-  e = tm.begin(5, st);
-  mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden, (float *)f_out.p,
-                  c->n_cu, st);
-  tm.end(5, e, st);
-  if (nerad_render)
-    mtxd::launch_nerad_apply(b, (const float *)f_out.p, cap, 1, st);
-  else
-    mtxd::launch_cache_apply(b, (const float *)f_out.p, cap, st, perm);
+  if (c->cache_fused && !nerad_render) {
+    // encode + MLP + L += T * out in one launch (field.hip k_field_cache_fused),
+    // timed as the encode
+    mtxd::field_cache_fused(c->field, b.cq_p, b.cq_d, b.cq_t, b.cq_count, cap, perm, xcd_split, c->field_frag.p,
+                            c->field_hidden, b.L[mtxd::kFinal], c->n_cu, st);
+    tm.end(4, e, st);
+  } else {
+    mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split,
+                       (int)c->encode_lm);
+    tm.end(4, e, st);
+    e = tm.begin(5, st);
+    mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
+                    (float *)f_out.p, c->n_cu, st);
+    tm.end(5, e, st);
+    if (nerad_render)
+      mtxd::launch_nerad_apply(b, (const float *)f_out.p, cap, 1, st);
+    else
+      mtxd::launch_cache_apply(b, (const float *)f_out.p, cap, st, perm);
+  }
   if (tm.on) {  // counted after the render's final synchronisation (fill_stats): no per-chunk sync
     if (!c->q_pinned && hipHostMalloc((void **)&c->q_pinned, 4 * kQSlots) != hipSuccess) c->q_pinned = nullptr;
     if (c->q_pinned && tm.q_used < kQSlots) {

@@ -259,6 +259,133 @@ __global__ __launch_bounds__(256) void k_field_mlp(const uint16_t *feat, const u
   }
 }
 
+// ---- the NRC cache pass fused: encode + MLP + apply (round 5) -----------
+// One block of 512 threads (8 waves) takes 256 cache queries at a time:
+// their feature rows are assembled in LDS (level-major lanes as in
+// k_field_encode_lm), each wave runs the fused MLP of k_field_mlp on 32 of
+// them (one 32-query N-tile) straight from LDS, and the lanes holding the
+// outputs add T * out to the path's L (k_cache_apply). The 128 B of features
+// and 12 B of outputs per query no longer go through HBM, and two launches
+// go. Every query's features, MLP column and L update are those of the
+// three-kernel path (MFMA output columns do not depend on their tile), so
+// the films are the same bits.
+constexpr uint32_t kFusedQ = 256;
+__global__ __launch_bounds__(512) void k_field_cache_fused(FieldEncoding e, const float4 *qp, const float4 *qd,
+                                                           const float4 *qt, const uint32_t *count, uint32_t n_max,
+                                                           const uint32_t *perm, int xcd_split, const half8 *wfrag,
+                                                           uint32_t n_frag, uint32_t n_hidden, float4 *L_final) {
+  extern __shared__ half8 fused_lds[];
+  half8 *w = fused_lds;                                                // n_frag x 64 fragments
+  uint16_t *row_h = reinterpret_cast<uint16_t *>(w + n_frag * 64);     // kFusedQ rows of 64 halfs
+  float4 *pn_s = reinterpret_cast<float4 *>(row_h + kFusedQ * kFieldPad);
+  for (uint32_t i = threadIdx.x; i < n_frag * 64; i += blockDim.x) w[i] = wfrag[i];
+  const uint32_t n = count ? min(*count, n_max) : n_max;
+  const uint32_t L = e.n_levels, F = e.n_features;
+  uint32_t lo = 0, hi = n, first = blockIdx.x, stride = gridDim.x;
+  if (xcd_split) {
+    const uint32_t g = blockIdx.x & 7u;
+    lo = (uint32_t)(((uint64_t)n * g) >> 3);
+    hi = (uint32_t)(((uint64_t)n * (g + 1)) >> 3);
+    first = blockIdx.x >> 3;
+    stride = gridDim.x >> 3;
+  }
+  const uint32_t lane = threadIdx.x & 63u, h = lane >> 5, col = lane & 31u, wave = threadIdx.x >> 6;
+  __syncthreads();
+  for (uint32_t q0 = lo + first * kFusedQ; q0 < hi; q0 += stride * kFusedQ) {
+    const uint32_t nq = min(kFusedQ, hi - q0);
+    // ---- encode: direct features per query, then the (query, level) items
+    if (threadIdx.x < kFusedQ) {
+      uint16_t *row = row_h + (size_t)kFieldPad * threadIdx.x;
+      if (threadIdx.x < nq) {
+        const uint32_t qs = perm ? perm[q0 + threadIdx.x] : q0 + threadIdx.x;
+        const float4 p = qp[qs], d = qd[qs];
+        const V3 pn = field_pnorm(e, V3{p.x, p.y, p.z});
+        pn_s[threadIdx.x] = make_float4(pn.x, pn.y, pn.z, 0.f);
+        field_features_direct(e, pn, V3{d.x, d.y, d.z}, row, kFieldPad);
+      } else {
+        for (uint32_t k = 0; k < kFieldPad; ++k) row[k] = 0;  // rows past n: zero MLP inputs
+      }
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t it = threadIdx.x; it < kFusedQ * L; it += 512) {
+      const uint32_t q = it & (kFusedQ - 1u), l = it / kFusedQ;
+      if (q < nq) {
+        const float4 pn = pn_s[q];
+        field_hashgrid_level(e, V3{pn.x, pn.y, pn.z}, l, row_h + (size_t)kFieldPad * q + 3 + F * l);
+      }
+    }
+    __syncthreads();
+    // ---- MLP: wave w on rows [32w, 32w + 32) (k_field_mlp with one N-tile)
+    if (wave * 32 < nq) {
+      const uint16_t *rb = row_h + (size_t)kFieldPad * (wave * 32 + col);
+      half8 bin[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) bin[ks] = *reinterpret_cast<const half8 *>(rb + ks * 16 + h * 8);
+      f32x16 acc[2];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[(mt * 4 + ks) * 64 + lane], bin[ks],
+                                                           ks == 0 ? zero16() : acc[mt], 0, 0, 0);
+      uint32_t base = 8;
+      for (uint32_t layer = 0; layer < n_hidden; ++layer, base += 8) {
+        half8 bf[4];
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+          for (int sgl = 0; sgl < 2; ++sgl) bf[2 * mt + sgl] = leaky_pack(acc[mt], sgl);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[(base + mt * 4 + ks) * 64 + lane], bf[ks],
+                                                             ks == 0 ? zero16() : acc[mt], 0, 0, 0);
+      }
+      half8 bf[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int sgl = 0; sgl < 2; ++sgl) bf[2 * mt + sgl] = leaky_pack(acc[mt], sgl);
+      f32x16 o = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) o = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[(base + ks) * 64 + lane], bf[ks], o, 0, 0, 0);
+      // ---- apply (k_cache_apply): C/D rows 0..2 in registers 0..2 of h = 0
+      const uint32_t q = wave * 32 + col;
+      if (h == 0 && q < nq) {
+        const uint32_t qs = perm ? perm[q0 + q] : q0 + q;
+        const float4 t = qt[qs];
+        const uint32_t path = __float_as_uint(t.w);
+        float4 Lp = L_final[path];
+        Lp.x = Lp.x + t.x * (float)(_Float16)o[0];
+        Lp.y = Lp.y + t.y * (float)(_Float16)o[1];
+        Lp.z = Lp.z + t.z * (float)(_Float16)o[2];
+        L_final[path] = Lp;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int field_cache_fused(const FieldEncoding &e, const float4 *qp, const float4 *qd, const float4 *qt,
+                      const uint32_t *count, uint32_t n_max, const uint32_t *perm, int xcd_split, const void *wfrag,
+                      uint32_t n_hidden, float4 *L_final, int n_cu, hipStream_t st) {
+  if (n_max == 0) return MTX_OK;
+  if (e.n_levels == 0 || e.n_levels > kFieldMaxLevels) {
+    mtx_set_error("field_cache_fused: unsupported n_levels %u", e.n_levels);
+    return MTX_E_ARG;
+  }
+  const uint32_t n_frag = field_frag_count(n_hidden);
+  const size_t lds = (size_t)n_frag * 64 * sizeof(half8) + (size_t)kFusedQ * kFieldPad * 2 + kFusedQ * sizeof(float4);
+  unsigned blocks = (unsigned)std::max<uint64_t>(
+      1, std::min<uint64_t>((n_max + kFusedQ - 1) / kFusedQ, (uint64_t)n_cu * 2));
+  if (xcd_split) blocks = (blocks + 7u) & ~7u;
+  hipLaunchKernelGGL(k_field_cache_fused, dim3(blocks), dim3(512), lds, st, e, qp, qd, qt, count, n_max, perm,
+                     xcd_split, (const half8 *)wfrag, n_frag, n_hidden, L_final);
+  return MTX_OK;
+}
+
 uint32_t field_frag_count(uint32_t n_hidden) { return 8 * (1 + n_hidden) + 4; }
 
 // Host: weight matrices (fp16 bits, W[out][in] row-major per layer: input

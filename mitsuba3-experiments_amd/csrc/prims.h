@@ -50,6 +50,11 @@ void field_bucket_queries(const mtx::FieldEncoding &e, const float4 *qp, const u
                           uint32_t *cursor, uint32_t *perm, int n_cu, hipStream_t st);
 // 24-bit Morton codes (8 bits per axis of the field's bounding box) of n queries
 void field_morton_keys(const mtx::FieldEncoding &e, const float4 *qp, uint32_t n, uint32_t *keys, hipStream_t st);
+// The NRC cache pass in one launch: encode + MLP + L_final[path] += T * out
+// (qt: T.xyz, path bits in .w), rows in perm order.
+int field_cache_fused(const mtx::FieldEncoding &e, const float4 *qp, const float4 *qd, const float4 *qt,
+                      const uint32_t *count, uint32_t n_max, const uint32_t *perm, int xcd_split, const void *wfrag,
+                      uint32_t n_hidden, float4 *L_final, int n_cu, hipStream_t st);
 int field_mlp(const uint16_t *feat, const uint32_t *count, uint32_t n_max, const void *wfrag, uint32_t n_hidden,
               float *out, int n_cu, hipStream_t st);
 
