@@ -617,27 +617,8 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
       }
     }
   };
-  while (true) {
-    if (!res.exhausted) {
-      const uint64_t idle = __ballot(!has);
-      if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
-        uint32_t k;
-        bool ok;
-        res.take(s, idle, lane, k, ok);
-        if (!has && ok) {
-          src.load(k, r, tbest, payload);
-          prim = 0xffffffffu;
-          bu = bv = 0.f;
-          node = 0;
-          tri = tri_end = 0;
-          sp = 0;
-          has = true;
-        }
-      }
-    }
-    if (__ballot(has) == 0) break;
-    // ---- one inner-node visit
-    if (has && node >= 0) {
+  // one inner-node visit of a lane (LDS tree top or global memory)
+  auto visit_node = [&]() {
       if (STATS) count_wave_iter(lane, &wave_iters[0]);
       int32_t cr[4];
       ++nv;
@@ -675,7 +656,28 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
       } else {
         pop_next();
       }
+  };
+  while (true) {
+    if (!res.exhausted) {
+      const uint64_t idle = __ballot(!has);
+      if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
+        uint32_t k;
+        bool ok;
+        res.take(s, idle, lane, k, ok);
+        if (!has && ok) {
+          src.load(k, r, tbest, payload);
+          prim = 0xffffffffu;
+          bu = bv = 0.f;
+          node = 0;
+          tri = tri_end = 0;
+          sp = 0;
+          has = true;
+        }
+      }
     }
+    if (__ballot(has) == 0) break;
+    // ---- one inner-node visit
+    if (has && node >= 0) visit_node();
     // ---- one triangle test
     if (has && tri < tri_end) {
       if (STATS) count_wave_iter(lane, &wave_iters[1]);
@@ -718,6 +720,29 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
   float tmax = 0.f;
   uint32_t oct = 0, gbase = 0, ghits = 0, tbase = 0, thits = 0;
   int sp = 0;
+  // one node visit: the nearest remaining child of the lane's node group
+  auto visit_occ = [&]() {
+    if (STATS) count_wave_iter(lane, &wave_iters[0]);
+    const uint32_t p = (uint32_t)ctz32(ghits >> 24);
+    ghits &= ~(1u << (24 + p));
+    const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
+    if (ghits >> 24) {
+      const uint2 g = make_uint2(gbase, ghits);
+      if (sp < lds_n) {
+        stk[sp * kTraceBlock] = g;
+      } else {
+        ovf[(size_t)(sp - lds_n) * s.ovf_threads] = g;
+        asm volatile("" ::: "memory");  // keeps the two stores apart (no pointer select + flat store)
+      }
+      ++sp;
+    }
+    ++nv;
+    const CwVisit v = cw_visit(s, r, oct, node, tmax, top, top_n);
+    gbase = v.child_base;
+    ghits = (v.hits & 0xff000000u) | v.imask;
+    tbase = v.tri_base;
+    thits = v.hits & 0x00ffffffu;
+  };
   while (true) {
     if (!res.exhausted) {
       const uint64_t idle = __ballot(!has);
@@ -739,28 +764,7 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
     }
     if (__ballot(has) == 0) break;
     // ---- one node visit: the nearest remaining child of the node group
-    if (has && thits == 0 && (ghits >> 24) != 0) {
-      if (STATS) count_wave_iter(lane, &wave_iters[0]);
-      const uint32_t p = (uint32_t)ctz32(ghits >> 24);
-      ghits &= ~(1u << (24 + p));
-      const uint32_t node = cw_inner_child(gbase, ghits & 0xffu, oct, p);
-      if (ghits >> 24) {
-        const uint2 g = make_uint2(gbase, ghits);
-        if (sp < lds_n) {
-          stk[sp * kTraceBlock] = g;
-        } else {
-          ovf[(size_t)(sp - lds_n) * s.ovf_threads] = g;
-          asm volatile("" ::: "memory");  // keeps the two stores apart (no pointer select + flat store)
-        }
-        ++sp;
-      }
-      ++nv;
-      const CwVisit v = cw_visit(s, r, oct, node, tmax, top, top_n);
-      gbase = v.child_base;
-      ghits = (v.hits & 0xff000000u) | v.imask;
-      tbase = v.tri_base;
-      thits = v.hits & 0x00ffffffu;
-    }
+    if (has && thits == 0 && (ghits >> 24) != 0) visit_occ();
     // ---- one triangle test of the triangle group
     if (has && thits != 0) {
       if (STATS) count_wave_iter(lane, &wave_iters[1]);
