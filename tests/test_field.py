@@ -169,8 +169,10 @@ def test_nrc_cache_morton_order_unchanged(tmp_path):
     """MTX_CACHE_SORT=1 encodes the cache queries in Morton order (sorted with
     the hash-grid group-by; measured slower); 2 groups them by region on the
     device, one eighth of the rows per XCD (also on the second wavefront of a
-    two-stream render: chunk_paths); queue order otherwise. All films are
-    identical (each query's features and MLP column are its own)."""
+    two-stream render: chunk_paths); queue order otherwise; the encode, MLP
+    and apply fused into one launch (MTX_CACHE_FUSED) or not, the level-major
+    or the query-major encoder (MTX_ENCODE_LM). All films are identical (each
+    query's features and MLP column are its own)."""
     import os
     import subprocess
     import sys
@@ -187,10 +189,13 @@ kw = {"chunk_paths": int(sys.argv[3])} if int(sys.argv[3]) else {}
 np.save(sys.argv[2], integ.render_film(sc, seed=7, spp=4, **kw))
 '''
     films = []
-    for flag, chunk in (("1", 0), ("0", 0), ("2", 0), ("2", 5000), ("0", 5000)):
-        f = tmp_path / f"f{flag}_{chunk}.npy"
+    # (order, chunk paths, fused encode+MLP+apply, level-major encoder)
+    for flag, chunk, fused, lm in (("1", 0, "0", "0"), ("0", 0, "0", "0"), ("2", 0, "1", "1"), ("2", 5000, "1", "1"),
+                                   ("0", 5000, "1", "1"), ("2", 0, "0", "1"), ("0", 0, "1", "0")):
+        f = tmp_path / f"f{flag}_{chunk}_{fused}_{lm}.npy"
         subprocess.run([sys.executable, "-c", code, os.path.join(root, "mitsuba3-experiments_amd"), str(f), str(chunk)],
-                       check=True, env=dict(os.environ, MTX_CACHE_SORT=flag), timeout=300)
+                       check=True, env=dict(os.environ, MTX_CACHE_SORT=flag, MTX_CACHE_FUSED=fused, MTX_ENCODE_LM=lm),
+                       timeout=300)
         films.append(np.load(f))
     for f in films[1:]:
         np.testing.assert_array_equal(films[0], f)
