@@ -161,9 +161,10 @@ struct mtx_ctx {
   uint32_t xcd_claim = 1;
   // closest hit of the wavefront kernels on the 8-wide tree (MTX_CLOSEST_CW=1)
   uint32_t closest_cw = MTX_CLOSEST_CW;
-  // path megakernel for wavefronts of at most this many paths (ReSTIR
-  // stage A halves; MTX_MEGA_PATHS, 0 = off; default 0xffffffff = the
-  // resident lanes of the megakernel's grid)
+  // ReSTIR GI: a band of at most this many paths runs its stage A in the
+  // per-lane megakernel on one wavefront (MTX_MEGA_PATHS, 0 = off; default
+  // 0xffffffff = twice the resident lanes of the megakernel's grid,
+  // 2 x mega_grid x kShadeBlock)
   uint32_t mega_paths = 0xffffffffu;
   int mega_grid = 0;
   // such a band's whole stage A (raygen .. collect) in one per-lane launch
