@@ -19,7 +19,9 @@ from .integrators import (  # noqa: F401
     Simple,
     develop,
     load_dict,
+    mtx_scene_of,
     register_integrator,
+    register_with_mitsuba,
 )
 
 __version__ = "0.1.0"

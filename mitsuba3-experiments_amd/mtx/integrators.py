@@ -431,24 +431,87 @@ def _bind_scene(ctx, scene) -> None:
     ctx.scene = scene  # keep the host arrays alive while bound
 
 
+# mi.Scene objects loaded through the wrapped mi.load_dict / mi.load_file:
+# id -> [the mi.Scene (kept alive: the id stays unique), its source, the mtx
+# scene built from that source on first use]
+_MI_SCENES: dict = {}
+
+
+def mtx_scene_of(scene):
+    """The :class:`mtx.scene.Scene` a registered plugin renders for `scene`:
+    itself, or the scene built from the dictionary / XML file an ``mi.Scene``
+    was loaded from (mi.load_dict / mi.load_file wrapped by
+    :func:`register_with_mitsuba`). Raises MtxError for an ``mi.Scene`` of
+    unknown origin."""
+    from .scene import Scene
+
+    if isinstance(scene, Scene):
+        return scene
+    entry = _MI_SCENES.get(id(scene))
+    if entry is None or entry[0] is not scene:
+        raise MtxError("mtx renders mtx.scene.Scene objects, or an mi.Scene loaded by mi.load_dict / mi.load_file "
+                       "after mtx.register_with_mitsuba() (its source dictionary / XML is converted); this mi.Scene "
+                       "has no recorded source")
+    if entry[2] is None:
+        kind, src, base = entry[1]
+        if kind == "dict":
+            from .mitsuba_dict import scene_from_dict
+            entry[2] = scene_from_dict(src, base_dir=base)
+        else:
+            from .scene import Scene as _S
+            entry[2] = _S.from_xml(src)
+    return entry[2]
+
+
+def _wrap_loaders(mi) -> None:
+    """mi.load_dict / mi.load_file record each loaded scene's source (once)."""
+    import copy
+    import os
+
+    if getattr(mi, "_mtx_wrapped", False):
+        return
+    load_dict, load_file = getattr(mi, "load_dict", None), getattr(mi, "load_file", None)
+    if load_dict is not None:
+        def _load_dict(d, *args, **kwargs):
+            obj = load_dict(d, *args, **kwargs)
+            if isinstance(d, dict) and d.get("type") == "scene":
+                _MI_SCENES[id(obj)] = [obj, ("dict", copy.copy(d), os.getcwd()), None]
+            return obj
+
+        mi.load_dict = _load_dict
+    if load_file is not None:
+        def _load_file(path, *args, **kwargs):
+            obj = load_file(path, *args, **kwargs)
+            _MI_SCENES[id(obj)] = [obj, ("xml", os.path.abspath(str(path)), None), None]
+            return obj
+
+        mi.load_file = _load_file
+    mi._mtx_wrapped = True
+
+
 def register_with_mitsuba(mi=None) -> bool:
     """With Mitsuba importable (it is not in this image: returns False), register
     every façade name (path.py:305, path-mis.py:158, pssmltsimple.py:145,
     restirgi.py:591, ...) as an ``mi.SamplingIntegrator`` subclass.
 
-    What this does and does not provide: the registered plugin reads its
-    properties through ``props.get`` (path.py:22-25) and forwards ``render`` /
-    ``sample`` to the mtx integrator, which runs on an :class:`mtx.scene.Scene`
-    (the bedroom proxy, OBJ/XML ingestion of ``mtx.scene.from_xml``). There is
-    no converter from a loaded ``mi.Scene`` (its meshes, BSDF plugins and
-    emitters) to the mtx scene: handing one to the plugin raises MtxError
-    instead of rendering something else. `mi` may be passed explicitly (tests
-    use a stand-in module)."""
+    The registered plugin reads its properties through ``props.get``
+    (path.py:22-25) and forwards ``render`` / ``sample`` to the mtx
+    integrator. It renders an :class:`mtx.scene.Scene`, or an ``mi.Scene``
+    that the script loaded with ``mi.load_dict`` / ``mi.load_file`` after this
+    call: those loaders are wrapped to record the scene's source, and the
+    plugin converts it (:mod:`mtx.mitsuba_dict` for dictionaries such as
+    ``mi.cornell_box()``, path.py:308-309 / path-mis.py:162 /
+    restirgi.py:595-599 / nrc.py:130-136; :meth:`mtx.scene.Scene.from_xml` for
+    files), so the reference scripts run unchanged. An ``mi.Scene`` of unknown
+    origin (or one using plugins outside the supported subset) raises
+    MtxError instead of rendering something else. `mi` may be passed
+    explicitly (tests use a stand-in module)."""
     if mi is None:
         try:
             import mitsuba as mi  # noqa: F401
         except Exception:
             return False
+    _wrap_loaders(mi)
     for name, ctor in list(_REGISTRY.items()):
         mi.register_integrator(name, _mitsuba_plugin(mi, name, ctor))
     return True
@@ -458,12 +521,7 @@ def _mitsuba_plugin(mi, name: str, ctor):
     """Constructor of the mi.SamplingIntegrator subclass wrapping `ctor`."""
 
     def _scene(scene):
-        from .scene import Scene
-
-        if not isinstance(scene, Scene):
-            raise MtxError(f"{name}: mtx renders mtx.scene.Scene objects; no mi.Scene converter exists "
-                           "(build the scene with mtx.scene.from_xml / mtx.scene.bedroom)")
-        return scene
+        return mtx_scene_of(scene)
 
     class Plugin(mi.SamplingIntegrator):
         def __init__(self, props):

@@ -164,6 +164,13 @@ class Scene:
                 N = np.zeros_like(P)
                 UV = (loc[:, :2] + 1) * 0.5
                 flags = 1  # face normals
+            elif sd["type"] == "cube":
+                # Mitsuba's cube: [-1, 1]^3, two outward-wound triangles per face
+                P, F = _cube_mesh()
+                P = P @ M[:3, :3].T + M[:3, 3]
+                N = np.zeros_like(P)
+                UV = np.zeros((len(P), 2))
+                flags = 1  # face normals
             elif base_dir and sd.get("filename") and objio.is_real_file(os.path.join(base_dir, sd["filename"])):
                 if sd["type"] != "obj":
                     raise ValueError(f"shape type {sd['type']!r} is not supported (obj, rectangle)")
@@ -385,6 +392,25 @@ class Scene:
         return s
 
 
+def _cube_mesh():
+    """The 12 triangles of [-1, 1]^3, counter-clockwise seen from outside."""
+    P, F = [], []
+    for axis in range(3):
+        for sign in (-1.0, 1.0):
+            u, v = (axis + 1) % 3, (axis + 2) % 3
+            quad = []
+            for a, b in ((-1, -1), (1, -1), (1, 1), (-1, 1)):
+                p = np.zeros(3)
+                p[axis], p[u], p[v] = sign, a, b
+                quad.append(p)
+            if sign < 0:
+                quad = quad[::-1]
+            base = len(P)
+            P.extend(quad)
+            F.extend([[base, base + 1, base + 2], [base, base + 2, base + 3]])
+    return np.array(P, np.float64), np.array(F, np.int64)
+
+
 def _camera(sensor: dict, W: int, H: int) -> _abi.Camera:
     M = _m4(sensor["to_world"])
     cam = _abi.Camera()
@@ -392,9 +418,21 @@ def _camera(sensor: dict, W: int, H: int) -> _abi.Camera:
     cam.axis_x[:] = M[:3, 0]
     cam.axis_y[:] = M[:3, 1]
     cam.axis_z[:] = M[:3, 2]
-    fov = float(sensor.get("fov", 45.0))  # fov_axis = x (default)
-    cam.tan_x = math.tan(math.radians(fov) * 0.5)
-    cam.tan_y = cam.tan_x * H / W
+    fov = float(sensor.get("fov", 45.0))
+    axis = sensor.get("fov_axis", "x")  # Mitsuba's perspective sensor: x (default), y, smaller, larger
+    if axis == "smaller":
+        axis = "x" if W <= H else "y"
+    elif axis == "larger":
+        axis = "x" if W >= H else "y"
+    t = math.tan(math.radians(fov) * 0.5)
+    if axis == "x":  # the other axis from the fp32-rounded one (as the fixtures were made)
+        cam.tan_x = t
+        cam.tan_y = cam.tan_x * H / W
+    elif axis == "y":
+        cam.tan_y = t
+        cam.tan_x = cam.tan_y * W / H
+    else:
+        raise ValueError(f"fov_axis {axis!r} is not supported (x, y, smaller, larger)")
     cam.near_clip = float(sensor.get("near_clip", 1e-2))
     cam.far_clip = float(sensor.get("far_clip", 1e4))
     cam.width, cam.height = W, H
