@@ -27,7 +27,7 @@ import numpy as np
 
 from ._lib import MtxError
 
-BSDF_TYPES = {"diffuse", "roughplastic", "plastic", "conductor", "roughconductor", "dielectric", "roughdielectric",
+BSDF_TYPES = {"diffuse", "roughplastic", "conductor", "roughconductor", "dielectric", "roughdielectric",
               "twosided", "mask"}
 SHAPE_TYPES = {"rectangle", "cube", "obj"}
 SENSOR_TYPES = {"perspective"}
@@ -74,6 +74,8 @@ def _bsdf(d: dict, key: str | None = None) -> dict:
         if len(nested) != 1:
             raise MtxError(f"{t}: expected exactly one nested bsdf, got {len(nested)}")
         out["nested"] = _bsdf(nested[0][1])
+    if t in ("conductor", "roughconductor") and d.get("material", "none") != "none":
+        raise MtxError(f"{t}: named conductor materials ({d['material']!r}) are not supported; give eta / k")
     for k, v in d.items():
         if k in ("type", "id") or (isinstance(v, dict) and v.get("type") in BSDF_TYPES):
             continue
@@ -120,6 +122,8 @@ def spec_from_dict(d: dict) -> dict:
             b = v.get("bsdf")
             if b is None:
                 sd["bsdf_inline"] = {"type": "diffuse", "reflectance": [0.5, 0.5, 0.5]}  # Mitsuba's default BSDF
+            elif not isinstance(b, dict):
+                raise MtxError(f"shape {key!r}: bsdf must be a dictionary")
             elif b.get("type") == "ref":
                 sd["bsdf"] = b["id"]
             else:

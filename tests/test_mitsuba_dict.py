@@ -166,6 +166,13 @@ def test_plugin_resolves_loaded_scenes():
     bad["env"] = {"type": "envmap", "filename": "sky.exr"}
     with pytest.raises(MtxError, match="unsupported"):
         spec_from_dict(bad)
+    gold = cornell_box()
+    gold["white"] = {"type": "conductor", "material": "Au"}
+    with pytest.raises(MtxError, match="named conductor"):
+        spec_from_dict(gold)
+    nolight = {k: v for k, v in cornell_box().items() if k != "light"}
+    with pytest.raises(MtxError, match="no area emitter"):
+        spec_from_dict(nolight)
 
 
 @pytest.mark.gpu
