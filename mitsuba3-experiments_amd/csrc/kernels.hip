@@ -127,6 +127,11 @@ struct ShadowSrc {
     pl.x = b.shadow[k].x;
   }
   __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
+#if MTX_SHADOW_SKIP_NOOP
+    // an occluded ray without NaN-flagged channels leaves L unchanged: no
+    // read-modify-write (the scattered 16-B store is the write amplification)
+    if (occluded && (__float_as_uint(pl.t.w) & 14u) == 0u) return;
+#endif
     float4 L = b.L[0][pl.li];
     apply_shadow(L, pl.t, pl.x, occluded);
     b.L[0][pl.li] = L;

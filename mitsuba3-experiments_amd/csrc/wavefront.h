@@ -56,6 +56,9 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_CLOSEST_CW
 #define MTX_CLOSEST_CW 0  // closest hit on the 8-wide tree (device_common.h trace_loop_closest_cw)
 #endif
+#ifndef MTX_SHADOW_SKIP_NOOP
+#define MTX_SHADOW_SKIP_NOOP 1  // k_trace_shadow: no L store for occluded rays that change nothing
+#endif
 #ifndef MTX_CACHE_SORT
 #define MTX_CACHE_SORT 2  // NRC cache query order (api.cpp run_cache): 0 as appended, 1 Morton sort, 2 region x XCD
 #endif
