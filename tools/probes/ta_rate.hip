@@ -24,9 +24,10 @@ constexpr int kIters = 4096;
 // lines, 2 one line per lane (64 lines), 3 coalesced (lane-contiguous),
 // 4 one line per lane, lanes of a 4-lane group read the 4 16-B parts of one
 // 64-B node (16 nodes, 8 lines). W: bytes per lane (4, 8, 16).
-template <int PAT, int W>
+template <int PAT, int W, int ACTIVE = 64>
 __global__ __launch_bounds__(256) void k_gather(const uint4 *__restrict__ buf, uint32_t mask16, uint4 *out) {
   const uint32_t lane = threadIdx.x & 63u;
+  if (lane >= (uint32_t)ACTIVE) return;  // partial waves: exec mask of the first ACTIVE lanes
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   uint32_t acc = 0;
   uint32_t base = wave * 1021u;
@@ -119,6 +120,12 @@ int main() {
     report("x4 same address", f, run(k_gather<0, 4>, buf, f.mask16, out, grid, e0, e1));
     report("x8 16 lines", f, run(k_gather<1, 8>, buf, f.mask16, out, grid, e0, e1));
     report("scalar 64-B node (4 x s_load_x4)", f, run(k_scalar, buf, f.mask16, out, grid, e0, e1));
+    report("x16 coalesced, 48 lanes", f, run(k_gather<3, 16, 48>, buf, f.mask16, out, grid, e0, e1));
+    report("x16 coalesced, 16 lanes", f, run(k_gather<3, 16, 16>, buf, f.mask16, out, grid, e0, e1));
+    report("x16 same address, 16 lanes", f, run(k_gather<0, 16, 16>, buf, f.mask16, out, grid, e0, e1));
+    report("x16 64 lines, 48 lanes", f, run(k_gather<2, 16, 48>, buf, f.mask16, out, grid, e0, e1));
+    report("x16 64 lines, 16 lanes", f, run(k_gather<2, 16, 16>, buf, f.mask16, out, grid, e0, e1));
+    report("x16 16 lines, 16 lanes", f, run(k_gather<1, 16, 16>, buf, f.mask16, out, grid, e0, e1));
   }
   CK(hipDeviceSynchronize());
   return 0;
