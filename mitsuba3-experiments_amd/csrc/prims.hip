@@ -252,17 +252,20 @@ __global__ void k_minmax(const float *__restrict__ p, uint64_t n3, float2 *parti
   if (threadIdx.x == 0) partial[blockIdx.x] = make_float2(smin[0], smax[0]);
 }
 
-// Bounding interval of k_minmax's m partials, reduced by one 256-thread
-// block in a fixed tree (every caller gets the same floats).
+// Bounding interval of k_minmax's m partials, reduced by the first 256
+// threads of the block in a fixed tree (every caller gets the same floats;
+// larger blocks' other threads only take the barriers).
 __device__ __forceinline__ float2 minmax_reduce(const float2 *partial, int m) {
   __shared__ float smin[256], smax[256];
-  float lo = INFINITY, hi = -INFINITY;
-  for (int i = threadIdx.x; i < m; i += 256) {
-    lo = fminf(lo, partial[i].x);
-    hi = fmaxf(hi, partial[i].y);
+  if (threadIdx.x < 256) {
+    float lo = INFINITY, hi = -INFINITY;
+    for (int i = threadIdx.x; i < m; i += 256) {
+      lo = fminf(lo, partial[i].x);
+      hi = fmaxf(hi, partial[i].y);
+    }
+    smin[threadIdx.x] = lo;
+    smax[threadIdx.x] = hi;
   }
-  smin[threadIdx.x] = lo;
-  smax[threadIdx.x] = hi;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) {
@@ -598,9 +601,14 @@ __global__ __launch_bounds__(256) void k_hash_cells(const float *__restrict__ p,
     cell[i] = hg_cell(p, n, i, bb.x, ext, fres, n_cells);
 }
 
+// Persistent (round 5): a workgroup takes tiles blockIdx.x, + gridDim.x, ...
+// and issues the next tile's loads before it sorts the current one, so that
+// with one 128-KB workgroup per CU the HBM reads overlap the LDS work instead
+// of alternating with it.
 template <int MODE, bool RANK>
 __global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__ keys, const float *__restrict__ value,
-                                                    uint64_t n, int s, int top, uint32_t *__restrict__ tab,
+                                                    uint64_t n, int s, int top, uint32_t tiles,
+                                                    uint32_t *__restrict__ tab,
                                                     typename SplitCfg<MODE>::Rec *__restrict__ out1,
                                                     uint32_t *__restrict__ slow) {
   if (blockIdx.x == 0 && threadIdx.x == 0) slow[0] = 0;  // level 2's slow-bucket count
@@ -612,106 +620,127 @@ __global__ __launch_bounds__(512) void k_tile_split(const uint32_t *__restrict__
   uint32_t *rows = lds;  // [8][B] u16 counters, two per word
   Rec *stage = (Rec *)(lds + 4 * B);
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint64_t t0 = (uint64_t)blockIdx.x * T;
-  const uint32_t tsize = (uint32_t)min((uint64_t)T, n - t0);
   uint32_t *row = rows + w * (B / 2);
   uint16_t *row16 = (uint16_t *)row;
-  for (uint32_t i = lane; i < B / 2; i += 64) row[i] = 0;
-  uint32_t key[R], val[R];
+  uint32_t tile = blockIdx.x;
+  if (tile >= tiles) return;
+  // the current tile's keys and the next tile's, in flight during this
+  // tile's sort
+  uint32_t key[R], val[R], nk[R], nv[R];
+  auto fetch = [&](uint32_t t, uint32_t *k, uint32_t *v) {
+    const uint64_t t0 = (uint64_t)t * T;
+    const uint32_t ts = (uint32_t)min((uint64_t)T, n - t0);
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t j = w * (T / 8) + r * 64 + lane;
-    const bool ok = j < tsize;
-    key[r] = ok ? keys[t0 + j] : 0u;
-    if (MODE == 1) val[r] = ok ? __float_as_uint(value[t0 + j]) : 0u;
-  }
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t j = w * (T / 8) + r * 64 + lane;
+      const bool ok = j < ts;
+      k[r] = ok ? keys[t0 + j] : 0u;
+      if (MODE == 1) v[r] = ok ? __float_as_uint(value[t0 + j]) : 0u;
+    }
+  };
+  fetch(tile, key, val);
+  while (true) {
+    const uint64_t t0 = (uint64_t)tile * T;
+    const uint32_t tsize = (uint32_t)min((uint64_t)T, n - t0);
+    const uint32_t next = tile + gridDim.x;
+    if (next < tiles) fetch(next, nk, nv);
+    for (uint32_t i = lane; i < B / 2; i += 64) row[i] = 0;
+    __syncthreads();  // the previous tile's stage has left LDS; rows zeroed
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t d = key[r] >> s;
-    if (w * (T / 8) + r * 64 + lane < tsize) atomicAdd(&row[d >> 1], 1u << ((d & 1u) << 4));
-  }
-  __syncthreads();
-  // digits [8 tid, 8 tid + 8): totals over the waves, tile-level exclusive
-  // scan, the table row, then each wave's base per digit (u16)
-  const uint32_t d0 = threadIdx.x * 8;
-  const bool mine = d0 < B;
-  uint32_t tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (mine) {
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t d = key[r] >> s;
+      if (w * (T / 8) + r * 64 + lane < tsize) atomicAdd(&row[d >> 1], 1u << ((d & 1u) << 4));
+    }
+    __syncthreads();
+    // digits [8 tid, 8 tid + 8): totals over the waves, tile-level exclusive
+    // scan, the table row, then each wave's base per digit (u16)
+    const uint32_t d0 = threadIdx.x * 8;
+    const bool mine = d0 < B;
+    uint32_t tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (mine) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 c = *(const uint4 *)&rows[q * (B / 2) + d0 / 2];
-      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+      for (int q = 0; q < 8; ++q) {
+        const uint4 c = *(const uint4 *)&rows[q * (B / 2) + d0 / 2];
+        const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        tot[2 * i] += cw[i] & 0xFFFFu;
-        tot[2 * i + 1] += cw[i] >> 16;
+        for (int i = 0; i < 4; ++i) {
+          tot[2 * i] += cw[i] & 0xFFFFu;
+          tot[2 * i + 1] += cw[i] >> 16;
+        }
       }
     }
-  }
-  uint32_t sum = 0;
+    uint32_t sum = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) sum += tot[i];
-  uint32_t all;
-  uint32_t run = block_excl_scan<8>(sum, s_wsum, &all);
-  if (mine) {
-    uint32_t st[8];
+    for (int i = 0; i < 8; ++i) sum += tot[i];
+    uint32_t all;
+    uint32_t run = block_excl_scan<8>(sum, s_wsum, &all);
+    if (mine) {
+      uint32_t st[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      st[i] = run;
-      run += tot[i];
-    }
-    uint4 *trow = (uint4 *)&tab[(uint64_t)blockIdx.x * B + d0];
-    trow[0] = make_uint4(st[0] | (st[1] << 16), st[1] | (st[2] << 16), st[2] | (st[3] << 16), st[3] | (st[4] << 16));
-    trow[1] = make_uint4(st[4] | (st[5] << 16), st[5] | (st[6] << 16), st[6] | (st[7] << 16), st[7] | (run << 16));
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      uint4 *cp = (uint4 *)&rows[q * (B / 2) + d0 / 2];
-      const uint4 c = *cp;
-      const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
-      uint32_t nw[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        nw[i] = st[2 * i] | (st[2 * i + 1] << 16);
-        st[2 * i] += cw[i] & 0xFFFFu;
-        st[2 * i + 1] += cw[i] >> 16;
+      for (int i = 0; i < 8; ++i) {
+        st[i] = run;
+        run += tot[i];
       }
-      *cp = make_uint4(nw[0], nw[1], nw[2], nw[3]);
-    }
-  }
-  __syncthreads();
-  const uint64_t lt = (1ull << lane) - 1ull;
+      uint4 *trow = (uint4 *)&tab[(uint64_t)tile * B + d0];
+      trow[0] = make_uint4(st[0] | (st[1] << 16), st[1] | (st[2] << 16), st[2] | (st[3] << 16), st[3] | (st[4] << 16));
+      trow[1] = make_uint4(st[4] | (st[5] << 16), st[5] | (st[6] << 16), st[6] | (st[7] << 16), st[7] | (run << 16));
 #pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t j = w * (T / 8) + r * 64 + lane;
-    const bool ok = j < tsize;
-    const uint32_t d = key[r] >> s;
-    uint32_t pos;
-    if constexpr (RANK) {
-      // same-address LDS atomics of one wave return in lane order (checked
-      // once per device, lds_lane_order()): the old value is the position
-      pos = ok ? (atomicAdd(&row[d >> 1], 1u << ((d & 1u) << 4)) >> ((d & 1u) << 4)) & 0xFFFFu : 0u;
-    } else {
-      const uint64_t peers = ms_match(d, top, __ballot(ok));
-      const uint32_t rank = (uint32_t)__popcll(peers & lt);
-      const uint32_t p0 = row16[d];
-      if (ok && rank == 0) row16[d] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
-      pos = p0 + rank;
+      for (int q = 0; q < 8; ++q) {
+        uint4 *cp = (uint4 *)&rows[q * (B / 2) + d0 / 2];
+        const uint4 c = *cp;
+        const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+        uint32_t nw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          nw[i] = st[2 * i] | (st[2 * i + 1] << 16);
+          st[2 * i] += cw[i] & 0xFFFFu;
+          st[2 * i + 1] += cw[i] >> 16;
+        }
+        *cp = make_uint4(nw[0], nw[1], nw[2], nw[3]);
+      }
     }
-    if (ok) {
-      if constexpr (MODE == 0)
-        stage[pos] = ((key[r] & L1) << 14) | j;
-      else
-        stage[pos] = make_uint2(val[r], key[r] & L1);
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t j = w * (T / 8) + r * 64 + lane;
+      const bool ok = j < tsize;
+      const uint32_t d = key[r] >> s;
+      uint32_t pos;
+      if constexpr (RANK) {
+        // same-address LDS atomics of one wave return in lane order (checked
+        // once per device, lds_lane_order()): the old value is the position
+        pos = ok ? (atomicAdd(&row[d >> 1], 1u << ((d & 1u) << 4)) >> ((d & 1u) << 4)) & 0xFFFFu : 0u;
+      } else {
+        const uint64_t peers = ms_match(d, top, __ballot(ok));
+        const uint32_t rank = (uint32_t)__popcll(peers & lt);
+        const uint32_t p0 = row16[d];
+        if (ok && rank == 0) row16[d] = (uint16_t)(p0 + (uint32_t)__popcll(peers));
+        pos = p0 + rank;
+      }
+      if (ok) {
+        if constexpr (MODE == 0)
+          stage[pos] = ((key[r] & L1) << 14) | j;
+        else
+          stage[pos] = make_uint2(val[r], key[r] & L1);
+      }
     }
-  }
-  __syncthreads();
-  // the sorted tile leaves as 16-B stores
-  constexpr uint32_t per = 16 / sizeof(Rec);
-  for (uint32_t j = threadIdx.x * per; j < tsize; j += 512 * per) {
-    if (j + per <= tsize) {
-      *(uint4 *)&out1[t0 + j] = *(const uint4 *)&stage[j];
-    } else {
-      for (uint32_t i = j; i < tsize; ++i) out1[t0 + i] = stage[i];
+    __syncthreads();
+    // the sorted tile leaves as 16-B stores
+    constexpr uint32_t per = 16 / sizeof(Rec);
+    for (uint32_t j = threadIdx.x * per; j < tsize; j += 512 * per) {
+      if (j + per <= tsize) {
+        *(uint4 *)&out1[t0 + j] = *(const uint4 *)&stage[j];
+      } else {
+        for (uint32_t i = j; i < tsize; ++i) out1[t0 + i] = stage[i];
+      }
+    }
+    if (next >= tiles) break;
+    tile = next;
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      key[r] = nk[r];
+      if (MODE == 1) val[r] = nv[r];
     }
   }
 }
@@ -1407,6 +1436,21 @@ int gb_attrs() {  // per call: the attribute belongs to the current device
   return MTX_OK;
 }
 
+// Level 1 launch: persistent k_tile_split, as many workgroups as fit on the
+// device at once (at most one per tile).
+template <int MODE>
+void tile_split_launch(const uint32_t *keys, const float *value, uint64_t n, int s, int top, uint32_t tiles,
+                       uint32_t *tab, typename SplitCfg<MODE>::Rec *out1, uint32_t *slow, hipStream_t st) {
+  const bool rank = lds_lane_order(st);
+  const uint32_t lds = split_lds<MODE>(top);
+  int dev = 0, ncu = 256, per = 1;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  auto kern = rank ? k_tile_split<MODE, true> : k_tile_split<MODE, false>;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 512, lds) != hipSuccess || per < 1) per = 1;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, (uint64_t)ncu * (uint32_t)per);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, keys, value, n, s, top, tiles, tab, out1, slow);
+}
+
 // Level 2 for 2^s local keys: k_bucket_fast over every bucket, then
 // k_bucket_slow over the buckets it listed (long buckets); with more tiles
 // than one level-2 group, k_bucket_slow over every bucket.
@@ -1507,12 +1551,7 @@ int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, u
     uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_cells + (1ull << g.s) - 1) >> g.s));
     const uint32_t hb = (uint32_t)std::min<uint64_t>(nblk(n, 256), 2048);  // 8 blocks per CU
     hipLaunchKernelGGL(k_hash_cells, dim3(hb), dim3(256), 0, st, p, n, res, n_cells, partial, m, cell);
-    if (lds_lane_order(st))
-      hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n,
-                         g.s, g.top, tab, out1, slow);
-    else
-      hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, cell, nullptr, n,
-                         g.s, g.top, tab, out1, slow);
+    tile_split_launch<0>(cell, nullptr, n, g.s, g.top, tiles, tab, out1, slow, st);
     return bk_launch<0>(out1, tab, tiles, g.s, g.top, n_cells, cell_size, cell_offset, sample_idx, nullptr, 0, slow,
                         st);
   }
@@ -1577,12 +1616,7 @@ int group_by_u32(const uint32_t *keys, uint64_t n, uint32_t n_keys, uint32_t *ke
     uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
     uint32_t *out1 = cv.take<uint32_t>(n);
     uint32_t *slow = cv.take<uint32_t>(1 + (((uint64_t)n_keys + (1ull << g.s) - 1) >> g.s));
-    if (lds_lane_order(st))
-      hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n,
-                         g.s, g.top, tab, out1, slow);
-    else
-      hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n,
-                         g.s, g.top, tab, out1, slow);
+    tile_split_launch<0>(keys, nullptr, n, g.s, g.top, tiles, tab, out1, slow, st);
     return bk_launch<0>(out1, tab, tiles, g.s, g.top, n_keys, key_size, key_offset, order, nullptr, 0, slow, st);
   }
   const uint64_t hn = ((uint64_t)1 << kMsMaxBits) * g.tiles;
@@ -1627,12 +1661,7 @@ int sort24(const uint32_t *keys, uint64_t n, uint32_t *perm, void *ws, hipStream
   uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
   uint32_t *out1 = cv.take<uint32_t>(n);
   uint32_t *slow = cv.take<uint32_t>(1 + ((1ull << 24) >> g.s));
-  if (lds_lane_order(st))
-    hipLaunchKernelGGL((k_tile_split<0, true>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n, g.s,
-                       g.top, tab, out1, slow);
-  else
-    hipLaunchKernelGGL((k_tile_split<0, false>), dim3(tiles), dim3(512), split_lds<0>(g.top), st, keys, nullptr, n,
-                       g.s, g.top, tab, out1, slow);
+  tile_split_launch<0>(keys, nullptr, n, g.s, g.top, tiles, tab, out1, slow, st);
   return bk_launch<0>(out1, tab, tiles, g.s, g.top, 1u << 24, nullptr, nullptr, perm, nullptr, 0, slow, st);
 }
 
@@ -1652,12 +1681,7 @@ int scatter_reduce_f32(int op, float *target, uint64_t n_target, const float *va
     uint32_t *tab = cv.take<uint32_t>((uint64_t)tiles << g.top);
     uint2 *out1 = cv.take<uint2>(n);
     uint32_t *slow = cv.take<uint32_t>(1 + ((n_target + (1ull << g.s) - 1) >> g.s));
-    if (lds_lane_order(st))
-      hipLaunchKernelGGL((k_tile_split<1, true>), dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n,
-                         g.s, g.top, tab, out1, slow);
-    else
-      hipLaunchKernelGGL((k_tile_split<1, false>), dim3(tiles), dim3(512), split_lds<1>(g.top), st, index, value, n,
-                         g.s, g.top, tab, out1, slow);
+    tile_split_launch<1>(index, value, n, g.s, g.top, tiles, tab, out1, slow, st);
     return bk_launch<1>(out1, tab, tiles, g.s, g.top, (uint32_t)n_target, nullptr, nullptr, nullptr, target, op, slow,
                         st);
   }
