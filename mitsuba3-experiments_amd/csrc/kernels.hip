@@ -251,6 +251,7 @@ struct ShadeIO {
   float4 nro, nrd, nthr, nprev;  // the next ray and state: k_shade stores them at the path's append slot
   float4 nL;                     // result and sampler state: at the append slot, or by path once the path ends
   uint4 nmisc;
+  float warm;                    // MTX_SHADE_WARM: the next entry's shading-record word (L2 warm-up)
 #if MTX_DIAG_STAMPS
   Stamps st;
 #endif
@@ -311,7 +312,7 @@ __device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, f
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
-                                           const float4 h, ShadeIO &io) {
+                                           const float4 h, ShadeIO &io, const float4 *warm = nullptr) {
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const float4 ro = b.ray_o[rp][qi], rd = b.ray_d[rp][qi];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
@@ -338,6 +339,9 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
 #if MTX_DIAG_STAMPS
   MTX_STAMP(io.st, 1);
 #endif
+  // the next queue entry's shading record, one word: its line is in L2 when
+  // the next iteration reads the record (k_shade, MTX_SHADE_WARM)
+  if (warm) io.warm = warm->x;
   if (kPrevOnEmitter && bounce != 0 && si.emitter >= 0) pv = b.prev[rp][qi];
   V3 prev_p = V3{pv.x, pv.y, pv.z};
   float spread = pv.w, a0 = rd.w;
@@ -922,10 +926,19 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     const uint32_t inext = i + stride;
     uint32_t path_n = 0;
     if (inext < count) path_n = ident ? inext : in_q[inext];
+#if MTX_SHADE_WARM
+    float4 hn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (inext < count) hn = b.hit[inext];
+    const uint32_t pn = __float_as_uint(hn.y);
+    const float4 *wp = (inext < count && pn != 0xffffffffu) ? s.shade_rec + 8 * (size_t)pn : nullptr;
+#else
+    const float4 *wp = nullptr;
+#endif
     ShadeIO io;
     io.emit = false;
     io.em_hi = false;
     io.query = false;
+    io.warm = 0.f;
 #if MTX_DIAG_STAMPS
     ++steps;
     MTX_STAMP(stp, 0);
@@ -945,11 +958,17 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
       else if constexpr (INT == MTX_INT_NERAD)
         cont = shade_nerad<true>(s, sv, b, bounce, path, i, h, io);
       else
-        cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io, wp);
     }
+    (void)wp;
     const uint32_t path_c = path;
     path = path_n;
+#if MTX_SHADE_WARM
+    h = hn;
+    asm volatile("" ::"v"(io.warm));  // the warm-up load completes in this iteration
+#else
     if (inext < count) h = b.hit[inext];
+#endif
 #if MTX_DIAG_STAMPS
     stp = io.st;
 #endif

@@ -56,6 +56,9 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_CLOSEST_CW
 #define MTX_CLOSEST_CW 0  // closest hit on the 8-wide tree (device_common.h trace_loop_closest_cw)
 #endif
+#ifndef MTX_SHADE_WARM
+#define MTX_SHADE_WARM 1  // k_shade: warm L2 with the next entry's shading record
+#endif
 #ifndef MTX_SHADOW_SKIP_NOOP
 #define MTX_SHADOW_SKIP_NOOP 1  // k_trace_shadow: no L store for occluded rays that change nothing
 #endif
