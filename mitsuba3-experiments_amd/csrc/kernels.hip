@@ -105,16 +105,18 @@ __device__ __forceinline__ void apply_shadow(float4 &L, float4 rt, float4 rx, bo
   }
 }
 
-// Any-hit traversal of the NEE shadow rays; unoccluded rays apply their
-// contribution to L (path-mis.py:117 fma form, path.py:259 / nrc.py:62 add
-// form).
+// Any-hit traversal of the NEE shadow rays. k_shade stores each record in
+// its final-value form (shadow_final): t = the path's L after an unoccluded
+// ray (fma(T, X, L), path-mis.py:117, or L + X, path.py:259 / nrc.py:62) with
+// the flags in t.w, x = the path's L before it. The finish is one store -- no
+// read of L: t.xyz with x.w when unoccluded; when occluded, nothing unless a
+// flagged channel must become NaN (then x, read from the record, with those
+// channels NaN).
 struct ShadowSrc {
-  // the lane carries its path and the record's contribution from the ray's
-  // start, so the finish is one L load + store instead of a record load
-  // followed by the dependent L load
   struct Payload {
     uint32_t k, li;  // record, L index of the target (plane * capacity + position)
-    float4 t, x;
+    float4 t;        // L after an unoccluded ray | flags
+    float lw;        // L.w (unchanged by the update)
   };
   WaveBuffers b;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, Payload &pl) const {
@@ -124,19 +126,32 @@ struct ShadowSrc {
     pl.k = k;
     pl.li = __float_as_uint(d4.w);
     pl.t = b.shadow[k].t;
-    pl.x = b.shadow[k].x;
+    pl.lw = b.shadow[k].x.w;
   }
   __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
-#if MTX_SHADOW_SKIP_NOOP
-    // an occluded ray without NaN-flagged channels leaves L unchanged: no
-    // read-modify-write (the scattered 16-B store is the write amplification)
-    if (occluded && (__float_as_uint(pl.t.w) & 14u) == 0u) return;
-#endif
-    float4 L = b.L[0][pl.li];
-    apply_shadow(L, pl.t, pl.x, occluded);
-    b.L[0][pl.li] = L;
+    const uint32_t fl = __float_as_uint(pl.t.w);
+    if (!occluded) {
+      b.L[0][pl.li] = make_float4(pl.t.x, pl.t.y, pl.t.z, pl.lw);
+    } else if (fl & 14u) {
+      float4 L = b.shadow[pl.k].x;
+      const float qnan = __uint_as_float(0x7fc00000u);
+      if (fl & 2u) L.x = qnan;
+      if (fl & 4u) L.y = qnan;
+      if (fl & 8u) L.z = qnan;
+      b.L[0][pl.li] = L;
+    }
+    // occluded without flags: L unchanged, nothing to store
   }
 };
+
+// A shadow record (make_shadow's T, X, flags) turned into its final-value
+// form against the path's L as k_shade stores it (apply_shadow's arithmetic).
+__device__ __forceinline__ void shadow_final(ShadowRec &rec, float4 L) {
+  float4 lv = L;
+  apply_shadow(lv, rec.t, rec.x, false);
+  rec.x = L;
+  rec.t = make_float4(lv.x, lv.y, lv.z, rec.t.w);
+}
 
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
@@ -991,9 +1006,11 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     }
     if (io.emit) {
       // the contribution goes to the path's L where the next shade (or the
-      // film) reads it
+      // film) reads it; the integrators that emit shadow rays (path-mis,
+      // path, nrc, pssmltpath; not the nerad ones) store io.nL there
       const uint32_t li = (kNerad || !cont) ? kFinal * b.capacity + path_c : (rp ^ 1u) * b.capacity + slot;
       io.rec.d.w = __uint_as_float(li);
+      shadow_final(io.rec, io.nL);
       b.shadow[sslot] = io.rec;
     }
 #if MTX_DIAG_STAMPS

@@ -59,9 +59,6 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_SHADE_WARM
 #define MTX_SHADE_WARM 1  // k_shade: warm L2 with the next entry's shading record
 #endif
-#ifndef MTX_SHADOW_SKIP_NOOP
-#define MTX_SHADOW_SKIP_NOOP 1  // k_trace_shadow: no L store for occluded rays that change nothing
-#endif
 #ifndef MTX_CACHE_SORT
 #define MTX_CACHE_SORT 2  // NRC cache query order (api.cpp run_cache): 0 as appended, 1 Morton sort, 2 region x XCD
 #endif
@@ -127,11 +124,14 @@ inline size_t stack_ovf_bytes(const DevScene &s) {
   return n > 8 ? n : 8;
 }
 
-// Shadow-ray record (64 B): o.xyz maxt | d.xyz L index | T.xyz flags | X.xyz 0
-// (L index = plane * capacity + position of the path's L, WaveBuffers)
-// flags bit0: fma form L = fma(T, X, L) (path-mis.py:117) else L = L + X
-// (path.py:259, nrc.py:62); bits 1..3: the occluded-case contribution of that
-// channel is NaN (non-finite BSDF value / MIS weight), see DESIGN.md.
+// Shadow-ray record (64 B): o.xyz maxt | d.xyz L index | t | x (L index =
+// plane * capacity + position of the path's L, WaveBuffers). As make_shadow
+// builds it: t = T.xyz flags, x = X.xyz 0; flags bit0: fma form
+// L = fma(T, X, L) (path-mis.py:117) else L = L + X (path.py:259, nrc.py:62);
+// bits 1..3: the occluded-case contribution of that channel is NaN
+// (non-finite BSDF value / MIS weight), see DESIGN.md. As k_shade stores it
+// (kernels.hip shadow_final): t = the L after an unoccluded ray | flags,
+// x = the L before it.
 constexpr int kFinal = 2;  // the per-path plane of L / misc
 
 struct ShadowRec {
