@@ -105,13 +105,16 @@ __device__ __forceinline__ void apply_shadow(float4 &L, float4 rt, float4 rx, bo
   }
 }
 
-// Any-hit traversal of the NEE shadow rays. k_shade stores each record in
-// its final-value form (shadow_final): t = the path's L after an unoccluded
+// Any-hit traversal of the NEE shadow rays. k_shade stores each record of
+// the integrators whose L it stores itself (path-mis, path, nrc, pssmltpath)
+// in its final-value form (shadow_final, flag kShadowFinal): t = the path's L after an unoccluded
 // ray (fma(T, X, L), path-mis.py:117, or L + X, path.py:259 / nrc.py:62) with
 // the flags in t.w, x = the path's L before it. The finish is one store -- no
 // read of L: t.xyz with x.w when unoccluded; when occluded, nothing unless a
 // flagged channel must become NaN (then x, read from the record, with those
 // channels NaN).
+constexpr uint32_t kShadowFinal = 16u;  // record flag: final-value form
+
 struct ShadowSrc {
   struct Payload {
     uint32_t k, li;  // record, L index of the target (plane * capacity + position)
@@ -130,6 +133,15 @@ struct ShadowSrc {
   }
   __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
     const uint32_t fl = __float_as_uint(pl.t.w);
+    if (!(fl & kShadowFinal)) {
+      // make_shadow's form (the nerad integrators keep L by path outside
+      // k_shade's stores): read-modify-write of L
+      if (occluded && (fl & 14u) == 0u) return;
+      float4 L = b.L[0][pl.li];
+      apply_shadow(L, pl.t, b.shadow[pl.k].x, occluded);
+      b.L[0][pl.li] = L;
+      return;
+    }
     if (!occluded) {
       b.L[0][pl.li] = make_float4(pl.t.x, pl.t.y, pl.t.z, pl.lw);
     } else if (fl & 14u) {
@@ -150,7 +162,7 @@ __device__ __forceinline__ void shadow_final(ShadowRec &rec, float4 L) {
   float4 lv = L;
   apply_shadow(lv, rec.t, rec.x, false);
   rec.x = L;
-  rec.t = make_float4(lv.x, lv.y, lv.z, rec.t.w);
+  rec.t = make_float4(lv.x, lv.y, lv.z, __uint_as_float(__float_as_uint(rec.t.w) | kShadowFinal));
 }
 
 template <bool STATS>
@@ -1010,7 +1022,7 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
       // path, nrc, pssmltpath; not the nerad ones) store io.nL there
       const uint32_t li = (kNerad || !cont) ? kFinal * b.capacity + path_c : (rp ^ 1u) * b.capacity + slot;
       io.rec.d.w = __uint_as_float(li);
-      shadow_final(io.rec, io.nL);
+      if constexpr (!kNerad) shadow_final(io.rec, io.nL);
       b.shadow[sslot] = io.rec;
     }
 #if MTX_DIAG_STAMPS
