@@ -107,7 +107,7 @@ __device__ __forceinline__ void apply_shadow(float4 &L, float4 rt, float4 rx, bo
 
 // Any-hit traversal of the NEE shadow rays. k_shade stores each record of
 // the integrators whose L it stores itself (path-mis, path, nrc, pssmltpath)
-// in its final-value form (shadow_final, flag kShadowFinal): t = the path's L after an unoccluded
+// in its final-value form (make_shadow with Lcur, flag kShadowFinal): t = the path's L after an unoccluded
 // ray (fma(T, X, L), path-mis.py:117, or L + X, path.py:259 / nrc.py:62) with
 // the flags in t.w, x = the path's L before it. The finish is one store -- no
 // read of L: t.xyz with x.w when unoccluded; when occluded, nothing unless a
@@ -155,15 +155,6 @@ struct ShadowSrc {
     // occluded without flags: L unchanged, nothing to store
   }
 };
-
-// A shadow record (make_shadow's T, X, flags) turned into its final-value
-// form against the path's L as k_shade stores it (apply_shadow's arithmetic).
-__device__ __forceinline__ void shadow_final(ShadowRec &rec, float4 L) {
-  float4 lv = L;
-  apply_shadow(lv, rec.t, rec.x, false);
-  rec.x = L;
-  rec.t = make_float4(lv.x, lv.y, lv.z, __uint_as_float(__float_as_uint(rec.t.w) | kShadowFinal));
-}
 
 template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_shadow(DevScene s, WaveBuffers b, uint32_t bounce) {
@@ -286,9 +277,12 @@ struct ShadeIO {
 
 // Builds the shadow record for an NEE contribution. fma_form: value = (T, X)
 // applied as fma(T, X, L); otherwise X is added. Xo is the contribution the
-// reference forms when the shadow ray is occluded (em_weight = 0).
+// reference forms when the shadow ray is occluded (em_weight = 0). With Lcur
+// (the path's L, final for this bounce: the integrators that k_shade stores
+// L for add nothing to L after their NEE) the record is built in its
+// final-value form (see ShadowSrc; k_shade completes x.w with L.w).
 __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteraction &si, const DirectionSample &ds,
-                                            V3 T, V3 X, V3 Xo, bool fma_form) {
+                                            V3 T, V3 X, V3 Xo, bool fma_form, const V3 *Lcur = nullptr) {
   uint32_t fl = fma_form ? 1u : 0u;
   bool vis_noop, occ_noop;
   if (fma_form) {
@@ -309,8 +303,31 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   const Ray sr = spawn_ray_to(si.p, si.n, ds.p);
   io.rec.o = make_float4(sr.o.x, sr.o.y, sr.o.z, sr.maxt);
   io.rec.d = make_float4(sr.d.x, sr.d.y, sr.d.z, 0.f);  // .w: the L index, set by k_shade after its append
-  io.rec.t = make_float4(T.x, T.y, T.z, __uint_as_float(fl));
-  io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
+  if (Lcur) {
+    float4 lv = make_float4(Lcur->x, Lcur->y, Lcur->z, 0.f);
+    apply_shadow(lv, make_float4(T.x, T.y, T.z, __uint_as_float(fl)), make_float4(X.x, X.y, X.z, 0.f), false);
+    io.rec.t = make_float4(lv.x, lv.y, lv.z, __uint_as_float(fl | kShadowFinal));
+    io.rec.x = make_float4(Lcur->x, Lcur->y, Lcur->z, 0.f);
+  } else {
+    io.rec.t = make_float4(T.x, T.y, T.z, __uint_as_float(fl));
+    io.rec.x = make_float4(X.x, X.y, X.z, 0.f);
+  }
+}
+
+// A shadow record applied to its path's L in registers (the path megakernels:
+// the record of make_shadow, in either form).
+__device__ __forceinline__ void apply_shadow_rec(float4 &L, const ShadowRec &rec, bool occluded) {
+  const uint32_t fl = __float_as_uint(rec.t.w);
+  if (!(fl & kShadowFinal)) {
+    apply_shadow(L, rec.t, rec.x, occluded);
+  } else if (!occluded) {
+    L = make_float4(rec.t.x, rec.t.y, rec.t.z, L.w);
+  } else {
+    const float qnan = __uint_as_float(0x7fc00000u);
+    if (fl & 2u) L.x = qnan;
+    if (fl & 4u) L.y = qnan;
+    if (fl & 8u) L.z = qnan;
+  }
 }
 
 // BSDF data for one shading point: the textured colour of the diffuse and
@@ -498,14 +515,14 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     if (active_em) {
       const V3 X = bsdf_val * em_weight * mi_em;
       const V3 Xo = bsdf_val * v3s(0.f) * mi_em;
-      make_shadow(io, si, ds, T, X, Xo, true);
+      make_shadow(io, si, ds, T, X, Xo, true, &L);
     }
   } else {
     const float mis_em = INT == MTX_INT_PATH ? mis_weight_a(ds.pdf, bsdf_pdf) : mis_weight_b(ds.pdf, bsdf_pdf);
     if (active_em) {
       const V3 P = T * bsdf_val * em_weight * mis_em;
       const V3 Po = T * bsdf_val * v3s(0.f) * mis_em;
-      make_shadow(io, si, ds, T, P, Po, false);
+      make_shadow(io, si, ds, T, P, Po, false, &L);
     }
   }
 
@@ -772,7 +789,7 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
     float epdf;
     bsdf_eval_pdf(bd, mat, si.uv, si.wi, wo, &ev, &epdf);
     const float mi_em = mis_weight_b(ds.pdf, epdf);
-    make_shadow(io, si, ds, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true);
+    make_shadow(io, si, ds, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true, &L);
   }
   b.vprop[vi] = make_float4(vwo.x, vwo.y, vwo.z, 0.f);  // :138
   b.vprop_es[vi] = make_float2(es.x, es.y);
@@ -1022,7 +1039,7 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
       // path, nrc, pssmltpath; not the nerad ones) store io.nL there
       const uint32_t li = (kNerad || !cont) ? kFinal * b.capacity + path_c : (rp ^ 1u) * b.capacity + slot;
       io.rec.d.w = __uint_as_float(li);
-      if constexpr (!kNerad) shadow_final(io.rec, io.nL);
+      if constexpr (!kNerad) io.rec.x.w = io.nL.w;  // final-value form: L.w (set after the NEE)
       b.shadow[sslot] = io.rec;
     }
 #if MTX_DIAG_STAMPS
@@ -1148,7 +1165,7 @@ __global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_path_mega(
       if (io.emit) {
         const float4 so = io.rec.o, sd = io.rec.d;
         const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
-        apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+        apply_shadow_rec(io.nL, io.rec, traverse_occ(s, ostk, sr, so.w, nv, tv));
       }
       ++bounce;
       if (cont && bounce < iters) {
@@ -1289,7 +1306,7 @@ __global__ __launch_bounds__(kShadeBlock, MTX_MEGA_MIN_BLOCKS) void k_rs_stage_a
         if (io.emit) {
           const float4 so = io.rec.o, sd = io.rec.d;
           const TraceRay sr = make_trace_ray(V3{so.x, so.y, so.z}, V3{sd.x, sd.y, sd.z}, so.w);
-          apply_shadow(io.nL, io.rec.t, io.rec.x, traverse_occ(s, ostk, sr, so.w, nv, tv));
+          apply_shadow_rec(io.nL, io.rec, traverse_occ(s, ostk, sr, so.w, nv, tv));
         }
         ++bounce;
         if (cont && bounce < iters) {

@@ -130,7 +130,7 @@ inline size_t stack_ovf_bytes(const DevScene &s) {
 // L = fma(T, X, L) (path-mis.py:117) else L = L + X (path.py:259, nrc.py:62);
 // bits 1..3: the occluded-case contribution of that channel is NaN
 // (non-finite BSDF value / MIS weight), see DESIGN.md. As k_shade stores it
-// for the integrators whose L it stores (kernels.hip shadow_final, flag bit
+// for the integrators whose L it stores (kernels.hip make_shadow, flag bit
 // 4): t = the L after an unoccluded ray | flags, x = the L before it.
 constexpr int kFinal = 2;  // the per-path plane of L / misc
 
