@@ -62,6 +62,7 @@ L2_GATHER_PEAK_GBS = 18800.0
 VMEM_PEAK_GBS = round(1024 / 16.9 * 256 * 2.4, 0)
 # node and triangle records as the device reads them (triangles packed to 36 B, mtx_scene_upload)
 NODE_BYTES, TRI_BYTES, RAY_BYTES, HIT_BYTES, OCC_BYTES = 64, 36, 32, 16, 4
+OCC_NODE_BYTES = 80  # the any-hit tree's 8-wide compressed node (mtx.h MTX_OCC_NODE_WORDS)
 # SURVEY §8d wavefront path state per lane per bounce, read + written
 SHADE_BYTES_PER_PATH_BOUNCE = 2 * 108 + 32
 
@@ -262,13 +263,13 @@ def main():
     # rank-local per-step figures (this rank's launches)
     alg_closest = (cnt["rays_closest"] * (RAY_BYTES + HIT_BYTES) + cnt["nodes_closest"] * NODE_BYTES
                    + cnt["tris_closest"] * TRI_BYTES)
-    alg_shadow = (cnt["rays_shadow"] * (RAY_BYTES + OCC_BYTES) + cnt["nodes_shadow"] * NODE_BYTES
+    alg_shadow = (cnt["rays_shadow"] * (RAY_BYTES + OCC_BYTES) + cnt["nodes_shadow"] * OCC_NODE_BYTES
                   + cnt["tris_shadow"] * TRI_BYTES)
     launches = max(1, cnt["trace_launches"])
     trace_ms = agg["trace_ms"] / K  # counters off
     trace_s = trace_ms / 1e3
     achieved = alg_closest / trace_s / 1e9 if trace_s > 0 else 0.0
-    names = {"closest": "mtxd::k_trace_closest<false>", "shadow": "mtxd::k_trace_shadow<false>",
+    names = {"closest": "mtxd::k_trace_closest<false, false>", "shadow": "mtxd::k_trace_shadow<false>",
              "shade": "mtxd::k_shade<2>"}
     traffic, traffic_src = (measured_traffic(list(names.values()), traffic_key(args)) if world == 1
                             else ({k: None for k in names.values()}, "N>1: PMC profiles are N=1"))
