@@ -163,7 +163,8 @@ def measured_units(kernels, key):
             reason = f"{os.path.basename(f)}: bench args differ"
             continue
         ks = d.get("kernels", {})
-        keep = ("ta_busy", "valu_busy", "salu_busy", "l1_l2_read_bytes_per_launch", "ta_cycles_per_vmem")
+        keep = ("ta_busy", "valu_busy", "salu_busy", "l1_l2_read_bytes_per_launch", "ta_cycles_per_vmem",
+                "vmem_insts_per_launch")
         return {k: ({x: ks[k][x] for x in keep} if k in ks else None) for k in kernels}, os.path.relpath(f, ROOT)
     return {k: None for k in kernels}, reason
 
@@ -296,6 +297,12 @@ def main():
         for kk, nn in (("trace_closest", names["closest"]), ("trace_shadow", names["shadow"]),
                        ("shade", names["shade"])):
             kernels[kk]["units"] = units[nn]
+        # vector-memory wave instructions per ray (PMC SQ_INSTS_VMEM_RD + _WR per launch)
+        for kk, rays, nl in (("trace_closest", cnt["rays_closest"], launches),
+                             ("trace_shadow", cnt["rays_shadow"], cnt["shadow_launches"])):
+            u = kernels[kk]["units"]
+            if u and u.get("vmem_insts_per_launch") and rays:
+                u["vmem_wave_insts_per_ray"] = round(u["vmem_insts_per_launch"] / (rays / max(1, nl)), 3)
         # the roofline object follows north_star's traversal kernel; the
         # kernel with the most time per step is named beside it
         big = max(kernels, key=lambda k: kernels[k]["ms_per_step"])
