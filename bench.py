@@ -165,7 +165,8 @@ def measured_units(kernels, key):
         ks = d.get("kernels", {})
         keep = ("ta_busy", "valu_busy", "salu_busy", "l1_l2_read_bytes_per_launch", "ta_cycles_per_vmem",
                 "vmem_insts_per_launch")
-        return {k: ({x: ks[k][x] for x in keep} if k in ks else None) for k in kernels}, os.path.relpath(f, ROOT)
+        return {k: ({x: ks[k][x] for x in keep if x in ks[k]} if k in ks else None) for k in kernels}, \
+            os.path.relpath(f, ROOT)
     return {k: None for k in kernels}, reason
 
 
