@@ -191,3 +191,29 @@ def test_plugin_renders_the_loaded_cornell_box(oracle):
     np.testing.assert_array_equal(film, ref)
     img = plug.render(mi_scene, None, 5, 16)
     assert img.shape == (64, 64, 3) and np.all(np.isfinite(img))
+
+
+def test_obj_shape_and_fov_axes(tmp_path):
+    """An `obj` shape with a `filename` (the scenes' meshes, scene.xml:221-738)
+    loads through the dictionary path; fov_axis x / y / smaller / larger follow
+    Mitsuba's perspective sensor on a non-square film."""
+    from mtx import MtxError
+    from mtx.mitsuba_dict import scene_from_dict
+
+    (tmp_path / "quad.obj").write_text("v -1 -1 0\nv 1 -1 0\nv 1 1 0\nv -1 1 0\nf 1 2 3 4\n")
+    d = cornell_box(64, 32)
+    d["mesh"] = {"type": "obj", "filename": "quad.obj", "to_world": T().translate([0.0, 0.0, -0.5]).scale(0.2),
+                 "bsdf": {"type": "ref", "id": "red"}}
+    sc = scene_from_dict(d, base_dir=str(tmp_path))
+    assert sc.n_tris == 36 + 2  # the quad, fan-triangulated
+    t = np.tan(np.radians(39.3077) / 2)
+    for axis, (tx, ty) in {"x": (t, t * 32 / 64), "y": (t * 64 / 32, t), "smaller": (t * 64 / 32, t),
+                           "larger": (t, t * 32 / 64)}.items():
+        d2 = cornell_box(64, 32)
+        d2["sensor"]["fov_axis"] = axis
+        cam = scene_from_dict(d2).camera
+        assert abs(cam.tan_x - tx) < 1e-5 and abs(cam.tan_y - ty) < 1e-5, axis
+    d3 = cornell_box()
+    d3["sensor"]["fov_axis"] = "diagonal"
+    with pytest.raises((MtxError, ValueError)):
+        scene_from_dict(d3)
