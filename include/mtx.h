@@ -194,8 +194,7 @@ typedef struct mtx_scene_desc {
    * tri_geom[occ_perm[i]] for every i and that it is a permutation; NULL
    * with given trees: derived at upload by matching the records, and the
    * trees rejected (MTX_E_ARG) unless occ_tri_geom is a permutation of
-   * tri_geom. The 8-wide closest-hit traversal reports scene triangles
-   * through it. */
+   * tri_geom. */
   const uint32_t *occ_perm;
 } mtx_scene_desc;
 
@@ -355,8 +354,8 @@ int mtx_sample_rays(mtx_ctx *ctx, const mtx_render_args *args, uint64_t n, const
 
 /* Raw closest-hit / any-hit traversal (Scene.ray_intersect / ray_test,
  * path-mis.py:69-71, restirgi.py:320). rays: 8n floats (o.xyz, tmax, d.xyz,
- * 0); any_hit: 0 closest hit (4-wide tree), 1 any hit, 2 closest hit on the
- * 8-wide tree (near-first sorted children, the same answer); hits: 4n words
+ * 0); any_hit: 0 closest hit (4-wide tree), 1 any hit (8-wide occlusion
+ * tree); hits: 4n words
  * (t, prim, u, v) for closest hit, or n words (1 = occluded) for any hit.
  * visits (optional, 2n u32): node and triangle visits. */
 int mtx_trace(mtx_ctx *ctx, uint64_t n, const float *rays, int any_hit, uint32_t *hits,

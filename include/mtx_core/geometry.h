@@ -245,78 +245,6 @@ MTX_HD uint32_t cw_node_hits(const TraceRay &r, uint32_t oct, float ox, float oy
   return hits;
 }
 
-// Closest hit on the 8-wide tree (round 5): the slab tests of cw_node_hits,
-// returning a sort key per slot -- hit inner child: (entry distance bits
-// with the low 3 bits cleared) | its rank among the node's inner children
-// (child = child_base + rank), else 0xffffffff -- and the hit leaves'
-// triangle bits (bit offset .. offset + n - 1, as cw_node_hits). Sorted
-// ascending (cw_sort8), the keys give the visit order: near first, near-ties
-// by rank. key_t(key) <= the child's entry distance: a conservative cull.
-MTX_HD uint32_t cw_node_keys(const TraceRay &r, uint32_t oct, float ox, float oy, float oz, uint32_t w3,
-                             uint32_t meta_lo, uint32_t meta_hi, const uint32_t q[12], float tfar, uint32_t key[8]) {
-  const float ax = wide_ldexp(r.idir.x, (int)(int8_t)(uint8_t)(w3 & 0xffu)), bx = (ox - r.o.x) * r.idir.x;
-  const float ay = wide_ldexp(r.idir.y, (int)(int8_t)(uint8_t)((w3 >> 8) & 0xffu)), by = (oy - r.o.y) * r.idir.y;
-  const float az = wide_ldexp(r.idir.z, (int)(int8_t)(uint8_t)((w3 >> 16) & 0xffu)), bz = (oz - r.o.z) * r.idir.z;
-  const bool nx_ = (oct & 1u) != 0, ny_ = (oct & 2u) != 0, nz_ = (oct & 4u) != 0;
-  const uint32_t imask = w3 >> 24;
-  uint32_t bits = 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t qlx = q[0 + h], qhx = q[2 + h], qly = q[4 + h], qhy = q[6 + h], qlz = q[8 + h], qhz = q[10 + h];
-    const uint32_t qnx = nx_ ? qhx : qlx, qfx = nx_ ? qlx : qhx;
-    const uint32_t qny = ny_ ? qhy : qly, qfy = ny_ ? qly : qhy;
-    const uint32_t qnz = nz_ ? qhz : qlz, qfz = nz_ ? qlz : qhz;
-    const uint32_t m4 = h ? meta_hi : meta_lo;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int sh = 8 * k, slot = 4 * h + k;
-#ifdef MTX_DEVICE_COMPILE
-      typedef float f2v __attribute__((ext_vector_type(2)));
-      const f2v tx = __builtin_elementwise_fma(f2v{(float)((qnx >> sh) & 255u), (float)((qfx >> sh) & 255u)},
-                                               f2v{ax, ax}, f2v{bx, bx});
-      const f2v ty = __builtin_elementwise_fma(f2v{(float)((qny >> sh) & 255u), (float)((qfy >> sh) & 255u)},
-                                               f2v{ay, ay}, f2v{by, by});
-      const f2v tz = __builtin_elementwise_fma(f2v{(float)((qnz >> sh) & 255u), (float)((qfz >> sh) & 255u)},
-                                               f2v{az, az}, f2v{bz, bz});
-      const float nx = tx.x, fx = tx.y, ny = ty.x, fy = ty.y, nz = tz.x, fz = tz.y;
-#else
-      const float nx = fmaf((float)((qnx >> sh) & 255u), ax, bx), fx = fmaf((float)((qfx >> sh) & 255u), ax, bx);
-      const float ny = fmaf((float)((qny >> sh) & 255u), ay, by), fy = fmaf((float)((qfy >> sh) & 255u), ay, by);
-      const float nz = fmaf((float)((qnz >> sh) & 255u), az, bz), fz = fmaf((float)((qfz >> sh) & 255u), az, bz);
-#endif
-      const float tmin = fmaxf(fmaxf(fmaxf(nx, ny), nz), 0.f);
-      const float tmax = fminf(fminf(fminf(fx, fy), fz), tfar);
-      const bool hit = tmin <= tmax;
-      const uint32_t m = (m4 >> sh) & 0xffu;
-      const bool inner = ((imask >> slot) & 1u) != 0;
-      const uint32_t rank = (uint32_t)popc32(imask & ((1u << slot) - 1u));
-      key[slot] = (hit && inner) ? ((f2u(tmin) & 0x7ffffff8u) | rank) : 0xffffffffu;  // +-0 alike
-      bits |= (hit && !inner) ? ((m >> 5) << (m & 31u)) : 0u;
-    }
-  }
-  return bits;
-}
-
-// Ascending sort of 8 keys (19 compare-exchanges, each one min + one max).
-MTX_HD void cw_sort8(uint32_t k[8]) {
-#define MTX_CX(i, j)                                  \
-  {                                                   \
-    const uint32_t a_ = k[i], b_ = k[j];              \
-    k[i] = a_ < b_ ? a_ : b_;                         \
-    k[j] = a_ < b_ ? b_ : a_;                         \
-  }
-  MTX_CX(0, 2) MTX_CX(1, 3) MTX_CX(4, 6) MTX_CX(5, 7)
-  MTX_CX(0, 4) MTX_CX(1, 5) MTX_CX(2, 6) MTX_CX(3, 7)
-  MTX_CX(0, 1) MTX_CX(2, 3) MTX_CX(4, 5) MTX_CX(6, 7)
-  MTX_CX(2, 4) MTX_CX(3, 5)
-  MTX_CX(1, 4) MTX_CX(3, 6)
-  MTX_CX(1, 2) MTX_CX(3, 4) MTX_CX(5, 6)
-#undef MTX_CX
-}
-
-// Entry distance bound of a sort key (the culling test: skip when > t_best).
-MTX_HD float cw_key_t(uint32_t key) { return u2f(key & 0x7ffffff8u); }
-
 // Node index of the inner child at hit-mask bit 24 + p (p = slot ^ oct).
 MTX_HD uint32_t cw_inner_child(uint32_t child_base, uint32_t imask, uint32_t oct, uint32_t p) {
   const uint32_t slot = p ^ oct;

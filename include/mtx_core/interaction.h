@@ -18,7 +18,6 @@ struct SceneView {
   const float *tri_geom;        // its leaf-order triangle records (the scene's triangle order)
   const int32_t *occ_nodes;     // occlusion BVH (mtx.h, 20 words per node)
   const float *occ_tri_geom;    // its own leaf-order copy of the records
-  const uint32_t *occ_perm;     // scene triangle of each occlusion leaf-order triangle
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;
   const float *vpos;

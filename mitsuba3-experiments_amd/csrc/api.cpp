@@ -130,7 +130,7 @@ struct mtx_ctx {
   bool has_nerad = false;
   uint32_t scene_n_shapes = 0;
   DevBuf nr_lhs, nr_qp, nr_qd, nr_Lrhs, nr_lanes;
-  DevBuf nodes, tri, occ_nodes, occ_tri, occ_prim, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
+  DevBuf nodes, tri, occ_nodes, occ_tri, tri_vidx, tri_shape, vpos, vnormal, vuv, shapes, materials, emitters, textures, texels, tables;
   mtxd::DevScene scene{};
   // wavefront
   DevBuf ray_o, ray_d, thr, L, prev, misc, pos, hit, q0, q1, shadow, counters, stats;
@@ -149,6 +149,7 @@ struct mtx_ctx {
   // scratch for sample_rays / trace / primitives
   DevBuf s0, s1, s2, s3, s4, s5, s6;
   int trace_grid = 0, shade_grid = 0;
+  size_t max_lds = 160 * 1024;  // LDS one workgroup may hold (gfx950: the CU's 160 KiB)
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
   uint32_t lds_stack = mtxd::kLdsStack;
@@ -159,8 +160,6 @@ struct mtx_ctx {
   uint32_t urefill = 24;  // refill a wave once 24 lanes are idle (16: closest +1.3 %, 32: +2 %; 4-wide BVH)
   uint32_t occ_urefill = 12;  // any hit on the 8-wide tree (MTX_OCC_UREFILL; 8-16 alike, 24: shadow +1 ms, 32/40: +2/+3 ms)
   uint32_t xcd_claim = 1;
-  // closest hit of the wavefront kernels on the 8-wide tree (MTX_CLOSEST_CW=1)
-  uint32_t closest_cw = MTX_CLOSEST_CW;
   // ReSTIR GI: a band of at most this many paths runs its stage A in the
   // per-lane megakernel on one wavefront (MTX_MEGA_PATHS, 0 = off; default
   // 0xffffffff = twice the resident lanes of the megakernel's grid,
@@ -227,6 +226,15 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   // grid is recomputed per scene: its LDS stack depends on the BVH depth).
   c->trace_grid = c->n_cu * 8;
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
+  {
+    // a gfx950 workgroup may hold the CU's whole 160 KiB of LDS (the attribute
+    // may report the 64 KiB that needs no opt-in; the kernels launch above it)
+    int v = 0;
+    c->max_lds = 160 * 1024;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, hip_device) == hipSuccess &&
+        (size_t)v > c->max_lds)
+      c->max_lds = (size_t)v;
+  }
   if (const char *e = getenv("MTX_LDS_STACK")) c->lds_stack = std::max(1, std::min(MTX_BVH_MAX_DEPTH + 1, atoi(e)));
   if (const char *e = getenv("MTX_LDS_TOP")) c->lds_top = (uint32_t)std::max(0, std::min(256, atoi(e)));
   if (const char *e = getenv("MTX_OCC_LDS_TOP")) c->occ_lds_top = (uint32_t)std::max(0, std::min(192, atoi(e)));
@@ -236,7 +244,6 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   if (const char *e = getenv("MTX_STREAMS")) c->streams = (uint32_t)std::max(1, std::min(2, atoi(e)));
   if (const char *e = getenv("MTX_TRACE_BATCH")) c->trace_batch = (uint32_t)std::max(1, std::min(1 << 16, atoi(e)));
   if (const char *e = getenv("MTX_UREFILL")) c->urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
-  if (const char *e = getenv("MTX_CLOSEST_CW")) c->closest_cw = atoi(e) ? 1u : 0u;
   if (const char *e = getenv("MTX_OCC_UREFILL")) c->occ_urefill = (uint32_t)std::max(1, std::min(64, atoi(e)));
   if (const char *e = getenv("MTX_XCD_CLAIM")) c->xcd_claim = atoi(e) != 0;
   if (const char *e = getenv("MTX_RS_FUSED")) c->rs_fused = atoi(e) ? 1u : 0u;
@@ -253,7 +260,7 @@ void mtx_ctx_destroy(mtx_ctx *c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->w2.stream) hipStreamSynchronize(c->w2.stream);
-  DevBuf *bufs[] = {&c->nodes,  &c->tri, &c->occ_nodes, &c->occ_tri, &c->occ_prim, &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
+  DevBuf *bufs[] = {&c->nodes,  &c->tri, &c->occ_nodes, &c->occ_tri, &c->tri_vidx, &c->tri_shape, &c->vpos,     &c->vnormal, &c->vuv,
                     &c->shapes, &c->materials, &c->emitters, &c->textures, &c->texels, &c->tables, &c->ray_o,
                     &c->ray_d,  &c->thr,     &c->L,        &c->prev,      &c->misc,     &c->pos,     &c->hit,
                     &c->q0,     &c->q1,      &c->shadow,   &c->counters, &c->xheads, &c->rs_heads,  &c->stats,    &c->contrib, &c->film,
@@ -362,23 +369,18 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   std::vector<uint32_t> occ_perm_v;
   const int32_t *occ_nodes = d->occ_nodes;
   const float *occ_geom = d->occ_tri_geom;
-  const uint32_t *occ_perm = d->occ_perm;
   uint32_t n_occ = d->n_occ_nodes;
   int rc = 0;
   if (!occ_given) {
     occ_nodes_v.resize(((size_t)d->n_tris + 1) * MTX_OCC_NODE_WORDS);
     occ_geom_v.resize(12 * (size_t)d->n_tris);
-    occ_perm_v.resize(d->n_tris);
     if ((rc = mtx_bvh_build_occlusion(d->tri_geom, d->n_tris, occ_nodes_v.data(), &n_occ, occ_geom_v.data(),
-                                      occ_perm_v.data(), nullptr)))
+                                      nullptr, nullptr)))
       return rc;
     occ_nodes = occ_nodes_v.data();
     occ_geom = occ_geom_v.data();
-    occ_perm = occ_perm_v.data();
-  } else if ((rc = occ_match(d, occ_perm_v))) {
+  } else if ((rc = occ_match(d, occ_perm_v))) {  // given trees: their records must be this scene's
     return rc;
-  } else {
-    occ_perm = occ_perm_v.data();
   }
   // Validate both trees (mtx.h) on the host so that no kernel can read out
   // of bounds, and find their depths (stack entries: a 4-wide level pushes
@@ -504,8 +506,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     if ((rc = upload(tree ? c->occ_tri : c->tri, g9.data(), g9.size(), st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));  // g9 is freed at scope exit
   }
-  if ((rc = upload(c->occ_prim, occ_perm, (size_t)d->n_tris, st))) return rc;
-  HIP_TRY(hipStreamSynchronize(st));  // occ_perm_v is freed at scope exit
   if ((rc = upload(c->tri_vidx, d->tri_vidx, 3ull * d->n_tris, st))) return rc;
   if ((rc = upload(c->tri_shape, d->tri_shape, (size_t)d->n_tris, st))) return rc;
   if ((rc = upload(c->vpos, d->vpos, 3ull * d->n_verts, st))) return rc;
@@ -556,7 +556,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.tri = (const float *)c->tri.p;
   s.occ_nodes = (const int4 *)c->occ_nodes.p;
   s.occ_tri = (const float *)c->occ_tri.p;
-  s.occ_prim = (const uint32_t *)c->occ_prim.p;
   s.tri_vidx = (const uint32_t *)c->tri_vidx.p;
   s.tri_shape = (const uint32_t *)c->tri_shape.p;
   s.vpos = (const float *)c->vpos.p;
@@ -581,8 +580,6 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.occ_stack_entries = occ_depth + 1;
   s.occ_lds_entries = std::min<uint32_t>(s.occ_stack_entries, c->occ_lds_stack);
   s.occ_lds_top = std::min<uint32_t>(n_occ, c->occ_lds_top);
-  s.cw_stack_entries = 7 * occ_depth + 1;
-  s.closest_cw = c->closest_cw;
   s.trace_batch = c->trace_batch;
   s.urefill = c->urefill;
   s.occ_urefill = c->occ_urefill;
@@ -867,7 +864,7 @@ struct Timer {
 // Encode + MLP + L += T * out for the chunk's compacted cache queries (on
 // `stream` with the feature / output buffers of the chunk's wavefront: the
 // context's by default, the second wavefront's in a two-stream render).
-void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false,
+int run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, bool nerad_render = false,
                hipStream_t stream = nullptr, DevBuf *feat = nullptr, DevBuf *out = nullptr, DevBuf *perm_buf = nullptr,
                DevBuf *cursor_buf = nullptr) {
   hipStream_t st = stream ? stream : c->stream;
@@ -900,24 +897,31 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
         perm = (const uint32_t *)c->cq_perm.p;
     }
   }
-  if (c->cache_fused && !nerad_render) {
+  // the fused pass only when its LDS fits a workgroup (n_hidden <= 14)
+  const bool fused = c->cache_fused && !nerad_render && mtxd::field_cache_fused_lds(c->field_hidden) <= c->max_lds;
+  int rc = MTX_OK;
+  if (fused) {
     // encode + MLP + L += T * out in one launch (field.hip k_field_cache_fused),
     // timed as the encode
-    mtxd::field_cache_fused(c->field, b.cq_p, b.cq_d, b.cq_t, b.cq_count, cap, perm, xcd_split, c->field_frag.p,
-                            c->field_hidden, b.L[mtxd::kFinal], c->n_cu, st);
+    rc = mtxd::field_cache_fused(c->field, b.cq_p, b.cq_d, b.cq_t, b.cq_count, cap, perm, xcd_split,
+                                 c->field_frag.p, c->field_hidden, b.L[mtxd::kFinal], c->n_cu, st);
     tm.end(4, e, st);
+    if (rc) return rc;
   } else {
-    mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split,
-                       (int)c->encode_lm);
+    rc = mtxd::field_encode(c->field, b.cq_p, b.cq_d, b.cq_count, cap, (uint16_t *)f_feat.p, st, perm, xcd_split,
+                            (int)c->encode_lm);
     tm.end(4, e, st);
+    if (rc) return rc;
     e = tm.begin(5, st);
-    mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
-                    (float *)f_out.p, c->n_cu, st);
+    rc = mtxd::field_mlp((const uint16_t *)f_feat.p, b.cq_count, cap, c->field_frag.p, c->field_hidden,
+                         (float *)f_out.p, c->n_cu, st);
     tm.end(5, e, st);
+    if (rc) return rc;
     if (nerad_render)
       mtxd::launch_nerad_apply(b, (const float *)f_out.p, cap, 1, st);
     else
       mtxd::launch_cache_apply(b, (const float *)f_out.p, cap, st, perm);
+    HIP_TRY(hipGetLastError());
   }
   if (tm.on) {  // counted after the render's final synchronisation (fill_stats): no per-chunk sync
     if (!c->q_pinned && hipHostMalloc((void **)&c->q_pinned, 4 * kQSlots) != hipSuccess) c->q_pinned = nullptr;
@@ -930,6 +934,7 @@ void run_cache(mtx_ctx *c, const mtxd::WaveBuffers &b, uint32_t cap, Timer &tm, 
         tm.cache_queries += nq;
     }
   }
+  return MTX_OK;
 }
 
 // One bounce of a chunk: closest hit, shade, NEE shadow rays.
@@ -1437,11 +1442,13 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     run_bounces(c, bc, p, tm, &n_trace, &n_shadow, &sc, st);
     if (nrc_cache) {
       if (second)
-        run_cache(c, bc, p.n_paths, tm, false, st, &c->w2.f_feat, &c->w2.f_out, &c->w2.cq_perm, &c->w2.cq_cursor);
+        rc = run_cache(c, bc, p.n_paths, tm, false, st, &c->w2.f_feat, &c->w2.f_out, &c->w2.cq_perm,
+                       &c->w2.cq_cursor);
       else
-        run_cache(c, b, p.n_paths, tm);
+        rc = run_cache(c, b, p.n_paths, tm);
+      if (rc) return rc;
     }
-    if (nerad_render) run_cache(c, b, p.n_paths, tm, true);
+    if (nerad_render && (rc = run_cache(c, b, p.n_paths, tm, true))) return rc;
     mtxd::launch_film_src(bc, p, (float4 *)c->contrib.p, st);
   }
   if (two) {  // the film gather reads both wavefronts' contributions
@@ -1591,8 +1598,8 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
     mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
     run_bounces(c, b, p, tm, &nt, &ns);
-    if (nrc_cache) run_cache(c, b, m, tm);
-    if (nerad_render) run_cache(c, b, m, tm, true);
+    if (nrc_cache && (rc = run_cache(c, b, m, tm))) return rc;
+    if (nerad_render && (rc = run_cache(c, b, m, tm, true))) return rc;
     mtxd::launch_collect(b, p, (float *)c->s2.p, (uint8_t *)c->s3.p, c->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));
@@ -1611,8 +1618,8 @@ int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *
     mtx_set_error("no scene uploaded");
     return MTX_E_NOSCENE;
   }
-  if (any_hit < 0 || any_hit > 2) {
-    mtx_set_error("mtx_trace: mode %d (0 closest hit, 1 any hit, 2 closest hit on the 8-wide tree)", any_hit);
+  if (any_hit < 0 || any_hit > 1) {
+    mtx_set_error("mtx_trace: mode %d (0 closest hit, 1 any hit)", any_hit);
     return MTX_E_ARG;
   }
   if (n == 0) return MTX_OK;

@@ -24,9 +24,7 @@ using namespace mtx;
 // (stride kTraceBlock: every kernel that calls traverse_closest / traverse_occ
 // runs blocks of kTraceBlock threads; k_path_mega asserts it.)
 inline size_t stack_bytes(const DevScene &s) {
-  size_t a = s.stack_entries, b = 2 * (size_t)s.occ_stack_entries;
-  const size_t c = 2 * (size_t)s.occ_lds_entries;  // traverse_closest_cw's LDS part
-  if (c > b) b = c;
+  const size_t a = s.stack_entries, b = 2 * (size_t)s.occ_stack_entries;
   return (a > b ? a : b) * sizeof(uint32_t) * kTraceBlock;
 }
 // The persistent kernels keep only the top lds_entries entries in LDS (so
@@ -796,216 +794,11 @@ __device__ __forceinline__ void trace_loop_occ(const DevScene &s, const Src &src
   }
 }
 
-// ===========================================================================
-// Closest hit on the 8-wide tree (round 5, MTX_CLOSEST_CW): a visit sorts the
-// hit inner children by entry distance (mtx_core/geometry.h cw_node_keys +
-// cw_sort8), keeps the nearest as the lane's pending node and pushes the
-// others far to near as (node, key) stack entries; the node's hit leaves'
-// triangles (its triangle group) are tested before the pending node is
-// visited. A pending or popped node whose entry distance (cw_key_t) is beyond
-// the current hit is dropped without a fetch. Triangles are the occlusion
-// tree's; hits report scene triangles (DevScene::occ_prim), exact t ties go
-// to the smaller scene triangle as in trace_closest. Visit order and counts
-// equal oracle/oracle.cpp trace_closest_cw.
-// ===========================================================================
-constexpr uint32_t kNoNode = 0xffffffffu;
-
-__device__ __forceinline__ uint32_t cw_visit_keys(const DevScene &s, const TraceRay &r, uint32_t oct, uint32_t node,
-                                                  float tbest, const int4 *top, int top_n, uint32_t key[8],
-                                                  uint32_t &child_base, uint32_t &tri_base) {
-  int4 a, b, q0, q1, q2;
-  if ((int)node < top_n) {
-    lds_node80(top, node, a, b, q0, q1, q2);
-  } else {
-    const int4 *np = s.occ_nodes + 5 * (size_t)node;
-    a = np[0];
-    b = np[1];
-    q0 = np[2];
-    q1 = np[3];
-    q2 = np[4];
-  }
-  const uint32_t q[12] = {(uint32_t)q0.x, (uint32_t)q0.y, (uint32_t)q0.z, (uint32_t)q0.w,
-                          (uint32_t)q1.x, (uint32_t)q1.y, (uint32_t)q1.z, (uint32_t)q1.w,
-                          (uint32_t)q2.x, (uint32_t)q2.y, (uint32_t)q2.z, (uint32_t)q2.w};
-  child_base = (uint32_t)b.x;
-  tri_base = (uint32_t)b.y;
-  const uint32_t bits = cw_node_keys(r, oct, __int_as_float(a.x), __int_as_float(a.y), __int_as_float(a.z),
-                                     (uint32_t)a.w, (uint32_t)b.z, (uint32_t)b.w, q, tbest, key);
-  cw_sort8(key);
-  return bits;
-}
-
-// Stack entry e of a lane (uint2): LDS below lds_n, the global spill area
-// above (kept apart so that no flat store through a selected pointer is
-// generated).
-__device__ __forceinline__ void stack_write(uint2 *stk, uint2 *ovf, int e, int lds_n, uint32_t ovf_threads, uint2 v) {
-  if (e < lds_n) {
-    stk[e * kTraceBlock] = v;
-  } else {
-    ovf[(size_t)(e - lds_n) * ovf_threads] = v;
-    asm volatile("" ::: "memory");
-  }
-}
-
-// After a visit: the pending node (nearest hit inner child) and the pushes of
-// the others, far first; returns the new stack size.
-__device__ __forceinline__ int cw_push_sorted(uint2 *stk, uint2 *ovf, int sp, int lds_n, uint32_t ovf_threads,
-                                              const uint32_t key[8], uint32_t child_base, uint32_t &nn,
-                                              uint32_t &nk) {
-  int n = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) n += key[j] != 0xffffffffu ? 1 : 0;
-  nn = n ? child_base + (key[0] & 7u) : kNoNode;
-  nk = key[0];
-#pragma unroll
-  for (int j = 7; j >= 1; --j)
-    if (j < n) stack_write(stk, ovf, sp + (n - 1 - j), lds_n, ovf_threads, make_uint2(child_base + (key[j] & 7u), key[j]));
-  return n > 1 ? sp + n - 1 : sp;
-}
-
-// Tie rule of the 8-wide closest hit: t smaller, or equal with the smaller
-// scene triangle (best == kNoNode: nothing hit yet).
-__device__ __forceinline__ bool cw_take(const DevScene &s, float t, float tbest, uint32_t pr, uint32_t best) {
-  if (t < tbest) return true;
-  if (t != tbest) return false;
-  return best == kNoNode || s.occ_prim[pr] < s.occ_prim[best];
-}
-
-// Per-thread form (mtx_trace closest hit on the 8-wide tree): stk / ovf as
-// in the persistent loop; prim_out is the scene triangle.
-__device__ __forceinline__ void traverse_closest_cw(const DevScene &s, uint2 *stk, uint2 *ovf, const TraceRay &r,
-                                                    float &tbest, uint32_t &prim_out, float &bu, float &bv,
-                                                    uint32_t &nv, uint32_t &tv) {
-  const uint32_t oct = ray_octant(r);
-  const int lds_n = (int)s.occ_lds_entries;
-  uint32_t nn = 0, nk = 0, best = kNoNode;
-  int sp = 0;
-  while (true) {
-    if (nn != kNoNode && cw_key_t(nk) <= tbest) {
-      uint32_t key[8], cb, tb;
-      ++nv;
-      uint32_t thits = cw_visit_keys(s, r, oct, nn, tbest, nullptr, 0, key, cb, tb);
-      sp = cw_push_sorted(stk, ovf, sp, lds_n, s.ovf_threads, key, cb, nn, nk);
-      while (thits) {
-        const uint32_t pr = tb + (uint32_t)ctz32(thits);
-        thits &= thits - 1u;
-        const TriGeom g = load_tri(s.occ_tri, pr);
-        float t, u, v;
-        ++tv;
-        if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v) && cw_take(s, t, tbest, pr, best)) {
-          tbest = t;
-          best = pr;
-          bu = u;
-          bv = v;
-        }
-      }
-      continue;
-    }
-    nn = kNoNode;
-    while (sp > 0) {
-      --sp;
-      const uint2 e = stack_read(stk, ovf, sp, lds_n, s.ovf_threads);
-      if (cw_key_t(e.y) <= tbest) {
-        nn = e.x;
-        nk = e.y;
-        break;
-      }
-    }
-    if (nn == kNoNode) break;
-  }
-  prim_out = best == kNoNode ? 0xffffffffu : s.occ_prim[best];
-}
-
-template <bool STATS, class Src>
-__device__ __forceinline__ void trace_loop_closest_cw(const DevScene &s, const Src &src, uint32_t count,
-                                                      uint32_t *heads, uint2 *stk, const int4 *top, uint32_t &nv,
-                                                      uint32_t &tv, uint32_t &nr, uint32_t *wave_iters) {
-  const uint32_t lane = lane_id();
-  uint2 *ovf = reinterpret_cast<uint2 *>(s.stack_ovf) + blockIdx.x * kTraceBlock + threadIdx.x;
-  const int lds_n = (int)s.occ_lds_entries, top_n = (int)s.occ_lds_top;
-  RayReservoir res;
-  if (!res.start(s, heads, count)) return;
-  bool has = false;
-  typename Src::Payload payload{};
-  TraceRay r;
-  float tbest = 0.f, bu = 0.f, bv = 0.f;
-  uint32_t oct = 0, best = kNoNode, nn = kNoNode, nk = 0, tbase = 0, thits = 0;
-  int sp = 0;
-  while (true) {
-    if (!res.exhausted) {
-      const uint64_t idle = __ballot(!has);
-      if ((uint32_t)__popcll(idle) >= s.urefill || idle == ~0ull) {
-        uint32_t k;
-        bool ok;
-        res.take(s, idle, lane, k, ok);
-        if (!has && ok) {
-          src.load(k, r, tbest, payload);
-          oct = ray_octant(r);
-          best = kNoNode;
-          bu = bv = 0.f;
-          nn = 0;  // the root
-          nk = 0;
-          thits = 0;
-          sp = 0;
-          has = true;
-        }
-      }
-    }
-    if (__ballot(has) == 0) break;
-    // ---- one node visit: the pending node, unless it lies beyond the hit
-    if (has && thits == 0 && nn != kNoNode) {
-      if (cw_key_t(nk) > tbest) {
-        nn = kNoNode;
-      } else {
-        if (STATS) count_wave_iter(lane, &wave_iters[0]);
-        ++nv;
-        uint32_t key[8], cb;
-        thits = cw_visit_keys(s, r, oct, nn, tbest, top, top_n, key, cb, tbase);
-        sp = cw_push_sorted(stk, ovf, sp, lds_n, s.ovf_threads, key, cb, nn, nk);
-      }
-    }
-    // ---- one triangle test of the triangle group
-    if (has && thits != 0) {
-      if (STATS) count_wave_iter(lane, &wave_iters[1]);
-      const uint32_t pr = tbase + (uint32_t)ctz32(thits);
-      thits &= thits - 1u;
-      const TriGeom g = load_tri(s.occ_tri, pr);
-      float t, u, v;
-      ++tv;
-      if (tri_intersect(r, g.p0, g.e1, g.e2, tbest, &t, &u, &v) && cw_take(s, t, tbest, pr, best)) {
-        tbest = t;
-        best = pr;
-        bu = u;
-        bv = v;
-      }
-    }
-    // ---- nothing pending: pop, dropping entries beyond the hit; or finish
-    if (has && thits == 0 && nn == kNoNode) {
-      while (sp > 0) {
-        --sp;
-        const uint2 e = stack_read(stk, ovf, sp, lds_n, s.ovf_threads);
-        if (cw_key_t(e.y) <= tbest) {
-          nn = e.x;
-          nk = e.y;
-          break;
-        }
-      }
-      if (nn == kNoNode) {
-        src.finish(payload, best != kNoNode, tbest, best == kNoNode ? 0xffffffffu : s.occ_prim[best], bu, bv);
-        has = false;
-        ++nr;
-      }
-    }
-  }
-}
-
 // The persistent traversal of a block: ANY = any hit on the occlusion tree,
 // else closest hit on the 4-wide tree. The block's dynamic LDS holds the
 // stack columns and then the tree top (persistent_stack_bytes), filled here
 // behind a barrier; every thread of the block calls this.
-// CW: closest hit on the 8-wide tree (trace_loop_closest_cw; its LDS is the
-// any-hit kernel's: node-group-sized stack entries and the 80-B tree top).
-template <bool ANY, bool STATS = false, bool CW = false, class Src>
+template <bool ANY, bool STATS = false, class Src>
 __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                            uint32_t &nv, uint32_t &tv, uint32_t &nr,
                                            uint32_t *wave_iters = nullptr) {
@@ -1017,15 +810,12 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     const uint32_t batch = max(64u, min(s.trace_batch, (count / n_grid_waves) & ~63u));
     if (blockIdx.x * (kTraceBlock / 64u) >= (count + batch - 1) / batch) return;
   }
-  if (ANY || CW) {
+  if (ANY) {
     uint2 *cols = reinterpret_cast<uint2 *>(trace_lds);
     int4 *top = reinterpret_cast<int4 *>(cols + s.occ_lds_entries * kTraceBlock);
     for (uint32_t i = threadIdx.x; i < 5 * s.occ_lds_top; i += kTraceBlock) top[i] = s.occ_nodes[i];
     __syncthreads();
-    if constexpr (CW && !ANY)
-      trace_loop_closest_cw<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
-    else
-      trace_loop_occ<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
+    trace_loop_occ<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
   } else {
     int32_t *cols = reinterpret_cast<int32_t *>(trace_lds);
     int4 *top = reinterpret_cast<int4 *>(cols + s.lds_entries * kTraceBlock);

@@ -377,16 +377,30 @@ int field_cache_fused(const FieldEncoding &e, const float4 *qp, const float4 *qd
     return MTX_E_ARG;
   }
   const uint32_t n_frag = field_frag_count(n_hidden);
-  const size_t lds = (size_t)n_frag * 64 * sizeof(half8) + (size_t)kFusedQ * kFieldPad * 2 + kFusedQ * sizeof(float4);
+  const size_t lds = field_cache_fused_lds(n_hidden);
   unsigned blocks = (unsigned)std::max<uint64_t>(
       1, std::min<uint64_t>((n_max + kFusedQ - 1) / kFusedQ, (uint64_t)n_cu * 2));
   if (xcd_split) blocks = (blocks + 7u) & ~7u;
   hipLaunchKernelGGL(k_field_cache_fused, dim3(blocks), dim3(512), lds, st, e, qp, qd, qt, count, n_max, perm,
                      xcd_split, (const half8 *)wfrag, n_frag, n_hidden, L_final);
+  const hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    mtx_set_error("field_cache_fused: launch failed (%zu B of LDS): %s", lds, hipGetErrorString(err));
+    return MTX_E_HIP;
+  }
   return MTX_OK;
 }
 
 uint32_t field_frag_count(uint32_t n_hidden) { return 8 * (1 + n_hidden) + 4; }
+
+// Dynamic LDS of k_field_cache_fused: the prepacked weight fragments + the
+// block's 256 feature rows + their T / path records (n_hidden 15 / 16 need
+// more than the 160 KB a workgroup may hold: run_cache then takes the
+// three-kernel path).
+size_t field_cache_fused_lds(uint32_t n_hidden) {
+  return (size_t)field_frag_count(n_hidden) * 64 * sizeof(half8) + (size_t)kFusedQ * kFieldPad * 2 +
+         kFusedQ * sizeof(float4);
+}
 
 // Host: weight matrices (fp16 bits, W[out][in] row-major per layer: input
 // n_in -> 64, n_hidden x 64 -> 64, 64 -> 3) -> MFMA A fragments.

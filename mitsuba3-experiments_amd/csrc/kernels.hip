@@ -60,14 +60,13 @@ struct ClosestSrc {
 // fits without spills. Shadow 56.4 -> 55.6 ms per step (A/B, one box, 3
 // rounds, round 2).
 #define MTX_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
-// CW: on the 8-wide tree (trace_loop_closest_cw), else the 4-wide tree.
-template <bool STATS, bool CW>
+template <bool STATS>
 __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   // dynamic LDS: stack columns + tree top (device_common.h trace_loop)
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
   uint32_t nv = 0, tv = 0, nr = 0, wi[2] = {0, 0};
-  trace_loop<false, STATS, CW>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, nv, tv, nr,
+  trace_loop<false, STATS>(s, src, b.counters[4 * bounce + 0], b.xheads + (2 * bounce) * kXSlotWords, nv, tv, nr,
                            wi);
   if (STATS) {
     unsigned long long a = wave_sum_u64(nv), c = wave_sum_u64(tv), n = wave_sum_u64(nr);
@@ -275,14 +274,31 @@ struct ShadeIO {
 #endif
 };
 
+// Which shadow-record form an integrator's NEE must use (ShadowSrc::finish
+// reads it from flag bit 4, kShadowFinal): true where k_shade itself stores
+// the path's L at the queue slot / final plane after the bounce, so the L the
+// record is built from is final for the bounce and the any-hit finish may
+// overwrite L without reading it (final-value form); false where L lives by
+// path outside k_shade's stores (the neural-radiosity RHS: k_nerad_apply adds
+// to it), so the finish must read-modify-write L. make_shadow<INT> checks the
+// choice at compile time: a new integrator that emits shadow rays must be
+// listed here (the round-5 nerad regression was this choice made wrongly).
+constexpr bool shadow_final_form(int INT) {
+  return INT == MTX_INT_PATH || INT == MTX_INT_PATH_MIS || INT == MTX_INT_NRC || INT == MTX_INT_PSSMLT_PATH;
+}
+constexpr bool shadow_rmw_form(int INT) { return INT == MTX_INT_NERAD_RHS; }
+
 // Builds the shadow record for an NEE contribution. fma_form: value = (T, X)
 // applied as fma(T, X, L); otherwise X is added. Xo is the contribution the
 // reference forms when the shadow ray is occluded (em_weight = 0). With Lcur
 // (the path's L, final for this bounce: the integrators that k_shade stores
 // L for add nothing to L after their NEE) the record is built in its
 // final-value form (see ShadowSrc; k_shade completes x.w with L.w).
+template <int INT, bool FINAL>
 __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteraction &si, const DirectionSample &ds,
                                             V3 T, V3 X, V3 Xo, bool fma_form, const V3 *Lcur = nullptr) {
+  static_assert(FINAL ? shadow_final_form(INT) : shadow_rmw_form(INT),
+                "shadow record form does not match where this integrator's L is stored (shadow_final_form)");
   uint32_t fl = fma_form ? 1u : 0u;
   bool vis_noop, occ_noop;
   if (fma_form) {
@@ -303,7 +319,7 @@ __device__ __forceinline__ void make_shadow(ShadeIO &io, const SurfaceInteractio
   const Ray sr = spawn_ray_to(si.p, si.n, ds.p);
   io.rec.o = make_float4(sr.o.x, sr.o.y, sr.o.z, sr.maxt);
   io.rec.d = make_float4(sr.d.x, sr.d.y, sr.d.z, 0.f);  // .w: the L index, set by k_shade after its append
-  if (Lcur) {
+  if constexpr (FINAL) {
     float4 lv = make_float4(Lcur->x, Lcur->y, Lcur->z, 0.f);
     apply_shadow(lv, make_float4(T.x, T.y, T.z, __uint_as_float(fl)), make_float4(X.x, X.y, X.z, 0.f), false);
     io.rec.t = make_float4(lv.x, lv.y, lv.z, __uint_as_float(fl | kShadowFinal));
@@ -515,14 +531,14 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
     if (active_em) {
       const V3 X = bsdf_val * em_weight * mi_em;
       const V3 Xo = bsdf_val * v3s(0.f) * mi_em;
-      make_shadow(io, si, ds, T, X, Xo, true, &L);
+      make_shadow<INT, true>(io, si, ds, T, X, Xo, true, &L);
     }
   } else {
     const float mis_em = INT == MTX_INT_PATH ? mis_weight_a(ds.pdf, bsdf_pdf) : mis_weight_b(ds.pdf, bsdf_pdf);
     if (active_em) {
       const V3 P = T * bsdf_val * em_weight * mis_em;
       const V3 Po = T * bsdf_val * v3s(0.f) * mis_em;
-      make_shadow(io, si, ds, T, P, Po, false, &L);
+      make_shadow<INT, true>(io, si, ds, T, P, Po, false, &L);
     }
   }
 
@@ -789,7 +805,7 @@ __device__ __forceinline__ bool shade_pssmlt_path(const DevScene &s, const Scene
     float epdf;
     bsdf_eval_pdf(bd, mat, si.uv, si.wi, wo, &ev, &epdf);
     const float mi_em = mis_weight_b(ds.pdf, epdf);
-    make_shadow(io, si, ds, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true, &L);
+    make_shadow<MTX_INT_PSSMLT_PATH, true>(io, si, ds, T, ev * em_weight * mi_em, ev * v3s(0.f) * mi_em, true, &L);
   }
   b.vprop[vi] = make_float4(vwo.x, vwo.y, vwo.z, 0.f);  // :138
   b.vprop_es[vi] = make_float2(es.x, es.y);
@@ -864,7 +880,7 @@ __device__ __forceinline__ bool shade_nerad(const DevScene &s, const SceneView &
     float pdf;
     bsdf_eval_pdf(sv.bsdf, mat, si.uv, si.wi, to_local(si.sh, ds.d), &val, &pdf);  // :198
     const float mis = mis_weight_b(ds.pdf, pdf);
-    make_shadow(io, si, ds, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :200
+    make_shadow<MTX_INT_NERAD_RHS, false>(io, si, ds, v3s(1.f), val * mis * em, val * mis * v3s(0.f), false);  // :200
     const float s1 = rng.next_1d();
     const V2 s2 = rng.next_2d();
     BSDFSample bs;
@@ -1542,9 +1558,7 @@ __global__ void k_collect(WaveBuffers b, ChunkParams p, float *L_out, uint8_t *v
 }
 
 // Raw traversal for mtx_trace: rays as (o.xyz, maxt), (d.xyz, 0). mode 0
-// closest hit (4-wide tree), 1 any hit, 2 closest hit on the 8-wide tree
-// (its stack spills to the wavefront's global area: the grid is at most the
-// persistent trace grid, grid-stride over the rays).
+// closest hit (4-wide tree), 1 any hit (8-wide occlusion tree).
 __device__ __forceinline__ void trace_raw_one(const DevScene &s, const float4 *rays, uint32_t i, int any_hit,
                                               uint32_t *hits, uint32_t *visits, int4 *raw_lds) {
   const float4 o4 = rays[2 * (size_t)i], d4 = rays[2 * (size_t)i + 1];
@@ -1554,12 +1568,7 @@ __device__ __forceinline__ void trace_raw_one(const DevScene &s, const float4 *r
   if (any_hit == 1) {
     hits[i] = traverse_occ(s, reinterpret_cast<uint32_t *>(raw_lds) + threadIdx.x, r, o4.w, nv, tv) ? 1u : 0u;
   } else {
-    if (any_hit == 2)
-      traverse_closest_cw(s, reinterpret_cast<uint2 *>(raw_lds) + threadIdx.x,
-                          reinterpret_cast<uint2 *>(s.stack_ovf) + blockIdx.x * kTraceBlock + threadIdx.x, r, tbest,
-                          prim, bu, bv, nv, tv);
-    else
-      traverse_closest(s, reinterpret_cast<int32_t *>(raw_lds) + threadIdx.x, r, tbest, prim, bu, bv, nv, tv);
+    traverse_closest(s, reinterpret_cast<int32_t *>(raw_lds) + threadIdx.x, r, tbest, prim, bu, bv, nv, tv);
     if (prim == 0xffffffffu) tbest = kInf;
     hits[4 * (size_t)i + 0] = __float_as_uint(tbest);
     hits[4 * (size_t)i + 1] = prim;
@@ -1734,18 +1743,11 @@ void launch_raygen_rays(const DevScene &s, const WaveBuffers &b, const ChunkPara
 }
 void launch_trace_closest(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                           hipStream_t st) {
-  const size_t lds = persistent_stack_bytes(s, s.closest_cw != 0);
-  if (s.closest_cw) {
-    if (stats)
-      hipLaunchKernelGGL((k_trace_closest<true, true>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
-    else
-      hipLaunchKernelGGL((k_trace_closest<false, true>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
-  } else {
-    if (stats)
-      hipLaunchKernelGGL((k_trace_closest<true, false>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
-    else
-      hipLaunchKernelGGL((k_trace_closest<false, false>), dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
-  }
+  const size_t lds = persistent_stack_bytes(s, false);
+  if (stats)
+    hipLaunchKernelGGL(k_trace_closest<true>, dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
+  else
+    hipLaunchKernelGGL(k_trace_closest<false>, dim3(grid), dim3(kTraceBlock), lds, st, s, b, bounce);
 }
 void launch_trace_shadow(const DevScene &s, const WaveBuffers &b, uint32_t bounce, uint32_t stats, int grid,
                          hipStream_t st) {
@@ -1786,10 +1788,8 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
 // fewer of the two trees' kernels).
 int trace_blocks_per_cu(const DevScene &s) {
   int nc = 0, na = 0;
-  if (s.closest_cw ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false, true>, kTraceBlock,
-                                                                 persistent_stack_bytes(s, true)) != hipSuccess
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false, false>, kTraceBlock,
-                                                                 persistent_stack_bytes(s, false)) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false>, kTraceBlock,
+                                                   persistent_stack_bytes(s, false)) != hipSuccess ||
       nc <= 0)
     nc = 4;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&na, k_trace_shadow<false>, kTraceBlock,

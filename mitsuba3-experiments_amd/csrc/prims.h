@@ -52,6 +52,7 @@ void field_bucket_queries(const mtx::FieldEncoding &e, const float4 *qp, const u
 void field_morton_keys(const mtx::FieldEncoding &e, const float4 *qp, uint32_t n, uint32_t *keys, hipStream_t st);
 // The NRC cache pass in one launch: encode + MLP + L_final[path] += T * out
 // (qt: T.xyz, path bits in .w), rows in perm order.
+size_t field_cache_fused_lds(uint32_t n_hidden);
 int field_cache_fused(const mtx::FieldEncoding &e, const float4 *qp, const float4 *qd, const float4 *qt,
                       const uint32_t *count, uint32_t n_max, const uint32_t *perm, int xcd_split, const void *wfrag,
                       uint32_t n_hidden, float4 *L_final, int n_cu, hipStream_t st);

@@ -53,9 +53,6 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_OCC_LDS_TOP
 #define MTX_OCC_LDS_TOP 48  // occlusion tree nodes copied into LDS per trace block (0 = none)
 #endif
-#ifndef MTX_CLOSEST_CW
-#define MTX_CLOSEST_CW 0  // closest hit on the 8-wide tree (device_common.h trace_loop_closest_cw)
-#endif
 #ifndef MTX_SHADE_WARM
 #define MTX_SHADE_WARM 1  // k_shade: warm L2 with the next entry's shading record
 #endif
@@ -80,7 +77,6 @@ struct DevScene {
   const float *tri;       // its leaf-order triangles, 9 floats each (v0, e1, e2; device_common.h load_tri)
   const int4 *occ_nodes;  // occlusion BVH: 5 x int4 per node (the 80-B ABI node, mtx.h)
   const float *occ_tri;   // its own leaf-order copy of the triangles (9 floats each)
-  const uint32_t *occ_prim;  // scene triangle of each occlusion leaf-order triangle (mtx_scene_desc occ_perm)
   const uint32_t *tri_vidx;
   const uint32_t *tri_shape;
   const float *vpos;
@@ -99,8 +95,6 @@ struct DevScene {
   uint32_t lds_top;        // persistent kernels: nodes [0, lds_top) read from a per-block LDS copy
   uint32_t occ_stack_entries, occ_lds_entries, occ_lds_top;  // the same for the occlusion tree
                                                              // (depth + 1 entries: 8-B node groups)
-  uint32_t cw_stack_entries;  // closest hit on the 8-wide tree: 7 x depth + 1 entries of (node, key)
-  uint32_t closest_cw;        // 1: closest hit on the 8-wide tree (MTX_CLOSEST_CW), 0: the 4-wide tree
   uint32_t trace_batch;    // persistent kernels: queue entries claimed per atomic
   void *stack_ovf;         // persistent kernels: entries beyond the LDS part, [entry][thread]
                            // (int32 node refs for closest hit, uint2 node groups for occlusion)
@@ -116,10 +110,7 @@ struct DevScene {
 // overlap).
 inline size_t stack_ovf_bytes(const DevScene &s) {
   const size_t a = (size_t)(s.stack_entries - s.lds_entries) * sizeof(int32_t);
-  size_t b = (size_t)(s.occ_stack_entries - s.occ_lds_entries) * sizeof(uint2);
-  const size_t c = (size_t)(s.cw_stack_entries > s.occ_lds_entries ? s.cw_stack_entries - s.occ_lds_entries : 0) *
-                   sizeof(uint2);
-  if (c > b) b = c;
+  const size_t b = (size_t)(s.occ_stack_entries - s.occ_lds_entries) * sizeof(uint2);
   const size_t n = (a > b ? a : b) * s.ovf_threads;
   return n > 8 ? n : 8;
 }

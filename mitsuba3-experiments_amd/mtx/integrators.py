@@ -114,13 +114,15 @@ class SamplingIntegrator:
     def render_film(self, scene, seed: int = 0, spp: int = 1, y0: int = 0, y1: int | None = None,
                     spp_total: int | None = None, sample_offset: int = 0, device: int | None = None,
                     out=None, stats: bool = False, chunk_paths: int = 0, counters: bool = False, ctx=None,
-                    extra_flags: int = 0):
+                    extra_flags: int = 0, sensor=None):
         """Raw film (rows y0-1..y1, cols -1..W) x RGBW. `out` may be a
         device tensor (torch, on the context's device) to keep the film in HBM.
         stats=True returns (film, stats) with per-kernel-class HIP-event
         times; counters=True also collects the traversal visit counters
-        (slower kernels: use it outside timed regions)."""
+        (slower kernels: use it outside timed regions). `sensor`: the camera
+        to render through (:func:`scene_with_sensor`; None = the scene's)."""
         ctx = ctx or context(device)
+        scene = scene_with_sensor(scene, sensor)
         _bind_scene(ctx, scene)
         a = self.render_args(scene, seed, spp, y0, y1, spp_total, sample_offset, chunk_paths,
                              flags=(2 if stats else 0) | (1 if stats and counters else 0))
@@ -138,8 +140,10 @@ class SamplingIntegrator:
         return (film, st.as_dict()) if stats else film
 
     def render(self, scene, sensor=None, seed: int = 0, spp: int = 1, develop: bool = True, evaluate: bool = True):
-        """SamplingIntegrator.render (path.py:103-192): TensorXf[H, W, 3]."""
-        film = self.render_film(scene, seed=seed, spp=spp)
+        """SamplingIntegrator.render (path.py:103-192) through `sensor` (the
+        scene's own when None / 0, as mi.render does; testpssmlt.py:45 passes
+        scene.sensors()[0]): TensorXf[H, W, 3] of the sensor's film."""
+        film = self.render_film(scene, seed=seed, spp=spp, sensor=sensor)
         return globals()["develop"](film) if develop else film
 
     # --------------------------------------------------------------- sample --
@@ -349,8 +353,10 @@ class RestirIntegrator(SamplingIntegrator):
 
     def render_film(self, scene, seed: int = 0, spp: int = 1, device: int | None = None, out=None,
                     stats: bool = False, counters: bool = False, y0: int = 0, y1: int | None = None,
-                    stage: str | None = None, ctx=None, **kwargs):
-        """One frame (restirgi.py:182-258); advances the frame counter.
+                    stage: str | None = None, ctx=None, sensor=None, **kwargs):
+        """One frame (restirgi.py:182-258) through `sensor` (None: the
+        scene's camera); advances the frame counter. The previous frame's
+        camera is the context's prev_sensor (restirgi.py:226-227, :247).
 
         Row bands (multi-GPU): render rows [y0, y1) in two calls,
         stage="A" (initial sample + temporal) and stage="B" (spatial + final +
@@ -358,6 +364,7 @@ class RestirIntegrator(SamplingIntegrator):
         (:func:`mtx.distributed.restir_band_frame`)."""
         if kwargs.get("sample_offset", 0) or kwargs.get("spp_total") not in (None, spp):
             raise MtxError("ReSTIR GI renders all samples of its pixels")
+        scene = scene_with_sensor(scene, sensor)
         y1 = scene.height if y1 is None else int(y1)
         if stage not in (None, "A", "B"):
             raise MtxError(f"stage must be None, 'A' or 'B', not {stage!r}")
@@ -372,9 +379,7 @@ class RestirIntegrator(SamplingIntegrator):
         if self.n > 0 and owner is not self:
             raise MtxError("another ReSTIR integrator rendered on this device context since the last frame")
         ctx._restir_owner = self
-        self._ctx = ctx
-        cam = scene.camera
-        check(lib().mtx_set_camera(ctx.handle, C.byref(cam)), "mtx_set_camera")
+        self._ctx = ctx  # _bind_scene pointed the device camera at this frame's sensor
         flags = {None: 0, "A": _abi.MTX_RESTIR_STAGE_A, "B": _abi.MTX_RESTIR_STAGE_B}[stage]
         result = super().render_film(scene, seed=seed, spp=spp, device=device, out=out, stats=stats,
                                      counters=counters, y0=y0, y1=y1, ctx=ctx, extra_flags=flags)
@@ -419,22 +424,83 @@ register_integrator("integrator", lambda props: Simple(props))  # simple.py:119
 register_integrator("nerad", lambda props: NeradIntegrator(props))
 
 
+def scene_with_sensor(scene, sensor):
+    """The scene seen through `sensor` -- the ``sensor`` argument of
+    SamplingIntegrator.render / mi.render (testpssmlt.py:45, pssmlt.py:167-175,
+    restirgi.py:182-190): None or 0 (the scene's own sensor), an
+    ``mtx_camera``, an object with a ``camera`` (``Scene.sensors()[i]``), a
+    ``perspective`` sensor dictionary, or an ``mi.Sensor`` loaded with the
+    wrapped ``mi.load_dict``. Shares the scene's arrays (same geometry: the
+    device scene is re-pointed at the camera, not re-uploaded, unless the film
+    size differs)."""
+    if sensor is None or (isinstance(sensor, int) and not isinstance(sensor, bool) and sensor == 0):
+        return scene
+    if isinstance(sensor, int):
+        raise MtxError(f"sensor index {sensor}: the scene has one sensor")
+    from .scene import camera_from_sensor
+    if isinstance(sensor, _abi.Camera):
+        cam = sensor
+    elif isinstance(getattr(sensor, "camera", None), _abi.Camera):
+        cam = sensor.camera
+    elif isinstance(sensor, dict):
+        from .mitsuba_dict import sensor_from_dict
+        cam = camera_from_sensor(sensor_from_dict(sensor))
+    else:
+        entry = _MI_OBJECTS.get(id(sensor))
+        if entry is None or entry[0]() is not sensor or entry[1][0] != "sensor":
+            raise MtxError(f"unsupported sensor {type(sensor).__name__}: pass None, an mtx_camera, "
+                           "Scene.sensors()[i], a perspective sensor dictionary or an mi.Sensor loaded by the "
+                           "wrapped mi.load_dict")
+        cam = camera_from_sensor(entry[1][1])
+    if bytes(cam) == bytes(scene.camera):
+        return scene
+    return scene.with_camera(cam)
+
+
 def _bind_scene(ctx, scene) -> None:
-    """Upload `scene` to the context's device once (keyed by identity + film)."""
-    key = (id(scene), scene.width, scene.height)
+    """Upload `scene` to the context's device once (keyed by its geometry and
+    film size); a scene sharing the bound geometry and film size with another
+    camera (Scene.with_camera, scene_with_sensor) only re-points the device
+    camera (mtx_set_camera)."""
+    key = (id(scene.nodes), scene.width, scene.height)
     if getattr(ctx, "_scene_key", None) == key:
+        if getattr(ctx, "_camera", None) != bytes(scene.camera):
+            check(lib().mtx_set_camera(ctx.handle, C.byref(scene.camera)), "mtx_set_camera")
+            ctx._camera = bytes(scene.camera)
+        ctx.scene = scene
         return
     d = scene.desc()
     check(lib().mtx_scene_upload(ctx.handle, C.byref(d)), "mtx_scene_upload")
     ctx._scene_key = key
+    ctx._camera = bytes(scene.camera)
     ctx._nerad_key = None  # surface tables (mtx_nerad_upload) belong to the previous scene
     ctx.scene = scene  # keep the host arrays alive while bound
 
 
-# mi.Scene objects loaded through the wrapped mi.load_dict / mi.load_file:
-# id -> [the mi.Scene (kept alive: the id stays unique), its source, the mtx
-# scene built from that source on first use]
-_MI_SCENES: dict = {}
+# mi.Scene / mi.Sensor objects loaded through the wrapped mi.load_dict /
+# mi.load_file: id -> [weak reference to the object, (kind, converted spec or
+# XML path, base dir) taken at load time, the mtx scene built on first
+# render]. An entry goes when its object is collected (objects that take no
+# weak reference are kept, at most _MI_STRONG_MAX of them).
+_MI_OBJECTS: dict = {}
+_MI_STRONG: list = []
+_MI_STRONG_MAX = 64
+
+
+def _record(obj, source) -> None:
+    import weakref
+
+    key = id(obj)
+    try:
+        ref = weakref.ref(obj)
+        weakref.finalize(obj, _MI_OBJECTS.pop, key, None)
+    except TypeError:
+        _MI_STRONG.append(obj)
+        if len(_MI_STRONG) > _MI_STRONG_MAX:
+            old = _MI_STRONG.pop(0)
+            _MI_OBJECTS.pop(id(old), None)
+        ref = (lambda o: (lambda: o))(obj)
+    _MI_OBJECTS[key] = [ref, source, None]
 
 
 def mtx_scene_of(scene):
@@ -447,16 +513,18 @@ def mtx_scene_of(scene):
 
     if isinstance(scene, Scene):
         return scene
-    entry = _MI_SCENES.get(id(scene))
-    if entry is None or entry[0] is not scene:
+    entry = _MI_OBJECTS.get(id(scene))
+    if entry is None or entry[0]() is not scene or entry[1][0] == "sensor":
         raise MtxError("mtx renders mtx.scene.Scene objects, or an mi.Scene loaded by mi.load_dict / mi.load_file "
                        "after mtx.register_with_mitsuba() (its source dictionary / XML is converted); this mi.Scene "
                        "has no recorded source")
     if entry[2] is None:
         kind, src, base = entry[1]
+        if kind == "error":
+            raise MtxError(src)
         if kind == "dict":
-            from .mitsuba_dict import scene_from_dict
-            entry[2] = scene_from_dict(src, base_dir=base)
+            from .mitsuba_dict import scene_from_spec
+            entry[2] = scene_from_spec(src, base_dir=base)
         else:
             from .scene import Scene as _S
             entry[2] = _S.from_xml(src)
@@ -464,9 +532,13 @@ def mtx_scene_of(scene):
 
 
 def _wrap_loaders(mi) -> None:
-    """mi.load_dict / mi.load_file record each loaded scene's source (once)."""
-    import copy
+    """mi.load_dict / mi.load_file record each loaded scene's (and
+    perspective sensor's) source, converted at load time (so later edits of
+    the dictionary do not change the recorded scene; an unsupported scene
+    loads in Mitsuba and raises when an mtx integrator renders it)."""
     import os
+
+    from .mitsuba_dict import SENSOR_TYPES, sensor_from_dict, spec_from_dict
 
     if getattr(mi, "_mtx_wrapped", False):
         return
@@ -475,14 +547,19 @@ def _wrap_loaders(mi) -> None:
         def _load_dict(d, *args, **kwargs):
             obj = load_dict(d, *args, **kwargs)
             if isinstance(d, dict) and d.get("type") == "scene":
-                _MI_SCENES[id(obj)] = [obj, ("dict", copy.copy(d), os.getcwd()), None]
+                try:
+                    _record(obj, ("dict", spec_from_dict(d), os.getcwd()))
+                except MtxError as e:
+                    _record(obj, ("error", str(e), None))  # the message only: no traceback frames kept
+            elif isinstance(d, dict) and d.get("type") in SENSOR_TYPES:
+                _record(obj, ("sensor", sensor_from_dict(d), None))
             return obj
 
         mi.load_dict = _load_dict
     if load_file is not None:
         def _load_file(path, *args, **kwargs):
             obj = load_file(path, *args, **kwargs)
-            _MI_SCENES[id(obj)] = [obj, ("xml", os.path.abspath(str(path)), None), None]
+            _record(obj, ("xml", os.path.abspath(str(path)), None))
             return obj
 
         mi.load_file = _load_file

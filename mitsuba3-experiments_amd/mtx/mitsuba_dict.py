@@ -18,8 +18,10 @@ fov_axis x / y / smaller / larger, near / far clip, ``hdrfilm`` size) with
 a ``to_world`` transform; BSDFs diffuse, roughplastic, conductor,
 roughconductor, dielectric, roughdielectric, twosided, mask, with rgb /
 scalar / bitmap values and ``ref`` references; shapes rectangle, cube and
-obj (``filename``), with an ``area`` emitter on rectangles. Anything else
-raises :class:`mtx.MtxError` rather than rendering a different scene.
+obj (``filename``, read from ``base_dir``), with an ``area`` emitter on
+rectangles. Anything else -- including an ``obj`` whose file is missing and
+environment emitters (``constant``, ``envmap``; see ENV_EMITTERS) -- raises
+:class:`mtx.MtxError` rather than rendering a different scene.
 """
 from __future__ import annotations
 
@@ -32,6 +34,13 @@ BSDF_TYPES = {"diffuse", "roughplastic", "conductor", "roughconductor", "dielect
 SHAPE_TYPES = {"rectangle", "cube", "obj"}
 SENSOR_TYPES = {"perspective"}
 _IGNORED = {"integrator", "sampler"}  # scene entries that do not describe geometry or appearance
+# Environment emitters: the reference integrators read them where a ray
+# escapes (path-mis.py:41 valid_ray = scene.environment() is not None;
+# path.py:239 / path-mis.py:84 si.emitter(scene).eval on a miss) and NEE picks
+# them among the scene's emitters. mtx's kernels evaluate rectangle area
+# emitters only and treat a miss as black, so a scene with one is refused.
+ENV_EMITTERS = {"constant", "envmap"}
+OTHER_EMITTERS = {"point", "spot", "directional", "projector", "directionalarea"}
 
 
 def _matrix(t):
@@ -129,6 +138,8 @@ def spec_from_dict(d: dict) -> dict:
             else:
                 sd["bsdf_inline"] = _bsdf(b)
             em = v.get("emitter")
+            if t == "obj" and not v.get("filename"):
+                raise MtxError(f"shape {key!r}: an obj shape needs a filename")
             if em is not None:
                 if em.get("type") != "area" or t != "rectangle":
                     raise MtxError(f"shape {key!r}: only area emitters on rectangles are supported")
@@ -136,6 +147,12 @@ def spec_from_dict(d: dict) -> dict:
             shapes.append(sd)
         elif t in _IGNORED or key in _IGNORED:
             continue
+        elif t in ENV_EMITTERS:
+            raise MtxError(f"scene entry {key!r}: environment emitter {t!r} is not supported -- mtx evaluates "
+                           "rectangle area emitters only and a ray that leaves the scene returns no radiance "
+                           "(path-mis.py:41 / :84 would read the environment there)")
+        elif t in OTHER_EMITTERS:
+            raise MtxError(f"scene entry {key!r}: {t!r} emitters are not supported (rectangle area emitters only)")
         else:
             raise MtxError(f"scene entry {key!r}: unsupported type {t!r}")
     if sensor is None:
@@ -149,9 +166,25 @@ def spec_from_dict(d: dict) -> dict:
 
 
 def scene_from_dict(d: dict, base_dir: str | None = None, tex_res: int = 512):
-    """mi.load_dict(d) for the supported subset -> :class:`mtx.scene.Scene`."""
+    """mi.load_dict(d) for the supported subset -> :class:`mtx.scene.Scene`.
+    Mesh and bitmap files are read from `base_dir` (default: the working
+    directory, as mi.load_dict resolves them); a missing one raises."""
+    return scene_from_spec(spec_from_dict(d), base_dir, tex_res)
+
+
+def scene_from_spec(spec: dict, base_dir: str | None = None, tex_res: int = 512):
+    """A converted spec (:func:`spec_from_dict`) -> :class:`mtx.scene.Scene`."""
     import os
 
     from .scene import Scene
 
-    return Scene.bedroom(spec=spec_from_dict(d), base_dir=base_dir or os.getcwd(), tex_res=tex_res)
+    return Scene.bedroom(spec=spec, base_dir=base_dir or os.getcwd(), tex_res=tex_res, strict=True)
+
+
+def sensor_from_dict(d: dict) -> dict:
+    """A ``perspective`` sensor dictionary (the ``sensor`` argument of
+    mi.render / SamplingIntegrator.render) -> the spec's sensor form."""
+    if not isinstance(d, dict) or d.get("type") not in SENSOR_TYPES:
+        raise MtxError(f"unsupported sensor {d.get('type') if isinstance(d, dict) else type(d).__name__!r} "
+                       "(perspective only)")
+    return _sensor(d)

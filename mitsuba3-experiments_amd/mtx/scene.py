@@ -42,13 +42,18 @@ class Scene:
     # ------------------------------------------------------------ building --
     @classmethod
     def bedroom(cls, width: int | None = None, height: int | None = None, scale: float = 1.0,
-                tex_res: int = 512, spec: dict | None = None, base_dir: str | None = None) -> "Scene":
+                tex_res: int = 512, spec: dict | None = None, base_dir: str | None = None,
+                strict: bool = False) -> "Scene":
         """The bedroom proxy. `scale` multiplies every triangle budget
         (1.0 = the versioned ≈1.83 M-triangle benchmark scene).
 
         With `base_dir` (the directory of the scene XML), meshes and bitmaps
         whose files exist there (and are not Git-LFS pointers) are loaded
-        from disk (:mod:`mtx.obj`); the others fall back to the proxy."""
+        from disk (:mod:`mtx.obj`); the others fall back to the proxy.
+        `strict` (scenes converted from Mitsuba dictionaries): a mesh or
+        bitmap without a readable file raises MtxError instead of falling back
+        to the proxy -- the scene would otherwise differ from the one the
+        dictionary describes."""
         from . import obj as objio
         spec = spec or load_bedroom_spec()
         s = cls()
@@ -70,6 +75,9 @@ class Scene:
             if full and objio.is_real_file(full):
                 img = objio.load_bitmap(full)
                 loaded.append(fn)
+            elif strict:
+                from ._lib import MtxError
+                raise MtxError(f"bitmap {fn!r}: no readable file under {base_dir!r}")
             else:
                 img = proxy.procedural_texture(fn, tex_res)
             off = sum(x.size for x in texels)
@@ -191,6 +199,11 @@ class Scene:
                 else:
                     flags |= 2
                 budgets[sd["id"]] = len(F)
+            elif strict:
+                from ._lib import MtxError
+                raise MtxError(f"shape {sd['id']!r} ({sd['type']}): "
+                               + (f"no readable file {sd['filename']!r} under {base_dir!r}" if sd.get("filename")
+                                  else "no filename"))
             else:
                 fam = sd["id"].split("_")[0]
                 k = family_count.get(fam, 0)
@@ -246,6 +259,7 @@ class Scene:
         s.camera = _camera(spec["sensor"], W, H)
         s._build_bvh(tri_vidx, tri_shape)
         s.meta = {"scene": "bedroom-proxy" if not loaded else "xml", "proxy_version": proxy.PROXY_VERSION,
+                  "fov_axis": spec["sensor"].get("fov_axis", "x"),
                   "scale": scale, "width": W, "height": H, "n_tris": int(s.n_tris), "budgets": budgets,
                   "bvh_depth": s.bvh_depth, "n_nodes": int(s.n_nodes), "occ_depth": s.occ_depth,
                   "n_occ_nodes": int(s.n_occ_nodes), "loaded_files": loaded}
@@ -312,16 +326,36 @@ class Scene:
         return int(self.camera.height)
 
     def with_film(self, width: int, height: int) -> "Scene":
-        """Same scene, different film resolution (same fov, aspect from the film)."""
-        import copy
-        s = copy.copy(self)
+        """Same scene, different film resolution: the fov along the sensor's
+        fov_axis is kept (Mitsuba's perspective sensor: x, y, or the smaller /
+        larger side of the new film), the other axis follows the aspect."""
         cam = _abi.Camera()
         C.pointer(cam)[0] = self.camera
+        W0, H0 = int(cam.width), int(cam.height)
+        t = cam.tan_x if _fov_axis(self.meta.get("fov_axis", "x"), W0, H0) == "x" else cam.tan_y
+        if _fov_axis(self.meta.get("fov_axis", "x"), width, height) == "x":
+            cam.tan_x = t
+            cam.tan_y = cam.tan_x * height / width
+        else:
+            cam.tan_y = t
+            cam.tan_x = cam.tan_y * width / height
         cam.width, cam.height = width, height
-        cam.tan_y = cam.tan_x * height / width
-        s.camera = cam
-        s.meta = dict(self.meta, width=width, height=height)
+        return self.with_camera(cam)
+
+    def with_camera(self, cam) -> "Scene":
+        """Same geometry and materials seen through another sensor (an
+        ``mtx_camera``; the film size may differ). Shares the arrays."""
+        import copy
+        s = copy.copy(self)
+        c2 = _abi.Camera()
+        C.pointer(c2)[0] = cam
+        s.camera = c2
+        s.meta = dict(self.meta, width=int(c2.width), height=int(c2.height))
         return s
+
+    def sensors(self) -> list:
+        """scene.sensors() (testpssmlt.py:45): the scene's one sensor."""
+        return [Sensor(self.camera)]
 
     def desc(self) -> _abi.SceneDesc:
         d = _abi.SceneDesc()
@@ -392,6 +426,19 @@ class Scene:
         return s
 
 
+class Sensor:
+    """A perspective sensor: the ``mtx_camera`` it renders through (what
+    ``scene.sensors()[i]`` hands to ``render(scene, sensor, ...)``)."""
+
+    def __init__(self, camera):
+        cam = _abi.Camera()
+        C.pointer(cam)[0] = camera
+        self.camera = cam
+
+    def film_size(self) -> tuple:
+        return int(self.camera.width), int(self.camera.height)
+
+
 def _cube_mesh():
     """The 12 triangles of [-1, 1]^3, counter-clockwise seen from outside."""
     P, F = [], []
@@ -411,6 +458,26 @@ def _cube_mesh():
     return np.array(P, np.float64), np.array(F, np.int64)
 
 
+def _fov_axis(axis: str, W: int, H: int) -> str:
+    """Mitsuba's perspective-sensor fov_axis x (default), y, smaller, larger
+    -> the film axis the fov is measured along."""
+    if axis == "smaller":
+        return "x" if W <= H else "y"
+    if axis == "larger":
+        return "x" if W >= H else "y"
+    if axis not in ("x", "y"):
+        raise ValueError(f"fov_axis {axis!r} is not supported (x, y, smaller, larger)")
+    return axis
+
+
+def camera_from_sensor(sensor: dict, W: int | None = None, H: int | None = None) -> _abi.Camera:
+    """A perspective sensor description (the spec form of mtx.xmlscene /
+    mtx.mitsuba_dict: fov, fov_axis, near / far clip, to_world, film) -> an
+    ``mtx_camera``; the film size from the sensor's film unless given."""
+    film = sensor.get("film", {}) or {}
+    return _camera(sensor, int(W or film.get("width", 768)), int(H or film.get("height", 576)))
+
+
 def _camera(sensor: dict, W: int, H: int) -> _abi.Camera:
     M = _m4(sensor["to_world"])
     cam = _abi.Camera()
@@ -419,20 +486,14 @@ def _camera(sensor: dict, W: int, H: int) -> _abi.Camera:
     cam.axis_y[:] = M[:3, 1]
     cam.axis_z[:] = M[:3, 2]
     fov = float(sensor.get("fov", 45.0))
-    axis = sensor.get("fov_axis", "x")  # Mitsuba's perspective sensor: x (default), y, smaller, larger
-    if axis == "smaller":
-        axis = "x" if W <= H else "y"
-    elif axis == "larger":
-        axis = "x" if W >= H else "y"
+    axis = _fov_axis(sensor.get("fov_axis", "x"), W, H)
     t = math.tan(math.radians(fov) * 0.5)
     if axis == "x":  # the other axis from the fp32-rounded one (as the fixtures were made)
         cam.tan_x = t
         cam.tan_y = cam.tan_x * H / W
-    elif axis == "y":
+    else:
         cam.tan_y = t
         cam.tan_x = cam.tan_y * W / H
-    else:
-        raise ValueError(f"fov_axis {axis!r} is not supported (x, y, smaller, larger)")
     cam.near_clip = float(sensor.get("near_clip", 1e-2))
     cam.far_clip = float(sensor.get("far_clip", 1e4))
     cam.width, cam.height = W, H

@@ -63,7 +63,6 @@ SceneView make_view(const mtx_scene_desc *d) {
   }
   s.occ_nodes = d->occ_nodes;
   s.occ_tri_geom = d->occ_tri_geom;
-  s.occ_perm = d->occ_perm;  // needed by trace_closest_cw only
   s.tri_vidx = d->tri_vidx;
   s.tri_shape = d->tri_shape;
   s.vpos = d->vpos;
@@ -211,227 +210,6 @@ bool trace_any(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visit
   if (nodes_visited) *nodes_visited = nv;
   if (tris_visited) *tris_visited = tv;
   return hit;
-}
-
-// Scalar closest-hit traversal of the 8-wide tree in the device kernels'
-// order (device_common.h trace_loop_closest_cw / traverse_closest_cw): a
-// visit takes the sorted keys of its hit inner children (mtx_core/
-// geometry.h cw_node_keys + cw_sort8), keeps the nearest as the pending node,
-// pushes the others far to near with their keys, and tests its hit leaves'
-// triangles (ascending bit) before the pending node; a pending or popped
-// node whose key distance exceeds the current hit is dropped unvisited. Ties
-// on t go to the smaller scene triangle (occ_perm), so the hit equals
-// trace_closest's.
-Hit trace_closest_cw(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited) {
-  if (!s.occ_perm) {
-    std::fprintf(stderr, "oracle: trace_closest_cw needs the scene desc's occ_perm\n");
-    std::abort();
-  }
-  TraceRay r = make_trace_ray(o, d, maxt);
-  const uint32_t oct = ray_octant(r);
-  float tbest = maxt, bu = 0.f, bv = 0.f;
-  uint32_t best = 0xffffffffu, nn = 0, nk = 0, nv = 0, tv = 0;
-  uint32_t stack[2 * (7 * MTX_BVH_MAX_DEPTH + 2)];
-  int sp = 0;
-  while (true) {
-    if (nn != 0xffffffffu && cw_key_t(nk) <= tbest) {
-      const uint32_t *w = reinterpret_cast<const uint32_t *>(s.occ_nodes) + MTX_OCC_NODE_WORDS * (size_t)nn;
-      const float *f = reinterpret_cast<const float *>(w);
-      ++nv;
-      uint32_t key[8];
-      uint32_t thits = cw_node_keys(r, oct, f[0], f[1], f[2], w[3], w[6], w[7], w + 8, tbest, key);
-      cw_sort8(key);
-      const uint32_t cb = w[4], tb = w[5];
-      int n = 0;
-      for (int j = 0; j < 8; ++j) n += key[j] != 0xffffffffu ? 1 : 0;
-      for (int j = n - 1; j >= 1; --j) {
-        stack[sp++] = cb + (key[j] & 7u);
-        stack[sp++] = key[j];
-      }
-      nn = n ? cb + (key[0] & 7u) : 0xffffffffu;
-      nk = key[0];
-      while (thits) {
-        const uint32_t pr = tb + (uint32_t)ctz32(thits);
-        thits &= thits - 1u;
-        const float *g = s.occ_tri_geom + 12 * (size_t)pr;
-        float t, u, v;
-        ++tv;
-        if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v) &&
-            (t < tbest || (t == tbest && (best == 0xffffffffu || s.occ_perm[pr] < s.occ_perm[best])))) {
-          tbest = t;
-          best = pr;
-          bu = u;
-          bv = v;
-        }
-      }
-      continue;
-    }
-    nn = 0xffffffffu;
-    while (sp > 0) {
-      const uint32_t k = stack[--sp], node = stack[--sp];
-      if (cw_key_t(k) <= tbest) {
-        nn = node;
-        nk = k;
-        break;
-      }
-    }
-    if (nn == 0xffffffffu) break;
-  }
-  if (nodes_visited) *nodes_visited = nv;
-  if (tris_visited) *tris_visited = tv;
-  if (best == 0xffffffffu) return Hit{kInf, 0.f, 0.f, 0xffffffffu};
-  return Hit{tbest, bu, bv, s.occ_perm[best]};
-}
-
-// Diagnostic (tools/cw_closest_experiment.py only): closest hit on the 8-wide
-// occlusion tree with a choice of child order, to size the visit counts of an
-// 8-wide closest-hit traversal before building it. mode 0: octant order (the
-// any-hit order); 1: the nearest hit inner child first, the rest in octant
-// order; 2: hit inner children in entry-distance order; 3: as 2, and a popped
-// child whose entry distance is beyond the current hit is skipped (a stack
-// entry carrying its distance). A visit tests the node's hit leaves'
-// triangles first (the triangle group), as trace_any does.
-static thread_local uint32_t g_cw_max_sp = 0;
-Hit trace_cw_closest(const SceneView &s, V3 o, V3 d, float maxt, int mode, uint32_t *nodes_visited,
-                     uint32_t *tris_visited) {
-  TraceRay r = make_trace_ray(o, d, maxt);
-  const uint32_t oct = ray_octant(r);
-  Hit h{maxt, 0.f, 0.f, 0xffffffffu};
-  float tbest = maxt;
-  struct Ent {
-    uint32_t node;
-    float t;
-  };
-  Ent stack[8 * (MTX_BVH_MAX_DEPTH + 2)];
-  int sp = 0;
-  stack[sp++] = Ent{0u, 0.f};
-  uint32_t nv = 0, tv = 0;
-  while (sp > 0) {
-    const Ent e = stack[--sp];
-    if (mode == 3 && e.t > tbest) continue;
-    const uint32_t *w = reinterpret_cast<const uint32_t *>(s.occ_nodes) + MTX_OCC_NODE_WORDS * (size_t)e.node;
-    const float *f = reinterpret_cast<const float *>(w);
-    ++nv;
-    const float ax = wide_ldexp(r.idir.x, (int)(int8_t)(uint8_t)(w[3] & 0xffu)), bx = (f[0] - r.o.x) * r.idir.x;
-    const float ay = wide_ldexp(r.idir.y, (int)(int8_t)(uint8_t)((w[3] >> 8) & 0xffu)), by = (f[1] - r.o.y) * r.idir.y;
-    const float az = wide_ldexp(r.idir.z, (int)(int8_t)(uint8_t)((w[3] >> 16) & 0xffu)), bz = (f[2] - r.o.z) * r.idir.z;
-    const uint32_t imask = w[3] >> 24, child_base = w[4], tri_base = w[5];
-    Ent kids[8];
-    uint32_t kpos[8];
-    int nk = 0;
-    for (uint32_t slot = 0; slot < 8; ++slot) {
-      const uint32_t hh = slot >> 2, k = slot & 3u;
-      const uint32_t m = (w[6 + hh] >> (8 * k)) & 0xffu;
-      if (m == 0) continue;
-      auto q = [&](int base) { return (float)((w[8 + base + hh] >> (8 * k)) & 0xffu); };
-      float lx = fmaf(q(0), ax, bx), hx = fmaf(q(2), ax, bx);
-      float ly = fmaf(q(4), ay, by), hy = fmaf(q(6), ay, by);
-      float lz = fmaf(q(8), az, bz), hz = fmaf(q(10), az, bz);
-      const float tmin = fmaxf(fmaxf(fmaxf(fminf(lx, hx), fminf(ly, hy)), fminf(lz, hz)), 0.f);
-      const float tmax = fminf(fminf(fminf(fmaxf(lx, hx), fmaxf(ly, hy)), fmaxf(lz, hz)), tbest);
-      if (!(tmin <= tmax)) continue;
-      if ((imask >> slot) & 1u) {
-        const uint32_t child = child_base + (uint32_t)popc32(imask & ((1u << slot) - 1u));
-        kids[nk] = Ent{child, tmin};
-        kpos[nk] = slot ^ oct;
-        ++nk;
-      } else {
-        const uint32_t cb = m >> 5, off = m & 31u, cnt = (uint32_t)popc32(cb);
-        for (uint32_t j = 0; j < cnt; ++j) {
-          const uint32_t prim = tri_base + off + j;
-          const float *g = s.occ_tri_geom + 12 * (size_t)prim;
-          float t, u, v;
-          ++tv;
-          if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v) &&
-              (t < tbest || (t == tbest && prim < h.prim))) {
-            tbest = t;
-            h = Hit{t, u, v, prim};
-          }
-        }
-      }
-    }
-    // visit order: octant positions ascending (mode 0), nearest first then
-    // octant (1), entry distance (2, 3)
-    int idx[8];
-    for (int i = 0; i < nk; ++i) idx[i] = i;
-    auto by_pos = [&](int a, int b) { return kpos[a] < kpos[b]; };
-    auto by_t = [&](int a, int b) { return kids[a].t < kids[b].t || (kids[a].t == kids[b].t && kpos[a] < kpos[b]); };
-    if (mode == 0) {
-      std::sort(idx, idx + nk, by_pos);
-    } else if (mode == 1) {
-      std::sort(idx, idx + nk, by_pos);
-      int best = 0;
-      for (int i = 1; i < nk; ++i)
-        if (by_t(idx[i], idx[best])) best = i;
-      std::rotate(idx, idx + best, idx + best + 1);
-    } else {
-      std::sort(idx, idx + nk, by_t);
-    }
-    for (int i = nk - 1; i >= 0; --i) stack[sp++] = kids[idx[i]];
-    if ((uint32_t)sp > g_cw_max_sp) g_cw_max_sp = (uint32_t)sp;
-  }
-  if (nodes_visited) *nodes_visited = nv;
-  if (tris_visited) *tris_visited = tv;
-  if (h.prim == 0xffffffffu) h.t = kInf;
-  return h;
-}
-
-// Diagnostic (tools/cw_closest_experiment.py only): trace_closest whose stack
-// entries carry the child's entry distance; a popped entry beyond the current
-// hit is dropped without a visit (or, for a leaf, without its triangle tests).
-// max_sp reports the deepest stack.
-Hit trace_closest_cull(const SceneView &s, V3 o, V3 d, float maxt, uint32_t *nodes_visited, uint32_t *tris_visited,
-                       uint32_t *max_sp) {
-  TraceRay r = make_trace_ray(o, d, maxt);
-  Hit h{maxt, 0.f, 0.f, 0xffffffffu};
-  float tbest = maxt;
-  int32_t stack[3 * MTX_BVH_MAX_DEPTH + 2];
-  float st[3 * MTX_BVH_MAX_DEPTH + 2];
-  int sp = 0;
-  int32_t node = 0;
-  uint32_t nv = 0, tv = 0, msp = 0;
-  while (true) {
-    if (node >= 0) {
-      const int32_t *w = s.nodes + MTX_BVH_NODE_WORDS * (size_t)node;
-      const float *f = reinterpret_cast<const float *>(w);
-      ++nv;
-      uint32_t key[4];
-      const int n = wide_node_order(r, f[0], f[1], f[2], (uint32_t)w[3], (uint32_t)w[8], (uint32_t)w[9],
-                                    (uint32_t)w[10], (uint32_t)w[11], (uint32_t)w[12], (uint32_t)w[13], tbest, key);
-      if (n > 0) {
-        for (int rr = n - 1; rr >= 1; --rr) {
-          st[sp] = u2f(key[rr] & 0x7ffffffcu);
-          stack[sp++] = wide_ref(key[rr], w[4], w[5], w[6], w[7]);
-        }
-        msp = msp > (uint32_t)sp ? msp : (uint32_t)sp;
-        node = wide_ref(key[0], w[4], w[5], w[6], w[7]);
-        continue;
-      }
-    } else {
-      uint32_t first, count;
-      leaf_decode(node, &first, &count);
-      for (uint32_t k = 0; k < count; ++k) {
-        uint32_t prim = first + k;
-        const float *g = s.tri_geom + 12 * (size_t)prim;
-        float t, u, v;
-        ++tv;
-        if (tri_intersect(r, V3{g[0], g[1], g[2]}, V3{g[4], g[5], g[6]}, V3{g[8], g[9], g[10]}, tbest, &t, &u, &v)) {
-          if (t < tbest || (t == tbest && prim < h.prim)) {
-            tbest = t;
-            h = Hit{t, u, v, prim};
-          }
-        }
-      }
-    }
-    while (sp > 0 && st[sp - 1] > tbest) --sp;
-    if (sp == 0) break;
-    node = stack[--sp];
-  }
-  if (nodes_visited) *nodes_visited = nv;
-  if (tris_visited) *tris_visited = tv;
-  if (max_sp) *max_sp = msp;
-  if (h.prim == 0xffffffffu) h.t = kInf;
-  return h;
 }
 
 Hit brute_closest(const SceneView &s, V3 o, V3 d, float maxt) {
@@ -860,9 +638,7 @@ int orc_trace(const mtx_scene_desc *d, uint64_t n, const float *rays, int any_hi
     if (any_hit == 1) {
       hits[i] = trace_any(s, o, dd, maxt, &nv, &tv) ? 1u : 0u;
     } else {
-      Hit h = brute             ? brute_closest(s, o, dd, maxt)
-              : any_hit == 2    ? trace_closest_cw(s, o, dd, maxt, &nv, &tv)
-                                : trace_closest(s, o, dd, maxt, &nv, &tv);
+      Hit h = brute ? brute_closest(s, o, dd, maxt) : trace_closest(s, o, dd, maxt, &nv, &tv);
       hits[4 * i + 0] = f2u(h.t);
       hits[4 * i + 1] = h.prim;
       hits[4 * i + 2] = f2u(h.u);
@@ -877,29 +653,6 @@ int orc_trace(const mtx_scene_desc *d, uint64_t n, const float *rays, int any_hi
 }
 
 // orc_trace with the per-node visit histogram of nodes [0, hist_len) (tools/ diagnostic)
-// Diagnostic: trace_cw_closest over n rays (8 floats each, as orc_trace);
-// hits 4 words (t, prim of the closest-hit tree's numbering is NOT used: the
-// occlusion tree's own triangle order), visits 2 words.
-int orc_trace_cw_closest(const mtx_scene_desc *d, uint64_t n, const float *rays, int mode, float *t_out,
-                         uint32_t *visits) {
-  SceneView s = make_view(d);
-#pragma omp parallel for schedule(dynamic, 256)
-  for (int64_t i = 0; i < (int64_t)n; ++i) {
-    const float *x = rays + 8 * i;
-    uint32_t nv = 0, tv = 0;
-    uint32_t msp = 0;
-    g_cw_max_sp = 0;
-    const Hit h = mode >= 16 ? trace_closest_cull(s, V3{x[0], x[1], x[2]}, V3{x[4], x[5], x[6]}, x[3], &nv, &tv, &msp)
-                             : trace_cw_closest(s, V3{x[0], x[1], x[2]}, V3{x[4], x[5], x[6]}, x[3], mode, &nv, &tv);
-    if (mode >= 16) nv |= msp << 16;
-    else nv |= (g_cw_max_sp - 1u) << 16;  // entries below the one being visited
-    t_out[i] = h.t;
-    visits[2 * i] = nv;
-    visits[2 * i + 1] = tv;
-  }
-  return 0;
-}
-
 int orc_node_visit_hist(const mtx_scene_desc *d, uint64_t n, const float *rays, int any_hit, uint64_t *hist,
                         uint32_t hist_len) {
   std::vector<uint32_t> hits(any_hit ? n : 4 * n);

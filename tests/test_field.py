@@ -141,6 +141,28 @@ def test_nrc_cache_film_bit_exact(small_scene, oracle, chunk):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_hidden", [14, 16])
+def test_nrc_cache_deep_field_bit_exact(small_scene, oracle, n_hidden):
+    """Fields deeper than the fused cache kernel's LDS allows (n_hidden 15 /
+    16 need more than the 160 KiB of a workgroup) take the three-kernel path
+    (encode, MLP, apply; api.cpp run_cache) instead of a failed launch: the
+    film still equals the oracle's composition bit for bit; n_hidden 14 is
+    the deepest fused case."""
+    from mtx import load_dict
+    from mtx.field import Field
+
+    field = Field(small_scene, seed=9, table_scale=1.0, n_hidden=n_hidden)
+    integ = load_dict({"type": "nrc", "field": field})
+    film = integ.render_film(small_scene, seed=4, spp=2)
+    a = integ.render_args(small_scene, 4, 2)
+    L, pos, q = oracle.render_samples_nrc_cache(small_scene, a)
+    m = q[:, 0] == 1
+    assert m.any()
+    L[m] = L[m] + q[m, 7:10] * field(q[m, 1:4], q[m, 4:7])
+    np.testing.assert_array_equal(film, oracle.film(small_scene.width, 0, small_scene.height, 2, L, pos))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("chunk", [0, 40000])
 def test_nrc_cache_two_streams_bit_exact(small_scene, oracle, chunk):
     """A render of >= 2^16 paths runs on two wavefronts / streams, each chunk's

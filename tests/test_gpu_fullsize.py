@@ -39,19 +39,16 @@ def _rays(scene, n, seed):
 
 
 def test_full_bedroom_trace_bit_exact(full_scene, oracle):
-    """Modes 0 (4-wide closest hit), 1 (any hit), 2 (closest hit on the
-    8-wide tree): hits and visit counts equal the oracle's; mode 2's hit
-    records equal mode 0's (the closest hit does not depend on the tree)."""
+    """Modes 0 (closest hit, 4-wide tree) and 1 (any hit, 8-wide occlusion
+    tree): hits and visit counts equal the oracle's."""
     from test_gpu_parity import _trace_gpu
 
     rays = _rays(full_scene, 1 << 16, 21)
-    for mode in (0, 1, 2):
+    for mode in (0, 1):
         g_hits, g_vis = _trace_gpu(full_scene, rays, mode)
         c_hits, c_vis = oracle.trace(full_scene, rays, mode)
         assert np.array_equal(g_hits, c_hits), f"mode={mode}"
         assert np.array_equal(g_vis, c_vis), f"mode={mode}"
-        if mode == 2:
-            assert np.array_equal(g_hits, oracle.trace(full_scene, rays, 0)[0])
 
 
 def test_full_bedroom_path_mis_film_bit_exact(full_scene, oracle):
@@ -86,7 +83,7 @@ from test_gpu_fullsize import _rays
 oracle.build()
 for sc in (scene.bedroom(width=64, height=36, scale=0.02, tex_res=64), scene.bedroom(width=96, height=54)):
     rays = _rays(sc, 1 << 14, 5)
-    for mode in (0, 1, 2):
+    for mode in (0, 1):
         g_hits, g_vis = _trace_gpu(sc, rays, mode)
         c_hits, c_vis = oracle.trace(sc, rays, mode)
         assert np.array_equal(g_hits, c_hits), ("hits", sc.n_tris, mode)
@@ -103,11 +100,8 @@ print("CHILD OK")
                                  {"MTX_LDS_STACK": "2", "MTX_LDS_TOP": "0", "MTX_OCC_LDS_STACK": "2",
                                   "MTX_OCC_LDS_TOP": "0"},
                                  {"MTX_XCD_CLAIM": "0", "MTX_TRACE_BATCH": "64"},
-                                 {"MTX_CLOSEST_CW": "1"},
-                                 {"MTX_CLOSEST_CW": "1", "MTX_OCC_LDS_STACK": "1", "MTX_OCC_LDS_TOP": "0"},
-                                 {"MTX_CLOSEST_CW": "0"}],
-                         ids=["spill-all", "spill2-notop", "noxcd-batch64", "cw8-closest", "cw8-closest-spill-notop",
-                              "bvh4-closest"])
+                                 {"MTX_OCC_LDS_STACK": "1", "MTX_OCC_LDS_TOP": "0"}],
+                         ids=["spill-all", "spill2-notop", "noxcd-batch64", "occ-spill-notop"])
 def test_traversal_variants_bit_exact(env):
     """Traversal variants selected at context creation: bit-exact hits,
     visit counts and films on the 2 % scene and on the full-size scene."""

@@ -164,7 +164,7 @@ def test_plugin_resolves_loaded_scenes():
 
     bad = cornell_box()
     bad["env"] = {"type": "envmap", "filename": "sky.exr"}
-    with pytest.raises(MtxError, match="unsupported"):
+    with pytest.raises(MtxError, match="environment emitter"):
         spec_from_dict(bad)
     gold = cornell_box()
     gold["white"] = {"type": "conductor", "material": "Au"}
@@ -217,3 +217,91 @@ def test_obj_shape_and_fov_axes(tmp_path):
     d3["sensor"]["fov_axis"] = "diagonal"
     with pytest.raises((MtxError, ValueError)):
         scene_from_dict(d3)
+
+
+@pytest.mark.parametrize("entry,match", [({"type": "constant", "radiance": {"type": "rgb", "value": 1.0}},
+                                          "environment emitter 'constant'"),
+                                         ({"type": "envmap", "filename": "sky.exr"}, "environment emitter 'envmap'"),
+                                         ({"type": "point", "position": [0, 0.5, 0]}, "'point' emitters"),
+                                         ({"type": "directional", "direction": [0, -1, 0]}, "'directional' emitters")])
+def test_environment_and_delta_emitters_rejected(entry, match):
+    """An environment emitter is what a reference integrator reads where a
+    ray escapes (path-mis.py:41 valid_ray, :84 / path.py:239 si.emitter on a
+    miss); mtx's kernels have none, so such a scene is refused with that
+    reason instead of rendering it black."""
+    from mtx import MtxError
+    from mtx.mitsuba_dict import spec_from_dict
+
+    d = cornell_box()
+    d["sky"] = entry
+    with pytest.raises(MtxError, match=match):
+        spec_from_dict(d)
+
+
+def test_obj_shape_needs_its_file(tmp_path):
+    """An obj shape whose file is missing (or that names none) raises instead
+    of falling back to the procedural proxy mesh (which would render another
+    scene)."""
+    from mtx import MtxError
+    from mtx.mitsuba_dict import scene_from_dict
+
+    d = cornell_box(16, 16)
+    d["mesh"] = {"type": "obj", "filename": "missing.obj", "bsdf": {"type": "ref", "id": "red"}}
+    with pytest.raises(MtxError, match="missing.obj"):
+        scene_from_dict(d, base_dir=str(tmp_path))
+    d["mesh"] = {"type": "obj", "bsdf": {"type": "ref", "id": "red"}}
+    with pytest.raises(MtxError, match="needs a filename"):
+        scene_from_dict(d, base_dir=str(tmp_path))
+    d["mesh"] = {"type": "diffuse"}
+    d["white"] = {"type": "diffuse", "reflectance": {"type": "bitmap", "filename": "nope.png"}}
+    del d["mesh"]
+    with pytest.raises(MtxError, match="nope.png"):
+        scene_from_dict(d, base_dir=str(tmp_path))
+
+
+def test_loaded_scene_is_recorded_at_load_time():
+    """The wrapped mi.load_dict converts the dictionary when it is loaded:
+    later edits of the dictionary do not change the rendered scene; a scene
+    outside the subset still loads (in Mitsuba) and raises when an mtx
+    integrator is asked to render it; entries go with their mi.Scene."""
+    import gc
+
+    from mtx import MtxError, integrators
+
+    mi = _fake_mi()
+    integrators.register_with_mitsuba(mi)
+    d = cornell_box(16, 16)
+    obj = mi.load_dict(d)
+    d["red"]["reflectance"]["value"] = [0.0, 0.0, 1.0]
+    d["small-box"]["type"] = "sphere"
+    sc = integrators.mtx_scene_of(obj)
+    cols = sorted(tuple(round(x, 4) for x in m.rgb) for m in sc.materials)
+    assert (0.5701, 0.043, 0.0444) in cols and sc.n_tris == 36
+    bad = cornell_box(16, 16)
+    bad["sky"] = {"type": "constant"}
+    bad_obj = mi.load_dict(bad)
+    try:
+        integrators.mtx_scene_of(bad_obj)
+        raise AssertionError("expected MtxError")
+    except MtxError as e:
+        assert "environment emitter" in str(e)
+    n = len(integrators._MI_OBJECTS)
+    del obj, bad_obj
+    gc.collect()
+    assert len(integrators._MI_OBJECTS) == n - 2
+
+
+def test_with_film_keeps_the_fov_axis():
+    """Scene.with_film keeps the fov along the sensor's fov_axis (Mitsuba's
+    perspective sensor), as a scene loaded at the new film size has it."""
+    from mtx.mitsuba_dict import scene_from_dict
+
+    for axis in ("x", "y", "smaller", "larger"):
+        d = cornell_box(64, 32)
+        d["sensor"]["fov_axis"] = axis
+        a = scene_from_dict(d).with_film(24, 40)
+        d2 = cornell_box(24, 40)
+        d2["sensor"]["fov_axis"] = axis
+        b = scene_from_dict(d2).camera
+        assert (a.camera.width, a.camera.height) == (24, 40)
+        assert abs(a.camera.tan_x - b.tan_x) < 1e-6 and abs(a.camera.tan_y - b.tan_y) < 1e-6, axis

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-5 GPU session: GPU tests of the given files under each library
+# GPU session: GPU tests of the given files under each library
 # variant (MTX_LIB_VARIANT), then an interleaved A/B of environment settings
 # (tools/env_ab.sh). Every GPU step has its own time limit; the first failure
 # ends the session.
-# Usage: tools/r5_session.sh TAG "TEST FILES|none" "VARIANTS (e.g. '- m1')" ROUNDS "ENV1" "ENV2" ...
+# Usage: tools/gpu_session.sh TAG "TEST FILES|none" "VARIANTS (e.g. '- m1')" ROUNDS "ENV1" "ENV2" ...
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
 TAG=$1; FILES=$2; VARS=$3; ROUNDS=$4; shift 4
