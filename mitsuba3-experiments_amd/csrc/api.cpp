@@ -148,7 +148,7 @@ struct mtx_ctx {
   DevBuf contrib, film;
   // scratch for sample_rays / trace / primitives
   DevBuf s0, s1, s2, s3, s4, s5, s6;
-  int trace_grid = 0, shade_grid = 0;
+  int trace_grid = 0, closest_grid = 0, shade_grid = 0;  // persistent grids: any hit, closest hit, shade
   size_t max_lds = 160 * 1024;  // LDS one workgroup may hold (gfx950: the CU's 160 KiB)
   // tuning knobs (environment, read at context creation): LDS stack entries
   // of the persistent traversal, chunk path order
@@ -224,7 +224,7 @@ int mtx_ctx_create(int hip_device, mtx_ctx **out) {
   }
   // Persistent grids: every CU filled to the kernels' occupancy (the trace
   // grid is recomputed per scene: its LDS stack depends on the BVH depth).
-  c->trace_grid = c->n_cu * 8;
+  c->trace_grid = c->closest_grid = c->n_cu * 8;
   c->shade_grid = c->n_cu * mtxd::shade_blocks_per_cu();
   {
     // a gfx950 workgroup may hold the CU's whole 160 KiB of LDS (the attribute
@@ -585,8 +585,9 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.occ_urefill = c->occ_urefill;
   s.xcd_claim = c->xcd_claim;
   c->trace_grid = c->n_cu * mtxd::trace_blocks_per_cu(s);
+  c->closest_grid = c->n_cu * mtxd::closest_blocks_per_cu(s);
   c->mega_grid = c->n_cu * mtxd::mega_blocks_per_cu(s);
-  s.ovf_threads = (uint32_t)c->trace_grid * mtxd::kTraceBlock;
+  s.ovf_threads = (uint32_t)std::max(c->trace_grid, c->closest_grid) * mtxd::kTraceBlock;
   if ((rc = dalloc(c->stack_ovf, mtxd::stack_ovf_bytes(s)))) return rc;
   s.stack_ovf = c->stack_ovf.p;
   c->has_scene = true;
@@ -951,7 +952,7 @@ void launch_bounce(mtx_ctx *c, const mtxd::WaveBuffers &b, const mtxd::ChunkPara
   const int div = (nerad && bounce >= 2) ? 8 : 1;
   if (!(nerad && bounce == 0)) {
     e = tm.begin(0, st);
-    mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->trace_grid / div), st);
+    mtxd::launch_trace_closest(s, b, bounce, p.stats, std::max(1, c->closest_grid / div), st);
     tm.end(0, e, st);
     ++*n_trace;
   }
@@ -1224,7 +1225,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
       HIP_TRY(reset_counters(bh[h], depth, sh[h]));
       mtxd::launch_raygen_camera(*sc[h], bh[h], ph[h], sh[h]);
       e = tm.begin(0, sh[h]);
-      mtxd::launch_trace_closest(*sc[h], bh[h], 0, ph[h].stats, c->trace_grid, sh[h]);
+      mtxd::launch_trace_closest(*sc[h], bh[h], 0, ph[h].stats, c->closest_grid, sh[h]);
       tm.end(0, e, sh[h]);
       ++*n_trace;
       HIP_TRY(reset_counters(bh[h], depth, sh[h]));

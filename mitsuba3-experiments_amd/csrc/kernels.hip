@@ -60,8 +60,11 @@ struct ClosestSrc {
 // fits without spills. Shadow 56.4 -> 55.6 ms per step (A/B, one box, 3
 // rounds, round 2).
 #define MTX_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#ifndef MTX_CLOSEST_WAVES
+#define MTX_CLOSEST_WAVES 8  // closest hit: waves/SIMD the register budget is sized for
+#endif
 template <bool STATS>
-__global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
+__global__ __launch_bounds__(kTraceBlock) __attribute__((amdgpu_waves_per_eu(MTX_CLOSEST_WAVES))) void k_trace_closest(DevScene s, WaveBuffers b, uint32_t bounce) {
   // dynamic LDS: stack columns + tree top (device_common.h trace_loop)
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const ClosestSrc src{b, b.queue[bounce & 1], b.ray_o[rp], b.ray_d[rp]};
@@ -1784,19 +1787,23 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
       hipLaunchKernelGGL(k_shade<MTX_INT_PATH_MIS>, dim3(grid), dim3(kShadeBlock), 0, st, s, b, p, bounce);
   }
 }
-// Resident blocks per CU of the persistent kernels (grid = n_cu x this; the
-// fewer of the two trees' kernels).
+// Resident blocks per CU of the persistent kernels (grid = n_cu x this):
+// the any-hit kernels (shadow, ReSTIR visibility) and the closest-hit kernel.
 int trace_blocks_per_cu(const DevScene &s) {
-  int nc = 0, na = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false>, kTraceBlock,
-                                                   persistent_stack_bytes(s, false)) != hipSuccess ||
-      nc <= 0)
-    nc = 4;
+  int na = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&na, k_trace_shadow<false>, kTraceBlock,
                                                    persistent_stack_bytes(s, true)) != hipSuccess ||
       na <= 0)
     na = 4;
-  return nc < na ? nc : na;
+  return na;
+}
+int closest_blocks_per_cu(const DevScene &s) {
+  int nc = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nc, k_trace_closest<false>, kTraceBlock,
+                                                   persistent_stack_bytes(s, false)) != hipSuccess ||
+      nc <= 0)
+    nc = 4;
+  return nc;
 }
 // MTX_DIAG_STAMPS builds: read (and zero) the shade stamp sums; -1 otherwise.
 int shade_stamps(unsigned long long *out) {

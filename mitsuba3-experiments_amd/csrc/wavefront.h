@@ -53,6 +53,11 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_OCC_LDS_TOP
 #define MTX_OCC_LDS_TOP 48  // occlusion tree nodes copied into LDS per trace block (0 = none)
 #endif
+#ifndef MTX_COOP_NODE
+// closest hit: a wave fetches its lanes' global nodes cooperatively, 4 lanes
+// per 64-B node, straight into LDS (LDS-DMA; device_common.h coop_fetch_nodes)
+#define MTX_COOP_NODE 0
+#endif
 #ifndef MTX_SHADE_WARM
 #define MTX_SHADE_WARM 1  // k_shade: warm L2 with the next entry's shading record
 #endif
@@ -222,7 +227,8 @@ struct ChunkParams {
 };
 
 // -------- launch wrappers (kernels.hip) --------
-int trace_blocks_per_cu(const DevScene &s);
+int trace_blocks_per_cu(const DevScene &s);    // any-hit kernels
+int closest_blocks_per_cu(const DevScene &s);  // k_trace_closest
 int shade_blocks_per_cu();
 int mega_blocks_per_cu(const DevScene &s);
 // all bounces of a short path-mis / path wavefront in one kernel (k_path_mega)

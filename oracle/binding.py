@@ -326,6 +326,21 @@ def probe(scene, op, inputs):
     return out
 
 
+def restir_probe(op, inputs):
+    """orc_restir_probe: the ReSTIR GI reservoir primitives of
+    mtx_core/restir.h item by item (op p_hat, similar, update, merge, J,
+    to_idx); 16 floats in and out per item."""
+    ops = {"p_hat": 0, "similar": 1, "update": 2, "merge": 3, "J": 4, "to_idx": 5}
+    a = np.asarray(inputs, np.float32)
+    x = np.zeros((len(a), 16), np.float32)
+    x[:, : a.shape[1]] = a
+    out = np.zeros_like(x)
+    L = lib()
+    L.orc_restir_probe.argtypes = [C.c_int, C.c_uint64, C.c_void_p, C.c_void_p]
+    assert L.orc_restir_probe(ops[op], len(x), x.ctypes.data, out.ctypes.data) == 0
+    return out
+
+
 def si_probe(items):
     """orc_si_probe: si_from_vertices item by item; items is (n, 40) float32
     (layout in oracle.cpp), returns (n, 24): p, n, s, t, ns, uv(+0), wi."""

@@ -1473,6 +1473,76 @@ int orc_probe(const mtx_scene_desc *d, int op, uint64_t n, const float *in, floa
   return 0;
 }
 
+// ReSTIR GI reservoir primitives of mtx_core/restir.h item by item, for the
+// float64 transcription of restirgi.py in tests/test_restir_pins.py. 16
+// floats in / out per item (u32 counts and pixel coordinates as exact
+// floats):
+//   op 0 p_hat(f = in[0..2]) -> out[0]                       (:84-85)
+//   op 1 similar(x_v, n_v of a = in[0..5], of b = in[6..11]) -> out[0] 0 / 1  (:175-180)
+//   op 2 res_update(w = in[0], M = in[1], wnew = in[2], active = in[3], u = in[4])
+//        -> out w, M, taken                                   (:120-134)
+//   op 3 res_merge_w(w = in[0], M = in[1], o.W = in[2], o.M = in[3], p = in[4],
+//        active = in[5], u = in[6]) -> out w, M, taken         (:136-141)
+//   op 4 jacobian_J(receiver = in[0..2], z.x_s = in[3..5], z.n_s = in[6..8],
+//        z.x_v = in[9..11]) -> out[0]                          (:42-53)
+//   op 5 pixel_index(x = in[0], y = in[1], W, H, spp, smp = in[2..5]) -> out[0]  (:170-173)
+int orc_restir_probe(int op, uint64_t n, const float *in, float *out) {
+  for (uint64_t i = 0; i < n; ++i) {
+    const float *a = in + 16 * i;
+    float *o = out + 16 * i;
+    for (int k = 0; k < 16; ++k) o[k] = 0.f;
+    auto v3 = [&](int k) { return V3{a[k], a[k + 1], a[k + 2]}; };
+    switch (op) {
+      case 0: o[0] = p_hat(v3(0)); break;
+      case 1: {
+        RSample x = rsample_zero(), y = rsample_zero();
+        x.x_v = v3(0);
+        x.n_v = v3(3);
+        y.x_v = v3(6);
+        y.n_v = v3(9);
+        o[0] = similar(x, y) ? 1.f : 0.f;
+        break;
+      }
+      case 2: {
+        RReservoir r = rres_zero();
+        r.w = a[0];
+        r.M = (uint32_t)a[1];
+        RSample s = rsample_zero();
+        s.valid = true;
+        res_update(r, s, a[2], a[3] != 0.f, a[4]);
+        o[0] = r.w;
+        o[1] = (float)r.M;
+        o[2] = r.z.valid ? 1.f : 0.f;
+        break;
+      }
+      case 3: {
+        RReservoir r = rres_zero();
+        r.w = a[0];
+        r.M = (uint32_t)a[1];
+        const bool taken = res_merge_w(r, a[2], (uint32_t)a[3], a[4], a[5] != 0.f, a[6]);
+        o[0] = r.w;
+        o[1] = (float)r.M;
+        o[2] = taken ? 1.f : 0.f;
+        break;
+      }
+      case 4: {
+        RReservoir nb = rres_zero();
+        nb.z.x_s = v3(3);
+        nb.z.n_s = v3(6);
+        nb.z.x_v = v3(9);
+        o[0] = jacobian_J(v3(0), nb);
+        break;
+      }
+      case 5:
+        o[0] = (float)pixel_index((int64_t)a[0], (int64_t)a[1], (uint32_t)a[2], (uint32_t)a[3], (uint32_t)a[4],
+                                  (uint32_t)a[5]);
+        break;
+      default: return -1;
+    }
+  }
+  return 0;
+}
+
 // Surface interaction from explicit vertex data (mtx_core/interaction.h
 // si_from_vertices, the arithmetic compute_si and the device's shading
 // records share) for the float64 pins of tests/test_shared_pins.py.
