@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MTX_ABI_VERSION 6
+#define MTX_ABI_VERSION 7
 
 enum {
   MTX_OK = 0,
@@ -352,6 +352,19 @@ int mtx_restir_state(mtx_ctx *ctx, int which, float *out, uint64_t n_floats);
 int mtx_sample_rays(mtx_ctx *ctx, const mtx_render_args *args, uint64_t n, const float *rays,
                     const uint32_t *lanes, uint32_t rng_skip, float *L, uint8_t *valid);
 
+/* Device-pointer forms (SURVEY §8b mtx_device_ptrs): the reference calls
+ * sample(), ray_intersect and its primitives on wavefront-wide Dr.Jit arrays
+ * that live on the GPU (path.py:194-202, prefix_sum.py:9-36,
+ * hashgrid.py:16-84, reductions.py:12-54). The *_dev functions take buffers
+ * in the context's device memory (hipMalloc'd; e.g. a torch CUDA tensor's
+ * data_ptr), with the layouts of their host twins, and copy nothing through
+ * the host: no staging copy, results written in place. Work runs on the
+ * context's stream and is complete on return (the caller orders its own
+ * producer of the inputs before the call). A host pointer is refused
+ * (MTX_E_ARG); device indices are range-checked on the device. */
+int mtx_sample_rays_dev(mtx_ctx *ctx, const mtx_render_args *args, uint64_t n, const float *rays,
+                        const uint32_t *lanes, uint32_t rng_skip, float *L, uint8_t *valid);
+
 /* Raw closest-hit / any-hit traversal (Scene.ray_intersect / ray_test,
  * path-mis.py:69-71, restirgi.py:320). rays: 8n floats (o.xyz, tmax, d.xyz,
  * 0); any_hit: 0 closest hit (4-wide tree), 1 any hit (8-wide occlusion
@@ -360,6 +373,9 @@ int mtx_sample_rays(mtx_ctx *ctx, const mtx_render_args *args, uint64_t n, const
  * visits (optional, 2n u32): node and triangle visits. */
 int mtx_trace(mtx_ctx *ctx, uint64_t n, const float *rays, int any_hit, uint32_t *hits,
               uint32_t *visits);
+/* mtx_trace on device buffers (Scene.ray_intersect on a device wavefront). */
+int mtx_trace_dev(mtx_ctx *ctx, uint64_t n, const float *rays, int any_hit, uint32_t *hits,
+                  uint32_t *visits);
 
 /* --------------------------- primitives --------------------------- */
 /* prefix_sum.py:9-36: inclusive (or exclusive) scan of u32, device-wide
@@ -368,11 +384,18 @@ int mtx_prefix_sum_u32(mtx_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t
 /* prefix_sum.py:9-36 with f32 data in Hillis-Steele summation order
  * (floor(log2 n)+1 passes x[j] += x[j-2^i]), bit-identical to the reference. */
 int mtx_prefix_sum_f32_hs(mtx_ctx *ctx, const float *in, float *out, uint64_t n);
+/* The two scans on device buffers (prefix_sum.py:9-36 on Dr.Jit arrays); the
+ * input is not modified. */
+int mtx_prefix_sum_u32_dev(mtx_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, int inclusive);
+int mtx_prefix_sum_f32_hs_dev(mtx_ctx *ctx, const float *in, float *out, uint64_t n);
 /* hashgrid.py:16-90: cell = hash(trunc((p-bbmin)/(bbmax-bbmin)*res)) % n_cells,
  * cell_size, exclusive cell_offset, and sample_idx (per-cell order ascending
  * by sample index). p: 3n floats (x[n], y[n], z[n] planes). */
 int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells,
                        uint32_t *cell, uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx);
+/* HashGrid(sample, ...) on device buffers (hashgrid.py:16-84 on Dr.Jit arrays). */
+int mtx_hashgrid_build_dev(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells,
+                           uint32_t *cell, uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx);
 /* reductions.py:12-54 scatter_reduce_with for func in {ADD=0, MIN=1, MAX=2,
  * MUL=3}: target[index[i]] = func(target[index[i]], value[i]), each target's
  * values applied in ascending i order (deterministic; the reference's order
@@ -382,6 +405,10 @@ int mtx_hashgrid_build(mtx_ctx *ctx, const float *p, uint64_t n, uint32_t resolu
  * tensors). target is read-modify-write. */
 int mtx_scatter_reduce_f32(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
                            const uint32_t *index, uint64_t n_value);
+/* scatter_reduce_with on device buffers (reductions.py:12-54 on Dr.Jit
+ * arrays); target is updated in place; an index >= n_target: MTX_E_ARG. */
+int mtx_scatter_reduce_f32_dev(mtx_ctx *ctx, int op, float *target, uint64_t n_target, const float *value,
+                               const uint32_t *index, uint64_t n_value);
 /* The stable group-by behind mtx_hashgrid_build / mtx_scatter_reduce_f32
  * for caller keys (< n_keys): key_size, exclusive key_offset and order
  * (element indices grouped by key, ascending inside a key). The Python

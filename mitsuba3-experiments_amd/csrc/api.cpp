@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -1551,8 +1552,53 @@ int mtx_restir_state(mtx_ctx *c, int which, float *out, uint64_t n_floats) {
   return MTX_OK;
 }
 
+// Device-pointer entry points (the *_dev functions of mtx.h): every buffer
+// must be memory of the context's device (hipMalloc'd, e.g. a torch CUDA
+// tensor's data_ptr); host memory is refused with MTX_E_ARG.
+static bool on_device(const mtx_ctx *c, const void *p) {
+  if (!p) return false;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky "invalid value" of an unregistered host pointer
+    return false;
+  }
+  return (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged) && at.device == c->device;
+}
+static int need_device(const mtx_ctx *c, const char *fn, std::initializer_list<const void *> ptrs) {
+  int k = 0;
+  for (const void *p : ptrs) {
+    if (p && !on_device(c, p)) {
+      mtx_set_error("%s: argument %d is not device memory of device %d", fn, k, c->device);
+      return MTX_E_ARG;
+    }
+    ++k;
+  }
+  return MTX_OK;
+}
+
+static int sample_rays_impl(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const float *rays,
+                            const uint32_t *lanes, uint32_t rng_skip, float *L, uint8_t *valid, bool dev);
+
 int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const float *rays, const uint32_t *lanes,
                     uint32_t rng_skip, float *L, uint8_t *valid) {
+  return sample_rays_impl(c, a, n, rays, lanes, rng_skip, L, valid, false);
+}
+
+int mtx_sample_rays_dev(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const float *rays, const uint32_t *lanes,
+                        uint32_t rng_skip, float *L, uint8_t *valid) {
+  if (c && n && (!rays || !lanes || !L || !valid)) {
+    mtx_set_error("mtx_sample_rays_dev: null buffer");
+    return MTX_E_ARG;
+  }
+  if (c && n) {
+    HIP_TRY(hipSetDevice(c->device));
+    if (int rc = need_device(c, "mtx_sample_rays_dev", {rays, lanes, L, valid})) return rc;
+  }
+  return sample_rays_impl(c, a, n, rays, lanes, rng_skip, L, valid, true);
+}
+
+static int sample_rays_impl(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const float *rays,
+                            const uint32_t *lanes, uint32_t rng_skip, float *L, uint8_t *valid, bool dev) {
   int rc = check_args(c, a);
   if (rc) return rc;
   if (a->integrator == MTX_INT_PSSMLT_SIMPLE || a->integrator == MTX_INT_PSSMLT_PATH ||
@@ -1572,17 +1618,27 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
   const bool nrc_cache = a->integrator == MTX_INT_NRC && (a->flags & 4u);
   const bool nerad_render = a->integrator == MTX_INT_NERAD;
   if ((nrc_cache || nerad_render) && (rc = ensure_cache(c, cap))) return rc;
-  if ((rc = dalloc(c->s0, 24ull * cap))) return rc;
-  if ((rc = dalloc(c->s1, 4ull * cap))) return rc;
-  if ((rc = dalloc(c->s2, 12ull * cap))) return rc;
-  if ((rc = dalloc(c->s3, 1ull * cap))) return rc;
+  if (!dev) {
+    if ((rc = dalloc(c->s0, 24ull * cap))) return rc;
+    if ((rc = dalloc(c->s1, 4ull * cap))) return rc;
+    if ((rc = dalloc(c->s2, 12ull * cap))) return rc;
+    if ((rc = dalloc(c->s3, 1ull * cap))) return rc;
+  }
   mtxd::WaveBuffers b = buffers(c);
   Timer tm{c, false};
   uint64_t nt = 0, ns = 0;
   for (uint64_t off = 0; off < n; off += cap) {
     const uint32_t m = (uint32_t)std::min<uint64_t>(cap, n - off);
-    HIP_TRY(hipMemcpyAsync(c->s0.p, rays + 6 * off, 24ull * m, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->s1.p, lanes + off, 4ull * m, hipMemcpyHostToDevice, c->stream));
+    // the chunk's rays / lanes / outputs: the caller's device buffers, or the
+    // context's staging copies of the host ones
+    const float *d_rays = dev ? rays + 6 * off : (const float *)c->s0.p;
+    const uint32_t *d_lanes = dev ? lanes + off : (const uint32_t *)c->s1.p;
+    float *d_L = dev ? L + 3 * off : (float *)c->s2.p;
+    uint8_t *d_valid = dev ? valid + off : (uint8_t *)c->s3.p;
+    if (!dev) {
+      HIP_TRY(hipMemcpyAsync(c->s0.p, rays + 6 * off, 24ull * m, hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(hipMemcpyAsync(c->s1.p, lanes + off, 4ull * m, hipMemcpyHostToDevice, c->stream));
+    }
     mtxd::ChunkParams p{};
     p.integrator = a->integrator;
     p.max_depth = a->max_depth;
@@ -1597,20 +1653,39 @@ int mtx_sample_rays(mtx_ctx *c, const mtx_render_args *a, uint64_t n, const floa
     p.nrc_cache = nrc_cache ? 1u : 0u;
     HIP_TRY(reset_counters(b, std::max<uint32_t>(a->max_depth, 1), c->stream));
     if (nrc_cache || nerad_render) HIP_TRY(hipMemsetAsync(b.cq_count, 0, 4, c->stream));
-    mtxd::launch_raygen_rays(c->scene, b, p, (const float *)c->s0.p, (const uint32_t *)c->s1.p, rng_skip, c->stream);
+    mtxd::launch_raygen_rays(c->scene, b, p, d_rays, d_lanes, rng_skip, c->stream);
     run_bounces(c, b, p, tm, &nt, &ns);
     if (nrc_cache && (rc = run_cache(c, b, m, tm))) return rc;
     if (nerad_render && (rc = run_cache(c, b, m, tm, true))) return rc;
-    mtxd::launch_collect(b, p, (float *)c->s2.p, (uint8_t *)c->s3.p, c->stream);
+    mtxd::launch_collect(b, p, d_L, d_valid, c->stream);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(valid + off, c->s3.p, m, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!dev) {
+      HIP_TRY(hipMemcpyAsync(L + 3 * off, c->s2.p, 12ull * m, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipMemcpyAsync(valid + off, c->s3.p, m, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));  // the staging buffers are reused by the next chunk
+    }
   }
+  if (dev) HIP_TRY(hipStreamSynchronize(c->stream));
   return MTX_OK;
 }
 
+static int trace_impl(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *hits, uint32_t *visits,
+                      bool dev);
+
 int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *hits, uint32_t *visits) {
+  return trace_impl(c, n, rays, any_hit, hits, visits, false);
+}
+
+int mtx_trace_dev(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *hits, uint32_t *visits) {
+  if (c && rays && hits && n) {
+    HIP_TRY(hipSetDevice(c->device));
+    if (int rc = need_device(c, "mtx_trace_dev", {rays, hits, visits})) return rc;
+  }
+  return trace_impl(c, n, rays, any_hit, hits, visits, true);
+}
+
+static int trace_impl(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *hits, uint32_t *visits,
+                      bool dev) {
   if (!c || !rays || !hits) {
     mtx_set_error("mtx_trace: null argument");
     return MTX_E_ARG;
@@ -1631,6 +1706,12 @@ int mtx_trace(mtx_ctx *c, uint64_t n, const float *rays, int any_hit, uint32_t *
   HIP_TRY(hipSetDevice(c->device));
   int rc;
   const size_t hit_words = any_hit == 1 ? n : 4 * n;
+  if (dev) {
+    mtxd::launch_trace_raw(c->scene, (const float4 *)rays, (uint32_t)n, any_hit, hits, visits, c->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MTX_OK;
+  }
   if ((rc = dalloc(c->s0, 32ull * n))) return rc;
   if ((rc = dalloc(c->s1, 4ull * hit_words))) return rc;
   if (visits && (rc = dalloc(c->s2, 8ull * n))) return rc;
@@ -1857,6 +1938,73 @@ int mtx_prefix_sum_f32_hs(mtx_ctx *c, const float *in, float *out, uint64_t n) {
   return MTX_OK;
 }
 
+int mtx_prefix_sum_u32_dev(mtx_ctx *c, const uint32_t *in, uint32_t *out, uint64_t n, int inclusive) {
+  if (!c || (n && (!in || !out))) {
+    mtx_set_error("mtx_prefix_sum_u32_dev: null argument");
+    return MTX_E_ARG;
+  }
+  if (n == 0) return MTX_OK;
+  if (n >= (1ull << 32)) {
+    mtx_set_error("mtx_prefix_sum_u32_dev: n >= 2^32");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = need_device(c, "mtx_prefix_sum_u32_dev", {in, out}))) return rc;
+  if ((rc = dalloc(c->s2, mtxd::scan_workspace_bytes(n)))) return rc;
+  if ((rc = prim_timer_begin(c))) return rc;
+  if ((rc = mtxd::scan_u32(in, out, n, inclusive, c->s2.p, c->stream))) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
+int mtx_prefix_sum_f32_hs_dev(mtx_ctx *c, const float *in, float *out, uint64_t n) {
+  if (!c || (n && (!in || !out))) {
+    mtx_set_error("mtx_prefix_sum_f32_hs_dev: null argument");
+    return MTX_E_ARG;
+  }
+  if (n == 0) return MTX_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = need_device(c, "mtx_prefix_sum_f32_hs_dev", {in, out}))) return rc;
+  if ((rc = dalloc(c->s1, 4 * n))) return rc;  // ping-pong partner of out
+  if ((rc = prim_timer_begin(c))) return rc;
+  if ((rc = mtxd::scan_f32_hs_to(in, out, (float *)c->s1.p, n, c->stream))) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
+int mtx_hashgrid_build_dev(mtx_ctx *c, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells,
+                           uint32_t *cell, uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx) {
+  if (!c || !p || !cell || !cell_size || !cell_offset || !sample_idx || n == 0 || n_cells == 0) {
+    mtx_set_error("mtx_hashgrid_build_dev: bad argument");
+    return MTX_E_ARG;
+  }
+  if (n >= (1ull << 31)) {
+    mtx_set_error("mtx_hashgrid_build_dev: n too large");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = need_device(c, "mtx_hashgrid_build_dev", {p, cell, cell_size, cell_offset, sample_idx}))) return rc;
+  if ((rc = dalloc(c->s5, mtxd::hashgrid_workspace_bytes(n, n_cells)))) return rc;
+  if ((rc = prim_timer_begin(c))) return rc;
+  if ((rc = mtxd::hashgrid_build(p, n, resolution, n_cells, cell, cell_size, cell_offset, sample_idx, c->s5.p,
+                                 c->stream)))
+    return rc;
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
 int mtx_hashgrid_build(mtx_ctx *c, const float *p, uint64_t n, uint32_t resolution, uint32_t n_cells, uint32_t *cell,
                        uint32_t *cell_size, uint32_t *cell_offset, uint32_t *sample_idx) {
   if (!c || !p || !cell || !cell_size || !cell_offset || !sample_idx || n == 0 || n_cells == 0) {
@@ -1956,6 +2104,41 @@ int mtx_group_by_u32_dev(mtx_ctx *c, const uint32_t *keys, uint64_t n, uint32_t 
   if ((rc = prim_timer_begin(c))) return rc;
   rc = mtxd::group_by_u32(keys, n, n_keys, key_size, key_offset, order, c->s5.p, c->stream);
   if (rc) return rc;
+  if ((rc = prim_timer_end(c))) return rc;
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  prim_timer_read(c);
+  return MTX_OK;
+}
+
+int mtx_scatter_reduce_f32_dev(mtx_ctx *c, int op, float *target, uint64_t n_target, const float *value,
+                               const uint32_t *index, uint64_t n_value) {
+  if (!c || !target || (n_value && (!value || !index)) || op < 0 || op > 3) {
+    mtx_set_error("mtx_scatter_reduce_f32_dev: bad argument");
+    return MTX_E_ARG;
+  }
+  if (n_value == 0 || n_target == 0) return MTX_OK;
+  if (n_value >= (1ull << 31) || n_target >= (1ull << 31)) {
+    mtx_set_error("mtx_scatter_reduce_f32_dev: size too large");
+    return MTX_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if ((rc = need_device(c, "mtx_scatter_reduce_f32_dev", {target, value, index}))) return rc;
+  if ((rc = dalloc(c->s3, mtxd::scatter_workspace_bytes(n_target, n_value)))) return rc;
+  if ((rc = dalloc(c->s6, 64))) return rc;
+  // the indices are device data: range-checked on the device first
+  HIP_TRY(hipMemsetAsync(c->s6.p, 0, 4, c->stream));
+  mtxd::keys_in_range(index, n_value, (uint32_t)n_target, (uint32_t *)c->s6.p, c->stream);
+  uint32_t bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, c->s6.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (bad) {
+    mtx_set_error("mtx_scatter_reduce_f32_dev: an index is >= n_target (%llu)", (unsigned long long)n_target);
+    return MTX_E_ARG;
+  }
+  if ((rc = prim_timer_begin(c))) return rc;
+  if ((rc = mtxd::scatter_reduce_f32(op, target, n_target, value, index, n_value, c->s3.p, c->stream))) return rc;
   if ((rc = prim_timer_end(c))) return rc;
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));

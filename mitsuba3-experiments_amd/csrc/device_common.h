@@ -170,7 +170,12 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t *counte
 // Inside a block step's range of the second queue the entries with p1_hi
 // follow the others (NEE shadow rays: the rays of one emitter together, so
 // the any-hit waves that claim them walk one light's shadow frusta).
-template <int BLOCK>
+// RAW: the barriers wait for LDS only (s_waitcnt lgkmcnt(0); s_barrier), not
+// for vector memory: an LDS-DMA in flight (k_shade's record prefetch) stays
+// in flight across them (__syncthreads() would wait vmcnt(0) for it).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int BLOCK, bool RAW = false>
 __device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint32_t *c, uint32_t parity,
                                               uint32_t &s0, uint32_t &s1) {
   constexpr int W = BLOCK / 64;
@@ -183,7 +188,10 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint
     wcnt[parity][1][wave] = (uint32_t)__popcll(ml);
     wcnt[parity][2][wave] = (uint32_t)__popcll(mh);
   }
-  __syncthreads();
+  if constexpr (RAW)
+    lds_barrier();
+  else
+    __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t0 = 0, tl = 0, th = 0;
 #pragma unroll
@@ -199,7 +207,10 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint
     bbase[parity][1] = (uint32_t)(base >> 32);
     bbase[parity][2] = (uint32_t)(base >> 32) + tl;
   }
-  __syncthreads();
+  if constexpr (RAW)
+    lds_barrier();
+  else
+    __syncthreads();
   uint32_t o0 = bbase[parity][0], ol = bbase[parity][1], oh = bbase[parity][2];
   for (uint32_t w = 0; w < wave; ++w) {
     o0 += wcnt[parity][0][w];

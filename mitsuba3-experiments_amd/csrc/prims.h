@@ -15,6 +15,8 @@ int scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, int inclusive, void 
 // device ping-pong buffers (a holds the input); *result points at the one
 // holding the output.
 int scan_f32_hs(float *a, float *b, uint64_t n, float **result, hipStream_t st);
+// the same from a read-only `in`; the result lands in `out` (tmp: n floats)
+int scan_f32_hs_to(const float *in, float *out, float *tmp, uint64_t n, hipStream_t st);
 
 size_t hashgrid_workspace_bytes(uint64_t n, uint32_t n_cells);
 int hashgrid_build(const float *p, uint64_t n, uint32_t res, uint32_t n_cells, uint32_t *cell, uint32_t *cell_size,

@@ -1323,6 +1323,27 @@ int scan_f32_hs(float *a, float *b, uint64_t n, float **result, hipStream_t st) 
   return MTX_OK;
 }
 
+// The same passes from a read-only input into `out`, with `tmp` as the
+// ping-pong partner: the LDS pass writes whichever of the two makes the
+// last global pass land in `out` (device-pointer entry points: the caller's
+// input is not clobbered and no copy-back is needed).
+int scan_f32_hs_to(const float *in, float *out, float *tmp, uint64_t n, hipStream_t st) {
+  if (n == 0) return MTX_OK;
+  int passes = 0;
+  while ((1ull << passes) < n) ++passes;
+  const int local = passes < kHsLog ? passes : kHsLog;
+  const int global = passes - local;
+  float *x = (global & 1) ? tmp : out, *y = (global & 1) ? out : tmp;
+  hipLaunchKernelGGL(k_hs_local, dim3(nblk(n, kHsTile)), dim3(256), 0, st, in, x, n, local);
+  for (int i = local; i < passes; ++i) {
+    hipLaunchKernelGGL(k_hs_pass, dim3(nblk(n, 256)), dim3(256), 0, st, x, y, n, 1ull << i);
+    float *t = x;
+    x = y;
+    y = t;
+  }
+  return MTX_OK;
+}
+
 static int bits_for(uint64_t k) {
   int b = 0;
   while (b < 32 && (1ull << b) < k) ++b;

@@ -58,6 +58,12 @@ constexpr uint32_t kOccLdsStack = 8;
 // per 64-B node, straight into LDS (LDS-DMA; device_common.h coop_fetch_nodes)
 #define MTX_COOP_NODE 0
 #endif
+#ifndef MTX_SHADE_DMA
+// k_shade (path-mis / path / nrc): the next step's 128-B shading records are
+// gathered into LDS by LDS-DMA while this step's appends run, 8 lanes per
+// record (kernels.hip dma_records); 0: read from global memory in the step
+#define MTX_SHADE_DMA 0
+#endif
 #ifndef MTX_SHADE_WARM
 #define MTX_SHADE_WARM 1  // k_shade: warm L2 with the next entry's shading record
 #endif

@@ -22,6 +22,8 @@ from .integrators import (  # noqa: F401
     mtx_scene_of,
     register_integrator,
     register_with_mitsuba,
+    scene_with_sensor,
+    trace_rays,
 )
 
 __version__ = "0.1.0"

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 6
+MTX_ABI_VERSION = 7
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -279,11 +279,17 @@ EXPORTS = [
     "mtx_restir_rows",
     "mtx_restir_state",
     "mtx_sample_rays",
+    "mtx_sample_rays_dev",
     "mtx_trace",
+    "mtx_trace_dev",
     "mtx_prefix_sum_u32",
     "mtx_prefix_sum_f32_hs",
+    "mtx_prefix_sum_u32_dev",
+    "mtx_prefix_sum_f32_hs_dev",
     "mtx_hashgrid_build",
+    "mtx_hashgrid_build_dev",
     "mtx_scatter_reduce_f32",
+    "mtx_scatter_reduce_f32_dev",
     "mtx_group_by_u32",
     "mtx_group_by_u32_dev",
     "mtx_field_upload",

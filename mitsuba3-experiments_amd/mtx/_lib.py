@@ -66,11 +66,17 @@ def lib() -> C.CDLL:
         "mtx_restir_rows": ([vp, C.c_int, u32, u32, vp, C.c_int], C.c_int),
         "mtx_restir_state": ([vp, C.c_int, vp, u64], C.c_int),
         "mtx_sample_rays": ([vp, C.POINTER(_abi.RenderArgs), u64, vp, vp, u32, vp, vp], C.c_int),
+        "mtx_sample_rays_dev": ([vp, C.POINTER(_abi.RenderArgs), u64, vp, vp, u32, vp, vp], C.c_int),
         "mtx_trace": ([vp, u64, vp, C.c_int, vp, vp], C.c_int),
+        "mtx_trace_dev": ([vp, u64, vp, C.c_int, vp, vp], C.c_int),
         "mtx_prefix_sum_u32": ([vp, vp, vp, u64, C.c_int], C.c_int),
         "mtx_prefix_sum_f32_hs": ([vp, vp, vp, u64], C.c_int),
+        "mtx_prefix_sum_u32_dev": ([vp, vp, vp, u64, C.c_int], C.c_int),
+        "mtx_prefix_sum_f32_hs_dev": ([vp, vp, vp, u64], C.c_int),
         "mtx_hashgrid_build": ([vp, vp, u64, u32, u32, vp, vp, vp, vp], C.c_int),
+        "mtx_hashgrid_build_dev": ([vp, vp, u64, u32, u32, vp, vp, vp, vp], C.c_int),
         "mtx_scatter_reduce_f32": ([vp, C.c_int, vp, u64, vp, vp, u64], C.c_int),
+        "mtx_scatter_reduce_f32_dev": ([vp, C.c_int, vp, u64, vp, vp, u64], C.c_int),
         "mtx_group_by_u32": ([vp, vp, u64, u32, vp, vp, vp], C.c_int),
         "mtx_group_by_u32_dev": ([vp, vp, u64, u32, vp, vp, vp], C.c_int),
         "mtx_field_train_init": ([vp, C.POINTER(_abi.FieldOpt)], C.c_int),

@@ -155,6 +155,8 @@ class SamplingIntegrator:
         (Dr.Jit's Array3f layout)."""
         obj = hasattr(ray, "o") and hasattr(ray, "d")
         o, d = (ray.o, ray.d) if obj else ray
+        if _is_cuda(o) or _is_cuda(d):
+            return self._sample_device(scene, sampler, o, d, obj)
         rays = np.ascontiguousarray(np.concatenate([_rows3(o, obj), _rows3(d, obj)], 1))
         n = len(rays)
         if len(sampler.lanes) != n:
@@ -167,6 +169,79 @@ class SamplingIntegrator:
         check(lib().mtx_sample_rays(ctx.handle, C.byref(a), n, rays.ctypes.data, sampler.lanes.ctypes.data,
                                     sampler.skip, L.ctypes.data, valid.ctypes.data), "mtx_sample_rays")
         return L, valid.astype(bool), []
+
+    def _sample_device(self, scene, sampler, o, d, obj):
+        """sample() on a wavefront already in HBM (torch CUDA tensors, as the
+        reference's Dr.Jit arrays are, path.py:194-202): rays, lanes, L and
+        valid stay on the device (mtx_sample_rays_dev); returns tensors."""
+        import torch
+
+        def rows(v):
+            t = torch.as_tensor(v, dtype=torch.float32, device=dev)
+            if t.dim() == 2 and t.shape[0] == 3 and (obj or t.shape[1] != 3):
+                t = t.T
+            elif t.dim() == 2 and t.shape == (3, 3):
+                raise MtxError("ambiguous 3x3 ray array: pass a ray object (Dr.Jit (3, N) fields) "
+                               "or (N, 3) tensors with N != 3")
+            return t.reshape(-1, 3)
+
+        dev = next(x.device for x in (o, d) if _is_cuda(x))
+        rays = torch.cat([rows(o), rows(d)], 1).contiguous()
+        n = rays.shape[0]
+        lanes = torch.as_tensor(np.asarray(sampler.lanes, np.uint32).view(np.int32), device=dev) \
+            if not _is_cuda(sampler.lanes) else sampler.lanes.to(torch.int32)
+        lanes = lanes.contiguous()
+        if len(lanes) != n:
+            raise MtxError("sampler lanes and rays differ in length")
+        L = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        valid = torch.empty(n, dtype=torch.uint8, device=dev)
+        ctx = context(dev.index if dev.index is not None else torch.cuda.current_device())
+        _bind_scene(ctx, scene)
+        a = self.render_args(scene, sampler.seed, 1)
+        torch.cuda.current_stream(dev).synchronize()  # libmtx runs on its own stream
+        check(lib().mtx_sample_rays_dev(ctx.handle, C.byref(a), n, rays.data_ptr(), lanes.data_ptr(), sampler.skip,
+                                        L.data_ptr(), valid.data_ptr()), "mtx_sample_rays_dev")
+        return L, valid.bool(), []
+
+
+def _is_cuda(x) -> bool:
+    import sys
+
+    torch = sys.modules.get("torch")
+    return torch is not None and isinstance(x, torch.Tensor) and x.is_cuda
+
+
+def trace_rays(scene, rays, any_hit: bool = False, visits: bool = False, device: int | None = None):
+    """Scene.ray_intersect / Scene.ray_test (path-mis.py:69-71, restirgi.py:320)
+    over a wavefront of rays: (N, 8) float32 rows (o.xyz, tmax, d.xyz, 0).
+    Closest hit: (N, 4) words (t, prim bits, u, v bits; t = inf on a miss);
+    any hit: (N,) 1 = occluded. A torch CUDA tensor is traced where it lies
+    (mtx_trace_dev) and the results are int32 tensors there; numpy goes
+    through mtx_trace. visits=True also returns (N, 2) node / triangle visits."""
+    if _is_cuda(rays):
+        import torch
+
+        r = rays.to(torch.float32).reshape(-1, 8).contiguous()
+        n = r.shape[0]
+        hits = torch.empty((n,) if any_hit else (n, 4), dtype=torch.int32, device=r.device)
+        vis = torch.empty((n, 2), dtype=torch.int32, device=r.device) if visits else None
+        ctx = context(r.device.index if r.device.index is not None else torch.cuda.current_device())
+        _bind_scene(ctx, scene)
+        torch.cuda.current_stream(r.device).synchronize()
+        if n:
+            check(lib().mtx_trace_dev(ctx.handle, n, r.data_ptr(), int(any_hit), hits.data_ptr(),
+                                      vis.data_ptr() if visits else None), "mtx_trace_dev")
+        return (hits, vis) if visits else hits
+    r = np.ascontiguousarray(rays, np.float32).reshape(-1, 8)
+    n = len(r)
+    hits = np.zeros((n,) if any_hit else (n, 4), np.uint32)
+    vis = np.zeros((n, 2), np.uint32) if visits else None
+    ctx = context(device)
+    _bind_scene(ctx, scene)
+    if n:
+        check(lib().mtx_trace(ctx.handle, n, r.ctypes.data, int(any_hit), hits.ctypes.data,
+                              vis.ctypes.data if visits else None), "mtx_trace")
+    return (hits, vis) if visits else hits
 
 
 class Path(SamplingIntegrator):

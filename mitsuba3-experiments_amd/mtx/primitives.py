@@ -10,9 +10,42 @@ ADD, MIN, MAX, MUL = 0, 1, 2, 3
 _OPS = {"add": ADD, "min": MIN, "max": MAX, "mul": MUL}
 
 
+def _dev_ctx(t):
+    """The context of a torch CUDA tensor's device, after the tensor's
+    producers on torch's stream have finished (libmtx runs on its own
+    stream; its *_dev calls return with their results complete)."""
+    import torch
+
+    dev = t.device
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    torch.cuda.current_stream(dev).synchronize()
+    return context(idx)
+
+
 def prefix_sum(x, inclusive: bool = True, device: int | None = None):
     """prefix_sum.py:9-36. u32 input: single-pass decoupled look-back scan.
-    f32 input: Hillis-Steele passes in the reference's exact summation order."""
+    f32 input: Hillis-Steele passes in the reference's exact summation order.
+    A torch CUDA tensor stays in HBM (mtx_prefix_sum_*_dev: no host copy;
+    u32 data as torch.int32 / torch.uint32 bits) and the result is one."""
+    if _torch_cuda(x):
+        import torch
+
+        t = x.contiguous()
+        out = torch.empty_like(t)
+        if len(t) == 0:
+            return out
+        ctx = _dev_ctx(t)
+        if t.dtype in (torch.int32, getattr(torch, "uint32", torch.int32)):
+            check(lib().mtx_prefix_sum_u32_dev(ctx.handle, t.data_ptr(), out.data_ptr(), len(t), int(inclusive)),
+                  "mtx_prefix_sum_u32_dev")
+        elif t.dtype == torch.float32:
+            if not inclusive:
+                raise ValueError("the Hillis-Steele f32 scan is inclusive (prefix_sum.py:25-32)")
+            check(lib().mtx_prefix_sum_f32_hs_dev(ctx.handle, t.data_ptr(), out.data_ptr(), len(t)),
+                  "mtx_prefix_sum_f32_hs_dev")
+        else:
+            raise TypeError("prefix_sum supports uint32 (int32 bits) and float32 tensors")
+        return out
     x = np.ascontiguousarray(x)
     out = np.zeros_like(x)
     ctx = context(device)
@@ -47,6 +80,22 @@ class HashGrid:
     produce, and a deterministic one), cell (per-sample cell index)."""
 
     def __init__(self, sample, resolution: int, n_cells: int | None = None, device: int | None = None):
+        if _torch_cuda(sample):  # a [3, n] float32 tensor in HBM: mtx_hashgrid_build_dev, int32 results there
+            import torch
+
+            p = sample.to(torch.float32).reshape(3, -1).contiguous()
+            n = p.shape[1]
+            self.n_samples, self.resolution = n, int(resolution)
+            self.n_cells = int(n_cells if n_cells is not None else n)
+            kw = {"dtype": torch.int32, "device": p.device}
+            self.cell, self.sample_idx = torch.empty(n, **kw), torch.empty(n, **kw)
+            self.cell_size, self.cell_offset = torch.empty(self.n_cells, **kw), torch.empty(self.n_cells, **kw)
+            ctx = _dev_ctx(p)
+            check(lib().mtx_hashgrid_build_dev(ctx.handle, p.data_ptr(), n, self.resolution, self.n_cells,
+                                               self.cell.data_ptr(), self.cell_size.data_ptr(),
+                                               self.cell_offset.data_ptr(), self.sample_idx.data_ptr()),
+                  "mtx_hashgrid_build_dev")
+            return
         p = np.ascontiguousarray(np.asarray(sample, np.float32).reshape(3, -1))
         n = p.shape[1]
         self.n_samples = n
@@ -192,12 +241,23 @@ def scatter_reduce_with(op, target, value, index, device: int | None = None):
         size, offset, order = group_by(idx, len(tgt), device)
         return fold_rounds(op, tgt, value, size, offset, order)
     if on_device:
-        # the fixed ops take host pointers (mtx_scatter_reduce_f32): one copy each way
+        # the fixed ops on HBM tensors (mtx_scatter_reduce_f32_dev): no host copy
         import torch
 
         dev = next(x.device for x in (target, value, index) if _torch_cuda(x))
-        host = [x.cpu().numpy() if _torch_cuda(x) else x for x in (target, value, index)]
-        return torch.as_tensor(scatter_reduce_with(op, *host, device=dev.index), device=dev)
+        t = torch.as_tensor(target, device=dev).to(torch.float32).clone().contiguous()
+        v = torch.as_tensor(value, device=dev).to(torch.float32).contiguous()
+        i = torch.as_tensor(index, device=dev)
+        if i.dtype not in (torch.int32, getattr(torch, "uint32", torch.int32)):
+            if len(i) and int(i.min().item()) < 0:
+                raise ValueError("scatter_reduce_with: index out of range")
+            i = i.to(torch.int32)
+        i = i.contiguous()
+        if len(v) and len(t):
+            ctx = _dev_ctx(t)
+            check(lib().mtx_scatter_reduce_f32_dev(ctx.handle, int(op), t.data_ptr(), len(t), v.data_ptr(),
+                                                   i.data_ptr(), len(v)), "mtx_scatter_reduce_f32_dev")
+        return t
     t = np.array(target, np.float32)
     v = np.ascontiguousarray(value, np.float32)
     i = np.ascontiguousarray(index, np.uint32)

@@ -126,7 +126,7 @@ def sample_rays(scene, args, rays, lanes, rng_skip=2):
 
 def trace(scene, rays, any_hit=False, brute=False):
     n = len(rays)
-    hits = np.zeros(n if int(any_hit) == 1 else 4 * n, np.uint32)  # any_hit 2: closest hit on the 8-wide tree
+    hits = np.zeros(n if int(any_hit) == 1 else 4 * n, np.uint32)
     visits = np.zeros(2 * n, np.uint32)
     d = scene.desc()
     lib().orc_trace(C.byref(d), n, np.ascontiguousarray(rays, np.float32).ctypes.data, int(any_hit), int(brute),

@@ -26,7 +26,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 6
+    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 7
 
 
 def test_struct_sizes_match_header():
