@@ -1960,3 +1960,13 @@ void launch_trace_raw(const DevScene &s, const float4 *rays, uint32_t n, int any
 }
 
 }  // namespace mtxd
+
+#ifdef MTX_TEST_BAD_SHADOW_FORM
+// tests/test_abi.py::test_shadow_record_form_is_checked: an integrator whose L
+// lives outside k_shade's stores asking for the final-value form must not compile.
+__device__ void mtx_bad_shadow_form(mtxd::ShadeIO &io, const mtx::SurfaceInteraction &si,
+                                    const mtx::DirectionSample &ds) {
+  const mtx::V3 L = mtx::v3s(0.f);
+  mtxd::make_shadow<MTX_INT_NERAD_RHS, true>(io, si, ds, L, L, L, true, &L);
+}
+#endif

@@ -5,6 +5,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 
 from conftest import ROOT
 
@@ -83,3 +84,25 @@ def test_roughplastic_tables():
     assert ((tab > 0) & (tab <= 1)).all()
     assert tab[-1] > 0.9  # normal incidence: ~4 % Fresnel reflectance
     assert 0.3 < internal.value < 0.8
+
+
+def test_shadow_record_form_is_checked():
+    """make_shadow<INT, FINAL> (kernels.hip) static_asserts that an
+    integrator's shadow-record form matches where its L is stored
+    (shadow_final_form): the round-5 nerad regression made at compile time.
+    A final-value record for the nerad RHS (L by path, read-modify-write
+    form) must not compile; the library's own instantiations do."""
+    import os
+    import shutil
+    import subprocess
+
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "mitsuba3-experiments_amd", "csrc", "kernels.hip")
+    cmd = [hipcc, "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(root, "include"), "-fsyntax-only", src]
+    ok = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert ok.returncode == 0, ok.stderr[-2000:]
+    bad = subprocess.run(cmd + ["-DMTX_TEST_BAD_SHADOW_FORM"], capture_output=True, text=True, timeout=300)
+    assert bad.returncode != 0 and "shadow record form does not match" in bad.stderr

@@ -396,11 +396,37 @@ def prims(args):
         fn()
         return time.perf_counter() - t0
 
+    import torch
+
+    def api_ms(fn, reps=3):
+        """End-to-end wall time of one API call (the call returns with its
+        results complete), best of reps: the device-tensor form (inputs and
+        outputs in HBM, *_dev entry points) and the numpy form (host copies
+        both ways) -- beside the kernels' HIP-event time."""
+        fn()
+        t = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            t.append((time.perf_counter() - t0) * 1e3)
+        return round(min(t), 3)
+
+    def api_extra(dev_fn, host_fn, kernel_ms):
+        return {"api_ms_device_tensors": api_ms(dev_fn), "api_ms_host_arrays": api_ms(host_fn, reps=2),
+                "kernel_ms": round(kernel_ms, 4),
+                "api_note": "end-to-end wall time of the Python call: device tensors (mtx_*_dev, no host copy) "
+                            "and numpy arrays (host<->device copies); kernel_ms is the HIP-event time of the "
+                            "device work alone (the line's value)"}
+
     rng = np.random.default_rng(0)
     # prefix_sum u32, n = 2^28 (SURVEY §8d): 8 B/element
     n = 1 << 28
     x = rng.integers(0, 1 << 16, n, dtype=np.uint32)
     ms = best(lambda: primitives.prefix_sum(x))
+    xt = torch.as_tensor(x.view(np.int32), device="cuda")
+    ext = api_extra(lambda: primitives.prefix_sum(xt), lambda: primitives.prefix_sum(x), ms)
+    del xt
     nc = 1 << 28
     c = cpu_time(lambda: oracle.prefix_sum_u32_mt(x[:nc]))
     ach = 8 * n / (ms / 1e3) / 1e9
@@ -411,12 +437,14 @@ def prims(args):
            "alg_bytes_per_launch": 8 * n},
           {"value": round(nc / c / 1e9, 4), "unit": "Gelem/s", "cores": _threads(), "kind": "port",
            "sample": f"same 2^28 elements ({c:.2f} s), oracle orc_prefix_sum_u32_mt (OpenMP, equal to the "
-                     "sequential restatement)"}, dtype="u32")
+                     "sequential restatement)"}, extra=ext, dtype="u32")
     del x
     # prefix_sum f32 in Hillis-Steele order, n = 2^24
     n = 1 << 24
     xf = rng.random(n, dtype=np.float32)
     ms = best(lambda: primitives.prefix_sum(xf))
+    xft = torch.as_tensor(xf, device="cuda")
+    ext = api_extra(lambda: primitives.prefix_sum(xft), lambda: primitives.prefix_sum(xf), ms)
     c = cpu_time(lambda: oracle.prefix_sum_f32_hs_mt(xf))
     passes = int(np.floor(np.log2(n))) + 1
     ach = 8 * n / (ms / 1e3) / 1e9
@@ -431,11 +459,14 @@ def prims(args):
            "hs_note": "bytes the reference's Hillis-Steele order needs with 11 passes fused in LDS "
                       "(12 B/element) + one 2-read/1-write pass per remaining level (12 B/element each)"},
           {"value": round(n / c / 1e9, 4), "unit": "Gelem/s", "cores": _threads(), "kind": "port",
-           "sample": f"same 2^24 elements ({c:.2f} s), oracle orc_prefix_sum_f32_hs_mt (OpenMP passes)"})
+           "sample": f"same 2^24 elements ({c:.2f} s), oracle orc_prefix_sum_f32_hs_mt (OpenMP passes)"}, extra=ext)
     # hash grid, n = 2^24 points, res 100, n_cells = n (hashgrid.py:16-84)
     n = 1 << 24
     p = rng.random((3, n), dtype=np.float32)
     ms = best(lambda: primitives.HashGrid(p, 100, n))
+    pt = torch.as_tensor(p, device="cuda")
+    ext = api_extra(lambda: primitives.HashGrid(pt, 100, n), lambda: primitives.HashGrid(p, 100, n), ms)
+    del pt
     nc = n
     c = cpu_time(lambda: oracle.hashgrid_mt(p, 100, nc))
     ach = 32 * n / (ms / 1e3) / 1e9
@@ -446,7 +477,8 @@ def prims(args):
            "peak": bench.HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None,
            "alg_bytes_per_launch": 32 * n, "note": "SURVEY §8d: ~32 B/sample"},
           {"value": round(nc / c / 1e6, 4), "unit": "Msamples/s", "cores": _threads(), "kind": "port",
-           "sample": f"same 2^24 points ({c:.2f} s), oracle orc_hashgrid_mt (OpenMP, parallel sort)"}, dtype="u32")
+           "sample": f"same 2^24 points ({c:.2f} s), oracle orc_hashgrid_mt (OpenMP, parallel sort)"}, extra=ext,
+          dtype="u32")
     del p
     # scatter_reduce add, nv = 2^24, nt = 2^20 (reductions.py:12-54)
     nv, nt = 1 << 24, 1 << 20
@@ -454,6 +486,9 @@ def prims(args):
     val = rng.random(nv, dtype=np.float32)
     tgt = np.zeros(nt, np.float32)
     ms = best(lambda: primitives.scatter_reduce_with("add", tgt, val, idx))
+    tt, vt, it = (torch.as_tensor(a, device="cuda") for a in (tgt, val, idx.view(np.int32)))
+    ext = api_extra(lambda: primitives.scatter_reduce_with("add", tt, vt, it),
+                    lambda: primitives.scatter_reduce_with("add", tgt, val, idx), ms)
     c = cpu_time(lambda: oracle.scatter_reduce_mt(0, tgt, val, idx))
     ach = 16 * nv / (ms / 1e3) / 1e9
     _line("scatter_reduce add Gvalues/sec (reductions.py:12-54), nv=2^24 nt=2^20", nv / (ms / 1e3) / 1e9,
@@ -465,7 +500,8 @@ def prims(args):
            "unit": "GB/s", "frac": round(ach / bench.HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_launch": 16 * nv,
            "note": "SURVEY §8d: 16 B/value"},
           {"value": round(nv / c / 1e9, 4), "unit": "Gvalues/s", "cores": _threads(), "kind": "port",
-           "sample": f"same {nv} values ({c:.2f} s), oracle orc_scatter_reduce_f32_mt (OpenMP, parallel sort)"})
+           "sample": f"same {nv} values ({c:.2f} s), oracle orc_scatter_reduce_f32_mt (OpenMP, parallel sort)"},
+          extra=ext)
 
 
 # ------------------------------------------------- radiance field (MFMA) --
