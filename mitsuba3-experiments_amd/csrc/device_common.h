@@ -32,11 +32,9 @@ inline size_t stack_bytes(const DevScene &s) {
 // area ([entry - lds_entries][thread], coalesced per depth), rarely touched.
 // Behind the stack columns each block holds an LDS copy of the first lds_top
 // nodes of its tree (the top of the breadth-first tree).
-// MTX_COOP_NODE: + a 64-B node slot per closest-hit lane (coop_fetch_nodes).
 inline size_t persistent_stack_bytes(const DevScene &s, bool occ) {
   return occ ? (size_t)s.occ_lds_entries * kTraceBlock * sizeof(uint2) + (size_t)s.occ_lds_top * 80
-             : (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t) + (size_t)s.lds_top * 64 +
-                   (MTX_COOP_NODE ? (size_t)kTraceBlock * 64 : 0);
+             : (size_t)s.lds_entries * kTraceBlock * sizeof(int32_t) + (size_t)s.lds_top * 64;
 }
 
 __device__ __forceinline__ SceneView make_view(const DevScene &s) {
@@ -170,12 +168,7 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t *counte
 // Inside a block step's range of the second queue the entries with p1_hi
 // follow the others (NEE shadow rays: the rays of one emitter together, so
 // the any-hit waves that claim them walk one light's shadow frusta).
-// RAW: the barriers wait for LDS only (s_waitcnt lgkmcnt(0); s_barrier), not
-// for vector memory: an LDS-DMA in flight (k_shade's record prefetch) stays
-// in flight across them (__syncthreads() would wait vmcnt(0) for it).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <int BLOCK, bool RAW = false>
+template <int BLOCK>
 __device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint32_t *c, uint32_t parity,
                                               uint32_t &s0, uint32_t &s1) {
   constexpr int W = BLOCK / 64;
@@ -188,10 +181,7 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint
     wcnt[parity][1][wave] = (uint32_t)__popcll(ml);
     wcnt[parity][2][wave] = (uint32_t)__popcll(mh);
   }
-  if constexpr (RAW)
-    lds_barrier();
-  else
-    __syncthreads();
+  __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t0 = 0, tl = 0, th = 0;
 #pragma unroll
@@ -207,10 +197,7 @@ __device__ __forceinline__ void block_append2(bool p0, bool p1, bool p1_hi, uint
     bbase[parity][1] = (uint32_t)(base >> 32);
     bbase[parity][2] = (uint32_t)(base >> 32) + tl;
   }
-  if constexpr (RAW)
-    lds_barrier();
-  else
-    __syncthreads();
+  __syncthreads();
   uint32_t o0 = bbase[parity][0], ol = bbase[parity][1], oh = bbase[parity][2];
   for (uint32_t w = 0; w < wave; ++w) {
     o0 += wcnt[parity][0][w];
@@ -256,53 +243,6 @@ __device__ __forceinline__ void lds_node64(const int4 *top, int32_t node, int4 &
   rf = make_int4(x1.x, x1.y, x1.z, x1.w);
   qa = make_int4(x2.x, x2.y, x2.z, x2.w);
   qb = make_int2(x3.x, x3.y);
-}
-
-// The 64-B node at LDS byte address la (the tree-top copy, or a lane's slot
-// of coop_fetch_nodes). The wait covers the LDS-DMA that filled the slot.
-__device__ __forceinline__ void lds_node64_at(uint32_t la, int4 &a, int4 &rf, int4 &qa, int2 &qb) {
-  typedef int v4i __attribute__((ext_vector_type(4)));
-  typedef int v2i __attribute__((ext_vector_type(2)));
-  v4i x0, x1, x2;
-  v2i x3;
-  asm volatile(
-      "s_waitcnt vmcnt(0)\n\t"
-      "ds_read_b128 %0, %4\n\t"
-      "ds_read_b128 %1, %4 offset:16\n\t"
-      "ds_read_b128 %2, %4 offset:32\n\t"
-      "ds_read_b64 %3, %4 offset:48\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
-      : "v"(la)
-      : "memory");
-  a = make_int4(x0.x, x0.y, x0.z, x0.w);
-  rf = make_int4(x1.x, x1.y, x1.z, x1.w);
-  qa = make_int4(x2.x, x2.y, x2.z, x2.w);
-  qb = make_int2(x3.x, x3.y);
-}
-
-// Cooperative node fetch (MTX_COOP_NODE): every lane of the wave calls it.
-// Lanes with `want` need global node `node`; instruction j fetches the nodes
-// of lanes 16j .. 16j + 15, four lanes per node (16 B each), so one
-// wave-instruction touches at most 16 nodes' lines instead of 64 (the TA
-// prices an instruction by the lines it touches: profiles/r3_ta_rate.txt).
-// LDS-DMA writes lane-linear (wave-uniform base + 16 B x lane): lane m's
-// node lands at wstage + 64 m.
-__device__ __forceinline__ void coop_fetch_nodes(const int4 *nodes, int32_t node, bool want, int4 *wstage,
-                                                 uint32_t lane) {
-  const uint64_t m = __ballot(want);
-  if (m == 0) return;
-  int32_t n[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) n[j] = __shfl(node, 16 * j + (int)(lane >> 2));
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t src = 16u * j + (lane >> 2);
-    if ((m >> src) & 1ull)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void *)(nodes + 4 * (size_t)n[j] + (lane & 3u)),
-          (__attribute__((address_space(3))) void *)(wstage + 64 * j), 16, 0, 0);
-  }
 }
 
 // Slab tests of a 4-wide node's children (words a, rf, qa, qb of mtx.h) and
@@ -644,7 +584,7 @@ __device__ __forceinline__ void count_wave_iter(uint32_t lane, uint32_t *ctr) {
 template <bool STATS, class Src>
 __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src &src, uint32_t count, uint32_t *heads,
                                                    int32_t *stk, const int4 *top, uint32_t &nv, uint32_t &tv,
-                                                   uint32_t &nr, uint32_t *wave_iters, int4 *wstage = nullptr) {
+                                                   uint32_t &nr, uint32_t *wave_iters) {
   const uint32_t lane = lane_id();
   int32_t *ovf = reinterpret_cast<int32_t *>(s.stack_ovf) + blockIdx.x * kTraceBlock + threadIdx.x;
   const int lds_n = (int)s.lds_entries, top_n = (int)s.lds_top;
@@ -680,20 +620,7 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
       if (STATS) count_wave_iter(lane, &wave_iters[0]);
       int32_t cr[4];
       ++nv;
-#if MTX_COOP_NODE
-      int n;
-      {
-        const uint32_t la = node < top_n
-                                ? (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)top + 64u * (uint32_t)node
-                                : (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char *)wstage + 64u * lane;
-        int4 a, rf, qa;
-        int2 qb;
-        lds_node64_at(la, a, rf, qa, qb);
-        n = wide_visit_regs(r, a, rf, qa, qb, tbest, cr);
-      }
-#else
       const int n = wide_visit(s, r, node, tbest, cr, top, top_n);
-#endif
       if (n > 0) {
         const int32_t c1 = cr[1], c2 = cr[2], c3 = cr[3];
         const int32_t e0 = n == 4 ? c3 : (n == 3 ? c2 : c1), e1 = n == 4 ? c2 : c1;
@@ -748,9 +675,6 @@ __device__ __forceinline__ void trace_loop_closest(const DevScene &s, const Src 
     }
     if (__ballot(has) == 0) break;
     // ---- one inner-node visit
-#if MTX_COOP_NODE
-    coop_fetch_nodes(s.nodes, node, has && node >= top_n, wstage, lane);
-#endif
     if (has && node >= 0) visit_node();
     // ---- one triangle test
     if (has && tri < tri_end) {
@@ -897,8 +821,7 @@ __device__ __forceinline__ void trace_loop(const DevScene &s, const Src &src, ui
     int4 *top = reinterpret_cast<int4 *>(cols + s.lds_entries * kTraceBlock);
     for (uint32_t i = threadIdx.x; i < 4 * s.lds_top; i += kTraceBlock) top[i] = s.nodes[i];
     __syncthreads();
-    int4 *wstage = top + 4 * s.lds_top + (threadIdx.x >> 6) * 256;  // this wave's 64 node slots (MTX_COOP_NODE)
-    trace_loop_closest<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters, wstage);
+    trace_loop_closest<STATS>(s, src, count, heads, cols + threadIdx.x, top, nv, tv, nr, wave_iters);
   }
 }
 

@@ -372,64 +372,10 @@ __device__ __forceinline__ bool end_valid(const WaveBuffers &b, uint32_t path, f
   (void)path;
   return lw != 0.f;
 }
-// MTX_SHADE_DMA: the shading records of a wave's 64 next queue entries,
-// gathered into the wave's 8-KB LDS slice by LDS-DMA with 8 lanes per record
-// (one wave-instruction touches 8 records' lines instead of 64). Instruction
-// k fetches the records of lanes 8k .. 8k + 7; its lane l writes 16 B at
-// wbuf + 1024 k + 16 l (lane-linear), i.e. record m = 8k + l / 8 at
-// wbuf + 128 m, slot l % 8 holding piece (slot - (m >> 1)) % 8: piece j of
-// lane m's record sits in slot (j + (m >> 1)) % 8, which keeps the 16 lanes of
-// each ds_read_b128 group on distinct banks. Every lane of the wave calls it.
-__device__ __forceinline__ void dma_records(const float4 *shade_rec, uint32_t prim, bool want, float4 *wbuf,
-                                            uint32_t lane) {
-  const uint64_t m = __ballot(want);
-  if (m == 0) return;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t src = 8u * k + (lane >> 3);
-    const uint32_t pr = (uint32_t)__shfl((int)prim, (int)src);
-    const uint32_t j = ((lane & 7u) - (src >> 1)) & 7u;
-    if ((m >> src) & 1ull)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void *)(shade_rec + 8 * (size_t)pr + j),
-          (__attribute__((address_space(3))) void *)(wbuf + 64 * k), 16, 0, 0);
-  }
-}
-
-// compute_si_dev with the record read from this lane's LDS copy (dma_records
-// layout; lrec = wbuf + 8 * lane): same floats, same arithmetic.
-__device__ __forceinline__ SurfaceInteraction compute_si_lds(const float4 *lrec, uint32_t lane, float t,
-                                                             uint32_t prim, float u, float v, V3 ray_d) {
-  if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of the previous step has landed
-  const uint32_t rot = (lane >> 1) & 7u;
-  auto piece = [&](uint32_t j) { return lrec[(j + rot) & 7u]; };
-  const float4 a = piece(0), b = piece(1), c = piece(2);
-  const uint32_t fl = __float_as_uint(c.w);
-  const bool use_n = (fl & 1u) != 0, use_uv = (fl & 2u) != 0;
-  V3 n0 = v3s(0.f), n1 = v3s(0.f), n2 = v3s(0.f);
-  V2 t0 = V2{0.f, 0.f}, t1 = t0, t2 = t0;
-  if (use_n) {
-    const float4 x = piece(3), y = piece(4), z = piece(5);
-    n0 = V3{x.x, x.y, x.z};
-    n1 = V3{y.x, y.y, y.z};
-    n2 = V3{z.x, z.y, z.z};
-  }
-  if (use_uv) {
-    const float4 x = piece(6), y = piece(7);
-    t0 = V2{x.x, x.y};
-    t1 = V2{x.z, x.w};
-    t2 = V2{y.x, y.y};
-  }
-  return si_from_vertices(t, prim, u, v, ray_d, V3{a.x, a.y, a.z}, V3{b.x, b.y, b.z}, V3{c.x, c.y, c.z},
-                          __float_as_uint(a.w), (int32_t)__float_as_uint(b.w), use_n, n0, n1, n2, use_uv, t0, t1, t2);
-}
-
 template <int INT>
 __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &sv, const WaveBuffers &b,
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
-                                           const float4 h, ShadeIO &io, const float4 *warm = nullptr,
-                                           const float4 *lrec = nullptr) {
+                                           const float4 h, ShadeIO &io, const float4 *warm = nullptr) {
   const uint32_t rp = (bounce + b.ray_par) & 1u;
   const float4 ro = b.ray_o[rp][qi], rd = b.ray_d[rp][qi];
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
@@ -452,9 +398,7 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
   V3 L = V3{Lr.x, Lr.y, Lr.z};
   float prev_pdf = Lr.w;
   const V3 ray_d = V3{rd.x, rd.y, rd.z};
-  const SurfaceInteraction si = lrec ? compute_si_lds(lrec, threadIdx.x & 63u, h.x, __float_as_uint(h.y), h.z, h.w,
-                                                      ray_d)
-                                     : compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
+  const SurfaceInteraction si = compute_si_dev(s, h.x, __float_as_uint(h.y), h.z, h.w, ray_d);
 #if MTX_DIAG_STAMPS
   MTX_STAMP(io.st, 1);
 #endif
@@ -1035,16 +979,7 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     path = ident ? i0 : in_q[i0];
     h = b.hit[i0];
   }
-  // MTX_SHADE_DMA: the step's shading records wait in LDS (dma_records),
-  // fetched while the previous step appended
-  constexpr bool kDma = MTX_SHADE_DMA && (INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH || INT == MTX_INT_NRC);
-  __shared__ float4 rec_lds[kDma ? kShadeBlock * 8 : 1];
-  const uint32_t lane = threadIdx.x & 63u;
-  float4 *wrec = rec_lds + (kDma ? (threadIdx.x >> 6) * 512 : 0);
-  if constexpr (kDma)
-    dma_records(s.shade_rec, __float_as_uint(h.y), blockIdx.x * kShadeBlock + threadIdx.x < count &&
-                                                       __float_as_uint(h.y) != 0xffffffffu,
-                wrec, lane);
+
 #if MTX_DIAG_STAMPS
   Stamps stp{};
   unsigned long long steps = 0;
@@ -1055,12 +990,11 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     const uint32_t inext = i + stride;
     uint32_t path_n = 0;
     if (inext < count) path_n = ident ? inext : in_q[inext];
-#if MTX_SHADE_WARM || MTX_SHADE_DMA
+#if MTX_SHADE_WARM
     float4 hn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (inext < count) hn = b.hit[inext];
     const uint32_t pn = __float_as_uint(hn.y);
-    const float4 *wp = (!kDma && MTX_SHADE_WARM && inext < count && pn != 0xffffffffu) ? s.shade_rec + 8 * (size_t)pn
-                                                                                      : nullptr;
+    const float4 *wp = (inext < count && pn != 0xffffffffu) ? s.shade_rec + 8 * (size_t)pn : nullptr;
 #else
     const float4 *wp = nullptr;
 #endif
@@ -1088,12 +1022,12 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
       else if constexpr (INT == MTX_INT_NERAD)
         cont = shade_nerad<true>(s, sv, b, bounce, path, i, h, io);
       else
-        cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io, wp, kDma ? wrec + 8 * lane : nullptr);
+        cont = shade_path<INT>(s, sv, b, p, bounce, path, i, h, io, wp);
     }
     (void)wp;
     const uint32_t path_c = path;
     path = path_n;
-#if MTX_SHADE_WARM || MTX_SHADE_DMA
+#if MTX_SHADE_WARM
     h = hn;
     asm volatile("" ::"v"(io.warm));  // the warm-up load completes in this iteration
 #else
@@ -1104,7 +1038,7 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     stp = io.st;
 #endif
     uint32_t slot, sslot;
-    block_append2<kShadeBlock, kDma>(cont, io.emit, io.emit && io.em_hi, out_cnt, parity, slot, sslot);
+    block_append2<kShadeBlock>(cont, io.emit, io.emit && io.em_hi, out_cnt, parity, slot, sslot);
     if (cont) {
       out_q[slot] = path_c;
       b.ray_o[rp ^ 1u][slot] = io.nro;
@@ -1132,10 +1066,6 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
 #if MTX_DIAG_STAMPS
     MTX_STAMP(stp, 6);
 #endif
-    // the next step's records (this step's were read in shade_path), issued
-    // once this step's state is stored (io is dead: no registers held across)
-    if constexpr (kDma) dma_records(s.shade_rec, __float_as_uint(h.y), inext < count && __float_as_uint(h.y) != 0xffffffffu,
-                                    wrec, lane);
     if constexpr (INT == MTX_INT_NRC || INT == MTX_INT_NERAD_RHS || INT == MTX_INT_NERAD) {
       if (INT != MTX_INT_NRC || p.nrc_cache) {
         const uint32_t q = block_reserve<kShadeBlock>(io.query ? 1u : 0u, b.cq_count);

@@ -53,17 +53,6 @@ constexpr uint32_t kOccLdsStack = 8;
 #ifndef MTX_OCC_LDS_TOP
 #define MTX_OCC_LDS_TOP 48  // occlusion tree nodes copied into LDS per trace block (0 = none)
 #endif
-#ifndef MTX_COOP_NODE
-// closest hit: a wave fetches its lanes' global nodes cooperatively, 4 lanes
-// per 64-B node, straight into LDS (LDS-DMA; device_common.h coop_fetch_nodes)
-#define MTX_COOP_NODE 0
-#endif
-#ifndef MTX_SHADE_DMA
-// k_shade (path-mis / path / nrc): the next step's 128-B shading records are
-// gathered into LDS by LDS-DMA while this step's appends run, 8 lanes per
-// record (kernels.hip dma_records); 0: read from global memory in the step
-#define MTX_SHADE_DMA 0
-#endif
 #ifndef MTX_SHADE_WARM
 #define MTX_SHADE_WARM 1  // k_shade: warm L2 with the next entry's shading record
 #endif
