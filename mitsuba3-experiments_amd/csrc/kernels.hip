@@ -31,7 +31,10 @@ using namespace mtx;
 
 // Minimum resident shade blocks per CU (caps the shade kernels' VGPRs: 3
 // blocks of 256 threads = 3 waves/SIMD at <= 168 VGPRs).
-constexpr int kShadeMinBlocks = 3;
+#ifndef MTX_SHADE_MIN_BLOCKS
+#define MTX_SHADE_MIN_BLOCKS 3
+#endif
+constexpr int kShadeMinBlocks = MTX_SHADE_MIN_BLOCKS;
 
 namespace mtxd {
 
