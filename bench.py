@@ -271,7 +271,7 @@ def main():
     trace_ms = agg["trace_ms"] / K  # counters off
     trace_s = trace_ms / 1e3
     achieved = alg_closest / trace_s / 1e9 if trace_s > 0 else 0.0
-    names = {"closest": "mtxd::k_trace_closest<false, false>", "shadow": "mtxd::k_trace_shadow<false>",
+    names = {"closest": "mtxd::k_trace_closest<false>", "shadow": "mtxd::k_trace_shadow<false>",
              "shade": "mtxd::k_shade<2>"}
     traffic, traffic_src = (measured_traffic(list(names.values()), traffic_key(args)) if world == 1
                             else ({k: None for k in names.values()}, "N>1: PMC profiles are N=1"))

@@ -29,7 +29,7 @@ def _threads():
     return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
 
-TRACE_KERNEL = "mtxd::k_trace_closest<false, false>"
+TRACE_KERNEL = "mtxd::k_trace_closest<false>"
 
 
 def _trace_roofline(cnt, trace_ms_per_unit, units_label, timed_launches=None, args=None):
