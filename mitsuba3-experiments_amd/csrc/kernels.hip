@@ -30,7 +30,10 @@
 using namespace mtx;
 
 // Minimum resident shade blocks per CU (caps the shade kernels' VGPRs: 3
-// blocks of 256 threads = 3 waves/SIMD at <= 168 VGPRs).
+// blocks of 256 threads = 3 waves/SIMD at <= 168 VGPRs). 4 blocks (<= 128
+// VGPRs) spill 26 VGPRs of k_shade<2>: shade 63.4 -> 74.6 ms per step, and
+// 69.4 ms with the NEE record staged in LDS (13 spilled); the record in LDS
+// at 3 blocks (149 VGPRs): 64.4 ms (profiles/r6e_ab_shade_vgpr_budget.jsonl).
 #ifndef MTX_SHADE_MIN_BLOCKS
 #define MTX_SHADE_MIN_BLOCKS 3
 #endif
@@ -1124,7 +1127,7 @@ __global__ void k_flush_tail(WaveBuffers b, uint32_t bounce, uint32_t integrator
 // depend on the visit order; same shading code), so the same bits. The block's
 // dynamic LDS holds one traversal stack column per thread (stack_bytes).
 #ifndef MTX_MEGA_MIN_BLOCKS
-#define MTX_MEGA_MIN_BLOCKS kShadeMinBlocks  // A/B: 4 = <= 128 VGPRs (spills), every band path resident at once
+#define MTX_MEGA_MIN_BLOCKS 3  // A/B: 4 = <= 128 VGPRs (spills), every band path resident at once
 #endif
 // The traversals index their LDS stack columns with the stride kTraceBlock and
 // stack_bytes() sizes the allocation with it: a megakernel block of another
