@@ -104,6 +104,12 @@ def spawn_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+# Kernel names (rocprofv3's short form) whose PMC traffic / units bench.py
+# attaches: the closest-hit and any-hit traversals and path-mis shade.
+PMC_KERNELS = {"closest": "mtxd::k_trace_closest<false>", "shadow": "mtxd::k_trace_shadow<false>",
+               "shade": "mtxd::k_shade<2>"}
+
+
 def src_sha() -> str:
     """Hash of the sources that make libmtx.so (kernels, host runtime, shared
     headers, build flags): a PMC profile is valid for the build it measured."""
@@ -271,8 +277,7 @@ def main():
     trace_ms = agg["trace_ms"] / K  # counters off
     trace_s = trace_ms / 1e3
     achieved = alg_closest / trace_s / 1e9 if trace_s > 0 else 0.0
-    names = {"closest": "mtxd::k_trace_closest<false>", "shadow": "mtxd::k_trace_shadow<false>",
-             "shade": "mtxd::k_shade<2>"}
+    names = PMC_KERNELS
     traffic, traffic_src = (measured_traffic(list(names.values()), traffic_key(args)) if world == 1
                             else ({k: None for k in names.values()}, "N>1: PMC profiles are N=1"))
     units, units_src = (measured_units(list(names.values()), traffic_key(args)) if world == 1

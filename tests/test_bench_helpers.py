@@ -52,3 +52,29 @@ def test_vmem_peak_from_probe():
     cyc = float(line.split()[-1])
     assert abs(cyc - 16.9) < 0.1
     assert abs(bench.VMEM_PEAK_GBS / (1024 / cyc * 256 * 2.4) - 1) < 0.005
+
+
+def test_pmc_kernel_names_exist_in_the_latest_profile():
+    """The kernel names bench.py looks up (PMC_KERNELS) are the ones the
+    newest committed rocprofv3 kernel trace of the headline bench reports: a
+    kernel's template signature changing without a new profile would leave
+    the bench line's traffic / units empty."""
+    import csv
+    import glob
+    import re
+
+    import bench
+
+    def rnd(path):
+        m = re.match(r"r(\d+)", os.path.basename(path))
+        return (int(m.group(1)) if m else -1, os.path.basename(path))
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_kernel_stats.csv")), key=rnd)
+    assert files
+    names = set()
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            n = row.get("Name") or row.get("KernelName") or ""
+            names.add(re.sub(r"^void ", "", n).split("(")[0])
+    for k in bench.PMC_KERNELS.values():
+        assert k in names, (k, os.path.basename(files[-1]))
