@@ -108,6 +108,48 @@ __device__ __forceinline__ uint32_t lane_id() {
   return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 }
 
+// Once-touched per-ray streams (ray planes, hit and shadow records, path
+// state) with the non-temporal policy (`nt`). MTX_NT_STREAM bits: 0 the
+// trace kernels' loads, 1 the shade kernel's loads, 2 its stores, 3 the trace
+// kernels' stores, 4 the camera raygen's stores, 5 the shade kernel's queue
+// entries and the film's reads. Default: the shade kernel's stores only
+// (shade 62.7 -> 60.6 ms per step); nt loads were slower (shade loads 61.2
+// -> 64.0 ms) or neutral, the other stores neutral, and the stores with
+// sc1 / sc0 sc1 / nt sc1 slower (66-72 ms): profiles/r6h_ab_nt_stream_bits.jsonl,
+// r6i_ab_nt_store_policy.jsonl.
+#ifndef MTX_NT_STREAM
+#define MTX_NT_STREAM 4
+#endif
+template <class T>
+struct NtVec {  // the vector type of a 4-, 8- or 16-B record for the nt builtins
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "4-, 8- or 16-B stream records");
+  typedef uint32_t type __attribute__((ext_vector_type(sizeof(T) / 4)));
+};
+template <int BIT, class T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+  if constexpr ((MTX_NT_STREAM >> BIT) & 1) {
+    using V = typename NtVec<T>::type;
+    const V v = __builtin_nontemporal_load(reinterpret_cast<const V *>(p));
+    T r;
+    __builtin_memcpy(&r, &v, sizeof(T));
+    return r;
+  } else {
+    return *p;
+  }
+}
+template <int BIT, class T>
+__device__ __forceinline__ void st_stream(T *p, const T &x) {
+  if constexpr ((MTX_NT_STREAM >> BIT) & 1) {
+    using V = typename NtVec<T>::type;
+    V v;
+    __builtin_memcpy(&v, &x, sizeof(T));
+    __builtin_nontemporal_store(v, reinterpret_cast<V *>(p));
+  } else {
+    *p = x;
+  }
+}
+constexpr int kNtTrace = 0, kNtShade = 1, kNtShadeSt = 2, kNtTraceSt = 3, kNtRaygen = 4, kNtQueue = 5;
+
 // Wave-level stream compaction: every lane of the wave must call this.
 // Returns the output slot of a lane with pred = true.
 __device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {

@@ -51,13 +51,13 @@ struct ClosestSrc {
   const uint32_t *queue;
   const float4 *ro, *rd;  // this bounce's ray planes, by queue position
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, uint32_t &payload) const {
-    const float4 o4 = ro[k], d4 = rd[k];
+    const float4 o4 = ld_stream<kNtTrace>(ro + k), d4 = ld_stream<kNtTrace>(rd + k);
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
     payload = k;
   }
   __device__ __forceinline__ void finish(uint32_t slot, bool, float t, uint32_t prim, float u, float v) const {
-    b.hit[slot] = make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v);
+    st_stream<kNtTraceSt>(b.hit + slot, make_float4(prim == 0xffffffffu ? kInf : t, __uint_as_float(prim), u, v));
   }
 };
 
@@ -131,12 +131,12 @@ struct ShadowSrc {
   };
   WaveBuffers b;
   __device__ __forceinline__ void load(uint32_t k, TraceRay &r, float &tmax, Payload &pl) const {
-    const float4 o4 = b.shadow[k].o, d4 = b.shadow[k].d;
+    const float4 o4 = ld_stream<kNtTrace>(&b.shadow[k].o), d4 = ld_stream<kNtTrace>(&b.shadow[k].d);
     r = make_trace_ray(V3{o4.x, o4.y, o4.z}, V3{d4.x, d4.y, d4.z}, o4.w);
     tmax = o4.w;
     pl.k = k;
     pl.li = __float_as_uint(d4.w);
-    pl.t = b.shadow[k].t;
+    pl.t = ld_stream<kNtTrace>(&b.shadow[k].t);
     pl.lw = b.shadow[k].x.w;
   }
   __device__ __forceinline__ void finish(const Payload &pl, bool occluded, float, uint32_t, float, float) const {
@@ -151,7 +151,7 @@ struct ShadowSrc {
       return;
     }
     if (!occluded) {
-      b.L[0][pl.li] = make_float4(pl.t.x, pl.t.y, pl.t.z, pl.lw);
+      st_stream<kNtTraceSt>(b.L[0] + pl.li, make_float4(pl.t.x, pl.t.y, pl.t.z, pl.lw));
     } else if (fl & 14u) {
       float4 L = b.shadow[pl.k].x;
       const float qnan = __uint_as_float(0x7fc00000u);
@@ -196,9 +196,10 @@ __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParam
   }
   // throughput = 1, eta = 1, L = 0, prev_bsdf_pdf = 1 (path-mis.py:45), prev_p = 0 are
   // not stored: the bounce-0 shade uses these constants (kInitThr / kInitL / kInitPrev)
-  b.ray_o[0][i] = make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt);  // queue position i (identity)
-  b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
-  b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16));
+  st_stream<kNtRaygen>(b.ray_o[0] + i, make_float4(ray.o.x, ray.o.y, ray.o.z, ray.maxt));  // queue position i (identity)
+  st_stream<kNtRaygen>(b.ray_d[0] + i, make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f));
+  st_stream<kNtRaygen>(b.misc[0] + i,
+                       make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, depth | (flags << 16)));
   b.pos[i] = pos;
   if (!p.ident0) b.queue[0][i] = i;
 }
@@ -383,16 +384,17 @@ __device__ __forceinline__ bool shade_path(const DevScene &s, const SceneView &s
                                            const ChunkParams &p, uint32_t bounce, uint32_t path, uint32_t qi,
                                            const float4 h, ShadeIO &io, const float4 *warm = nullptr) {
   const uint32_t rp = (bounce + b.ray_par) & 1u;
-  const float4 ro = b.ray_o[rp][qi], rd = b.ray_d[rp][qi];
+  const float4 ro = ld_stream<kNtShade>(b.ray_o[rp] + qi), rd = ld_stream<kNtShade>(b.ray_d[rp] + qi);
   // bounce 0: the state init_path / k_rs_begin would have stored (not read)
-  const float4 th = bounce == 0 ? kInitThr : b.thr[rp][qi], Lr = bounce == 0 ? kInitL : b.L[rp][qi];
+  const float4 th = bounce == 0 ? kInitThr : ld_stream<kNtShade>(b.thr[rp] + qi),
+               Lr = bounce == 0 ? kInitL : ld_stream<kNtShade>(b.L[rp] + qi);
   // prev (previous vertex, NRC spread): path-mis / path read it only for the
   // emission MIS of an emitter hit (pdf_emitter_direction is 0 otherwise), so
   // they load it below once the hit's emitter is known
   constexpr bool kPrevOnEmitter = INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH;
   float4 pv = kInitPrev;
-  if (!kPrevOnEmitter && bounce != 0) pv = b.prev[rp][qi];
-  const uint4 mi = b.misc[rp][qi];
+  if (!kPrevOnEmitter && bounce != 0) pv = ld_stream<kNtShade>(b.prev[rp] + qi);
+  const uint4 mi = ld_stream<kNtShade>(b.misc[rp] + qi);
   io.nL = Lr;  // an exit that changes neither keeps them
   io.nmisc = mi;
   Pcg32 rng;
@@ -982,8 +984,8 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
   const bool ident = bounce == 0 && p.ident0;
   if (blockIdx.x * kShadeBlock + threadIdx.x < count) {
     const uint32_t i0 = blockIdx.x * kShadeBlock + threadIdx.x;
-    path = ident ? i0 : in_q[i0];
-    h = b.hit[i0];
+    path = ident ? i0 : ld_stream<kNtQueue>(in_q + i0);
+    h = ld_stream<kNtShade>(b.hit + i0);
   }
 
 #if MTX_DIAG_STAMPS
@@ -995,7 +997,7 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     const uint32_t i = base + threadIdx.x;
     const uint32_t inext = i + stride;
     uint32_t path_n = 0;
-    if (inext < count) path_n = ident ? inext : in_q[inext];
+    if (inext < count) path_n = ident ? inext : ld_stream<kNtQueue>(in_q + inext);
 #if MTX_SHADE_WARM
     float4 hn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (inext < count) hn = b.hit[inext];
@@ -1037,7 +1039,7 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     h = hn;
     asm volatile("" ::"v"(io.warm));  // the warm-up load completes in this iteration
 #else
-    if (inext < count) h = b.hit[inext];
+    if (inext < count) h = ld_stream<kNtShade>(b.hit + inext);
 #endif
 
 #if MTX_DIAG_STAMPS
@@ -1046,19 +1048,19 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
     uint32_t slot, sslot;
     block_append2<kShadeBlock>(cont, io.emit, io.emit && io.em_hi, out_cnt, parity, slot, sslot);
     if (cont) {
-      out_q[slot] = path_c;
-      b.ray_o[rp ^ 1u][slot] = io.nro;
-      b.ray_d[rp ^ 1u][slot] = io.nrd;
-      if constexpr (!kNerad) b.thr[rp ^ 1u][slot] = io.nthr;
+      st_stream<kNtQueue>(out_q + slot, path_c);
+      st_stream<kNtShadeSt>(b.ray_o[rp ^ 1u] + slot, io.nro);
+      st_stream<kNtShadeSt>(b.ray_d[rp ^ 1u] + slot, io.nrd);
+      if constexpr (!kNerad) st_stream<kNtShadeSt>(b.thr[rp ^ 1u] + slot, io.nthr);
       if constexpr (INT == MTX_INT_PATH_MIS || INT == MTX_INT_PATH || INT == MTX_INT_NRC || INT == MTX_INT_PSSMLT_PATH)
-        b.prev[rp ^ 1u][slot] = io.nprev;
+        st_stream<kNtShadeSt>(b.prev[rp ^ 1u] + slot, io.nprev);
       if constexpr (!kNerad) {
-        b.L[rp ^ 1u][slot] = io.nL;
-        b.misc[rp ^ 1u][slot] = io.nmisc;
+        st_stream<kNtShadeSt>(b.L[rp ^ 1u] + slot, io.nL);
+        st_stream<kNtShadeSt>(b.misc[rp ^ 1u] + slot, io.nmisc);
       }
     } else if (!kNerad && valid) {
-      b.L[kFinal][path_c] = io.nL;
-      if (!p.drop_end_misc) b.misc[kFinal][path_c] = io.nmisc;
+      st_stream<kNtShadeSt>(b.L[kFinal] + path_c, io.nL);
+      if (!p.drop_end_misc) st_stream<kNtShadeSt>(b.misc[kFinal] + path_c, io.nmisc);
     }
     if (io.emit) {
       // the contribution goes to the path's L where the next shade (or the
@@ -1067,7 +1069,11 @@ __global__ __launch_bounds__(kShadeBlock, kShadeMinBlocks) void k_shade(DevScene
       const uint32_t li = (kNerad || !cont) ? kFinal * b.capacity + path_c : (rp ^ 1u) * b.capacity + slot;
       io.rec.d.w = __uint_as_float(li);
       if constexpr (!kNerad) io.rec.x.w = io.nL.w;  // final-value form: L.w (set after the NEE)
-      b.shadow[sslot] = io.rec;
+      ShadowRec *sr = b.shadow + sslot;
+      st_stream<kNtShadeSt>(&sr->o, io.rec.o);
+      st_stream<kNtShadeSt>(&sr->d, io.rec.d);
+      st_stream<kNtShadeSt>(&sr->t, io.rec.t);
+      st_stream<kNtShadeSt>(&sr->x, io.rec.x);
     }
 #if MTX_DIAG_STAMPS
     MTX_STAMP(stp, 6);
@@ -1480,9 +1486,9 @@ __global__ __launch_bounds__(64) void k_film_src_staged(WaveBuffers b, ChunkPara
       const uint32_t e = (uint32_t)it * 64 + lane, j = e / S, sm = e % S;
       if (q0 + j < p.n_px && sm < ns) {
         const uint32_t path = (q0 + j) * p.spp + s0 + sm;
-        float4 l = b.L[kFinal][path];
+        float4 l = ld_stream<kNtQueue>(b.L[kFinal] + path);
         if (mask_valid && !end_valid(b, path, l.w)) l = make_float4(0.f, 0.f, 0.f, 0.f);
-        const float2 ps = b.pos[path];
+        const float2 ps = ld_stream<kNtQueue>(b.pos + path);
         sv[0][j][sm] = l.x;
         sv[1][j][sm] = l.y;
         sv[2][j][sm] = l.z;
