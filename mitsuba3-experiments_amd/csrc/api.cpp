@@ -1285,7 +1285,7 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
     }
     mtxd::launch_restir_final(c->scene, b, p, r, st);
     mtxd::launch_film_src(b, p, (float4 *)c->contrib.p, st);
-    mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, 1, st);
+    mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, 1, 1u, st);
   }
   HIP_TRY(hipGetLastError());
   if (only_a) {
@@ -1352,6 +1352,18 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
   // sample-sharded film renders: 8 partial slots (GPU-count-invariant films,
   // DESIGN.md "Film"); PSSMLT splats and ReSTIR frames: one
   const uint32_t film_slots = (mlt || a->integrator == MTX_INT_RESTIR_GI) ? 1u : 8u;
+  // the slots [sample_offset, sample_offset + spp) falls in (FilmSlots: slot k
+  // takes global samples [end(k - 1), end(k)), slot 7 everything past end(6))
+  uint32_t slot_mask = 1u;
+  if (film_slots == 8) {
+    slot_mask = 0;
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint64_t lo = k ? mtx::film_slot_end(k - 1, a->spp_total) : 0u;
+      const uint64_t hi = k < 7 ? mtx::film_slot_end(k, a->spp_total) : ~0ull;
+      if (std::max<uint64_t>(lo, a->sample_offset) < std::min<uint64_t>(hi, (uint64_t)a->sample_offset + a->spp))
+        slot_mask |= 1u << k;
+    }
+  }
   if ((rc = dalloc(c->contrib, 9ull * 16 * band_px * film_slots))) return rc;
   const size_t film_floats = 4ull * (W + 2) * (a->y1 - a->y0 + 2);
   float4 *film_dev = (float4 *)film_rgbw;
@@ -1415,6 +1427,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     p.band_y0 = a->y0;
     p.band_px = (a->y1 - a->y0) * W;
     p.film_slots = film_slots;
+    p.slot_mask = slot_mask;
     p.n_paths = p.n_px * a->spp;
     p.nrc_c = a->nrc_c;
     p.stats = want_stats ? 1 : 0;
@@ -1457,7 +1470,7 @@ int mtx_render(mtx_ctx *c, const mtx_render_args *a, float *film_rgbw, int film_
     HIP_TRY(hipEventRecord(c->w2.done, c->w2.stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->w2.done, 0));
   }
-  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, film_slots, c->stream);
+  mtxd::launch_film_gather((const float4 *)c->contrib.p, film_dev, W, a->y0, a->y1, film_slots, slot_mask, c->stream);
   tm.end(3, e_all);
   HIP_TRY(hipGetLastError());
   if (!film_on_device)

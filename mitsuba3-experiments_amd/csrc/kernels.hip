@@ -1430,18 +1430,20 @@ __device__ __forceinline__ void film_accumulate(float4 acc[9], int x, int y, flo
 // divergence) and writes all 8 slots (zeros for slots without samples);
 // otherwise one slot. contrib: [slot][9][band_px].
 struct FilmSlots {
-  uint32_t cur, end, T;
+  uint32_t cur, end, T, mask;
   bool eight;
   __device__ __forceinline__ void init(const ChunkParams &p) {
     eight = p.film_slots == 8;
+    mask = eight ? p.slot_mask : 1u;
     T = p.spp_total;
     cur = 0;
     end = eight ? film_slot_end(0, T) : 0xffffffffu;
   }
   __device__ __forceinline__ void flush(float4 acc[9], float4 *contrib, const ChunkParams &p, size_t o) {
+    const bool used = (mask >> cur) & 1u;  // a slot without samples of this render stays unwritten
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
-      contrib[((size_t)cur * 9 + k) * p.band_px + o] = acc[k];
+      if (used) contrib[((size_t)cur * 9 + k) * p.band_px + o] = acc[k];
       acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     ++cur;
@@ -1529,9 +1531,11 @@ __global__ void k_film_src(WaveBuffers b, ChunkParams p, float4 *contrib) {
 }
 
 // Stage 2: per film pixel and slot the 9 neighbours in (dy, dx) order, then
-// the slots' fixed binary tree (film_tree8) when nslots == 8.
+// the slots' fixed binary tree (film_tree8) when nslots == 8. Slots outside
+// slot_mask hold no sample of the render: they are zero, not read (a sum
+// that starts at +0 never becomes -0, so adding their +0 changes nothing).
 __global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, uint32_t y0, uint32_t y1,
-                              uint32_t nslots) {
+                              uint32_t nslots, uint32_t slot_mask) {
   const uint32_t FW = W + 2, FH = (y1 - y0) + 2;
   const size_t P = (size_t)(y1 - y0) * W;  // contrib: [slot][9][band pixels]
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1541,6 +1545,10 @@ __global__ void k_film_gather(const float4 *contrib, float4 *film, uint32_t W, u
   const uint32_t ns = nslots == 8 ? 8u : 1u;
   for (uint32_t k = 0; k < ns; ++k) {
     float r = 0.f, g = 0.f, bl = 0.f, w = 0.f;
+    if (ns == 8 && !((slot_mask >> k) & 1u)) {
+      sl[k] = V4{r, g, bl, w};
+      continue;
+    }
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
@@ -1886,9 +1894,10 @@ void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib
     hipLaunchKernelGGL(k_film_src_staged, dim3(blocks_for(p.n_px, 64)), dim3(64), 0, st, b, p, contrib);
 }
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
-                        uint32_t nslots, hipStream_t st) {
+                        uint32_t nslots, uint32_t slot_mask, hipStream_t st) {
   const uint64_t n = (uint64_t)(width + 2) * (y1 - y0 + 2);
-  hipLaunchKernelGGL(k_film_gather, dim3(blocks_for(n, 256)), dim3(256), 0, st, contrib, film, width, y0, y1, nslots);
+  hipLaunchKernelGGL(k_film_gather, dim3(blocks_for(n, 256)), dim3(256), 0, st, contrib, film, width, y0, y1, nslots,
+                     slot_mask);
 }
 void launch_collect(const WaveBuffers &b, const ChunkParams &p, float *L_out, uint8_t *valid_out, hipStream_t st) {
   hipLaunchKernelGGL(k_collect, dim3(blocks_for(p.n_paths, 256)), dim3(256), 0, st, b, p, L_out, valid_out);

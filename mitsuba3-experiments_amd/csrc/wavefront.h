@@ -211,6 +211,8 @@ struct ChunkParams {
   uint32_t band_y0;     // first row of the rendered band (film/contrib origin)
   uint32_t band_px;     // pixels of the band (contrib: film_slots x 9 planes of band_px float4)
   uint32_t film_slots;  // 8: partial-slot film (mtx_core/common.h film_slot); 0 / 1: one slot
+  uint32_t slot_mask;   // film_slots == 8: the slots this render's samples fall in (the others are
+                        // neither written nor read: they are zero, and x + 0 is x in the slot tree)
   uint32_t n_paths;
   float nrc_c;
   uint32_t stats;
@@ -243,7 +245,7 @@ void launch_shade(const DevScene &s, const WaveBuffers &b, const ChunkParams &p,
                   hipStream_t st);
 void launch_film_src(const WaveBuffers &b, const ChunkParams &p, float4 *contrib, hipStream_t st);
 void launch_film_gather(const float4 *contrib, float4 *film, uint32_t width, uint32_t y0, uint32_t y1,
-                        uint32_t nslots, hipStream_t st);
+                        uint32_t nslots, uint32_t slot_mask, hipStream_t st);
 void launch_mlt_init(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_begin(const DevScene &s, const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
 void launch_mlt_end(const WaveBuffers &b, const ChunkParams &p, hipStream_t st);
