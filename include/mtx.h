@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define MTX_ABI_VERSION 7
+#define MTX_ABI_VERSION 8
 
 enum {
   MTX_OK = 0,
@@ -196,6 +196,13 @@ typedef struct mtx_scene_desc {
    * trees rejected (MTX_E_ARG) unless occ_tri_geom is a permutation of
    * tri_geom. */
   const uint32_t *occ_perm;
+  /* constant environment emitter (Mitsuba `constant`, the scene.environment()
+   * of path-mis.py:41 / pssmltpath.py:39 / restirgi.py:475; mtx_core/interaction.h):
+   * has_env != 0 adds it as emitter index n_emitters, picked uniformly with the
+   * area emitters; its bounding sphere is that of the vertices' box. With
+   * has_env, n_emitters may be 0. (ABI 8) */
+  float env_radiance[3];
+  uint32_t has_env;
 } mtx_scene_desc;
 
 /* Integrators (the reference scripts whose sample() loop is replaced). */

@@ -1,9 +1,11 @@
 // mtx_core/interaction.h — surface interactions, ray spawning, the rectangle
-// area emitter, the perspective sensor and the two MIS weight variants.
+// area emitter, the constant environment emitter, the perspective sensor and
+// the two MIS weight variants.
 // Upstream semantics restated (unverifiable offline):
 //   Mesh::compute_surface_interaction, Interaction::spawn_ray(_to),
 //   Scene::sample_emitter_direction / pdf_emitter_direction,
-//   AreaEmitter + Rectangle, PerspectiveCamera::sample_ray.
+//   AreaEmitter + Rectangle, ConstantBackgroundEmitter (`constant`),
+//   PerspectiveCamera::sample_ray.
 #pragma once
 #include "../mtx.h"
 #include "bsdf.h"
@@ -27,9 +29,38 @@ struct SceneView {
   const mtx_material *materials;
   const mtx_emitter *emitters;
   BsdfData bsdf;
-  uint32_t n_tris, n_emitters;
+  uint32_t n_tris, n_emitters;  // n_emitters: area emitters
   mtx_camera camera;
+  // constant environment (scene.environment(), path-mis.py:41): emitter index
+  // n_emitters when has_env; the scene's bounding sphere (env_bsphere)
+  uint32_t has_env;
+  float env_radiance[3], env_center[3], env_radius;
 };
+
+// The environment's emitter index (after the area emitters), -1 without one,
+// and the number of emitters the uniform pick chooses from.
+MTX_HD int32_t env_index(const SceneView &s) { return s.has_env ? (int32_t)s.n_emitters : -1; }
+MTX_HD uint32_t emitter_count(const SceneView &s) { return s.n_emitters + (s.has_env ? 1u : 0u); }
+
+// ConstantBackgroundEmitter::set_scene: the bounding sphere of the scene's
+// bounding box (centre, |centre - min|), its radius grown by a ray epsilon.
+MTX_HD void env_bsphere(const float *vpos, uint32_t n_verts, float center[3], float *radius) {
+  V3 lo = v3s(kInf), hi = v3s(-kInf);
+  for (uint32_t i = 0; i < n_verts; ++i) {
+    lo = V3{fminf(lo.x, vpos[3 * i]), fminf(lo.y, vpos[3 * i + 1]), fminf(lo.z, vpos[3 * i + 2])};
+    hi = V3{fmaxf(hi.x, vpos[3 * i]), fmaxf(hi.y, vpos[3 * i + 1]), fmaxf(hi.z, vpos[3 * i + 2])};
+  }
+  if (n_verts == 0 || !(lo.x <= hi.x && lo.y <= hi.y && lo.z <= hi.z)) {  // invalid box
+    center[0] = center[1] = center[2] = 0.f;
+    *radius = kRayEpsilon;
+    return;
+  }
+  const V3 c = (lo + hi) * 0.5f;
+  center[0] = c.x;
+  center[1] = c.y;
+  center[2] = c.z;
+  *radius = fmaxf(kRayEpsilon, norm(c - lo) * (1.f + kRayEpsilon));
+}
 
 struct SurfaceInteraction {
   float t;
@@ -94,7 +125,11 @@ MTX_HD SurfaceInteraction si_from_vertices(float t, uint32_t prim, float u, floa
 }
 
 MTX_HD SurfaceInteraction compute_si(const SceneView &s, float t, uint32_t prim, float u, float v, V3 ray_d) {
-  if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
+  if (prim == 0xffffffffu) {  // a miss: si.emitter(scene) is the environment, if any
+    SurfaceInteraction si = si_invalid(t, prim, ray_d);
+    si.emitter = env_index(s);
+    return si;
+  }
   const uint32_t i0 = s.tri_vidx[3 * prim + 0], i1 = s.tri_vidx[3 * prim + 1], i2 = s.tri_vidx[3 * prim + 2];
   const V3 p0 = load3(s.vpos, i0), p1 = load3(s.vpos, i1), p2 = load3(s.vpos, i2);
   const mtx_shape sh = s.shapes[s.tri_shape[prim]];
@@ -149,12 +184,32 @@ struct DirectionSample {
 // AreaEmitter::sample_direction (one-sided). Returns the emitter weight
 // (radiance / pdf, times the emitter count); `ds.pdf` includes the pick pdf.
 MTX_HD V3 sample_emitter_direction(const SceneView &s, V3 ref_p, V2 u, DirectionSample *ds) {
-  const uint32_t count = s.n_emitters;
+  const uint32_t count = emitter_count(s);
   const float count_f = (float)count;
   float scaled = u.x * count_f;
   uint32_t index = (uint32_t)scaled;
   if (index > count - 1u) index = count - 1u;
   u.x = scaled - (float)index;
+  if ((int32_t)index == env_index(s)) {
+    // ConstantBackgroundEmitter::sample_direction: a uniform sphere direction
+    // and a target point two bounding radii away (the radius grown to reach
+    // a reference point outside the sphere); weight radiance / pdf
+    const V3 d = square_to_uniform_sphere(u);
+    const V3 ctr = V3{s.env_center[0], s.env_center[1], s.env_center[2]};
+    const float radius = fmaxf(s.env_radius, norm(ref_p - ctr));
+    const float dist = 2.f * radius;
+    ds->p = fma3(d, dist, ref_p);
+    ds->n = -d;
+    ds->d = d;
+    ds->dist = dist;
+    ds->pdf = square_to_uniform_sphere_pdf(d);
+    ds->emitter = (int32_t)index;
+    V3 spec = V3{s.env_radiance[0], s.env_radiance[1], s.env_radiance[2]} / ds->pdf;
+    ds->pdf *= 1.f / count_f;
+    spec = spec * count_f;
+    if (!(ds->pdf != 0.f)) spec = v3s(0.f);
+    return spec;
+  }
   const mtx_emitter e = s.emitters[index];
   // Rectangle::sample_position: to_world.transform_affine((2u-1, 2v-1, 0))
   float lx = fmaf(u.x, 2.f, -1.f), ly = fmaf(u.y, 2.f, -1.f);
@@ -187,16 +242,20 @@ MTX_HD V3 sample_emitter_direction(const SceneView &s, V3 ref_p, V2 u, Direction
 // shape pdf_position * dist^2 / |cos|, zero unless the emitter faces ref.
 MTX_HD float pdf_emitter_direction(const SceneView &s, int32_t emitter, V3 ds_d, float ds_dist, V3 ds_n) {
   if (emitter < 0) return 0.f;
+  if (emitter == env_index(s))  // ConstantBackgroundEmitter::pdf_direction
+    return square_to_uniform_sphere_pdf(ds_d) * (1.f / (float)emitter_count(s));
   const mtx_emitter e = s.emitters[emitter];
   float dp = absdot(ds_d, ds_n);
   float pdf = e.inv_area * ((dp != 0.f) ? sqr(ds_dist) / dp : 0.f);
   if (!(dot(ds_d, ds_n) < 0.f)) pdf = 0.f;
-  return pdf * (1.f / (float)s.n_emitters);
+  return pdf * (1.f / (float)emitter_count(s));
 }
 
 // AreaEmitter::eval(si): radiance if the front side is seen.
 MTX_HD V3 emitter_eval(const SceneView &s, int32_t emitter, V3 wi_local) {
   if (emitter < 0) return v3s(0.f);
+  if (emitter == env_index(s))  // ConstantBackgroundEmitter::eval: the radiance, any direction
+    return V3{s.env_radiance[0], s.env_radiance[1], s.env_radiance[2]};
   const mtx_emitter e = s.emitters[emitter];
   if (!(wi_local.z > 0.f)) return v3s(0.f);
   return V3{e.radiance[0], e.radiance[1], e.radiance[2]};

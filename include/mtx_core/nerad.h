@@ -61,14 +61,6 @@ MTX_HD V2 square_to_uniform_triangle(V2 s) {
   return V2{1.f - t, t * s.y};
 }
 
-MTX_HD V3 square_to_uniform_sphere(V2 s) {
-  const float z = fmaf(-2.f, s.y, 1.f);
-  const float r = safe_sqrt(fmaf(-z, z, 1.f));
-  float sn, cs;
-  dsincos(kTwoPi * s.x, &sn, &cs);
-  return V3{r * cs, r * sn, z};
-}
-
 // Surface-area tables of a scene (built on the host, mtx/nerad.py): the
 // shape distribution and, per shape, the distribution over its triangles
 // (tri_dist[shape] views into the concatenated pmf / cdf arrays, whose

@@ -40,6 +40,17 @@ MTX_HD V3 square_to_uniform_hemisphere(V2 s) {
 }
 MTX_HD float square_to_uniform_hemisphere_pdf(V3) { return kInvTwoPi; }
 
+// Uniform sphere (the constant environment's direction sampling):
+// z = 1 - 2 s.y, r = safe_sqrt(1 - z^2), phi = 2 pi s.x.
+MTX_HD V3 square_to_uniform_sphere(V2 s) {
+  const float z = fmaf(-2.f, s.y, 1.f);
+  const float r = safe_sqrt(fmaf(-z, z, 1.f));
+  float sn, cs;
+  dsincos(kTwoPi * s.x, &sn, &cs);
+  return V3{r * cs, r * sn, z};
+}
+MTX_HD float square_to_uniform_sphere_pdf(V3) { return kInvFourPi; }
+
 MTX_HD V2 square_to_uniform_disk(V2 s) {
   float r = sqrtf(s.x);
   float sn, cs;

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "mtx.h"
+#include "mtx_core/interaction.h"
 #include "prims.h"
 #include "wavefront.h"
 
@@ -355,7 +356,7 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
     return MTX_E_ARG;
   }
   if (!d->nodes || !d->tri_geom || !d->tri_vidx || !d->tri_shape || !d->vpos || !d->shapes || !d->materials ||
-      d->n_tris == 0 || d->n_nodes == 0 || d->n_emitters == 0 || !d->emitters) {
+      d->n_tris == 0 || d->n_nodes == 0 || (d->n_emitters == 0 && !d->has_env) || (d->n_emitters && !d->emitters)) {
     mtx_set_error("mtx_scene_upload: incomplete scene (need geometry, BVH, shapes, materials, >=1 emitter)");
     return MTX_E_ARG;
   }
@@ -572,6 +573,9 @@ int mtx_scene_upload(mtx_ctx *c, const mtx_scene_desc *d) {
   s.n_tris = d->n_tris;
   s.n_emitters = d->n_emitters;
   s.camera = d->camera;
+  s.has_env = d->has_env ? 1u : 0u;
+  for (int k = 0; k < 3; ++k) s.env_radiance[k] = d->env_radiance[k];
+  mtx::env_bsphere(d->vpos, d->n_verts, s.env_center, &s.env_radius);
   // LDS per trace block (8 blocks of 256 threads per CU fill the 160 KB):
   // closest hit 16 x 4-B stack entries per lane + 64 nodes of 64 B,
   // occlusion 8 x 8-B entries + 48 nodes of 80 B
@@ -1072,6 +1076,13 @@ int render_restir(mtx_ctx *c, const mtx_render_args *a, float4 *film_dev, Timer 
   if (a->sample_offset != 0 || a->spp_total != spp) {
     mtx_set_error("mtx_render: ReSTIR GI needs spp_total = spp and sample_offset = 0");
     return MTX_E_ARG;
+  }
+  if (c->scene.has_env) {
+    // restirgi.py's reservoirs keep the first secondary hit (x_s, n_s) and
+    // its visibility; a secondary ray escaping to an environment has no such
+    // point, and the reference's handling of it is not restated here
+    mtx_set_error("mtx_render: ReSTIR GI with an environment emitter is not supported");
+    return MTX_E_UNSUPPORTED;
   }
   const uint64_t n64 = (uint64_t)W * H * spp;
   if (n64 * 18 >= (1ull << 32)) {

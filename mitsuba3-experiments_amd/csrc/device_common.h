@@ -55,6 +55,12 @@ __device__ __forceinline__ SceneView make_view(const DevScene &s) {
   v.n_tris = s.n_tris;
   v.n_emitters = s.n_emitters;
   v.camera = s.camera;
+  v.has_env = s.has_env;
+  for (int k = 0; k < 3; ++k) {
+    v.env_radiance[k] = s.env_radiance[k];
+    v.env_center[k] = s.env_center[k];
+  }
+  v.env_radius = s.env_radius;
   return v;
 }
 
@@ -66,7 +72,11 @@ __device__ __forceinline__ SceneView make_view(const DevScene &s) {
 //   normals, bit1 uvs) | r3..r5 n0..n2 | r6 uv0, uv1 | r7 uv2
 __device__ __forceinline__ SurfaceInteraction compute_si_dev(const DevScene &s, float t, uint32_t prim, float u,
                                                              float v, V3 ray_d) {
-  if (prim == 0xffffffffu) return si_invalid(t, prim, ray_d);
+  if (prim == 0xffffffffu) {  // a miss: the environment, if any (compute_si)
+    SurfaceInteraction si = si_invalid(t, prim, ray_d);
+    si.emitter = s.has_env ? (int32_t)s.n_emitters : -1;
+    return si;
+  }
   const float4 *r = s.shade_rec + 8 * (size_t)prim;
   const float4 a = r[0], b = r[1], c = r[2];
   const uint32_t fl = __float_as_uint(c.w);

@@ -184,11 +184,12 @@ __global__ __launch_bounds__(kTraceBlock) MTX_TRACE_ATTR void k_trace_shadow(Dev
 // Ray generation
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void init_path(const WaveBuffers &b, const ChunkParams &p, uint32_t i, const Ray &ray,
-                                          const Pcg32 &rng, float2 pos) {
+                                          const Pcg32 &rng, float2 pos, bool env) {
   uint32_t depth = 0, flags = 0;
   if (p.integrator == MTX_INT_PATH_MIS) {
     depth = 0;
-    flags = PF_PREV_DELTA;  // prev_bsdf_delta = True (path-mis.py:46)
+    // prev_bsdf_delta = True (path-mis.py:46); valid_ray = scene.environment() is not None (:41)
+    flags = PF_PREV_DELTA | (env ? PF_VALID_RAY : 0u);
   } else if (p.integrator == MTX_INT_SIMPLE) {
     depth = 0;  // simple.py:27
   } else {
@@ -219,7 +220,7 @@ __global__ void k_raygen_camera(DevScene s, WaveBuffers b, ChunkParams p) {
   const float sx = (float)x + u.x, sy = (float)y + u.y;
   const V2 adj = V2{sx / (float)p.width, sy / (float)p.height};
   const Ray ray = camera_ray(s.camera, adj);  // path.py:60-62
-  init_path(b, p, i, ray, rng, make_float2(sx, sy));
+  init_path(b, p, i, ray, rng, make_float2(sx, sy), s.has_env != 0);
 }
 
 __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const float *rays, const uint32_t *lanes,
@@ -231,7 +232,7 @@ __global__ void k_raygen_rays(DevScene s, WaveBuffers b, ChunkParams p, const fl
   for (uint32_t k = 0; k < rng_skip; ++k) rng.next_u32();
   const float *r = rays + 6 * (size_t)i;
   Ray ray{V3{r[0], r[1], r[2]}, V3{r[3], r[4], r[5]}, kLargest};
-  init_path(b, p, i, ray, rng, make_float2(0.f, 0.f));
+  init_path(b, p, i, ray, rng, make_float2(0.f, 0.f), s.has_env != 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1669,8 +1670,9 @@ __global__ void k_mlt_begin(DevScene s, WaveBuffers b, ChunkParams p) {
   b.ray_d[0][i] = make_float4(ray.d.x, ray.d.y, ray.d.z, 0.f);
   b.thr[0][i] = make_float4(1.f, 1.f, 1.f, 1.f);
   b.L[0][i] = make_float4(0.f, 0.f, 0.f, 1.f);  // prev_bsdf_pdf = 1 (queue position i)
-  // pssmltpath.py:42-44: prev_si zero, prev_bsdf_delta = True
-  const uint32_t fl = p.integrator == MTX_INT_PSSMLT_PATH ? (PF_PREV_DELTA << 16) : 0u;
+  // pssmltpath.py:39-44: prev_si zero, prev_bsdf_delta = True, valid_ray = scene.environment() is not None
+  const uint32_t fl =
+      p.integrator == MTX_INT_PSSMLT_PATH ? ((PF_PREV_DELTA | (s.has_env ? PF_VALID_RAY : 0u)) << 16) : 0u;
   if (p.integrator == MTX_INT_PSSMLT_PATH) b.prev[0][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   b.misc[0][i] = make_uint4((uint32_t)rng.state, (uint32_t)(rng.state >> 32), rng.seq, fl);
   if (!p.ident0) b.queue[0][i] = i;

@@ -103,6 +103,9 @@ struct DevScene {
   uint32_t occ_urefill;    // the same for the any-hit kernels
   uint32_t xcd_claim;      // persistent kernels: claim rays from the own XCD's queue segment first
   mtx_camera camera;
+  // constant environment (mtx_core/interaction.h SceneView: emitter index n_emitters)
+  uint32_t has_env;
+  float env_radiance[3], env_center[3], env_radius;
 };
 
 // Global spill area of a wavefront's traversals (the deeper of the two

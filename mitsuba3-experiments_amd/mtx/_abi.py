@@ -3,7 +3,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-MTX_ABI_VERSION = 7
+MTX_ABI_VERSION = 8
 
 MTX_MAT_DIFFUSE = 1
 MTX_MAT_ROUGHPLASTIC = 2
@@ -134,6 +134,8 @@ class SceneDesc(C.Structure):
         ("n_occ_nodes", C.c_uint32),
         ("pad1", C.c_uint32),
         ("occ_perm", C.c_void_p),
+        ("env_radiance", C.c_float * 3),
+        ("has_env", C.c_uint32),
     ]
 
 

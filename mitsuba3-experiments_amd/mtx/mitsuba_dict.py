@@ -19,8 +19,9 @@ a ``to_world`` transform; BSDFs diffuse, roughplastic, conductor,
 roughconductor, dielectric, roughdielectric, twosided, mask, with rgb /
 scalar / bitmap values and ``ref`` references; shapes rectangle, cube and
 obj (``filename``, read from ``base_dir``), with an ``area`` emitter on
-rectangles. Anything else -- including an ``obj`` whose file is missing and
-environment emitters (``constant``, ``envmap``; see ENV_EMITTERS) -- raises
+rectangles; a ``constant`` environment emitter (``radiance`` rgb or float;
+mtx_core/interaction.h). Anything else -- including an ``obj`` whose file is
+missing and ``envmap`` environments (see ENV_EMITTERS) -- raises
 :class:`mtx.MtxError` rather than rendering a different scene.
 """
 from __future__ import annotations
@@ -37,8 +38,9 @@ _IGNORED = {"integrator", "sampler"}  # scene entries that do not describe geome
 # Environment emitters: the reference integrators read them where a ray
 # escapes (path-mis.py:41 valid_ray = scene.environment() is not None;
 # path.py:239 / path-mis.py:84 si.emitter(scene).eval on a miss) and NEE picks
-# them among the scene's emitters. mtx's kernels evaluate rectangle area
-# emitters only and treat a miss as black, so a scene with one is refused.
+# them among the scene's emitters. mtx evaluates a ``constant`` one (uniform
+# radiance, uniform sphere sampling); an ``envmap`` (a bitmap over the sphere
+# with its own importance sampling) is refused.
 ENV_EMITTERS = {"constant", "envmap"}
 OTHER_EMITTERS = {"point", "spot", "directional", "projector", "directionalarea"}
 
@@ -111,7 +113,7 @@ def spec_from_dict(d: dict) -> dict:
     """A ``mi.load_dict`` scene dictionary -> the mtx scene spec."""
     if d.get("type") != "scene":
         raise MtxError(f"expected a scene dictionary (type 'scene'), got {d.get('type')!r}")
-    sensor, bsdfs, shapes = None, {}, []
+    sensor, bsdfs, shapes, env = None, {}, [], None
     for key, v in d.items():
         if key == "type" or not isinstance(v, dict):
             continue
@@ -147,22 +149,29 @@ def spec_from_dict(d: dict) -> dict:
             shapes.append(sd)
         elif t in _IGNORED or key in _IGNORED:
             continue
+        elif t == "constant":
+            if env is not None:
+                raise MtxError("more than one environment emitter")
+            env = {"type": "constant", "radiance": _value(v.get("radiance", 1.0))}
         elif t in ENV_EMITTERS:
             raise MtxError(f"scene entry {key!r}: environment emitter {t!r} is not supported -- mtx evaluates "
-                           "rectangle area emitters only and a ray that leaves the scene returns no radiance "
-                           "(path-mis.py:41 / :84 would read the environment there)")
+                           "rectangle area emitters and a constant environment only "
+                           "(path-mis.py:41 / :84 would read the envmap where a ray escapes)")
         elif t in OTHER_EMITTERS:
             raise MtxError(f"scene entry {key!r}: {t!r} emitters are not supported (rectangle area emitters only)")
         else:
             raise MtxError(f"scene entry {key!r}: unsupported type {t!r}")
     if sensor is None:
         raise MtxError("the scene has no perspective sensor")
-    if not any("emitter" in s for s in shapes):
-        raise MtxError("the scene has no area emitter")
+    if env is None and not any("emitter" in s for s in shapes):
+        raise MtxError("the scene has no emitter")
     for s in shapes:
         if "bsdf" in s and s["bsdf"] not in bsdfs:
             raise MtxError(f"shape {s['id']!r} references the unknown bsdf {s['bsdf']!r}")
-    return {"defaults": {}, "integrator": d.get("integrator"), "sensor": sensor, "bsdfs": bsdfs, "shapes": shapes}
+    spec = {"defaults": {}, "integrator": d.get("integrator"), "sensor": sensor, "bsdfs": bsdfs, "shapes": shapes}
+    if env is not None:
+        spec["environment"] = env
+    return spec
 
 
 def scene_from_dict(d: dict, base_dir: str | None = None, tex_res: int = 512):

@@ -29,6 +29,12 @@ def _m4(vals):
     return np.asarray(vals, dtype=np.float64).reshape(4, 4)
 
 
+def _rgb3(v):
+    """A radiance given as one float or three."""
+    a = np.asarray(v, dtype=np.float64).reshape(-1)
+    return np.repeat(a, 3) if a.size == 1 else a[:3]
+
+
 class Scene:
     """Host-side scene: numpy arrays in the mtx.h layout plus the BVH.
 
@@ -38,6 +44,7 @@ class Scene:
 
     def __init__(self):
         self.meta = {}
+        self.env_radiance = None  # constant environment radiance (rgb) or None
 
     # ------------------------------------------------------------ building --
     @classmethod
@@ -257,6 +264,8 @@ class Scene:
         s.tables = np.ascontiguousarray(np.concatenate(tables) if tables else np.zeros(1, np.float32))
         s.n_tables = int(sum(x.size for x in tables))
         s.camera = _camera(spec["sensor"], W, H)
+        env = spec.get("environment")
+        s.env_radiance = None if env is None else tuple(float(x) for x in _rgb3(env["radiance"]))
         s._build_bvh(tri_vidx, tri_shape)
         s.meta = {"scene": "bedroom-proxy" if not loaded else "xml", "proxy_version": proxy.PROXY_VERSION,
                   "fov_axis": spec["sensor"].get("fov_axis", "x"),
@@ -387,6 +396,9 @@ class Scene:
         d.n_occ_nodes = self.n_occ_nodes
         self.occ_perm = np.ascontiguousarray(self.occ_perm, np.uint32)
         d.occ_perm = self.occ_perm.ctypes.data
+        env = getattr(self, "env_radiance", None)
+        d.has_env = 0 if env is None else 1
+        d.env_radiance[:] = (0.0, 0.0, 0.0) if env is None else env
         return d
 
     def save(self, path: str):
@@ -400,7 +412,9 @@ class Scene:
                  camera=np.frombuffer(bytes(self.camera), np.uint8),
                  meta=np.frombuffer(json.dumps(self.meta).encode(), np.uint8),
                  counts=np.array([self.n_tris, self.n_nodes, self.n_textures, self.n_tables, self.bvh_depth,
-                                  self.n_occ_nodes, self.occ_depth], np.int64))
+                                  self.n_occ_nodes, self.occ_depth], np.int64),
+                 env=np.array([0.0, 0.0, 0.0, 0.0] if getattr(self, "env_radiance", None) is None
+                              else [1.0, *self.env_radiance], np.float32))
 
     @classmethod
     def load(cls, path: str) -> "Scene":
@@ -423,6 +437,8 @@ class Scene:
         s.meta = json.loads(z["meta"].tobytes().decode())
         (s.n_tris, s.n_nodes, s.n_textures, s.n_tables, s.bvh_depth, s.n_occ_nodes,
          s.occ_depth) = (int(x) for x in z["counts"])
+        env = z["env"] if "env" in z.files else np.zeros(4, np.float32)
+        s.env_radiance = tuple(float(x) for x in env[1:]) if env[0] else None
         return s
 
 

@@ -138,4 +138,12 @@ def parse_scene_xml(path: str, overrides: dict | None = None) -> dict:
         if fn:
             sd["lfs_size"] = lfs_pointer_size(os.path.join(base, fn))
         shapes.append(sd)
-    return {"defaults": defaults, "integrator": integrator, "sensor": sensor, "bsdfs": bsdfs, "shapes": shapes}
+    spec = {"defaults": defaults, "integrator": integrator, "sensor": sensor, "bsdfs": bsdfs, "shapes": shapes}
+    envs = root.findall("emitter")  # top-level emitters: environments
+    for e in envs:
+        t = _subst(e.get("type"), defaults)
+        if t != "constant" or len(envs) > 1:
+            from ._lib import MtxError
+            raise MtxError(f"{path}: top-level emitter {t!r}: only one constant environment is supported")
+        spec["environment"] = {"type": "constant", "radiance": _props(e, defaults).get("radiance", 1.0)}
+    return spec

@@ -77,6 +77,9 @@ SceneView make_view(const mtx_scene_desc *d) {
   s.n_tris = d->n_tris;
   s.n_emitters = d->n_emitters;
   s.camera = d->camera;
+  s.has_env = d->has_env ? 1u : 0u;
+  for (int k = 0; k < 3; ++k) s.env_radiance[k] = d->env_radiance[k];
+  env_bsphere(d->vpos, d->n_verts, s.env_center, &s.env_radius);
   return s;
 }
 
@@ -270,7 +273,7 @@ V3 orc_path_mis(const SceneView &s, Pcg32 &rng, Ray ray, uint32_t max_depth, uin
   V3 throughput = v3s(1.f), result = v3s(0.f);
   float eta = 1.f;
   uint32_t depth = 0;
-  bool valid_ray = false;  // scene.environment() is None for the bedroom (:41)
+  bool valid_ray = s.has_env != 0;  // scene.environment() is not None (:41; None for the bedroom)
   V3 prev_p = v3s(0.f);
   float prev_bsdf_pdf = 1.f;
   bool prev_bsdf_delta = true;

@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_symbol():
     L = _lib.lib()
     for name in _declared():
         assert hasattr(L, name), name
-    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 7
+    assert L.mtx_abi_version() == _lib._abi.MTX_ABI_VERSION == 8
 
 
 def test_struct_sizes_match_header():
@@ -42,6 +42,35 @@ def test_struct_sizes_match_header():
     assert C.sizeof(_abi.TrainStats) == 88
     assert C.sizeof(_abi.NeradTables) == 96
     assert C.sizeof(_abi.NeradArgs) == 20
+
+
+def test_struct_layouts_match_the_c_compiler(tmp_path):
+    """Every ctypes mirror of an include/mtx.h struct has the C compiler's
+    size and field offsets (gcc on the header itself)."""
+    import shutil
+    import subprocess
+
+    from mtx import _abi
+
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    structs = {"SceneDesc": "mtx_scene_desc", "RenderArgs": "mtx_render_args", "Camera": "mtx_camera",
+               "Material": "mtx_material", "Emitter": "mtx_emitter"}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mtx.h"', "int main(void) {"]
+    for py, c in structs.items():
+        lines.append(f'  printf("{py} size %zu\\n", sizeof({c}));')
+        for f, _ in getattr(_abi, py)._fields_:
+            lines.append(f'  printf("{py} {f} %zu\\n", offsetof({c}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    for line in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        py, field, val = line.split()
+        T = getattr(_abi, py)
+        got = C.sizeof(T) if field == "size" else getattr(T, field).offset
+        assert got == int(val), (py, field, got, int(val))
 
 
 def test_ctx_create_without_gpu_fails_cleanly():

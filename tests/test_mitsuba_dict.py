@@ -171,7 +171,7 @@ def test_plugin_resolves_loaded_scenes():
     with pytest.raises(MtxError, match="named conductor"):
         spec_from_dict(gold)
     nolight = {k: v for k, v in cornell_box().items() if k != "light"}
-    with pytest.raises(MtxError, match="no area emitter"):
+    with pytest.raises(MtxError, match="no emitter"):
         spec_from_dict(nolight)
 
 
@@ -219,16 +219,15 @@ def test_obj_shape_and_fov_axes(tmp_path):
         scene_from_dict(d3)
 
 
-@pytest.mark.parametrize("entry,match", [({"type": "constant", "radiance": {"type": "rgb", "value": 1.0}},
-                                          "environment emitter 'constant'"),
-                                         ({"type": "envmap", "filename": "sky.exr"}, "environment emitter 'envmap'"),
+@pytest.mark.parametrize("entry,match", [({"type": "envmap", "filename": "sky.exr"}, "environment emitter 'envmap'"),
                                          ({"type": "point", "position": [0, 0.5, 0]}, "'point' emitters"),
                                          ({"type": "directional", "direction": [0, -1, 0]}, "'directional' emitters")])
 def test_environment_and_delta_emitters_rejected(entry, match):
     """An environment emitter is what a reference integrator reads where a
     ray escapes (path-mis.py:41 valid_ray, :84 / path.py:239 si.emitter on a
-    miss); mtx's kernels have none, so such a scene is refused with that
-    reason instead of rendering it black."""
+    miss); mtx evaluates a constant one (tests/test_environment.py), an envmap
+    is refused with that reason instead of rendering it black, and so are
+    delta lights."""
     from mtx import MtxError
     from mtx.mitsuba_dict import spec_from_dict
 
@@ -278,7 +277,7 @@ def test_loaded_scene_is_recorded_at_load_time():
     cols = sorted(tuple(round(x, 4) for x in m.rgb) for m in sc.materials)
     assert (0.5701, 0.043, 0.0444) in cols and sc.n_tris == 36
     bad = cornell_box(16, 16)
-    bad["sky"] = {"type": "constant"}
+    bad["sky"] = {"type": "envmap", "filename": "sky.exr"}
     bad_obj = mi.load_dict(bad)
     try:
         integrators.mtx_scene_of(bad_obj)
