@@ -162,7 +162,7 @@ def test_restir_with_environment_is_refused():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("scene_kind", ["furnace", "cornell_sky"])
-@pytest.mark.parametrize("name", ["path_test", "mypath", "integrator"])
+@pytest.mark.parametrize("name", ["path_test", "mypath", "integrator", "nrc"])
 def test_environment_gpu_bit_exact(oracle, scene_kind, name):
     """The kernels' environment (miss emission with MIS, NEE pick, far-point
     shadow rays, valid_ray) against the oracle, bit for bit."""
@@ -171,7 +171,7 @@ def test_environment_gpu_bit_exact(oracle, scene_kind, name):
 
     d = furnace(32, 32, albedo=0.8) if scene_kind == "furnace" else with_sky(cornell_box(32, 32), [0.4, 0.5, 0.6])
     sc = scene_from_dict(d)
-    integ = load_dict({"type": name, "max_depth": 8})
+    integ = load_dict({"type": name, "max_depth": 8} if name != "nrc" else {"type": name})
     film = integ.render_film(sc, seed=11, spp=8)
     ref = oracle.render(sc, integ.render_args(sc, 11, 8))
     np.testing.assert_array_equal(film, ref)
