@@ -13,10 +13,11 @@ for i in $(seq 1 $ROUNDS); do
       rc=$?; [ $rc -ne 0 ] && { tail -5 $OUT/wlab_$TAG.err; exit $rc; }
       python3 -c "
 import json, sys
-d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
-k = {n: v.get('ms_per_step') for n, v in (d.get('kernels') or {}).items()}
-print(json.dumps({'workload': sys.argv[4], 'env': sys.argv[2], 'round': int(sys.argv[3]), 'value': d['value'],
-                  'unit': d['unit'], 'ms': d['ms_per_step'], 'kernels': k}))" $OUT/wlab_$TAG.tmp "$e" $i $w | tee -a $OUT/wlab_$TAG.jsonl
+for line in open(sys.argv[1]).read().strip().splitlines():  # one line per metric (prims: several)
+    d = json.loads(line)
+    k = {n: v.get('ms_per_step') for n, v in (d.get('kernels') or {}).items() if isinstance(v, dict)}
+    print(json.dumps({'workload': sys.argv[4], 'env': sys.argv[2], 'round': int(sys.argv[3]), 'metric': d['metric'][:40],
+                      'value': d['value'], 'unit': d['unit'], 'ms': d['ms_per_step'], 'kernels': k}))" $OUT/wlab_$TAG.tmp "$e" $i $w | tee -a $OUT/wlab_$TAG.jsonl
     done
   done
 done
