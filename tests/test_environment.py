@@ -175,3 +175,20 @@ def test_environment_gpu_bit_exact(oracle, scene_kind, name):
     film = integ.render_film(sc, seed=11, spp=8)
     ref = oracle.render(sc, integ.render_args(sc, 11, 8))
     np.testing.assert_array_equal(film, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["pssmlt_simple", "pssmlt"])
+def test_environment_pssmlt_gpu_bit_exact(oracle, name):
+    """PSSMLT chains under a sky (pssmltpath.py:39 valid_ray from the
+    environment; escaped proposals see its radiance): 60 Metropolis
+    iterations, film bit-identical to the oracle."""
+    from mtx import load_dict
+    from mtx.mitsuba_dict import scene_from_dict
+
+    sc = scene_from_dict(with_sky(cornell_box(24, 24), [0.4, 0.5, 0.6]))
+    integ = load_dict({"type": name, "iterations": 60})
+    film = integ.render_film(sc, seed=4, spp=2)
+    ref = oracle.pssmlt_render(sc, integ.render_args(sc, 4, 2), 60)
+    np.testing.assert_array_equal(film, ref)
+    assert film[..., 3].sum() > 0
